@@ -1,0 +1,192 @@
+/*
+ * uvio_hp.h — C ABI of the MI355X-native uvio/OpenVINS hot path
+ * (track -> propagate -> MSCKF/SLAM/UWB update -> EKF update).
+ *
+ * This is the drop-in boundary.  The reference exposes C++ classes, not a C ABI
+ * (SURVEY.md §8b); every entry point below names the reference interface it
+ * replaces (path:line relative to the reference checkout).  All functions return
+ * an int status: 0 = ok, < 0 = UVIO_HP_E_*.  They never call exit(); the
+ * reference's fatal paths (std::exit on negative covariance diagonal,
+ * StateHelper.cpp:112,181; propagation backwards, Propagator.cpp:39,46) become
+ * UVIO_HP_E_NUMERIC / UVIO_HP_E_ORDER and leave the handle in a defined state.
+ *
+ * Threading (mirrors the reference, SURVEY §8b "Threading"): uvio_hp_feed_imu may be
+ * called concurrently with the other feeds (IMU buffer is mutex-guarded like
+ * Propagator::imu_data_mtx, Propagator.h:68); camera / sim / UWB feeds must be
+ * serialized by the caller (single update thread, ROS1Visualizer.h:173).
+ *
+ * No torch / Eigen / OpenCV types cross this boundary: plain pointers and sizes.
+ */
+#ifndef UVIO_HP_H
+#define UVIO_HP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UVIO_HP_OK 0
+#define UVIO_HP_E_ARG (-1)      /* bad argument / size */
+#define UVIO_HP_E_STATE (-2)    /* not initialized, or call not valid in this state */
+#define UVIO_HP_E_DEVICE (-3)   /* HIP runtime error or no MI355X device */
+#define UVIO_HP_E_NUMERIC (-4)  /* negative covariance diagonal (ref: std::exit) */
+#define UVIO_HP_E_CONFIG (-5)   /* config file missing / unparsable */
+#define UVIO_HP_E_ORDER (-6)    /* measurement out of order (ref: std::exit in Propagator) */
+#define UVIO_HP_E_CAPACITY (-7) /* a compile-time capacity was exceeded */
+
+#define UVIO_HP_MAX_CAMS 4
+#define UVIO_HP_MAX_ANCHORS 16
+
+/* ---- option structs: the keys of estimator_config.yaml / kalibr_*.yaml / uwb_*.yaml ---- */
+
+typedef struct {
+  int model;       /* 0 = radtan (pinhole-radtan, CamRadtan.h), 1 = equidistant (CamEqui.h) */
+  int width, height;
+  double intrinsics[8]; /* fx fy cx cy d0 d1 d2 d3 (CamBase::set_value, CamBase.h:56) */
+  double q_ItoC[4];     /* JPL quaternion of R_ItoC (x y z w), from T_imu_cam (VioManagerOptions.h) */
+  double p_IinC[3];
+} uvio_hp_camera_t;
+
+typedef struct {
+  uint64_t id;
+  int fix;
+  double p_AinG[3];
+  double const_bias, dist_bias;
+  double cov_diag[5]; /* p p p c d (UVioManagerOptions.h:80) */
+} uvio_hp_anchor_t;
+
+typedef struct {
+  /* StateOptions (ov_msckf/src/state/StateOptions.h:41-96) */
+  int do_fej;
+  int integration;            /* 0 discrete, 1 rk4, 2 analytical */
+  int num_cameras;
+  int use_stereo;
+  int do_calib_camera_pose;
+  int do_calib_camera_intrinsics;
+  int do_calib_camera_timeoffset;
+  int do_calib_imu_intrinsics;
+  int do_calib_imu_g_sensitivity;
+  int imu_model;              /* 0 kalibr, 1 rpng */
+  int max_clone_size;
+  int max_slam_features;
+  int max_slam_in_update;
+  int max_msckf_in_update;
+  int max_aruco_features;
+  int feat_rep_msckf;         /* LandmarkRepresentation (LandmarkRepresentation.h:38) */
+  int feat_rep_slam;
+  double dt_slam_delay;
+  double gravity_mag;
+  double calib_camimu_dt;
+  /* UpdaterOptions (UpdaterOptions.h:33-44) */
+  double msckf_sigma_pix, msckf_chi2_multipler;
+  double slam_sigma_pix, slam_chi2_multipler;
+  /* NoiseManager (Propagator.h:44) */
+  double sigma_w, sigma_a, sigma_wb, sigma_ab;
+  /* IMU intrinsics initial values (kalibr_imu_chain.yaml: Tw, Ta, Tg, R_IMUtoGYRO, R_IMUtoACC) */
+  double imu_dw[6], imu_da[6], imu_tg[9];
+  double q_GYROtoIMU[4], q_ACCtoIMU[4];
+  /* FeatureInitializerOptions (FeatureInitializerOptions.h:33-70) */
+  int fi_triangulate_1d, fi_refine_features, fi_max_runs;
+  double fi_init_lamda, fi_max_lamda, fi_min_dx, fi_min_dcost, fi_lam_mult;
+  double fi_min_dist, fi_max_dist, fi_max_baseline, fi_max_cond_number;
+  /* cameras */
+  uvio_hp_camera_t cams[UVIO_HP_MAX_CAMS];
+  /* TrackKLT front-end (estimator_config.yaml: num_pts .. histogram_method) */
+  int num_pts, fast_threshold, grid_x, grid_y, min_px_dist;
+  int histogram_method;       /* 0 none, 1 histogram, 2 clahe */
+  int downsample_cameras;
+  double track_frequency;
+  /* uvio (UVioManagerOptions.h:52-90, UVioStateOptions.h:45, UVioUpdaterOptions.h:46) */
+  int use_uwb;
+  int do_calib_uwb_extrinsics;
+  double prior_uwb_imu_cov;
+  double uwb_sigma_range, uwb_chi2_multipler;
+  double min_dist_to_use_uwb;
+  double p_IinU[3];           /* uwb_extrinsics = -p_UinI */
+  int n_anchors_to_fix;
+  int n_anchors;
+  uvio_hp_anchor_t anchors[UVIO_HP_MAX_ANCHORS];
+  /* runtime */
+  int record_timing;          /* keep per-frame stage timings (VioManager.cpp:631-644 schema) */
+} uvio_hp_options_t;
+
+/* Per-frame stage timings in seconds, the reference CSV schema
+ * "# timestamp (sec),tracking,propagation,msckf update,slam update,slam delayed,re-tri & marg,total"
+ * (VioManager.cpp:117-121, rows :631-644). */
+typedef struct {
+  double timestamp;
+  double tracking, propagation, msckf_update, slam_update, slam_delayed, marg, total;
+  int n_msckf, n_slam, n_slam_delayed, n_clones, cov_dim;
+  int msckf_rows;   /* stacked rows m before compression */
+  int msckf_cols;   /* H columns n */
+} uvio_hp_timing_t;
+
+typedef struct uvio_hp uvio_hp_t;
+
+/* ---- options ---- */
+/* Defaults of the reference option structs (StateOptions.h, UpdaterOptions.h, ...). */
+int uvio_hp_options_default(uvio_hp_options_t *opts);
+/* Parse estimator_config.yaml (+ relative_config_imu / relative_config_imucam / config_uwb files)
+ * with the reference's keys (YamlParser, opencv_yaml_parse.h:65-163; VioManagerOptions::print_and_load). */
+int uvio_hp_options_load(const char *estimator_config_path, uvio_hp_options_t *opts);
+
+/* ---- lifetime ---- */
+/* replaces ov_msckf::VioManager::VioManager(VioManagerOptions&) (VioManager.cpp:50) and
+ * uvio::UVioManager::UVioManager (uvio/src/core/UVioManager.cpp:26). device = HIP ordinal. */
+int uvio_hp_create(const uvio_hp_options_t *opts, int device, uvio_hp_t **out);
+int uvio_hp_destroy(uvio_hp_t *h);
+const char *uvio_hp_last_error(const uvio_hp_t *h);
+
+/* ---- feeds (VioManager.h:75-96, UVioManager.h:48-60) ---- */
+/* VioManager::initialize_with_gt(Matrix<17,1>) (VioManagerHelper.cpp:40): x = [t, q_GtoI(4), p, v, bg, ba] */
+int uvio_hp_initialize_with_gt(uvio_hp_t *h, const double x[17]);
+/* VioManager::feed_measurement_imu (VioManager.cpp:166) */
+int uvio_hp_feed_imu(uvio_hp_t *h, double t, const double wm[3], const double am[3]);
+/* VioManager::feed_measurement_simulation (VioManager.cpp:191) — TrackSIM path.  For camera i
+ * (i < ncam) there are counts[i] features; ids/uv are concatenated over cameras, uv as (u,v) pairs. */
+int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const int *counts,
+                            const uint64_t *ids, const float *uv);
+/* VioManager::feed_measurement_camera / UVioManager::feed_measurement_camera (UVioManager.h:48).
+ * imgs[i] is a u8 W x H image with row stride strides[i]; masks may be NULL. */
+int uvio_hp_feed_camera(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
+                        const int *strides, const uint8_t *const *masks);
+/* UVioManager::feed_measurement_uwb (UVioManager.cpp:61): one UwbData message */
+int uvio_hp_feed_uwb(uvio_hp_t *h, double t, int n, const uint64_t *anchor_ids, const double *ranges);
+/* UVioManager::try_to_initialize_uwb_anchors (UVioManager.cpp:81) */
+int uvio_hp_init_anchors(uvio_hp_t *h, int n, const uvio_hp_anchor_t *anchors);
+
+/* ---- getters (VioManager.h:99-111) ---- */
+int uvio_hp_initialized(const uvio_hp_t *h, int *out);
+/* IMU value [q(4) p(3) v(3) bg(3) ba(3)] and the state time */
+int uvio_hp_get_imu_state(uvio_hp_t *h, double *t, double out[16]);
+/* covariance dimension N (State::max_covariance_size, State.h:88) */
+int uvio_hp_get_cov_dim(uvio_hp_t *h, int *n);
+/* dense N x N covariance into out with leading dimension ld (row-major) */
+int uvio_hp_get_cov(uvio_hp_t *h, double *out, int ld);
+/* the state mean in State::_variables order (each variable's value(): quat 4 + ...);
+ * *len receives the number of doubles written; meta (optional, 3 ints per variable:
+ * kind, covariance id, covariance size) */
+int uvio_hp_get_state_vector(uvio_hp_t *h, double *out, int cap, int *len, int *meta, int meta_cap, int *nvars);
+/* timings of the last processed frame */
+int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out);
+/* number of clones and their timestamps (ascending) */
+int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
+
+/* ---- inner (kernel-level) boundary used by parity tests ---- */
+/* StateHelper::EKFUpdate (StateHelper.cpp:116) on a standalone covariance: P (N x N, row-major,
+ * in/out, host memory), H (r x n, row-major) whose column j maps to covariance index H_index[j]
+ * (the H_order blocks flattened), residual (r), isotropic noise sigma2.  dx_out (N) receives K*res.
+ * The update runs on the device (same kernels as the manager). */
+int uvio_hp_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r,
+                       const double *res, double sigma2, double *dx_out);
+/* UpdaterHelper::measurement_compress_inplace (UpdaterHelper.cpp:456) semantics: A = [H | res]
+ * (m x (n+1), row-major) -> the (n+1) x (n+1) upper-triangular R factor of A (rows of the reference's
+ * compressed [H|res] up to a per-row sign; the last row holds the residual norm not explained by H). */
+int uvio_hp_compress(const double *A, int m, int n, double *R_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UVIO_HP_H */

@@ -1,0 +1,175 @@
+// ORACLE — test infrastructure only (see la.h header).
+// C ABI of the CPU restatement, mirroring include/uvio_hp.h entry points with an orc_ prefix so
+// tests / bench.py's cpu_baseline leg can drive both implementations with identical inputs.
+#include <cstring>
+#include <string>
+
+#include "manager.h"
+
+using namespace orc;
+
+struct orc_handle {
+  Manager m;
+  std::string err;
+  explicit orc_handle(const uvio_hp_options_t &o) : m(o) {}
+};
+
+extern "C" {
+
+int orc_create(const uvio_hp_options_t *opts, orc_handle **out) {
+  if (!opts || !out) return UVIO_HP_E_ARG;
+  *out = new orc_handle(*opts);
+  return 0;
+}
+int orc_destroy(orc_handle *h) {
+  delete h;
+  return 0;
+}
+int orc_initialize_with_gt(orc_handle *h, const double x[17]) {
+  h->m.initialize_with_gt(x);
+  return 0;
+}
+int orc_feed_imu(orc_handle *h, double t, const double wm[3], const double am[3]) {
+  h->m.feed_imu(t, wm, am);
+  return 0;
+}
+int orc_feed_simulation(orc_handle *h, double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
+                        const float *uv) {
+  std::vector<int> camids(cam_ids, cam_ids + ncam);
+  std::vector<std::vector<std::pair<size_t, std::pair<float, float>>>> feats(ncam);
+  size_t k = 0;
+  for (int i = 0; i < ncam; i++)
+    for (int j = 0; j < counts[i]; j++, k++) feats[i].push_back({(size_t)ids[k], {uv[2 * k], uv[2 * k + 1]}});
+  return h->m.feed_simulation(t, camids, feats);
+}
+int orc_feed_uwb(orc_handle *h, double t, int n, const uint64_t *anchor_ids, const double *ranges) {
+  std::vector<std::pair<size_t, double>> r;
+  for (int i = 0; i < n; i++) r.push_back({(size_t)anchor_ids[i], ranges[i]});
+  return h->m.feed_uwb(t, r);
+}
+int orc_init_anchors(orc_handle *h, int n, const uvio_hp_anchor_t *a) {
+  std::vector<uvio_hp_anchor_t> v(a, a + n);
+  return h->m.init_anchors(v);
+}
+int orc_get_imu_state(orc_handle *h, double *t, double out[16]) {
+  *t = h->m.state.timestamp;
+  for (int k = 0; k < 16; k++) out[k] = h->m.state.imu->val[k];
+  return 0;
+}
+int orc_get_cov_dim(orc_handle *h, int *n) {
+  *n = h->m.state.Cov.r;
+  return 0;
+}
+int orc_get_cov(orc_handle *h, double *out, int ld) {
+  const Mat &C = h->m.state.Cov;
+  for (int i = 0; i < C.r; i++)
+    for (int j = 0; j < C.c; j++) out[(size_t)i * ld + j] = C(i, j);
+  return 0;
+}
+int orc_get_state_vector(orc_handle *h, double *out, int cap, int *len, int *meta, int meta_cap, int *nvars) {
+  int k = 0, nv = 0;
+  for (auto &v : h->m.state.variables) {
+    if (meta && 3 * nv + 2 < meta_cap) {
+      meta[3 * nv] = v->kind;
+      meta[3 * nv + 1] = v->id;
+      meta[3 * nv + 2] = v->size;
+    }
+    for (int i = 0; i < v->val.r; i++) {
+      if (k < cap) out[k] = v->val[i];
+      k++;
+    }
+    nv++;
+  }
+  *len = k;
+  if (nvars) *nvars = nv;
+  return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
+}
+int orc_get_timing(orc_handle *h, uvio_hp_timing_t *out) {
+  *out = h->m.timing;
+  return 0;
+}
+int orc_get_clone_times(orc_handle *h, double *out, int cap, int *n) {
+  int k = 0;
+  for (auto &c : h->m.state.clones) {
+    if (k < cap) out[k] = c.first;
+    k++;
+  }
+  *n = k;
+  return 0;
+}
+
+// StateHelper::EKFUpdate on a standalone covariance (variables = one Vec of size N)
+int orc_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res, double sigma2,
+                   double *dx_out) {
+  uvio_hp_options_t o;
+  std::memset(&o, 0, sizeof(o));
+  o.num_cameras = 0;
+  State s(o);
+  s.variables.clear();
+  auto big = make_vec(N);
+  big->id = 0;
+  s.variables.push_back(big);
+  s.Cov = Mat(N, N);
+  std::memcpy(s.Cov.d.data(), P, sizeof(double) * N * N);
+  // one size-1 reference per H column (H_order of scalar slices)
+  std::vector<VarP> slices;
+  std::vector<Ref> order;
+  for (int j = 0; j < n; j++) order.push_back(Ref{big.get(), H_index[j], 1});
+  Mat Hm(r, n), rm(r, 1);
+  std::memcpy(Hm.d.data(), H, sizeof(double) * r * n);
+  std::memcpy(rm.d.data(), res, sizeof(double) * r);
+  Mat before = big->val;
+  bool ok = StateHelper::EKFUpdate(s, order, Hm, rm, sigma2);
+  std::memcpy(P, s.Cov.d.data(), sizeof(double) * N * N);
+  for (int i = 0; i < N; i++) dx_out[i] = big->val[i] - before[i];
+  return ok ? 0 : UVIO_HP_E_NUMERIC;
+}
+
+// UpdaterHelper::measurement_compress_inplace on [H | res]: returns R (n+1 x n+1) of the Givens
+// sweep applied to the augmented matrix (the reference applies it to H and res jointly).
+int orc_compress(const double *A, int m, int n, double *R_out) {
+  Mat H(m, n + 1);
+  std::memcpy(H.d.data(), A, sizeof(double) * m * (n + 1));
+  Givens G;
+  int nc = n + 1;
+  for (int c = 0; c < nc; c++) {
+    for (int row = m - 1; row > c; row--) {
+      G.make(H(row - 1, c), H(row, c));
+      for (int j = c; j < nc; j++) G.apply(H(row - 1, j), H(row, j));
+    }
+  }
+  for (int i = 0; i < nc; i++)
+    for (int j = 0; j < nc; j++) R_out[i * nc + j] = (i < m && j >= i) ? H(i, j) : 0.0;
+  return 0;
+}
+
+double orc_chi2_quantile95(int dof) { return chi2_quantile95(dof); }
+
+// Camera model entry points for fixture / finite-difference tests
+int orc_camera_distort(const uvio_hp_camera_t *c, int n, const double *xy, double *uv, double *dz_dzn, double *dz_dzeta) {
+  Camera cam;
+  cam.model = c->model;
+  cam.w = c->width;
+  cam.h = c->height;
+  for (int k = 0; k < 8; k++) cam.v[k] = c->intrinsics[k];
+  for (int i = 0; i < n; i++) {
+    double u, v;
+    cam.distort_d(xy[2 * i], xy[2 * i + 1], u, v);
+    uv[2 * i] = u;
+    uv[2 * i + 1] = v;
+    Mat a, b;
+    cam.distort_jacobian(xy[2 * i], xy[2 * i + 1], a, b);
+    if (dz_dzn) std::memcpy(dz_dzn + 4 * i, a.d.data(), 4 * sizeof(double));
+    if (dz_dzeta) std::memcpy(dz_dzeta + 16 * i, b.d.data(), 16 * sizeof(double));
+  }
+  return 0;
+}
+int orc_camera_undistort(const uvio_hp_camera_t *c, int n, const float *uv, float *xy) {
+  Camera cam;
+  cam.model = c->model;
+  for (int k = 0; k < 8; k++) cam.v[k] = c->intrinsics[k];
+  for (int i = 0; i < n; i++) cam.undistort_f(uv[2 * i], uv[2 * i + 1], xy[2 * i], xy[2 * i + 1]);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,282 @@
+// ORACLE — test infrastructure only (see la.h header).
+#include "manager.h"
+
+#include <algorithm>
+
+namespace orc {
+
+using clk = std::chrono::steady_clock;
+static double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+Manager::Manager(const uvio_hp_options_t &opt)
+    : o(opt), state(opt), prop(opt), msckf(opt), slam(opt), uwb(opt), currid(4 * (size_t)opt.max_aruco_features + 1) {
+  // UVioManager ctor (UVioManager.cpp:33-58)
+  if (o.use_uwb) {
+    if (o.do_calib_uwb_extrinsics) {
+      std::vector<Ref> H_order = {imu_q_ref(state)};
+      Mat H_R(3, 3), H_L = Mat::Identity(3), R = o.prior_uwb_imu_cov * Mat::Identity(3), res(3, 1);
+      StateHelper::initialize_invertible(state, state.calib_UWBtoIMU, H_order, H_R, H_L, R, res);
+      for (int k = 0; k < 3; k++) state.calib_UWBtoIMU->val[k] = state.calib_UWBtoIMU->fej[k] = o.p_IinU[k];
+    }
+    if (o.n_anchors > 0) {
+      std::vector<uvio_hp_anchor_t> a(o.anchors, o.anchors + o.n_anchors);
+      init_anchors(a);
+    }
+  }
+}
+
+// VioManagerHelper.cpp:40-76
+void Manager::initialize_with_gt(const double x[17]) {
+  for (int k = 0; k < 16; k++) state.imu->val[k] = state.imu->fej[k] = x[1 + k];
+  Mat Cov = std::pow(0.02, 2) * Mat::Identity(15);
+  for (int k = 0; k < 3; k++) {
+    Cov(k, k) = std::pow(0.017, 2);
+    Cov(3 + k, 3 + k) = std::pow(0.05, 2);
+    Cov(6 + k, 6 + k) = std::pow(0.01, 2);
+  }
+  StateHelper::set_initial_covariance(state, Cov, {ref_of(state.imu)});
+  state.timestamp = x[0];
+  startup_time = x[0];
+  is_initialized = true;
+  db.cleanup_measurements(state.timestamp);
+}
+
+// VioManager.cpp:166-189
+void Manager::feed_imu(double t, const double wm[3], const double am[3]) {
+  double oldest_time = state.margtimestep();
+  if (oldest_time > state.timestamp) oldest_time = -1;
+  if (!is_initialized) oldest_time = t - 2.0 + state.calib_dt->val[0] - 0.10;
+  ImuData d;
+  d.t = t;
+  for (int k = 0; k < 3; k++) {
+    d.wm[k] = wm[k];
+    d.am[k] = am[k];
+  }
+  prop.feed_imu(d, oldest_time);
+}
+
+// UVioManager.cpp:61-79
+int Manager::feed_uwb(double t, const std::vector<std::pair<size_t, double>> &ranges) {
+  if (!(is_initialized && anchors_initialized && distance > o.min_dist_to_use_uwb)) return 0;
+  if (state.timestamp >= t) return 0;
+  UwbMsg m;
+  m.t = t;
+  for (auto &r : ranges) m.ranges[r.first] = r.second;
+  past_uwb.insert({t, m});
+  return 0;
+}
+
+// UVioManager.cpp:81-113, 207-266
+int Manager::init_anchors(const std::vector<uvio_hp_anchor_t> &anchors) {
+  if (anchors.empty()) return 0;
+  for (const auto &a : anchors) {
+    if (state.anchors.find(a.id) != state.anchors.end()) continue;
+    auto v = std::make_shared<Var>(K_ANCHOR, 5, 5);
+    v->anchor_id = a.id;
+    v->fixed = a.fix != 0;
+    double x[5] = {a.p_AinG[0], a.p_AinG[1], a.p_AinG[2], a.const_bias, a.dist_bias};
+    for (int k = 0; k < 5; k++) v->val[k] = v->fej[k] = x[k];
+    state.anchors.insert({(size_t)a.id, v});
+    if (!a.fix) {
+      std::vector<Ref> H_order = {imu_q_ref(state)};
+      Mat H_R(5, 3), H_L = Mat::Identity(5), R = Mat::Identity(5), res(5, 1);
+      StateHelper::initialize_invertible(state, v, H_order, H_R, H_L, R, res);
+      Mat cov(5, 5);
+      for (int k = 0; k < 5; k++) cov(k, k) = a.cov_diag[k];
+      StateHelper::set_initial_covariance(state, cov, {ref_of(v)});
+    }
+  }
+  anchors_initialized = true;
+  return 0;
+}
+
+// UVioManager.cpp:308-344
+int Manager::do_uwb_propagate_update(const UwbMsg &m) {
+  bool valid = false;
+  for (auto &r : m.ranges)
+    if (state.anchors.find(r.first) != state.anchors.end()) {
+      valid = true;
+      break;
+    }
+  if (!valid) return 0;
+  if (!prop.propagate_uwb(state, m.t)) return 0;
+  if (state.timestamp != m.t) return 0;
+  for (auto &r : m.ranges) {
+    if (state.anchors.find(r.first) != state.anchors.end()) {
+      int rc = uwb.update_single(state, m.t, r.first, r.second);
+      if (rc < 0) return rc;
+    }
+  }
+  return 0;
+}
+
+// VioManager.cpp:191-254 + TrackSIM.cpp:30-79 (+ the UVIO UWB loop of UVioManager.cpp:178-188)
+int Manager::feed_simulation(double t, const std::vector<int> &camids,
+                             const std::vector<std::vector<std::pair<size_t, std::pair<float, float>>>> &feats) {
+  auto rT1 = clk::now();
+  for (size_t i = 0; i < camids.size(); i++) {
+    int cam_id = camids[i];
+    const Camera &cam = state.cams.at(cam_id);
+    for (const auto &f : feats[i]) {
+      size_t id = f.first + currid;
+      float un, vn;
+      cam.undistort_f(f.second.first, f.second.second, un, vn);
+      db.update_feature(id, t, cam_id, f.second.first, f.second.second, un, vn);
+    }
+  }
+  auto rT2 = clk::now();
+  timing = uvio_hp_timing_t{};
+  timing.tracking = secs(rT1, rT2);
+  if (!is_initialized) return UVIO_HP_E_STATE;
+  if (!past_uwb.empty()) {
+    for (auto it = past_uwb.begin(); it != past_uwb.lower_bound(t); it++) {
+      if (it->first < t && it->first > state.timestamp) {
+        int rc = do_uwb_propagate_update(it->second);
+        if (rc < 0) return rc;
+      }
+    }
+    past_uwb.erase(past_uwb.begin(), past_uwb.upper_bound(t));
+  }
+  int rc = do_feature_propagate_update(t, camids);
+  auto rT7 = clk::now();
+  timing.total = secs(rT1, rT7);
+  return rc;
+}
+
+// VioManager.cpp:323-651
+int Manager::do_feature_propagate_update(double t, const std::vector<int> &camids) {
+  auto rT2 = clk::now();
+  if (state.timestamp > t) return UVIO_HP_E_ORDER;
+  if (state.timestamp != t) {
+    int st = 0;
+    if (!prop.propagate_and_clone(state, t, &st)) return st;
+  }
+  auto rT3 = clk::now();
+  timing.timestamp = t;
+  timing.propagation = secs(rT2, rT3);
+  timing.n_clones = (int)state.clones.size();
+  timing.cov_dim = state.Cov.r;
+  if ((int)state.clones.size() < std::min(state.opt.max_clone_size, 5)) return 0;
+  if (state.timestamp != t) return 0;
+
+  std::vector<FeatP> feats_lost, feats_marg, feats_slam;
+  feats_lost = db.features_not_containing_newer(state.timestamp, false, true);
+  if ((int)state.clones.size() > state.opt.max_clone_size || (int)state.clones.size() > 5)
+    feats_marg = db.features_containing(state.margtimestep(), false, true);
+  auto it1 = feats_lost.begin();
+  while (it1 != feats_lost.end()) {
+    bool found = false;
+    for (const auto &p : (*it1)->uvs)
+      if (std::find(camids.begin(), camids.end(), (int)p.first) != camids.end()) {
+        found = true;
+        break;
+      }
+    if (found)
+      it1++;
+    else
+      it1 = feats_lost.erase(it1);
+  }
+  it1 = feats_lost.begin();
+  while (it1 != feats_lost.end()) {
+    if (std::find(feats_marg.begin(), feats_marg.end(), *it1) != feats_marg.end())
+      it1 = feats_lost.erase(it1);
+    else
+      it1++;
+  }
+  std::vector<FeatP> feats_maxtracks;
+  auto it2 = feats_marg.begin();
+  while (it2 != feats_marg.end()) {
+    bool reached_max = false;
+    for (const auto &cams : (*it2)->timestamps)
+      if ((int)cams.second.size() > state.opt.max_clone_size) {
+        reached_max = true;
+        break;
+      }
+    if (reached_max) {
+      feats_maxtracks.push_back(*it2);
+      it2 = feats_marg.erase(it2);
+    } else {
+      it2++;
+    }
+  }
+  int curr_aruco_tags = 0;
+  for (auto &l : state.features_SLAM)
+    if ((int)l.second->featid <= 4 * state.opt.max_aruco_features) curr_aruco_tags++;
+  if (state.opt.max_slam_features > 0 && t - startup_time >= state.opt.dt_slam_delay &&
+      (int)state.features_SLAM.size() < state.opt.max_slam_features + curr_aruco_tags) {
+    int amount_to_add = (state.opt.max_slam_features + curr_aruco_tags) - (int)state.features_SLAM.size();
+    int valid_amount = (amount_to_add > (int)feats_maxtracks.size()) ? (int)feats_maxtracks.size() : amount_to_add;
+    if (valid_amount > 0) {
+      feats_slam.insert(feats_slam.end(), feats_maxtracks.end() - valid_amount, feats_maxtracks.end());
+      feats_maxtracks.erase(feats_maxtracks.end() - valid_amount, feats_maxtracks.end());
+    }
+  }
+  for (auto &landmark : state.features_SLAM) {
+    FeatP feat2 = db.get_feature(landmark.second->featid);
+    if (feat2 != nullptr) feats_slam.push_back(feat2);
+    bool current_unique_cam = std::find(camids.begin(), camids.end(), landmark.second->unique_cam) != camids.end();
+    if (feat2 == nullptr && current_unique_cam) landmark.second->should_marg = true;
+    if (landmark.second->fail_count > 1) landmark.second->should_marg = true;
+  }
+  StateHelper::marginalize_slam(state);
+  std::vector<FeatP> feats_slam_DELAYED, feats_slam_UPDATE;
+  for (auto &f : feats_slam) {
+    if (state.features_SLAM.find(f->featid) != state.features_SLAM.end())
+      feats_slam_UPDATE.push_back(f);
+    else
+      feats_slam_DELAYED.push_back(f);
+  }
+  std::vector<FeatP> featsup_MSCKF = feats_lost;
+  featsup_MSCKF.insert(featsup_MSCKF.end(), feats_marg.begin(), feats_marg.end());
+  featsup_MSCKF.insert(featsup_MSCKF.end(), feats_maxtracks.begin(), feats_maxtracks.end());
+  auto compare_feat = [](const FeatP &a, const FeatP &b) -> bool {
+    size_t asize = 0, bsize = 0;
+    for (const auto &p : a->timestamps) asize += p.second.size();
+    for (const auto &p : b->timestamps) bsize += p.second.size();
+    return asize < bsize;
+  };
+  std::sort(featsup_MSCKF.begin(), featsup_MSCKF.end(), compare_feat);
+  if ((int)featsup_MSCKF.size() > state.opt.max_msckf_in_update)
+    featsup_MSCKF.erase(featsup_MSCKF.begin(), featsup_MSCKF.end() - state.opt.max_msckf_in_update);
+  timing.n_msckf = (int)featsup_MSCKF.size();
+  last_msckf = UpdateStats{};
+  int rc = msckf.update(state, featsup_MSCKF, &last_msckf);
+  if (rc < 0) return rc;
+  timing.msckf_rows = last_msckf.rows_stacked;
+  timing.msckf_cols = last_msckf.cols;
+  auto rT4 = clk::now();
+  std::vector<FeatP> feats_slam_UPDATE_TEMP;
+  while (!feats_slam_UPDATE.empty()) {
+    size_t k = std::min((size_t)state.opt.max_slam_in_update, feats_slam_UPDATE.size());
+    std::vector<FeatP> tmp(feats_slam_UPDATE.begin(), feats_slam_UPDATE.begin() + k);
+    feats_slam_UPDATE.erase(feats_slam_UPDATE.begin(), feats_slam_UPDATE.begin() + k);
+    rc = slam.update(state, tmp);
+    if (rc < 0) return rc;
+    feats_slam_UPDATE_TEMP.insert(feats_slam_UPDATE_TEMP.end(), tmp.begin(), tmp.end());
+  }
+  auto rT5 = clk::now();
+  timing.n_slam_delayed = (int)feats_slam_DELAYED.size();
+  rc = slam.delayed_init(state, feats_slam_DELAYED);
+  if (rc < 0) return rc;
+  auto rT6 = clk::now();
+  for (auto &f : featsup_MSCKF) f->to_delete = true;
+  db.cleanup();
+  rc = slam.change_anchors(state);
+  if (rc < 0) return rc;
+  if ((int)state.clones.size() > state.opt.max_clone_size) db.cleanup_measurements(state.margtimestep());
+  StateHelper::marginalize_old_clone(state);
+  auto rT7 = clk::now();
+  timing.msckf_update = secs(rT3, rT4);
+  timing.slam_update = secs(rT4, rT5);
+  timing.slam_delayed = secs(rT5, rT6);
+  timing.marg = secs(rT6, rT7);
+  timing.n_slam = (int)state.features_SLAM.size();
+  if (timelastupdate != -1 && state.clones.find(timelastupdate) != state.clones.end()) {
+    Mat dx = state.imu->pos() - state.clones.at(timelastupdate)->pos();
+    distance += norm(dx);
+  }
+  timelastupdate = t;
+  return 0;
+}
+
+}  // namespace orc

@@ -1,0 +1,58 @@
+// ORACLE — test infrastructure only (see la.h header).
+// Restatement of ov_msckf/src/update/UpdaterHelper.cpp:32-487, UpdaterMSCKF.cpp:58-295,
+// UpdaterSLAM.cpp:61-647 and uvio/src/update/{UpdaterUWB.cpp:13-90, UVioUpdaterHelper.cpp:147-241}.
+#pragma once
+#include "feat.h"
+
+namespace orc {
+
+struct HelperFeature {
+  size_t featid;
+  const Feature *f;  // uvs / uvs_norm / timestamps (copies in the reference; same iteration order)
+  int rep;
+  int anchor_cam_id = -1;
+  double anchor_clone_timestamp = -1;
+  Mat p_FinA = Mat(3, 1), p_FinA_fej = Mat(3, 1), p_FinG = Mat(3, 1), p_FinG_fej = Mat(3, 1);
+};
+
+namespace UpdaterHelper {
+void get_feature_jacobian_representation(State &s, HelperFeature &f, Mat &H_f, std::vector<Mat> &H_x,
+                                         std::vector<Ref> &x_order);
+void get_feature_jacobian_full(State &s, HelperFeature &f, Mat &H_f, Mat &H_x, Mat &res, std::vector<Ref> &x_order);
+void nullspace_project_inplace(Mat &H_f, Mat &H_x, Mat &res);
+void measurement_compress_inplace(Mat &H_x, Mat &res);
+}  // namespace UpdaterHelper
+
+struct UpdateStats {
+  int rows_stacked = 0, cols = 0, accepted = 0, rows_compressed = 0;
+};
+
+struct UpdaterMSCKF {
+  double sigma_pix_sq, chi2_mult;
+  std::map<int, double> chi_squared_table;
+  FeatureInitializer init;
+  UpdaterMSCKF(const uvio_hp_options_t &o);
+  // returns <0 on fatal numeric error
+  int update(State &s, std::vector<FeatP> &feature_vec, UpdateStats *st = nullptr);
+};
+
+struct UpdaterSLAM {
+  double sigma_pix_sq, chi2_mult;
+  std::map<int, double> chi_squared_table;
+  FeatureInitializer init;
+  UpdaterSLAM(const uvio_hp_options_t &o);
+  int delayed_init(State &s, std::vector<FeatP> &feature_vec);
+  int update(State &s, std::vector<FeatP> &feature_vec);
+  int change_anchors(State &s);
+  int perform_anchor_change(State &s, VarP landmark, double new_anchor_timestamp, size_t new_cam_id);
+};
+
+struct UpdaterUWB {
+  double sigma_range, chi2_mult;
+  std::map<int, double> chi_squared_table;
+  UpdaterUWB(const uvio_hp_options_t &o);
+  // returns 1 if applied, 0 if gated, <0 on fatal error
+  int update_single(State &s, double timestamp, size_t anchor_id, double range);
+};
+
+}  // namespace orc

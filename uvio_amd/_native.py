@@ -1,0 +1,136 @@
+"""ctypes mirror of include/uvio_hp.h (structs + loader).
+
+The product library ``uvio_amd/libuvio_hp.so`` is built in-tree (``python -m uvio_amd.build``).
+There is no fallback: if the library cannot be loaded the import of the facade raises.
+"""
+import ctypes as C
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "uvio_amd", "libuvio_hp.so")
+
+MAX_CAMS = 4
+MAX_ANCHORS = 16
+
+OK = 0
+E_ARG, E_STATE, E_DEVICE, E_NUMERIC, E_CONFIG, E_ORDER, E_CAPACITY = -1, -2, -3, -4, -5, -6, -7
+ERRNAMES = {0: "OK", -1: "E_ARG", -2: "E_STATE", -3: "E_DEVICE", -4: "E_NUMERIC", -5: "E_CONFIG", -6: "E_ORDER",
+            -7: "E_CAPACITY"}
+
+
+class Camera(C.Structure):
+    _fields_ = [("model", C.c_int), ("width", C.c_int), ("height", C.c_int), ("intrinsics", C.c_double * 8),
+                ("q_ItoC", C.c_double * 4), ("p_IinC", C.c_double * 3)]
+
+
+class Anchor(C.Structure):
+    _fields_ = [("id", C.c_uint64), ("fix", C.c_int), ("p_AinG", C.c_double * 3), ("const_bias", C.c_double),
+                ("dist_bias", C.c_double), ("cov_diag", C.c_double * 5)]
+
+
+class Options(C.Structure):
+    _fields_ = [
+        ("do_fej", C.c_int), ("integration", C.c_int), ("num_cameras", C.c_int), ("use_stereo", C.c_int),
+        ("do_calib_camera_pose", C.c_int), ("do_calib_camera_intrinsics", C.c_int),
+        ("do_calib_camera_timeoffset", C.c_int), ("do_calib_imu_intrinsics", C.c_int),
+        ("do_calib_imu_g_sensitivity", C.c_int), ("imu_model", C.c_int), ("max_clone_size", C.c_int),
+        ("max_slam_features", C.c_int), ("max_slam_in_update", C.c_int), ("max_msckf_in_update", C.c_int),
+        ("max_aruco_features", C.c_int), ("feat_rep_msckf", C.c_int), ("feat_rep_slam", C.c_int),
+        ("dt_slam_delay", C.c_double), ("gravity_mag", C.c_double), ("calib_camimu_dt", C.c_double),
+        ("msckf_sigma_pix", C.c_double), ("msckf_chi2_multipler", C.c_double),
+        ("slam_sigma_pix", C.c_double), ("slam_chi2_multipler", C.c_double),
+        ("sigma_w", C.c_double), ("sigma_a", C.c_double), ("sigma_wb", C.c_double), ("sigma_ab", C.c_double),
+        ("imu_dw", C.c_double * 6), ("imu_da", C.c_double * 6), ("imu_tg", C.c_double * 9),
+        ("q_GYROtoIMU", C.c_double * 4), ("q_ACCtoIMU", C.c_double * 4),
+        ("fi_triangulate_1d", C.c_int), ("fi_refine_features", C.c_int), ("fi_max_runs", C.c_int),
+        ("fi_init_lamda", C.c_double), ("fi_max_lamda", C.c_double), ("fi_min_dx", C.c_double),
+        ("fi_min_dcost", C.c_double), ("fi_lam_mult", C.c_double), ("fi_min_dist", C.c_double),
+        ("fi_max_dist", C.c_double), ("fi_max_baseline", C.c_double), ("fi_max_cond_number", C.c_double),
+        ("cams", Camera * MAX_CAMS),
+        ("num_pts", C.c_int), ("fast_threshold", C.c_int), ("grid_x", C.c_int), ("grid_y", C.c_int),
+        ("min_px_dist", C.c_int), ("histogram_method", C.c_int), ("downsample_cameras", C.c_int),
+        ("track_frequency", C.c_double),
+        ("use_uwb", C.c_int), ("do_calib_uwb_extrinsics", C.c_int), ("prior_uwb_imu_cov", C.c_double),
+        ("uwb_sigma_range", C.c_double), ("uwb_chi2_multipler", C.c_double), ("min_dist_to_use_uwb", C.c_double),
+        ("p_IinU", C.c_double * 3), ("n_anchors_to_fix", C.c_int), ("n_anchors", C.c_int),
+        ("anchors", Anchor * MAX_ANCHORS),
+        ("record_timing", C.c_int),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [("timestamp", C.c_double), ("tracking", C.c_double), ("propagation", C.c_double),
+                ("msckf_update", C.c_double), ("slam_update", C.c_double), ("slam_delayed", C.c_double),
+                ("marg", C.c_double), ("total", C.c_double), ("n_msckf", C.c_int), ("n_slam", C.c_int),
+                ("n_slam_delayed", C.c_int), ("n_clones", C.c_int), ("cov_dim", C.c_int),
+                ("msckf_rows", C.c_int), ("msckf_cols", C.c_int)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_P = C.POINTER
+_D = C.c_double
+_I = C.c_int
+
+# (name, restype, argtypes) for the product C ABI; the oracle exports the same entries with orc_
+SIGNATURES = [
+    ("options_default", _I, [_P(Options)]),
+    ("options_load", _I, [C.c_char_p, _P(Options)]),
+    ("create", _I, [_P(Options), _I, _P(C.c_void_p)]),
+    ("destroy", _I, [C.c_void_p]),
+    ("last_error", C.c_char_p, [C.c_void_p]),
+    ("initialize_with_gt", _I, [C.c_void_p, _P(_D)]),
+    ("feed_imu", _I, [C.c_void_p, _D, _P(_D), _P(_D)]),
+    ("feed_simulation", _I, [C.c_void_p, _D, _I, _P(_I), _P(_I), _P(C.c_uint64), _P(C.c_float)]),
+    ("feed_camera", _I, [C.c_void_p, _D, _I, _P(_I), _P(_P(C.c_uint8)), _P(_I), _P(_P(C.c_uint8))]),
+    ("feed_uwb", _I, [C.c_void_p, _D, _I, _P(C.c_uint64), _P(_D)]),
+    ("init_anchors", _I, [C.c_void_p, _I, _P(Anchor)]),
+    ("initialized", _I, [C.c_void_p, _P(_I)]),
+    ("get_imu_state", _I, [C.c_void_p, _P(_D), _P(_D)]),
+    ("get_cov_dim", _I, [C.c_void_p, _P(_I)]),
+    ("get_cov", _I, [C.c_void_p, _P(_D), _I]),
+    ("get_state_vector", _I, [C.c_void_p, _P(_D), _I, _P(_I), _P(_I), _I, _P(_I)]),
+    ("get_timing", _I, [C.c_void_p, _P(Timing)]),
+    ("get_clone_times", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
+    ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
+    ("compress", _I, [_P(_D), _I, _I, _P(_D)]),
+]
+
+# every symbol declared in include/uvio_hp.h
+EXPORTED = ["uvio_hp_" + s[0] for s in SIGNATURES]
+
+
+def bind(lib, prefix, names=None):
+    for name, res, args in SIGNATURES:
+        if names is not None and name not in names:
+            continue
+        f = getattr(lib, prefix + name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def load():
+    """Load libuvio_hp.so (built in-tree).  Raises if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libuvio_hp.so not built: run `python -m uvio_amd.build` (hipcc, gfx950)")
+        _lib = bind(C.CDLL(LIB_PATH), "uvio_hp_")
+    return _lib
+
+
+def check(rc, lib=None, handle=None, what=""):
+    if rc != 0:
+        msg = ""
+        if lib is not None and handle is not None:
+            try:
+                msg = (lib.uvio_hp_last_error(handle) or b"").decode()
+            except Exception:  # noqa: BLE001
+                msg = ""
+        raise RuntimeError("%s failed: %s %s" % (what, ERRNAMES.get(rc, rc), msg))
+    return rc

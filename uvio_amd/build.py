@@ -1,0 +1,84 @@
+"""Build the in-tree native libraries.
+
+* ``uvio_amd/libuvio_hp.so`` — the product: host orchestration (C++) + gfx950 HIP kernels, C ABI
+  declared in ``include/uvio_hp.h``.  Compiled with hipcc --offload-arch=gfx950 only.
+* ``oracle/build/liboracle.so`` — the CPU restatement used as the parity checker (test infrastructure).
+
+Usage: ``python -m uvio_amd.build`` (or ``__graft_entry__.build()``).
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "uvio_amd", "csrc")
+LIB = os.path.join(ROOT, "uvio_amd", "libuvio_hp.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = [
+    "options.cpp",
+    "engine_state.cpp",
+    "engine_prop.cpp",
+    "engine_update.cpp",
+    "capi.cpp",
+    "kernels_cov.hip",
+    "kernels_feat.hip",
+]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_product(force=False, verbose=False):
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    hdrs = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    hdrs.append(os.path.join(ROOT, "include", "uvio_hp.h"))
+    if not force and not _newer(LIB, srcs + hdrs):
+        return LIB
+    objdir = os.path.join(ROOT, "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    procs = []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not force and not _newer(o, [s] + hdrs):
+            continue
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+               "-Wall", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
+               "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+        if s.endswith(".hip"):
+            cmd[1:1] = ["-x", "hip"]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((s, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for s, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out.decode())
+            raise RuntimeError("hipcc failed on %s" % s)
+        elif verbose and out:
+            sys.stderr.write(out.decode())
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
+    subprocess.check_call(cmd)
+    return LIB
+
+
+def build_oracle():
+    odir = os.path.join(ROOT, "oracle")
+    subprocess.check_call(["make", "-s", "-C", odir])
+    return os.path.join(odir, "build", "liboracle.so")
+
+
+def build_all(force=False, verbose=False):
+    lib = build_product(force=force, verbose=verbose)
+    orc = build_oracle()
+    return lib, orc
+
+
+if __name__ == "__main__":
+    print(build_all(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,172 @@
+// extern "C" boundary of libuvio_hp.so (declared in include/uvio_hp.h).  Every entry converts
+// exceptions into status codes: the library never exits the process.
+#include <cstring>
+#include <string>
+
+#include "engine.h"
+
+using namespace uvhp;
+
+struct uvio_hp {
+  Engine *e = nullptr;
+  std::string err;
+};
+
+#define HP_GUARD(h, body)                                    \
+  try {                                                      \
+    body                                                     \
+  } catch (const HpError &ex) {                              \
+    if (h) (h)->err = ex.what();                             \
+    return ex.code;                                          \
+  } catch (const std::exception &ex) {                       \
+    if (h) (h)->err = ex.what();                             \
+    return UVIO_HP_E_DEVICE;                                 \
+  }
+
+extern "C" {
+
+int uvio_hp_options_default(uvio_hp_options_t *opts) {
+  if (!opts) return UVIO_HP_E_ARG;
+  options_default(opts);
+  return 0;
+}
+
+int uvio_hp_options_load(const char *path, uvio_hp_options_t *opts) {
+  if (!path || !opts) return UVIO_HP_E_ARG;
+  std::string err;
+  return options_load(path, opts, &err);
+}
+
+int uvio_hp_create(const uvio_hp_options_t *opts, int device, uvio_hp_t **out) {
+  if (!opts || !out) return UVIO_HP_E_ARG;
+  *out = nullptr;
+  uvio_hp_t *h = new uvio_hp_t();
+  try {
+    h->e = new Engine(*opts, device);
+  } catch (const HpError &ex) {
+    int c = ex.code;
+    delete h;
+    return c;
+  } catch (const std::exception &ex) {
+    delete h;
+    return UVIO_HP_E_DEVICE;
+  }
+  *out = h;
+  return 0;
+}
+
+int uvio_hp_destroy(uvio_hp_t *h) {
+  if (!h) return UVIO_HP_E_ARG;
+  delete h->e;
+  delete h;
+  return 0;
+}
+
+const char *uvio_hp_last_error(const uvio_hp_t *h) { return h ? h->err.c_str() : "null handle"; }
+
+int uvio_hp_initialize_with_gt(uvio_hp_t *h, const double x[17]) {
+  if (!h || !x) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->initialize_with_gt(x); return 0;)
+}
+
+int uvio_hp_feed_imu(uvio_hp_t *h, double t, const double wm[3], const double am[3]) {
+  if (!h || !wm || !am) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->feed_imu(t, wm, am); return 0;)
+}
+
+int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
+                            const float *uv) {
+  if (!h || ncam <= 0 || !cam_ids || !counts) return UVIO_HP_E_ARG;
+  HP_GUARD(h, return h->e->feed_simulation(t, ncam, cam_ids, counts, ids, uv);)
+}
+
+int uvio_hp_feed_camera(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
+                        const int *strides, const uint8_t *const *masks) {
+  (void)t;
+  (void)ncam;
+  (void)cam_ids;
+  (void)imgs;
+  (void)strides;
+  (void)masks;
+  if (!h) return UVIO_HP_E_ARG;
+  h->err = "image front-end (TrackKLT) not built in this version";
+  return UVIO_HP_E_STATE;
+}
+
+int uvio_hp_feed_uwb(uvio_hp_t *h, double t, int n, const uint64_t *ids, const double *ranges) {
+  if (!h || n < 0) return UVIO_HP_E_ARG;
+  HP_GUARD(h, return h->e->feed_uwb(t, n, ids, ranges);)
+}
+
+int uvio_hp_init_anchors(uvio_hp_t *h, int n, const uvio_hp_anchor_t *a) {
+  if (!h || n < 0) return UVIO_HP_E_ARG;
+  HP_GUARD(h, return h->e->init_anchors(n, a);)
+}
+
+int uvio_hp_initialized(const uvio_hp_t *h, int *out) {
+  if (!h || !out) return UVIO_HP_E_ARG;
+  *out = h->e->initialized() ? 1 : 0;
+  return 0;
+}
+
+int uvio_hp_get_imu_state(uvio_hp_t *h, double *t, double out[16]) {
+  if (!h || !t || !out) return UVIO_HP_E_ARG;
+  *t = h->e->timestamp();
+  std::memcpy(out, h->e->imu().val, sizeof(double) * 16);
+  return 0;
+}
+
+int uvio_hp_get_cov_dim(uvio_hp_t *h, int *n) {
+  if (!h || !n) return UVIO_HP_E_ARG;
+  *n = h->e->cov_dim();
+  return 0;
+}
+
+int uvio_hp_get_cov(uvio_hp_t *h, double *out, int ld) {
+  if (!h || !out || ld < h->e->cov_dim()) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->get_cov(out, ld); return 0;)
+}
+
+int uvio_hp_get_state_vector(uvio_hp_t *h, double *out, int cap, int *len, int *meta, int meta_cap, int *nvars) {
+  if (!h || !out || !len) return UVIO_HP_E_ARG;
+  int k = h->e->state_vector(out, cap, meta, meta_cap, nvars);
+  *len = k;
+  return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
+}
+
+int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out) {
+  if (!h || !out) return UVIO_HP_E_ARG;
+  *out = h->e->timing();
+  return 0;
+}
+
+int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n) {
+  if (!h || !n) return UVIO_HP_E_ARG;
+  auto t = h->e->clone_times();
+  for (int i = 0; i < (int)t.size() && i < cap; i++) out[i] = t[i];
+  *n = (int)t.size();
+  return 0;
+}
+
+int uvio_hp_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
+                       double sigma2, double *dx_out) {
+  try {
+    return Engine::ekf_update_standalone(P, N, H_index, n, H, r, res, sigma2, dx_out);
+  } catch (const HpError &ex) {
+    return ex.code;
+  } catch (...) {
+    return UVIO_HP_E_DEVICE;
+  }
+}
+
+int uvio_hp_compress(const double *A, int m, int n, double *R_out) {
+  try {
+    return Engine::compress_standalone(A, m, n, R_out);
+  } catch (const HpError &ex) {
+    return ex.code;
+  } catch (...) {
+    return UVIO_HP_E_DEVICE;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,212 @@
+// Host orchestration of the MI355X hot path.  The host keeps the state *mean* and the variable
+// bookkeeping (ids / sizes, like ov_type::Type::_id) and decides what to update; every operation on
+// the covariance P runs on the device, where P stays resident for the whole run.
+//
+// Reference surfaces mirrored: ov_msckf::VioManager (VioManager.cpp:50-651),
+// uvio::UVioManager (UVioManager.cpp:26-344), Propagator (Propagator.cpp:33-1015),
+// StateHelper (StateHelper.cpp:36-645), UpdaterMSCKF/SLAM (UpdaterMSCKF.cpp, UpdaterSLAM.cpp),
+// UpdaterUWB (UpdaterUWB.cpp), FeatureDatabase (FeatureDatabase.cpp).
+#pragma once
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "hp_common.h"
+#include "kernels.h"
+
+namespace uvhp {
+
+enum VKind { V_IMU = 0, V_VEC = 1, V_QUAT = 2, V_POSE = 3, V_LANDMARK = 4, V_ANCHOR = 5 };
+
+// ov_type::Type bookkeeping + value / first estimate
+struct Var {
+  VKind kind;
+  int id = -1, size = 0, vlen = 0;
+  double val[16] = {0}, fej[16] = {0};
+  // landmark
+  size_t featid = 0;
+  int rep = 0, anchor_cam = -1, unique_cam = -1, fail_count = 0;
+  double anchor_time = -1;
+  bool should_marg = false;
+  // uwb anchor
+  uint64_t anchor_id = 0;
+  bool fixed = false;
+  Var(VKind k, int sz, int vl) : kind(k), size(sz), vlen(vl) {}
+  void update(const double *dx);  // Type::update family (JPLQuat.h:114, IMU.h:78, Vec.h:55, ...)
+  void xyz(bool fej_, double *out) const;          // Landmark::get_xyz (Landmark.cpp:26)
+  void set_xyz(const double *p, bool fej_);        // Landmark::set_from_xyz (Landmark.cpp:65)
+};
+using VarP = std::shared_ptr<Var>;
+
+struct Feature {
+  size_t featid = 0;
+  bool to_delete = false;
+  // per camera, in libstdc++ unordered_map order (iteration order = the reference's)
+  std::unordered_map<size_t, std::vector<std::pair<float, float>>> uvs, uvs_norm;
+  std::unordered_map<size_t, std::vector<double>> timestamps;
+  int anchor_cam_id = -1;
+  double anchor_clone_timestamp = -1;
+  double p_FinA[3] = {0, 0, 0}, p_FinG[3] = {0, 0, 0};
+  void clean_old_measurements(const std::vector<double> &valid);
+  void clean_older_measurements(double t);
+  int count() const {
+    int c = 0;
+    for (auto &p : timestamps) c += (int)p.second.size();
+    return c;
+  }
+};
+using FeatP = std::shared_ptr<Feature>;
+
+struct ImuSample {
+  double t, wm[3], am[3];
+};
+
+// Device-resident buffers (allocated once at create, sized from the config)
+struct DeviceBufs {
+  hipStream_t stream = nullptr;
+  int ldp = 0;               // P capacity / leading dimension
+  double *P = nullptr, *P2 = nullptr;
+  double *T = nullptr;       // propagation scratch (ldp x 64)
+  double *Phi = nullptr, *Q = nullptr, *dnc = nullptr;
+  int *iold = nullptr;
+  // update batch
+  int max_feat = 0, max_meas_total = 0, max_vars_total = 0, max_rows = 0, ldh = 0, max_ncol = 0;
+  DFeat *feats = nullptr;
+  DMeas *meas = nullptr;
+  DVar *vars = nullptr;
+  DClone *clones = nullptr;
+  DCam *cams = nullptr;
+  DFeatOut *fout = nullptr;
+  double *chi2 = nullptr;
+  double *H = nullptr;       // H_all (max_rows x ldh)
+  double *partials = nullptr;
+  double *R = nullptr;       // compressed (ncol x ncol, + global Cholesky scratch)
+  int *hidx = nullptr;
+  EkfScratch ekf{};
+  // pinned host staging
+  void *pin = nullptr;
+  size_t pin_bytes = 0;
+  double *dx_host = nullptr;
+  int *neg_host = nullptr;
+  DFeatOut *fout_host = nullptr;
+};
+
+class Engine {
+ public:
+  explicit Engine(const uvio_hp_options_t &o, int device);
+  ~Engine();
+
+  void initialize_with_gt(const double x[17]);
+  void feed_imu(double t, const double wm[3], const double am[3]);
+  int feed_simulation(double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids, const float *uv);
+  int feed_uwb(double t, int n, const uint64_t *ids, const double *ranges);
+  int init_anchors(int n, const uvio_hp_anchor_t *a);
+
+  // getters
+  bool initialized() const { return is_initialized_; }
+  double timestamp() const { return timestamp_; }
+  const Var &imu() const { return *imu_; }
+  int cov_dim() const { return N_; }
+  void get_cov(double *out, int ld);
+  int state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars);
+  uvio_hp_timing_t timing() const { return timing_; }
+  std::vector<double> clone_times() const;
+
+  // standalone kernel-level entry points (parity tests)
+  static int ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
+                                   double sigma2, double *dx_out);
+  static int compress_standalone(const double *A, int m, int n, double *R_out);
+
+ private:
+  uvio_hp_options_t o_;
+  int device_;
+  DeviceBufs d_;
+  // ---- state (host mean + bookkeeping) ----
+  double timestamp_ = -1;
+  VarP imu_, calib_dt_, dw_, da_, tg_, qg_, qa_, p_IinU_;
+  std::map<double, VarP> clones_;
+  std::unordered_map<size_t, VarP> slam_;
+  std::unordered_map<size_t, VarP> calib_pose_, calib_intr_;
+  std::unordered_map<size_t, VarP> anchors_;
+  CamParams cams_[UVIO_HP_MAX_CAMS];
+  std::vector<VarP> vars_;
+  int N_ = 0;
+  // ---- propagator ----
+  std::mutex imu_mtx_;
+  std::vector<ImuSample> imu_data_;
+  bool have_last_prop_time_offset_ = false;
+  double last_prop_time_offset_ = 0;
+  // ---- feature database (TrackSIM's) ----
+  std::unordered_map<size_t, FeatP> db_;
+  size_t currid_;
+  // ---- manager ----
+  bool is_initialized_ = false;
+  double startup_time_ = -1, distance_ = 0, timelastupdate_ = -1;
+  bool anchors_initialized_ = false;
+  std::map<double, std::unordered_map<size_t, double>> past_uwb_;
+  uvio_hp_timing_t timing_{};
+  std::vector<double> chi2_table_;
+
+  // covariance ops (device)
+  void alloc_device();
+  void upload_P_full(const std::vector<double> &Ph, int N);
+  void download_P(std::vector<double> &Ph);
+  void cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
+                     const std::vector<double> &Q);
+  VarP clone_imu_pose(const double *dnc, bool do_dt);
+  void marginalize(const VarP &v);
+  void check_neg_diag(const char *who);
+  void ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx, const double *resdev,
+                       int res_stride, double sigma2);
+  void apply_dx(const double *dx);
+  void initialize_invertible_host(const VarP &v, const std::vector<std::pair<int, int>> &H_order,
+                                  const std::vector<double> &H_R, const std::vector<double> &H_L,
+                                  const std::vector<double> &R, const std::vector<double> &res);
+  void set_initial_covariance(const std::vector<double> &cov, const std::vector<VarP> &order);
+
+  // propagator (host mean + Phi/Qd, device covariance)
+  std::vector<ImuSample> select_imu_readings(double t0, double t1);
+  void accumulate_phi(const std::vector<ImuSample> &prop, std::vector<double> &Phi, std::vector<double> &Qd, int n);
+  void predict_and_compute(const ImuSample &a, const ImuSample &b, double *F, double *Qd, int n);
+  void last_w(const std::vector<ImuSample> &prop, double *w);
+  std::vector<int> phi_order_ids(int *n);
+  int propagate_and_clone(double t);
+  int propagate_uwb(double t);
+
+  // updates
+  int do_feature_propagate_update(double t, const std::vector<int> &camids);
+  int msckf_update(std::vector<FeatP> &feats);
+  int slam_update(std::vector<FeatP> &feats);
+  int slam_delayed_init(std::vector<FeatP> &feats);
+  int slam_change_anchors();
+  int uwb_update_single(size_t anchor_id, double range);
+  void marginalize_slam();
+  void marginalize_old_clone();
+  void db_update(size_t id, double t, size_t cam, float u, float v, float un, float vn);
+  double margtimestep() const {
+    double t = INFINITY;
+    for (auto &c : clones_)
+      if (c.first < t) t = c.first;
+    return t;
+  }
+
+  // batch construction for the per-feature kernel
+  struct Batch {
+    std::vector<DFeat> feats;
+    std::vector<DMeas> meas;
+    std::vector<DVar> vars;
+    std::vector<DClone> clones;
+    std::vector<DCam> cams;
+    std::vector<int> hidx;     // canonical column -> covariance id
+    std::vector<FeatP> fptrs;
+    int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;
+    std::map<double, int> slot_of_time;
+  };
+  void build_clone_cam_tables(Batch &b, bool include_landmarks);
+  int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool compress, std::vector<DFeatOut> &outs);
+};
+
+}  // namespace uvhp

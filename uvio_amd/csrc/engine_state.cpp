@@ -1,0 +1,578 @@
+// Engine: state layout, device buffers and covariance operations.
+#include <algorithm>
+#include <cstring>
+
+#include "engine.h"
+
+namespace uvhp {
+
+// ---- Type::update family ----
+void Var::update(const double *dx) {
+  if (kind == V_IMU || kind == V_POSE || kind == V_QUAT) {
+    quat_boxplus(val, dx);
+    for (int i = 3; i < size; i++) val[i + 1] += dx[i];
+  } else {
+    for (int i = 0; i < size; i++) val[i] += dx[i];
+  }
+}
+
+// Landmark::get_xyz (Landmark.cpp:26-63); representation ids of LandmarkRepresentation.h:38
+void Var::xyz(bool getfej, double *o) const {
+  const double *p = getfej ? fej : val;
+  switch (rep) {
+    case 0:
+    case 2:
+      o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+      break;
+    case 1:
+    case 3:
+      o[0] = (1 / p[2]) * cos(p[0]) * sin(p[1]);
+      o[1] = (1 / p[2]) * sin(p[0]) * sin(p[1]);
+      o[2] = (1 / p[2]) * cos(p[1]);
+      break;
+    case 4:
+      // reference quirk (Landmark.cpp:47-52): the fej value is ignored for this representation
+      o[0] = (1 / val[2]) * val[0];
+      o[1] = (1 / val[2]) * val[1];
+      o[2] = 1 / val[2];
+      break;
+    default:
+      o[0] = o[1] = o[2] = 0;
+  }
+}
+void Var::set_xyz(const double *p, bool isfej) {
+  double *d = isfej ? fej : val;
+  switch (rep) {
+    case 0:
+    case 2:
+      d[0] = p[0]; d[1] = p[1]; d[2] = p[2];
+      break;
+    case 1:
+    case 3: {
+      double g_rho = 1 / sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+      d[0] = atan2(p[1], p[0]);
+      d[1] = acos(g_rho * p[2]);
+      d[2] = g_rho;
+      break;
+    }
+    case 4:
+      d[0] = p[0] / p[2];
+      d[1] = p[1] / p[2];
+      d[2] = 1 / p[2];
+      break;
+    default:
+      break;
+  }
+}
+
+// ---- Feature (Feature.cpp:26-111) ----
+void Feature::clean_old_measurements(const std::vector<double> &valid) {
+  for (auto &pair : timestamps) {
+    auto &ts = pair.second;
+    auto &u = uvs[pair.first];
+    auto &un = uvs_norm[pair.first];
+    size_t w = 0;
+    for (size_t i = 0; i < ts.size(); i++)
+      if (std::find(valid.begin(), valid.end(), ts[i]) != valid.end()) {
+        ts[w] = ts[i];
+        u[w] = u[i];
+        un[w] = un[i];
+        w++;
+      }
+    ts.resize(w);
+    u.resize(w);
+    un.resize(w);
+  }
+}
+void Feature::clean_older_measurements(double t) {
+  for (auto &pair : timestamps) {
+    auto &ts = pair.second;
+    auto &u = uvs[pair.first];
+    auto &un = uvs_norm[pair.first];
+    size_t w = 0;
+    for (size_t i = 0; i < ts.size(); i++)
+      if (!(ts[i] <= t)) {
+        ts[w] = ts[i];
+        u[w] = u[i];
+        un[w] = un[i];
+        w++;
+      }
+    ts.resize(w);
+    u.resize(w);
+    un.resize(w);
+  }
+}
+
+static VarP mk(VKind k, int size, int vlen) { return std::make_shared<Var>(k, size, vlen); }
+
+// State::State (State.cpp:28-166) + UVioManager ctor (UVioManager.cpp:26-58)
+Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) {
+  if (o_.num_cameras < 1 || o_.num_cameras > UVIO_HP_MAX_CAMS) throw HpError(UVIO_HP_E_ARG, "num_cameras out of range");
+  currid_ = 4 * (size_t)o_.max_aruco_features + 1;  // TrackBase::currid (TrackBase.cpp:34)
+  int cur = 0;
+  imu_ = mk(V_IMU, 15, 16);
+  imu_->val[3] = imu_->fej[3] = 1;
+  imu_->id = cur;
+  vars_.push_back(imu_);
+  cur += 15;
+  dw_ = mk(V_VEC, 6, 6);
+  da_ = mk(V_VEC, 6, 6);
+  tg_ = mk(V_VEC, 9, 9);
+  qg_ = mk(V_QUAT, 3, 4);
+  qa_ = mk(V_QUAT, 3, 4);
+  for (int k = 0; k < 6; k++) dw_->val[k] = dw_->fej[k] = o_.imu_dw[k], da_->val[k] = da_->fej[k] = o_.imu_da[k];
+  for (int k = 0; k < 9; k++) tg_->val[k] = tg_->fej[k] = o_.imu_tg[k];
+  for (int k = 0; k < 4; k++) qg_->val[k] = qg_->fej[k] = o_.q_GYROtoIMU[k], qa_->val[k] = qa_->fej[k] = o_.q_ACCtoIMU[k];
+  if (o_.do_calib_imu_intrinsics) {
+    for (auto &v : {dw_, da_}) {
+      v->id = cur;
+      vars_.push_back(v);
+      cur += v->size;
+    }
+    if (o_.do_calib_imu_g_sensitivity) {
+      tg_->id = cur;
+      vars_.push_back(tg_);
+      cur += 9;
+    }
+    VarP q = (o_.imu_model == 0) ? qg_ : qa_;
+    q->id = cur;
+    vars_.push_back(q);
+    cur += 3;
+  }
+  calib_dt_ = mk(V_VEC, 1, 1);
+  calib_dt_->val[0] = calib_dt_->fej[0] = o_.calib_camimu_dt;
+  if (o_.do_calib_camera_timeoffset) {
+    calib_dt_->id = cur;
+    vars_.push_back(calib_dt_);
+    cur += 1;
+  }
+  for (int i = 0; i < o_.num_cameras; i++) {
+    VarP pose = mk(V_POSE, 6, 7), intr = mk(V_VEC, 8, 8);
+    const uvio_hp_camera_t &c = o_.cams[i];
+    for (int k = 0; k < 4; k++) pose->val[k] = pose->fej[k] = c.q_ItoC[k];
+    for (int k = 0; k < 3; k++) pose->val[4 + k] = pose->fej[4 + k] = c.p_IinC[k];
+    for (int k = 0; k < 8; k++) intr->val[k] = intr->fej[k] = c.intrinsics[k];
+    calib_pose_.insert({(size_t)i, pose});
+    calib_intr_.insert({(size_t)i, intr});
+    cams_[i].model = c.model;
+    cams_[i].w = c.width;
+    cams_[i].h = c.height;
+    for (int k = 0; k < 8; k++) cams_[i].v[k] = c.intrinsics[k];
+    if (o_.do_calib_camera_pose) {
+      pose->id = cur;
+      vars_.push_back(pose);
+      cur += 6;
+    }
+    if (o_.do_calib_camera_intrinsics) {
+      intr->id = cur;
+      vars_.push_back(intr);
+      cur += 8;
+    }
+  }
+  N_ = cur;
+  chi2_table_ = std::vector<double>(1000, 0.0);
+  alloc_device();
+  // initial covariance (State.cpp:133-165): built once on the host, then resident on the device
+  std::vector<double> Ph((size_t)N_ * N_, 0.0);
+  for (int i = 0; i < N_; i++) Ph[(size_t)i * N_ + i] = 1e-6;
+  auto setd = [&](int id, int n, double v) {
+    for (int k = 0; k < n; k++) Ph[(size_t)(id + k) * N_ + id + k] = v;
+  };
+  if (o_.do_calib_imu_intrinsics) {
+    setd(dw_->id, 6, 0.005 * 0.005);
+    setd(da_->id, 6, 0.008 * 0.008);
+    if (o_.do_calib_imu_g_sensitivity) setd(tg_->id, 9, 0.005 * 0.005);
+    setd((o_.imu_model == 0 ? qg_ : qa_)->id, 3, 0.005 * 0.005);
+  }
+  if (o_.do_calib_camera_timeoffset) setd(calib_dt_->id, 1, 0.01 * 0.01);
+  for (int i = 0; i < o_.num_cameras; i++) {
+    if (o_.do_calib_camera_pose) {
+      setd(calib_pose_.at(i)->id, 3, 0.005 * 0.005);
+      setd(calib_pose_.at(i)->id + 3, 3, 0.015 * 0.015);
+    }
+    if (o_.do_calib_camera_intrinsics) {
+      setd(calib_intr_.at(i)->id, 4, 1.0);
+      setd(calib_intr_.at(i)->id + 4, 4, 0.005 * 0.005);
+    }
+  }
+  upload_P_full(Ph, N_);
+  // uvio
+  p_IinU_ = mk(V_VEC, 3, 3);
+  for (int k = 0; k < 3; k++) p_IinU_->val[k] = p_IinU_->fej[k] = o_.p_IinU[k];
+  if (o_.use_uwb) {
+    if (o_.do_calib_uwb_extrinsics) {
+      std::vector<double> HR(9, 0.0), HL(9, 0.0), R(9, 0.0), res(3, 0.0);
+      for (int k = 0; k < 3; k++) HL[4 * k] = 1.0, R[4 * k] = o_.prior_uwb_imu_cov;
+      initialize_invertible_host(p_IinU_, {{imu_->id, 3}}, HR, HL, R, res);
+      for (int k = 0; k < 3; k++) p_IinU_->val[k] = p_IinU_->fej[k] = o_.p_IinU[k];
+    }
+    if (o_.n_anchors > 0) init_anchors(o_.n_anchors, o_.anchors);
+  }
+}
+
+Engine::~Engine() {
+  hipSetDevice(device_);
+  void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
+                  d_.fout, d_.chi2, d_.H, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
+                  d_.ekf.dx, d_.ekf.neg};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+  if (d_.pin) hipHostFree(d_.pin);
+  if (d_.stream) hipStreamDestroy(d_.stream);
+}
+
+template <typename T>
+static void dalloc(T **p, size_t n) {
+  HP_HIP(hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T)));
+}
+
+// Capacities from the config (DESIGN.md "Data layout"): P is sized for the largest state the
+// config can reach (IMU + intrinsics + dt + cams + (max_clones+1) clones + max_slam landmarks +
+// anchors + p_IinU), so appends / deletions never reallocate.
+void Engine::alloc_device() {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_)
+    throw HpError(UVIO_HP_E_DEVICE, "no HIP device " + std::to_string(device_));
+  HP_HIP(hipSetDevice(device_));
+  HP_HIP(hipStreamCreateWithFlags(&d_.stream, hipStreamNonBlocking));
+  int C = o_.max_clone_size + 2;
+  int K = o_.num_cameras;
+  int cap = N_ + 6 * C + 3 * std::max(o_.max_slam_features, 0) + 5 * UVIO_HP_MAX_ANCHORS + 3 + 8;
+  cap = (cap + 7) / 8 * 8;
+  d_.ldp = cap;
+  dalloc(&d_.P, (size_t)cap * cap);
+  dalloc(&d_.P2, (size_t)cap * cap);
+  dalloc(&d_.T, (size_t)cap * 64);
+  dalloc(&d_.Phi, 64 * 64);
+  dalloc(&d_.Q, 64 * 64);
+  dalloc(&d_.dnc, 8);
+  dalloc(&d_.iold, 256);
+  // update batch capacities
+  int maxf = std::max(o_.max_msckf_in_update, 1);
+  maxf = std::min(maxf, 4096);
+  maxf = std::max(maxf, std::max(o_.max_slam_in_update, o_.max_slam_features));
+  maxf = std::min(std::max(maxf, 64), 8192);
+  d_.max_feat = maxf;
+  int meas_per_feat = std::min(C * K, kMaxMeasPerFeat);
+  d_.max_meas_total = maxf * meas_per_feat;
+  d_.max_vars_total = maxf * kMaxVarsPerFeat;
+  d_.max_rows = maxf * 2 * meas_per_feat;
+  d_.max_ncol = cap + 1;
+  d_.ldh = (d_.max_ncol + 7) / 8 * 8;
+  dalloc(&d_.feats, maxf);
+  dalloc(&d_.meas, d_.max_meas_total);
+  dalloc(&d_.vars, d_.max_vars_total);
+  dalloc(&d_.clones, C + 4);
+  dalloc(&d_.cams, UVIO_HP_MAX_CAMS);
+  dalloc(&d_.fout, maxf);
+  dalloc(&d_.chi2, 1000);
+  dalloc(&d_.H, (size_t)d_.max_rows * d_.ldh);
+  int maxch = (d_.max_rows + 511) / 512 + 1;
+  dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
+  dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
+  dalloc(&d_.hidx, d_.max_ncol + d_.max_rows);
+  int rmax = std::max(d_.max_ncol, 2 * 64 * 25);
+  dalloc(&d_.ekf.M, (size_t)cap * rmax);
+  dalloc(&d_.ekf.W, (size_t)cap * rmax);
+  dalloc(&d_.ekf.S, (size_t)3 * rmax * rmax);
+  dalloc(&d_.ekf.y, rmax);
+  dalloc(&d_.ekf.dx, cap);
+  dalloc(&d_.ekf.neg, 4);
+  // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
+  for (int i = 1; i < 1000; i++) chi2_table_[i] = chi2_quantile95(i);
+  HP_HIP(hipMemcpy(d_.chi2, chi2_table_.data(), 1000 * sizeof(double), hipMemcpyHostToDevice));
+  // pinned staging: batch upload + small downloads
+  d_.pin_bytes = sizeof(DFeat) * maxf + sizeof(DMeas) * d_.max_meas_total + sizeof(DVar) * d_.max_vars_total +
+                 sizeof(DClone) * (C + 4) + sizeof(DCam) * UVIO_HP_MAX_CAMS + sizeof(int) * (d_.max_ncol + d_.max_rows) +
+                 sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 4096;
+  HP_HIP(hipHostMalloc(&d_.pin, d_.pin_bytes, hipHostMallocDefault));
+  char *pb = (char *)d_.pin + d_.pin_bytes - (sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 64);
+  d_.dx_host = (double *)pb;
+  d_.neg_host = (int *)(pb + sizeof(double) * (cap + 8));
+  d_.fout_host = (DFeatOut *)(pb + sizeof(double) * (cap + 16));
+}
+
+void Engine::upload_P_full(const std::vector<double> &Ph, int N) {
+  HP_HIP(hipMemcpy2DAsync(d_.P, sizeof(double) * d_.ldp, Ph.data(), sizeof(double) * N, sizeof(double) * N, N,
+                          hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+}
+void Engine::download_P(std::vector<double> &Ph) {
+  Ph.assign((size_t)N_ * N_, 0.0);
+  if (N_ == 0) return;
+  HP_HIP(hipMemcpy2DAsync(Ph.data(), sizeof(double) * N_, d_.P, sizeof(double) * d_.ldp, sizeof(double) * N_, N_,
+                          hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+}
+void Engine::get_cov(double *out, int ld) {
+  HP_HIP(hipMemcpy2DAsync(out, sizeof(double) * ld, d_.P, sizeof(double) * d_.ldp, sizeof(double) * N_, N_,
+                          hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+}
+
+// StateHelper::EKFPropagation on the device (StateHelper.cpp:36-114)
+void Engine::cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
+                           const std::vector<double> &Q) {
+  int q = (int)iold.size();
+  if (p > 64 || q > 256) throw HpError(UVIO_HP_E_CAPACITY, "propagation block too large");
+  HP_HIP(hipMemcpyAsync(d_.Phi, Phi.data(), sizeof(double) * p * q, hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.Q, Q.data(), sizeof(double) * p * p, hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.iold, iold.data(), sizeof(int) * q, hipMemcpyHostToDevice, d_.stream));
+  launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, d_.iold, q, d_.Phi, d_.Q, d_.T);
+}
+
+void Engine::check_neg_diag(const char *who) {
+  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
+  launch_check_diag(d_.stream, d_.P, d_.ldp, N_, d_.ekf.neg);
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
+}
+
+// StateHelper::clone(imu->pose()) + augment_clone (StateHelper.cpp:341-391, 579-616)
+VarP Engine::clone_imu_pose(const double *dnc, bool do_dt) {
+  if (N_ + 6 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
+  if (do_dt) HP_HIP(hipMemcpyAsync(d_.dnc, dnc, sizeof(double) * 6, hipMemcpyHostToDevice, d_.stream));
+  launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, d_.dnc, do_dt ? 1 : 0);
+  VarP pose = mk(V_POSE, 6, 7);
+  for (int k = 0; k < 7; k++) pose->val[k] = imu_->val[k], pose->fej[k] = imu_->fej[k];
+  pose->id = N_;
+  N_ += 6;
+  vars_.push_back(pose);
+  return pose;
+}
+
+// StateHelper::marginalize (StateHelper.cpp:271-339)
+void Engine::marginalize(const VarP &m) {
+  int m0 = m->id, ms = m->size;
+  launch_marginalize(d_.stream, d_.P, d_.P2, d_.ldp, N_, m0, ms);
+  std::swap(d_.P, d_.P2);
+  std::vector<VarP> keep;
+  for (auto &v : vars_)
+    if (v != m) {
+      if (v->id > m0) v->id -= ms;
+      keep.push_back(v);
+    }
+  vars_ = keep;
+  m->id = -1;
+  N_ -= ms;
+}
+
+void Engine::apply_dx(const double *dx) {
+  for (auto &v : vars_) v->update(dx + v->id);
+  if (o_.do_calib_camera_intrinsics)
+    for (auto &c : calib_intr_)
+      for (int k = 0; k < 8; k++) cams_[c.first].v[k] = c.second->val[k];
+}
+
+// EKF update of P on the device with rows H (r x n, ld) / residual; dx applied to the host mean
+void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx,
+                             const double *resdev, int res_stride, double sigma2) {
+  if (r <= 0) return;
+  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
+  launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, d_.hidx, resdev, res_stride, sigma2, d_.ekf);
+  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+  apply_dx(d_.dx_host);
+}
+
+// StateHelper::set_initial_covariance (StateHelper.cpp:199-223).  Start-up only (initialize_with_gt,
+// anchor init): P is read back, the blocks are written, and P is re-uploaded.
+void Engine::set_initial_covariance(const std::vector<double> &cov, const std::vector<VarP> &order) {
+  std::vector<double> Ph;
+  download_P(Ph);
+  int ii = 0;
+  for (auto &a : order) {
+    int kk = 0;
+    for (auto &b : order) {
+      for (int i = 0; i < a->size; i++)
+        for (int j = 0; j < b->size; j++) {
+          int ncov = 0;
+          for (auto &c : order) ncov += c->size;
+          Ph[(size_t)(a->id + i) * N_ + b->id + j] = cov[(size_t)(ii + i) * ncov + kk + j];
+        }
+      kk += b->size;
+    }
+    ii += a->size;
+  }
+  for (int i = 0; i < N_; i++)
+    for (int j = 0; j < i; j++) Ph[(size_t)i * N_ + j] = Ph[(size_t)j * N_ + i];
+  upload_P_full(Ph, N_);
+}
+
+// StateHelper::initialize_invertible (StateHelper.cpp:484-577) — start-up only (UWB extrinsic /
+// anchor initialization in the UVioManager ctor, UVioManager.cpp:33-55, 221-247).
+void Engine::initialize_invertible_host(const VarP &v, const std::vector<std::pair<int, int>> &H_order,
+                                        const std::vector<double> &H_R, const std::vector<double> &H_L,
+                                        const std::vector<double> &R, const std::vector<double> &res) {
+  int r = (int)res.size(), sz = v->size;
+  int nh = 0;
+  for (auto &h : H_order) nh += h.second;
+  std::vector<int> idx;
+  for (auto &h : H_order)
+    for (int k = 0; k < h.second; k++) idx.push_back(h.first + k);
+  std::vector<double> Ph;
+  download_P(Ph);
+  int N = N_;
+  // M_a = P[:, idx] H_R^T (N x r)
+  std::vector<double> Ma((size_t)N * r, 0.0);
+  for (int i = 0; i < N; i++)
+    for (int a = 0; a < r; a++) {
+      double s = 0;
+      for (int k = 0; k < nh; k++) s += Ph[(size_t)i * N + idx[k]] * H_R[a * nh + k];
+      Ma[(size_t)i * r + a] = s;
+    }
+  // M = H_R P_small H_R^T + R
+  std::vector<double> M((size_t)r * r);
+  for (int a = 0; a < r; a++)
+    for (int b = 0; b < r; b++) {
+      double s = 0;
+      for (int k = 0; k < nh; k++) s += H_R[a * nh + k] * Ma[(size_t)idx[k] * r + b];
+      M[a * r + b] = s + R[a * r + b];
+    }
+  // H_L^-1 (small, Gauss-Jordan)
+  std::vector<double> A = H_L, Inv((size_t)sz * sz, 0.0);
+  for (int i = 0; i < sz; i++) Inv[i * sz + i] = 1;
+  for (int c = 0; c < sz; c++) {
+    int piv = c;
+    for (int i = c + 1; i < sz; i++)
+      if (std::fabs(A[i * sz + c]) > std::fabs(A[piv * sz + c])) piv = i;
+    for (int j = 0; j < sz; j++) std::swap(A[c * sz + j], A[piv * sz + j]), std::swap(Inv[c * sz + j], Inv[piv * sz + j]);
+    double d = A[c * sz + c];
+    for (int j = 0; j < sz; j++) A[c * sz + j] /= d, Inv[c * sz + j] /= d;
+    for (int i = 0; i < sz; i++)
+      if (i != c) {
+        double f = A[i * sz + c];
+        for (int j = 0; j < sz; j++) A[i * sz + j] -= f * A[c * sz + j], Inv[i * sz + j] -= f * Inv[c * sz + j];
+      }
+  }
+  int Nn = N + sz;
+  std::vector<double> Pn((size_t)Nn * Nn, 0.0);
+  for (int i = 0; i < N; i++) std::memcpy(&Pn[(size_t)i * Nn], &Ph[(size_t)i * N], sizeof(double) * N);
+  for (int i = 0; i < N; i++)
+    for (int a = 0; a < sz; a++) {
+      double s = 0;
+      for (int b = 0; b < r; b++) s += Ma[(size_t)i * r + b] * Inv[a * sz + b];
+      Pn[(size_t)i * Nn + N + a] = -s;
+      Pn[(size_t)(N + a) * Nn + i] = -s;
+    }
+  for (int a = 0; a < sz; a++)
+    for (int b = 0; b < sz; b++) {
+      double s = 0;
+      for (int c = 0; c < r; c++)
+        for (int e = 0; e < r; e++) s += Inv[a * sz + c] * M[c * r + e] * Inv[b * sz + e];
+      Pn[(size_t)(N + a) * Nn + N + b] = s;
+    }
+  std::vector<double> dxv(sz, 0.0);
+  for (int a = 0; a < sz; a++)
+    for (int b = 0; b < r; b++) dxv[a] += Inv[a * sz + b] * res[b];
+  v->update(dxv.data());
+  v->id = N;
+  vars_.push_back(v);
+  N_ = Nn;
+  upload_P_full(Pn, Nn);
+}
+
+int Engine::state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars) {
+  int k = 0, nv = 0;
+  for (auto &v : vars_) {
+    if (meta && 3 * nv + 2 < meta_cap) {
+      meta[3 * nv] = v->kind;
+      meta[3 * nv + 1] = v->id;
+      meta[3 * nv + 2] = v->size;
+    }
+    for (int i = 0; i < v->vlen; i++) {
+      if (k < cap) out[k] = v->val[i];
+      k++;
+    }
+    nv++;
+  }
+  if (nvars) *nvars = nv;
+  return k;
+}
+
+std::vector<double> Engine::clone_times() const {
+  std::vector<double> t;
+  for (auto &c : clones_) t.push_back(c.first);
+  return t;
+}
+
+}  // namespace uvhp
+
+namespace uvhp {
+
+// Standalone StateHelper::EKFUpdate on a caller-provided covariance (kernel-level parity entry):
+// the same device kernels the manager uses, on temporary device buffers.
+int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r,
+                                  const double *res, double sigma2, double *dx_out) {
+  if (!P || N <= 0 || n <= 0 || r <= 0 || !H || !res || !H_index || !dx_out) return UVIO_HP_E_ARG;
+  for (int j = 0; j < n; j++)
+    if (H_index[j] < 0 || H_index[j] >= N) return UVIO_HP_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return UVIO_HP_E_DEVICE;
+  hipStream_t s;
+  HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  int ldh = n + 1;
+  double *dP, *dH, *dM, *dW, *dS, *dy, *ddx;
+  int *dI, *dneg;
+  dalloc(&dP, (size_t)N * N);
+  dalloc(&dH, (size_t)r * ldh);
+  dalloc(&dM, (size_t)N * r);
+  dalloc(&dW, (size_t)N * r);
+  dalloc(&dS, (size_t)3 * r * r);
+  dalloc(&dy, r);
+  dalloc(&ddx, N);
+  dalloc(&dI, n);
+  dalloc(&dneg, 1);
+  std::vector<double> Ha((size_t)r * ldh);
+  for (int i = 0; i < r; i++) {
+    std::memcpy(&Ha[(size_t)i * ldh], H + (size_t)i * n, sizeof(double) * n);
+    Ha[(size_t)i * ldh + n] = res[i];
+  }
+  HP_HIP(hipMemcpyAsync(dP, P, sizeof(double) * N * N, hipMemcpyHostToDevice, s));
+  HP_HIP(hipMemcpyAsync(dH, Ha.data(), sizeof(double) * Ha.size(), hipMemcpyHostToDevice, s));
+  HP_HIP(hipMemcpyAsync(dI, H_index, sizeof(int) * n, hipMemcpyHostToDevice, s));
+  HP_HIP(hipMemsetAsync(dneg, 0, sizeof(int), s));
+  EkfScratch sc{dM, dW, dS, dy, ddx, dneg};
+  launch_ekf_update(s, dP, N, N, dH, ldh, r, n, dI, dH + n, ldh, sigma2, sc);
+  int neg = 0;
+  HP_HIP(hipMemcpyAsync(P, dP, sizeof(double) * N * N, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipMemcpyAsync(dx_out, ddx, sizeof(double) * N, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipMemcpyAsync(&neg, dneg, sizeof(int), hipMemcpyDeviceToHost, s));
+  HP_HIP(hipStreamSynchronize(s));
+  void *ptrs[] = {dP, dH, dM, dW, dS, dy, ddx, dI, dneg};
+  for (void *p : ptrs) hipFree(p);
+  hipStreamDestroy(s);
+  return neg > 0 ? UVIO_HP_E_NUMERIC : 0;
+}
+
+// Standalone measurement compression: R factor of [H | res] (m x (n+1)) via the Gram + Cholesky kernels
+int Engine::compress_standalone(const double *A, int m, int n, double *R_out) {
+  if (!A || m <= 0 || n <= 0 || !R_out) return UVIO_HP_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return UVIO_HP_E_DEVICE;
+  hipStream_t s;
+  HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  int ncol = n + 1;
+  int nch = gram_num_chunks(m);
+  double *dA, *dPart, *dR;
+  dalloc(&dA, (size_t)m * ncol);
+  dalloc(&dPart, (size_t)nch * ncol * ncol);
+  dalloc(&dR, (size_t)2 * ncol * ncol);
+  HP_HIP(hipMemcpyAsync(dA, A, sizeof(double) * m * ncol, hipMemcpyHostToDevice, s));
+  int nc2 = 0;
+  launch_gram(s, dA, m, ncol, ncol, dPart, &nc2);
+  launch_gram_reduce_chol(s, dPart, nc2, ncol, dR, ncol);
+  HP_HIP(hipMemcpyAsync(R_out, dR, sizeof(double) * ncol * ncol, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipStreamSynchronize(s));
+  hipFree(dA);
+  hipFree(dPart);
+  hipFree(dR);
+  hipStreamDestroy(s);
+  return 0;
+}
+
+}  // namespace uvhp

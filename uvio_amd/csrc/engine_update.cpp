@@ -1,0 +1,1015 @@
+// Engine: per-frame manager logic (VioManager.cpp:166-651, UVioManager.cpp:61-344), feature database
+// (FeatureDatabase.cpp:59-263) and the update orchestration (UpdaterMSCKF.cpp:58-295,
+// UpdaterSLAM.cpp:61-647, UpdaterUWB.cpp:53-90) over the device kernels.
+#include <algorithm>
+#include <cstring>
+
+#include "engine.h"
+
+namespace uvhp {
+
+using clk = std::chrono::steady_clock;
+static double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+// ---- chi-squared 0.95 quantile (boost::math::quantile(chi_squared(dof), 0.95), UpdaterMSCKF.cpp:52-55) ----
+static double gamma_p(double a, double x) {
+  if (x <= 0) return 0.0;
+  double gln = std::lgamma(a);
+  if (x < a + 1.0) {
+    double ap = a, sum = 1.0 / a, del = sum;
+    for (int n = 0; n < 100000; n++) {
+      ap += 1;
+      del *= x / ap;
+      sum += del;
+      if (std::fabs(del) < std::fabs(sum) * 1e-17) break;
+    }
+    return sum * std::exp(-x + a * std::log(x) - gln);
+  }
+  double b = x + 1.0 - a, c = 1e300, d = 1.0 / b, h = d;
+  for (int i = 1; i < 100000; i++) {
+    double an = -i * (i - a);
+    b += 2.0;
+    d = an * d + b;
+    if (std::fabs(d) < 1e-300) d = 1e-300;
+    c = b + an / c;
+    if (std::fabs(c) < 1e-300) c = 1e-300;
+    d = 1.0 / d;
+    double del = d * c;
+    h *= del;
+    if (std::fabs(del - 1.0) < 1e-17) break;
+  }
+  return 1.0 - std::exp(-x + a * std::log(x) - gln) * h;
+}
+double chi2_quantile95(int dof) {
+  double a = 0.5 * dof, lo = 0, hi = std::max(10.0, 4.0 * dof + 50);
+  for (int it = 0; it < 200; it++) {
+    double mid = 0.5 * (lo + hi);
+    if (gamma_p(a, 0.5 * mid) < 0.95)
+      lo = mid;
+    else
+      hi = mid;
+    if (hi - lo < 1e-14 * std::max(1.0, hi)) break;
+  }
+  return 0.5 * (lo + hi);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// VioManagerHelper.cpp:40-76
+void Engine::initialize_with_gt(const double x[17]) {
+  for (int k = 0; k < 16; k++) imu_->val[k] = imu_->fej[k] = x[1 + k];
+  std::vector<double> cov(15 * 15, 0.0);
+  for (int k = 0; k < 15; k++) cov[k * 15 + k] = 0.02 * 0.02;
+  for (int k = 0; k < 3; k++) {
+    cov[k * 15 + k] = 0.017 * 0.017;
+    cov[(3 + k) * 15 + 3 + k] = 0.05 * 0.05;
+    cov[(6 + k) * 15 + 6 + k] = 0.01 * 0.01;
+  }
+  set_initial_covariance(cov, {imu_});
+  timestamp_ = x[0];
+  startup_time_ = x[0];
+  is_initialized_ = true;
+  // FeatureDatabase::cleanup_measurements(t)
+  for (auto it = db_.begin(); it != db_.end();) {
+    it->second->clean_older_measurements(timestamp_);
+    if (it->second->count() < 1)
+      it = db_.erase(it);
+    else
+      it++;
+  }
+}
+
+// VioManager.cpp:166-189 + Propagator::feed_imu (Propagator.h:65-91)
+void Engine::feed_imu(double t, const double wm[3], const double am[3]) {
+  double oldest = margtimestep();
+  if (oldest > timestamp_) oldest = -1;
+  if (!is_initialized_) oldest = t - 2.0 + calib_dt_->val[0] - 0.10;
+  ImuSample s;
+  s.t = t;
+  for (int k = 0; k < 3; k++) s.wm[k] = wm[k], s.am[k] = am[k];
+  std::lock_guard<std::mutex> lk(imu_mtx_);
+  imu_data_.push_back(s);
+  double cut = oldest - 0.10;
+  if (cut >= 0) {
+    auto it = imu_data_.begin();
+    while (it != imu_data_.end() && it->t < cut) it++;
+    // measurements arrive in time order: erase the prefix (same result as the reference's scan)
+    bool sorted = true;
+    for (auto jt = it; jt != imu_data_.end(); ++jt)
+      if (jt->t < cut) sorted = false;
+    if (sorted)
+      imu_data_.erase(imu_data_.begin(), it);
+    else
+      imu_data_.erase(std::remove_if(imu_data_.begin(), imu_data_.end(), [&](const ImuSample &a) { return a.t < cut; }),
+                      imu_data_.end());
+  }
+}
+
+// FeatureDatabase::update_feature (FeatureDatabase.cpp:59-85)
+void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float un, float vn) {
+  auto it = db_.find(id);
+  FeatP f;
+  if (it != db_.end()) {
+    f = it->second;
+  } else {
+    f = std::make_shared<Feature>();
+    f->featid = id;
+    db_[id] = f;
+  }
+  f->uvs[cam].push_back({u, v});
+  f->uvs_norm[cam].push_back({un, vn});
+  f->timestamps[cam].push_back(t);
+}
+
+// UVioManager.cpp:61-79
+int Engine::feed_uwb(double t, int n, const uint64_t *ids, const double *ranges) {
+  if (!(is_initialized_ && anchors_initialized_ && distance_ > o_.min_dist_to_use_uwb)) return 0;
+  if (timestamp_ >= t) return 0;
+  auto &m = past_uwb_[t];
+  for (int i = 0; i < n; i++) m[(size_t)ids[i]] = ranges[i];
+  return 0;
+}
+
+// UVioManager.cpp:81-113 / 207-266
+int Engine::init_anchors(int n, const uvio_hp_anchor_t *a) {
+  if (n <= 0) return 0;
+  for (int i = 0; i < n; i++) {
+    if (anchors_.find(a[i].id) != anchors_.end()) continue;
+    VarP v = std::make_shared<Var>(V_ANCHOR, 5, 5);
+    v->anchor_id = a[i].id;
+    v->fixed = a[i].fix != 0;
+    double x[5] = {a[i].p_AinG[0], a[i].p_AinG[1], a[i].p_AinG[2], a[i].const_bias, a[i].dist_bias};
+    for (int k = 0; k < 5; k++) v->val[k] = v->fej[k] = x[k];
+    anchors_.insert({(size_t)a[i].id, v});
+    if (!a[i].fix) {
+      std::vector<double> HR(15, 0.0), HL(25, 0.0), R(25, 0.0), res(5, 0.0);
+      for (int k = 0; k < 5; k++) HL[6 * k] = 1.0, R[6 * k] = 1.0;
+      initialize_invertible_host(v, {{imu_->id, 3}}, HR, HL, R, res);
+      std::vector<double> cov(25, 0.0);
+      for (int k = 0; k < 5; k++) cov[6 * k] = a[i].cov_diag[k];
+      set_initial_covariance(cov, {v});
+    }
+  }
+  anchors_initialized_ = true;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// VioManager.cpp:191-254 + TrackSIM.cpp:30-79 (+ the UVIO range loop of UVioManager.cpp:178-188)
+int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
+                            const float *uv) {
+  auto rT1 = clk::now();
+  size_t k = 0;
+  std::vector<int> camids;
+  for (int i = 0; i < ncam; i++) {
+    int cid = cam_ids[i];
+    if (cid < 0 || cid >= o_.num_cameras) return UVIO_HP_E_ARG;
+    camids.push_back(cid);
+    for (int j = 0; j < counts[i]; j++, k++) {
+      float un, vn;
+      cam_undistort_f(cams_[cid], uv[2 * k], uv[2 * k + 1], un, vn);
+      db_update((size_t)ids[k] + currid_, t, cid, uv[2 * k], uv[2 * k + 1], un, vn);
+    }
+  }
+  auto rT2 = clk::now();
+  timing_ = uvio_hp_timing_t{};
+  timing_.tracking = secs(rT1, rT2);
+  if (!is_initialized_) return UVIO_HP_E_STATE;
+  if (!past_uwb_.empty()) {
+    for (auto it = past_uwb_.begin(); it != past_uwb_.lower_bound(t); it++) {
+      if (it->first < t && it->first > timestamp_) {
+        bool valid = false;
+        for (auto &r : it->second)
+          if (anchors_.count(r.first)) valid = true;
+        if (!valid) continue;
+        if (propagate_uwb(it->first) != 0) continue;
+        for (auto &r : it->second)
+          if (anchors_.count(r.first)) uwb_update_single(r.first, r.second);
+      }
+    }
+    past_uwb_.erase(past_uwb_.begin(), past_uwb_.upper_bound(t));
+  }
+  int rc = do_feature_propagate_update(t, camids);
+  timing_.total = secs(rT1, clk::now());
+  return rc;
+}
+
+// VioManager.cpp:323-651
+int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids) {
+  auto rT2 = clk::now();
+  if (timestamp_ > t) return UVIO_HP_E_ORDER;
+  if (timestamp_ != t) {
+    int rc = propagate_and_clone(t);
+    if (rc) return rc;
+  }
+  // the device queue is in order; wait here only so the stage timings are attributable
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  auto rT3 = clk::now();
+  timing_.timestamp = t;
+  timing_.propagation = secs(rT2, rT3);
+  timing_.n_clones = (int)clones_.size();
+  timing_.cov_dim = N_;
+  if ((int)clones_.size() < std::min(o_.max_clone_size, 5)) return 0;
+  if (timestamp_ != t) return 0;
+
+  std::vector<FeatP> feats_lost, feats_marg, feats_slam;
+  // FeatureDatabase::features_not_containing_newer(t, false, true)
+  for (auto &kv : db_) {
+    if (kv.second->to_delete) continue;
+    bool newer = false;
+    for (auto &p : kv.second->timestamps) {
+      newer = (!p.second.empty() && p.second.back() >= timestamp_);
+      if (newer) break;
+    }
+    if (!newer) feats_lost.push_back(kv.second);
+  }
+  if ((int)clones_.size() > o_.max_clone_size || (int)clones_.size() > 5) {
+    double mt = margtimestep();
+    for (auto &kv : db_) {
+      if (kv.second->to_delete) continue;
+      bool has = false;
+      for (auto &p : kv.second->timestamps) {
+        has = std::find(p.second.begin(), p.second.end(), mt) != p.second.end();
+        if (has) break;
+      }
+      if (has) feats_marg.push_back(kv.second);
+    }
+  }
+  {
+    std::vector<FeatP> keep;
+    for (auto &f : feats_lost) {
+      bool found = false;
+      for (auto &p : f->uvs)
+        if (std::find(camids.begin(), camids.end(), (int)p.first) != camids.end()) {
+          found = true;
+          break;
+        }
+      if (found && std::find(feats_marg.begin(), feats_marg.end(), f) == feats_marg.end()) keep.push_back(f);
+    }
+    feats_lost = keep;
+  }
+  std::vector<FeatP> feats_maxtracks;
+  {
+    std::vector<FeatP> keep;
+    for (auto &f : feats_marg) {
+      bool reached = false;
+      for (auto &p : f->timestamps)
+        if ((int)p.second.size() > o_.max_clone_size) {
+          reached = true;
+          break;
+        }
+      if (reached)
+        feats_maxtracks.push_back(f);
+      else
+        keep.push_back(f);
+    }
+    feats_marg = keep;
+  }
+  int curr_aruco = 0;
+  for (auto &l : slam_)
+    if ((int)l.second->featid <= 4 * o_.max_aruco_features) curr_aruco++;
+  if (o_.max_slam_features > 0 && t - startup_time_ >= o_.dt_slam_delay &&
+      (int)slam_.size() < o_.max_slam_features + curr_aruco) {
+    int amount = (o_.max_slam_features + curr_aruco) - (int)slam_.size();
+    int valid = std::min(amount, (int)feats_maxtracks.size());
+    if (valid > 0) {
+      feats_slam.insert(feats_slam.end(), feats_maxtracks.end() - valid, feats_maxtracks.end());
+      feats_maxtracks.erase(feats_maxtracks.end() - valid, feats_maxtracks.end());
+    }
+  }
+  for (auto &lm : slam_) {
+    auto it = db_.find(lm.second->featid);
+    FeatP f2 = (it == db_.end()) ? nullptr : it->second;
+    if (f2) feats_slam.push_back(f2);
+    bool cur = std::find(camids.begin(), camids.end(), lm.second->unique_cam) != camids.end();
+    if (!f2 && cur) lm.second->should_marg = true;
+    if (lm.second->fail_count > 1) lm.second->should_marg = true;
+  }
+  marginalize_slam();
+  std::vector<FeatP> slam_delayed, slam_upd;
+  for (auto &f : feats_slam) {
+    if (slam_.find(f->featid) != slam_.end())
+      slam_upd.push_back(f);
+    else
+      slam_delayed.push_back(f);
+  }
+  std::vector<FeatP> up = feats_lost;
+  up.insert(up.end(), feats_marg.begin(), feats_marg.end());
+  up.insert(up.end(), feats_maxtracks.begin(), feats_maxtracks.end());
+  std::sort(up.begin(), up.end(), [](const FeatP &a, const FeatP &b) { return a->count() < b->count(); });
+  if ((int)up.size() > o_.max_msckf_in_update) up.erase(up.begin(), up.end() - o_.max_msckf_in_update);
+  timing_.n_msckf = (int)up.size();
+  int rc = msckf_update(up);
+  if (rc) return rc;
+  auto rT4 = clk::now();
+  while (!slam_upd.empty()) {
+    size_t k = std::min((size_t)std::max(o_.max_slam_in_update, 1), slam_upd.size());
+    std::vector<FeatP> tmp(slam_upd.begin(), slam_upd.begin() + k);
+    slam_upd.erase(slam_upd.begin(), slam_upd.begin() + k);
+    rc = slam_update(tmp);
+    if (rc) return rc;
+  }
+  auto rT5 = clk::now();
+  timing_.n_slam_delayed = (int)slam_delayed.size();
+  rc = slam_delayed_init(slam_delayed);
+  if (rc) return rc;
+  auto rT6 = clk::now();
+  for (auto &f : up) f->to_delete = true;
+  // FeatureDatabase::cleanup
+  for (auto it = db_.begin(); it != db_.end();) {
+    if (it->second->to_delete)
+      it = db_.erase(it);
+    else
+      it++;
+  }
+  rc = slam_change_anchors();
+  if (rc) return rc;
+  if ((int)clones_.size() > o_.max_clone_size) {
+    double mt = margtimestep();
+    for (auto it = db_.begin(); it != db_.end();) {
+      it->second->clean_older_measurements(mt);
+      if (it->second->count() < 1)
+        it = db_.erase(it);
+      else
+        it++;
+    }
+  }
+  marginalize_old_clone();
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  auto rT7 = clk::now();
+  timing_.msckf_update = secs(rT3, rT4);
+  timing_.slam_update = secs(rT4, rT5);
+  timing_.slam_delayed = secs(rT5, rT6);
+  timing_.marg = secs(rT6, rT7);
+  timing_.n_slam = (int)slam_.size();
+  timing_.cov_dim = N_;
+  if (timelastupdate_ != -1 && clones_.find(timelastupdate_) != clones_.end()) {
+    const double *a = imu_->val + 4, *b = clones_.at(timelastupdate_)->val + 4;
+    double d[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+    distance_ += norm3(d);
+  }
+  timelastupdate_ = t;
+  return 0;
+}
+
+// StateHelper::marginalize_slam (StateHelper.cpp:631-645)
+void Engine::marginalize_slam() {
+  for (auto it = slam_.begin(); it != slam_.end();) {
+    if (it->second->should_marg && (int)it->first > 4 * o_.max_aruco_features) {
+      marginalize(it->second);
+      it = slam_.erase(it);
+    } else {
+      it++;
+    }
+  }
+}
+
+// StateHelper::marginalize_old_clone (StateHelper.cpp:618-629)
+void Engine::marginalize_old_clone() {
+  if ((int)clones_.size() > o_.max_clone_size) {
+    double mt = margtimestep();
+    marginalize(clones_.at(mt));
+    clones_.erase(mt);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Batch tables: clone slots (time order), cameras, canonical columns (calib blocks, clones, landmarks)
+void Engine::build_clone_cam_tables(Batch &b, bool include_landmarks) {
+  b.clones.clear();
+  b.cams.clear();
+  b.hidx.clear();
+  b.slot_of_time.clear();
+  int canon = 0;
+  for (int c = 0; c < o_.num_cameras; c++) {
+    DCam dc{};
+    const VarP &pose = calib_pose_.at(c);
+    quat_2_Rot(pose->val, dc.R_ItoC);
+    for (int k = 0; k < 3; k++) dc.p_IinC[k] = pose->val[4 + k];
+    dc.cam = cams_[c];
+    dc.pid_ext = o_.do_calib_camera_pose ? pose->id : -1;
+    dc.pid_intr = o_.do_calib_camera_intrinsics ? calib_intr_.at(c)->id : -1;
+    dc.canon_ext = dc.canon_intr = -1;
+    if (o_.do_calib_camera_pose) {
+      dc.canon_ext = canon;
+      for (int k = 0; k < 6; k++) b.hidx.push_back(pose->id + k);
+      canon += 6;
+    }
+    if (o_.do_calib_camera_intrinsics) {
+      dc.canon_intr = canon;
+      for (int k = 0; k < 8; k++) b.hidx.push_back(calib_intr_.at(c)->id + k);
+      canon += 8;
+    }
+    b.cams.push_back(dc);
+  }
+  int slot = 0;
+  for (auto &c : clones_) {
+    DClone d{};
+    quat_2_Rot(c.second->val, d.R);
+    quat_2_Rot(c.second->fej, d.Rf);
+    for (int k = 0; k < 3; k++) d.p[k] = c.second->val[4 + k], d.pf[k] = c.second->fej[4 + k];
+    d.pid = c.second->id;
+    d.canon = canon;
+    for (int k = 0; k < 6; k++) b.hidx.push_back(c.second->id + k);
+    canon += 6;
+    b.slot_of_time[c.first] = slot++;
+    b.clones.push_back(d);
+  }
+  (void)include_landmarks;
+  b.n_canon = canon;
+}
+
+// Builds the per-feature measurement / variable tables in the reference iteration order
+// (get_feature_jacobian_full's x_order, UpdaterHelper.cpp:200-262) and appends them to the batch.
+static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
+                        std::map<double, int> &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
+                        std::vector<DMeas> &meas, std::vector<DVar> &vars, int &rows, const Var *landmark,
+                        int landmark_canon) {
+  DFeat F{};
+  F.meas_off = (int)meas.size();
+  F.var_off = (int)vars.size();
+  F.rep = rep;
+  F.mode = mode;
+  // anchor (FeatureInitializer.cpp:35-45): camera with most measurements (first max in map order),
+  // anchor time = its last measurement
+  size_t anchor_cam = 0, most = 0;
+  for (auto &p : f->timestamps)
+    if (p.second.size() > most) {
+      anchor_cam = p.first;
+      most = p.second.size();
+    }
+  double anchor_time = f->timestamps.at(anchor_cam).back();
+  if (landmark) {
+    anchor_cam = (size_t)landmark->anchor_cam;
+    anchor_time = landmark->anchor_time;
+  }
+  F.anchor_cam = (int)anchor_cam;
+  F.anchor_slot = slot_of_time.at(anchor_time);
+  int loc = 0;
+  std::map<int, int> clone_loc;  // slot -> local col
+  std::vector<int> ext_loc(UVIO_HP_MAX_CAMS, -1), intr_loc(UVIO_HP_MAX_CAMS, -1);
+  for (auto &p : f->timestamps) {
+    int c = (int)p.first;
+    if (o.do_calib_camera_pose) {
+      vars.push_back(DVar{cams[c].pid_ext, cams[c].canon_ext, 6, loc});
+      ext_loc[c] = loc;
+      loc += 6;
+    }
+    if (o.do_calib_camera_intrinsics) {
+      vars.push_back(DVar{cams[c].pid_intr, cams[c].canon_intr, 8, loc});
+      intr_loc[c] = loc;
+      loc += 8;
+    }
+    for (size_t m = 0; m < p.second.size(); m++) {
+      int s = slot_of_time.at(p.second[m]);
+      if (!clone_loc.count(s)) {
+        clone_loc[s] = loc;
+        vars.push_back(DVar{clones[s].pid, clones[s].canon, 6, loc});
+        loc += 6;
+      }
+    }
+  }
+  bool rel = (rep == 2 || rep == 3 || rep == 4 || rep == 5);
+  if (rel) {
+    if (!clone_loc.count(F.anchor_slot)) {
+      clone_loc[F.anchor_slot] = loc;
+      vars.push_back(DVar{clones[F.anchor_slot].pid, clones[F.anchor_slot].canon, 6, loc});
+      loc += 6;
+    }
+    if (o.do_calib_camera_pose && ext_loc[F.anchor_cam] < 0) {
+      ext_loc[F.anchor_cam] = loc;
+      vars.push_back(DVar{cams[F.anchor_cam].pid_ext, cams[F.anchor_cam].canon_ext, 6, loc});
+      loc += 6;
+    }
+    F.lc_anchor_clone = clone_loc.at(F.anchor_slot);
+    F.lc_anchor_ext = ext_loc[F.anchor_cam];
+  }
+  if (landmark) {
+    F.lm_pid = landmark->id;
+    F.lm_loc = loc;
+    vars.push_back(DVar{landmark->id, landmark_canon, landmark->size, loc});
+    loc += landmark->size;
+    double p[3], pf[3];
+    landmark->xyz(false, p);
+    landmark->xyz(true, pf);
+    for (int k = 0; k < 3; k++) F.p_in[k] = p[k], F.p_in_fej[k] = pf[k];
+  }
+  F.nf = loc;
+  F.nvar = (int)vars.size() - F.var_off;
+  for (auto &p : f->timestamps) {
+    int c = (int)p.first;
+    const auto &u = f->uvs.at(p.first);
+    const auto &un = f->uvs_norm.at(p.first);
+    for (size_t m = 0; m < p.second.size(); m++) {
+      DMeas d{};
+      d.u = u[m].first;
+      d.v = u[m].second;
+      d.un = un[m].first;
+      d.vn = un[m].second;
+      d.cam = c;
+      d.slot = slot_of_time.at(p.second[m]);
+      d.lc_clone = clone_loc.at(d.slot);
+      d.lc_ext = ext_loc[c];
+      d.lc_intr = intr_loc[c];
+      meas.push_back(d);
+    }
+  }
+  F.nmeas = (int)meas.size() - F.meas_off;
+  F.row_off = rows;
+  rows += (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
+  feats.push_back(F);
+}
+
+// Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
+// Returns the number of stacked rows written to H_all.
+int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool, std::vector<DFeatOut> &outs) {
+  int nf = (int)b.feats.size();
+  if (nf == 0) return 0;
+  if (nf > d_.max_feat || (int)b.meas.size() > d_.max_meas_total || (int)b.vars.size() > d_.max_vars_total ||
+      b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol)
+    throw HpError(UVIO_HP_E_CAPACITY, "update batch exceeds device capacity");
+  int max_meas = 0, max_nf = 0;
+  for (auto &F : b.feats) {
+    max_meas = std::max(max_meas, F.nmeas);
+    max_nf = std::max(max_nf, F.nf);
+  }
+  if (max_meas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
+  size_t lds = feature_lds_bytes(max_meas, max_nf);
+  if (lds + 4096 > 160 * 1024) throw HpError(UVIO_HP_E_CAPACITY, "feature LDS footprint too large");
+  // pack into pinned staging, one async copy per table
+  char *pb = (char *)d_.pin;
+  auto stage = [&](void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return;
+    std::memcpy(pb, src, bytes);
+    HP_HIP(hipMemcpyAsync(dst, pb, bytes, hipMemcpyHostToDevice, d_.stream));
+    pb += (bytes + 255) / 256 * 256;
+  };
+  stage(d_.feats, b.feats.data(), sizeof(DFeat) * nf);
+  stage(d_.meas, b.meas.data(), sizeof(DMeas) * b.meas.size());
+  stage(d_.vars, b.vars.data(), sizeof(DVar) * b.vars.size());
+  stage(d_.clones, b.clones.data(), sizeof(DClone) * b.clones.size());
+  stage(d_.cams, b.cams.data(), sizeof(DCam) * b.cams.size());
+  stage(d_.hidx, b.hidx.data(), sizeof(int) * b.hidx.size());
+  DBatchParams bp{};
+  bp.nfeat = nf;
+  bp.n_canon = b.n_canon;
+  bp.ldh = d_.ldh;
+  bp.ldp = d_.ldp;
+  bp.sigma_pix_sq = sigma_pix_sq;
+  bp.chi2_mult = chi2_mult;
+  bp.do_fej = o_.do_fej;
+  bp.calib_ext = o_.do_calib_camera_pose;
+  bp.calib_intr = o_.do_calib_camera_intrinsics;
+  bp.fi_max_runs = o_.fi_max_runs;
+  bp.fi_refine = o_.fi_refine_features;
+  bp.fi_tri1d = o_.fi_triangulate_1d;
+  bp.fi_init_lamda = o_.fi_init_lamda;
+  bp.fi_max_lamda = o_.fi_max_lamda;
+  bp.fi_min_dx = o_.fi_min_dx;
+  bp.fi_min_dcost = o_.fi_min_dcost;
+  bp.fi_lam_mult = o_.fi_lam_mult;
+  bp.fi_min_dist = o_.fi_min_dist;
+  bp.fi_max_dist = o_.fi_max_dist;
+  bp.fi_max_baseline = o_.fi_max_baseline;
+  bp.fi_max_cond = o_.fi_max_cond_number;
+  launch_feature_linearize(d_.stream, bp, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams, d_.P, d_.chi2, d_.H, d_.fout,
+                           max_meas, max_nf);
+  HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  outs.assign(d_.fout_host, d_.fout_host + nf);
+  (void)mode;
+  return b.rows;
+}
+
+// UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295)
+int Engine::msckf_update(std::vector<FeatP> &fv) {
+  if (fv.empty()) return 0;
+  std::vector<double> clonetimes;
+  for (auto &c : clones_) clonetimes.push_back(c.first);
+  std::vector<FeatP> keep;
+  for (auto &f : fv) {
+    f->clean_old_measurements(clonetimes);
+    if (f->count() < 2)
+      f->to_delete = true;
+    else
+      keep.push_back(f);
+  }
+  fv = keep;
+  if (fv.empty()) return 0;
+  if (o_.feat_rep_msckf != 0 && o_.feat_rep_msckf != 4)
+    throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
+  Batch b;
+  build_clone_cam_tables(b, false);
+  for (auto &f : fv)
+    add_feature(this, f, 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf, o_, b.cams, b.slot_of_time, b.clones,
+                b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+  std::vector<DFeatOut> outs;
+  int m = run_batch(b, 0, o_.msckf_sigma_pix * o_.msckf_sigma_pix, o_.msckf_chi2_multipler, true, outs);
+  int acc = 0, acc_rows = 0;
+  for (size_t i = 0; i < outs.size(); i++) {
+    fv[i]->to_delete = true;
+    for (int k = 0; k < 3; k++) fv[i]->p_FinG[k] = outs[i].p_FinG[k], fv[i]->p_FinA[k] = outs[i].p_FinA[k];
+    if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
+  }
+  timing_.msckf_rows = acc_rows;
+  timing_.msckf_cols = b.n_canon;
+  if (acc == 0 || m < 1) return 0;
+  int n = b.n_canon, ncol = n + 1;
+  double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
+  if (m > n) {
+    // measurement compression (UpdaterHelper.cpp:456-487) as CholeskyQR of [H | r]
+    int nch = 0;
+    launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
+    launch_gram_reduce_chol(d_.stream, d_.partials, nch, ncol, d_.R, d_.ldh);
+    ekf_update_rows(d_.R, d_.ldh, n, n, b.hidx, d_.R + n, d_.ldh, s2);
+  } else {
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
+  }
+  return 0;
+}
+
+// UpdaterSLAM::update (UpdaterSLAM.cpp:253-479)
+int Engine::slam_update(std::vector<FeatP> &fv) {
+  if (fv.empty()) return 0;
+  std::vector<double> clonetimes;
+  for (auto &c : clones_) clonetimes.push_back(c.first);
+  std::vector<FeatP> keep;
+  for (auto &f : fv) {
+    f->clean_old_measurements(clonetimes);
+    int ct = f->count();
+    if (ct < 1)
+      f->to_delete = true;
+    else
+      keep.push_back(f);
+  }
+  fv = keep;
+  if (fv.empty()) return 0;
+  Batch b;
+  build_clone_cam_tables(b, true);
+  // landmark columns appended to the canonical set
+  std::vector<int> lm_canon;
+  for (auto &f : fv) {
+    const VarP &lm = slam_.at(f->featid);
+    lm_canon.push_back(b.n_canon);
+    for (int k = 0; k < lm->size; k++) b.hidx.push_back(lm->id + k);
+    b.n_canon += lm->size;
+  }
+  for (size_t i = 0; i < fv.size(); i++) {
+    const VarP &lm = slam_.at(fv[i]->featid);
+    if (lm->rep != 0 && lm->rep != 2 && lm->rep != 4)
+      throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
+    add_feature(this, fv[i], 1, lm->rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows,
+                lm.get(), lm_canon[i]);
+  }
+  std::vector<DFeatOut> outs;
+  double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+  int m = run_batch(b, 1, s2, o_.slam_chi2_multipler, false, outs);
+  int acc = 0;
+  for (size_t i = 0; i < outs.size(); i++) {
+    fv[i]->to_delete = true;
+    if (outs[i].status == 3) slam_.at(fv[i]->featid)->fail_count++;
+    if (outs[i].status == 0) acc++;
+  }
+  if (acc == 0 || m < 1) return 0;
+  int n = b.n_canon, ncol = n + 1;
+  if (m > n) {
+    int nch = 0;
+    launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
+    launch_gram_reduce_chol(d_.stream, d_.partials, nch, ncol, d_.R, d_.ldh);
+    ekf_update_rows(d_.R, d_.ldh, n, n, b.hidx, d_.R + n, d_.ldh, s2);
+  } else {
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
+  }
+  return 0;
+}
+
+// UpdaterSLAM::delayed_init (UpdaterSLAM.cpp:61-251) + StateHelper::initialize (StateHelper.cpp:393-482).
+// Triangulation of the whole batch runs first (as in the reference); each accepted landmark then
+// initializes and updates the state before the next one is linearized.
+int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
+  if (fv.empty()) return 0;
+  std::vector<double> clonetimes;
+  for (auto &c : clones_) clonetimes.push_back(c.first);
+  std::vector<FeatP> keep;
+  for (auto &f : fv) {
+    f->clean_old_measurements(clonetimes);
+    if (f->count() < 2)
+      f->to_delete = true;
+    else
+      keep.push_back(f);
+  }
+  fv = keep;
+  if (fv.empty()) return 0;
+  int rep = o_.feat_rep_slam;
+  if (rep != 0 && rep != 2 && rep != 4) throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
+  double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+  // 1) triangulate + refine all features against the pre-update state (UpdaterSLAM.cpp:119-141)
+  std::vector<DFeatOut> tri;
+  {
+    Batch b;
+    build_clone_cam_tables(b, false);
+    for (auto &f : fv)
+      add_feature(this, f, 2, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+    run_batch(b, 2, s2, o_.slam_chi2_multipler, false, tri);
+  }
+  for (size_t i = 0; i < fv.size(); i++) {
+    FeatP &f = fv[i];
+    if (tri[i].status == 1 || tri[i].status == 2) {
+      f->to_delete = true;
+      continue;
+    }
+    // anchor (host rule, identical to the kernel's) and triangulated position
+    size_t anchor_cam = 0, most = 0;
+    for (auto &p : f->timestamps)
+      if (p.second.size() > most) anchor_cam = p.first, most = p.second.size();
+    f->anchor_cam_id = (int)anchor_cam;
+    f->anchor_clone_timestamp = f->timestamps.at(anchor_cam).back();
+    for (int k = 0; k < 3; k++) f->p_FinA[k] = tri[i].p_FinA[k], f->p_FinG[k] = tri[i].p_FinG[k];
+    // 2) linearize at the current state (mode 3 = given triangulation, nullspace-split rows)
+    VarP lm = std::make_shared<Var>(V_LANDMARK, 3, 3);
+    lm->featid = f->featid;
+    lm->rep = rep;
+    lm->unique_cam = f->anchor_cam_id;
+    lm->anchor_cam = f->anchor_cam_id;
+    lm->anchor_time = f->anchor_clone_timestamp;
+    bool relr = (rep == 2 || rep == 4);
+    lm->set_xyz(relr ? f->p_FinA : f->p_FinG, false);
+    lm->set_xyz(relr ? f->p_FinA : f->p_FinG, true);
+    Batch b;
+    build_clone_cam_tables(b, false);
+    add_feature(this, f, 3, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+    // mode 3: linearize at the batch triangulation (p_in = p_FinA, p_in_fej = p_FinG), as the reference
+    // triangulates the whole batch before the per-feature initialize loop
+    for (int k = 0; k < 3; k++) b.feats[0].p_in[k] = f->p_FinA[k], b.feats[0].p_in_fej[k] = f->p_FinG[k];
+    std::vector<DFeatOut> o1;
+    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1);
+    if (o1[0].status != 0) {
+      f->to_delete = true;
+      continue;
+    }
+    // 3) initialize_invertible with rows 0..2, EKF update with rows 3..
+    int n = b.n_canon;
+    double HL[9], HLinv[9];
+    std::memcpy(HL, o1[0].HfR, sizeof(HL));
+    // inverse of the 3x3 upper-triangular H_finit (colPivHouseholderQr-equivalent for invertible H)
+    {
+      double A[9];
+      std::memcpy(A, HL, sizeof(A));
+      double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) + A[2] * (A[3] * A[7] - A[4] * A[6]);
+      HLinv[0] = (A[4] * A[8] - A[5] * A[7]) / det;
+      HLinv[1] = (A[2] * A[7] - A[1] * A[8]) / det;
+      HLinv[2] = (A[1] * A[5] - A[2] * A[4]) / det;
+      HLinv[3] = (A[5] * A[6] - A[3] * A[8]) / det;
+      HLinv[4] = (A[0] * A[8] - A[2] * A[6]) / det;
+      HLinv[5] = (A[2] * A[3] - A[0] * A[5]) / det;
+      HLinv[6] = (A[3] * A[7] - A[4] * A[6]) / det;
+      HLinv[7] = (A[1] * A[6] - A[0] * A[7]) / det;
+      HLinv[8] = (A[0] * A[4] - A[1] * A[3]) / det;
+    }
+    if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
+    HP_HIP(hipMemcpyAsync(d_.hidx, b.hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
+    HP_HIP(hipMemcpyAsync(d_.Phi, HLinv, sizeof(double) * 9, hipMemcpyHostToDevice, d_.stream));
+    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, d_.hidx, d_.Phi, s2, d_.ekf);
+    // landmark value update H_Linv * resinit (residual column of rows 0..2)
+    double resinit[3];
+    HP_HIP(hipMemcpy2DAsync(resinit, sizeof(double), d_.H + n, sizeof(double) * d_.ldh, sizeof(double), 3,
+                            hipMemcpyDeviceToHost, d_.stream));
+    HP_HIP(hipStreamSynchronize(d_.stream));
+    double dl[3];
+    for (int a = 0; a < 3; a++) dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
+    lm->update(dl);
+    lm->id = N_;
+    vars_.push_back(lm);
+    N_ += 3;
+    slam_.insert({f->featid, lm});
+    f->to_delete = true;
+    int nup = 2 * b.feats[0].nmeas - 3;
+    if (nup > 0) ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2);
+  }
+  return 0;
+}
+
+// UpdaterSLAM::change_anchors / perform_anchor_change (UpdaterSLAM.cpp:481-647)
+int Engine::slam_change_anchors() {
+  if ((int)clones_.size() <= o_.max_clone_size) return 0;
+  double mt = margtimestep();
+  for (auto &kv : slam_) {
+    VarP lm = kv.second;
+    if (lm->rep == 0 || lm->rep == 1) continue;
+    if (lm->anchor_time != mt) continue;
+    // old / new anchor camera poses
+    auto cam_pose = [&](int cam, const VarP &clone, bool fej, double *R_GtoC, double *p_CinG) {
+      double Ric[9], Rgi[9], t[3];
+      quat_2_Rot(calib_pose_.at(cam)->val, Ric);
+      quat_2_Rot(fej ? clone->fej : clone->val, Rgi);
+      m3_mul(Ric, Rgi, R_GtoC);
+      m3t_vec(R_GtoC, calib_pose_.at(cam)->val + 4, t);
+      const double *p = (fej ? clone->fej : clone->val) + 4;
+      for (int k = 0; k < 3; k++) p_CinG[k] = p[k] - t[k];
+    };
+    VarP iold = clones_.at(lm->anchor_time), inew = clones_.at(timestamp_);
+    int cam = lm->anchor_cam;
+    double p_old[3], p_old_fej[3];
+    lm->xyz(false, p_old);
+    lm->xyz(true, p_old_fej);
+    auto transfer = [&](bool fej, const double *pin, double *pout) {
+      double Ro[9], po[3], Rn[9], pn[3], Ron[9], d[3], t[3];
+      cam_pose(cam, iold, fej, Ro, po);
+      cam_pose(cam, inew, fej, Rn, pn);
+      m3_mul_bt(Rn, Ro, Ron);
+      for (int k = 0; k < 3; k++) d[k] = po[k] - pn[k];
+      m3_vec(Rn, d, t);
+      double a[3];
+      m3_vec(Ron, pin, a);
+      for (int k = 0; k < 3; k++) pout[k] = a[k] + t[k];
+    };
+    double p_new[3], p_new_fej[3];
+    transfer(false, p_old, p_new);
+    transfer(true, p_old_fej, p_new_fej);
+    // representation Jacobians (get_feature_jacobian_representation, UpdaterHelper.cpp:90-168)
+    auto rep_jac = [&](const VarP &anchor, const double *pFA_in, double *Hf, double *Hanc, double *Hcal) {
+      double Ric[9], Rgi[9], pIinC[3], pIinG[3], pFA[3];
+      quat_2_Rot(calib_pose_.at(cam)->val, Ric);
+      for (int k = 0; k < 3; k++) pIinC[k] = calib_pose_.at(cam)->val[4 + k];
+      quat_2_Rot(anchor->val, Rgi);
+      for (int k = 0; k < 3; k++) pIinG[k] = anchor->val[4 + k], pFA[k] = pFA_in[k];
+      if (o_.do_fej) {
+        double d0[3] = {pFA[0] - pIinC[0], pFA[1] - pIinC[1], pFA[2] - pIinC[2]}, t1[3], t2[3], best[3];
+        m3t_vec(Ric, d0, t1);
+        m3t_vec(Rgi, t1, t2);
+        for (int k = 0; k < 3; k++) best[k] = t2[k] + pIinG[k];
+        quat_2_Rot(anchor->fej, Rgi);
+        for (int k = 0; k < 3; k++) pIinG[k] = anchor->fej[4 + k];
+        double d1[3] = {best[0] - pIinG[0], best[1] - pIinG[1], best[2] - pIinG[2]}, u[3];
+        m3_vec(Rgi, d1, u);
+        m3_vec(Ric, u, t1);
+        for (int k = 0; k < 3; k++) pFA[k] = t1[k] + pIinC[k];
+      }
+      double RIT[9], RCT[9], RCG[9], Sk[9], Tm[9];
+      m3_transpose(Rgi, RIT);
+      m3_transpose(Ric, RCT);
+      m3_mul(RIT, RCT, RCG);
+      double dd[3] = {pFA[0] - pIinC[0], pFA[1] - pIinC[1], pFA[2] - pIinC[2]}, w[3];
+      m3t_vec(Ric, dd, w);
+      skew(w, Sk);
+      m3_mul(RIT, Sk, Tm);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          Hanc[6 * i + j] = -Tm[3 * i + j];
+          Hanc[6 * i + 3 + j] = (i == j);
+        }
+      skew(dd, Sk);
+      m3_mul(RCG, Sk, Tm);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          Hcal[6 * i + j] = -Tm[3 * i + j];
+          Hcal[6 * i + 3 + j] = -RCG[3 * i + j];
+        }
+      if (lm->rep == 2) {
+        std::memcpy(Hf, RCG, sizeof(double) * 9);
+      } else {
+        double alpha = pFA[0] / pFA[2], beta = pFA[1] / pFA[2], rho = 1 / pFA[2];
+        double d[9] = {1.0 / rho, 0, -(1.0 / (rho * rho)) * alpha, 0, 1.0 / rho, -(1.0 / (rho * rho)) * beta, 0, 0,
+                       -(1.0 / (rho * rho))};
+        m3_mul(RCG, d, Hf);
+      }
+    };
+    double Hf_old[9], Ha_old[18], Hc_old[18], Hf_new[9], Ha_new[18], Hc_new[18];
+    double pA_old[3], pA_new_tmp[3];
+    lm->xyz(false, pA_old);
+    rep_jac(iold, pA_old, Hf_old, Ha_old, Hc_old);
+    // new representation at the new anchor: the reference passes new_feat with p_FinA = transferred value
+    std::memcpy(pA_new_tmp, p_new, sizeof(p_new));
+    rep_jac(inew, pA_new_tmp, Hf_new, Ha_new, Hc_new);
+    // Phi order: x_order_old (anchor clone, calib), x_order_new (new clone, calib dup), landmark
+    std::vector<std::pair<int, int>> order;  // (cov id, size)
+    std::vector<int> col_anchor_old, col_cal, col_anchor_new;
+    int cur = 0;
+    order.push_back({iold->id, 6});
+    int c_old = cur;
+    cur += 6;
+    int c_cal = -1;
+    if (o_.do_calib_camera_pose) {
+      order.push_back({calib_pose_.at(cam)->id, 6});
+      c_cal = cur;
+      cur += 6;
+    }
+    int c_new = cur;
+    order.push_back({inew->id, 6});
+    cur += 6;
+    int c_lm = cur;
+    order.push_back({lm->id, 3});
+    cur += 3;
+    double Hinv[9];
+    {
+      double *A = Hf_new;
+      double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) + A[2] * (A[3] * A[7] - A[4] * A[6]);
+      Hinv[0] = (A[4] * A[8] - A[5] * A[7]) / det;
+      Hinv[1] = (A[2] * A[7] - A[1] * A[8]) / det;
+      Hinv[2] = (A[1] * A[5] - A[2] * A[4]) / det;
+      Hinv[3] = (A[5] * A[6] - A[3] * A[8]) / det;
+      Hinv[4] = (A[0] * A[8] - A[2] * A[6]) / det;
+      Hinv[5] = (A[2] * A[3] - A[0] * A[5]) / det;
+      Hinv[6] = (A[3] * A[7] - A[4] * A[6]) / det;
+      Hinv[7] = (A[1] * A[6] - A[0] * A[7]) / det;
+      Hinv[8] = (A[0] * A[4] - A[1] * A[3]) / det;
+    }
+    std::vector<double> Phi((size_t)3 * cur, 0.0), Q(9, 0.0);
+    auto addblk = [&](int col, const double *H36, double sgn) {
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 6; j++) {
+          double s = 0;
+          for (int k = 0; k < 3; k++) s += Hinv[3 * i + k] * H36[6 * k + j];
+          Phi[(size_t)i * cur + col + j] += sgn * s;
+        }
+    };
+    addblk(c_old, Ha_old, 1.0);
+    if (c_cal >= 0) addblk(c_cal, Hc_old, 1.0);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += Hinv[3 * i + k] * Hf_old[3 * k + j];
+        Phi[(size_t)i * cur + c_lm + j] = s;
+      }
+    addblk(c_new, Ha_new, -1.0);
+    if (c_cal >= 0) addblk(c_cal, Hc_new, -1.0);
+    std::vector<int> iold_ids;
+    for (auto &o : order)
+      for (int k = 0; k < o.second; k++) iold_ids.push_back(o.first + k);
+    cov_propagate(lm->id, 3, iold_ids, Phi, Q);
+    lm->anchor_time = timestamp_;
+    lm->set_xyz(p_new, false);
+    lm->set_xyz(p_new_fej, true);
+  }
+  return 0;
+}
+
+// UpdaterUWB::update_single (UpdaterUWB.cpp:53-90) + UVioUpdaterHelper::get_uwb_jacobian_single
+// (UVioUpdaterHelper.cpp:147-241).  One row; chi2 gate on the device-computed innovation variance.
+int Engine::uwb_update_single(size_t anchor_id, double range) {
+  auto it = anchors_.find(anchor_id);
+  if (it == anchors_.end()) return 0;
+  const VarP &an = it->second;
+  std::vector<int> hidx;
+  for (int k = 0; k < 6; k++) hidx.push_back(imu_->id + k);
+  int n = 6;
+  int c_cal = -1, c_anc = -1;
+  if (o_.do_calib_uwb_extrinsics) {
+    c_cal = n;
+    for (int k = 0; k < 3; k++) hidx.push_back(p_IinU_->id + k);
+    n += 3;
+  }
+  if (!an->fixed) {
+    c_anc = n;
+    for (int k = 0; k < 5; k++) hidx.push_back(an->id + k);
+    n += 5;
+  }
+  double R[9], mp[3], t[3], pU[3];
+  quat_2_Rot(imu_->val, R);
+  for (int k = 0; k < 3; k++) mp[k] = -p_IinU_->val[k];
+  m3t_vec(R, mp, t);
+  for (int k = 0; k < 3; k++) pU[k] = t[k] + imu_->val[4 + k];
+  double d[3] = {an->val[0] - pU[0], an->val[1] - pU[1], an->val[2] - pU[2]};
+  double dn = norm3(d);
+  double beta = an->val[4], gam = an->val[3];
+  double res = range - ((1 + beta) * dn + gam);
+  double Hn[3] = {d[0] / dn, d[1] / dn, d[2] / dn};
+  std::vector<double> H(n + 1, 0.0);
+  double S[9], RS[9];
+  skew(mp, S);
+  m3_mul_at(R, S, RS);  // R^T skew(-p_IinU)
+  for (int j = 0; j < 3; j++) {
+    H[j] = (1 + beta) * (Hn[0] * RS[j] + Hn[1] * RS[3 + j] + Hn[2] * RS[6 + j]);
+    H[3 + j] = (1 + beta) * (-Hn[j]);
+  }
+  double HnRT[3];
+  m3_vec(R, Hn, HnRT);  // (H_n R^T)_j = sum_k Hn_k R_jk ... row vector H_n * R^T
+  for (int j = 0; j < 3; j++) HnRT[j] = Hn[0] * R[3 * j] + Hn[1] * R[3 * j + 1] + Hn[2] * R[3 * j + 2];
+  if (c_cal >= 0)
+    for (int j = 0; j < 3; j++) H[c_cal + j] = (1 + beta) * HnRT[j];
+  if (c_anc >= 0) {
+    for (int j = 0; j < 3; j++) H[c_anc + j] = (1 + beta) * HnRT[j];  // reference quirk, kept
+    H[c_anc + 3] = 1;
+    H[c_anc + 4] = dn;
+  }
+  H[n] = res;
+  double s2 = o_.uwb_sigma_range * o_.uwb_sigma_range;
+  // upload row + index, phase A (M, S), read S, gate, phase B
+  HP_HIP(hipMemcpyAsync(d_.R, H.data(), sizeof(double) * (n + 1), hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
+  launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, d_.R, n + 1, 1, n, d_.hidx, s2, d_.ekf);
+  double Sval;
+  HP_HIP(hipMemcpyAsync(&Sval, d_.ekf.S + 2, sizeof(double), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  double chi2 = res * res / Sval;
+  if (chi2 > o_.uwb_chi2_multipler * chi2_table_[1]) return 0;
+  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
+  launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, d_.R + n, 1, d_.ekf);
+  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "UWB EKFUpdate: negative covariance diagonal");
+  apply_dx(d_.dx_host);
+  return 1;
+}
+
+}  // namespace uvhp

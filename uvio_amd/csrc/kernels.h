@@ -1,0 +1,137 @@
+// Device data layouts and launch wrappers for the gfx950 kernels (kernels_*.hip).
+//
+// The covariance P is a dense row-major FP64 matrix resident in HBM for the whole run with a fixed
+// leading dimension `ld` (capacity computed from the config, DESIGN.md "Data layout"); the active
+// block is N x N in the top-left corner.  Variable ids are host-mirrored exactly like
+// ov_type::Type::_id (State.cpp:28-166, StateHelper.cpp:271-391).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hp_math.h"
+
+namespace uvhp {
+
+constexpr int kMaxMeasPerFeat = 64;  // m_f <= 64 (one lane per measurement in the geometry wave)
+constexpr int kMaxVarsPerFeat = 48;  // clones + per-cam calib blocks of one feature
+constexpr int kMaxCams = 4;
+
+// One clone slot (time order, State::_clones_IMU map order)
+struct DClone {
+  double R[9], p[3];    // R_GtoI, p_IinG (current)
+  double Rf[9], pf[3];  // first estimates
+  int pid;              // covariance id of the clone PoseJPL
+  int canon;            // canonical H column of the clone block
+  int pad[2];
+};
+
+// One camera: extrinsic (R_ItoC, p_IinC), intrinsics, covariance ids / canonical columns
+struct DCam {
+  double R_ItoC[9], p_IinC[3];
+  CamParams cam;
+  int pid_ext, pid_intr;      // -1 if not calibrated
+  int canon_ext, canon_intr;  // -1 if not calibrated
+};
+
+// One measurement of a feature (uv in raw pixels, uvn normalized; float as in ov_core::Feature)
+struct DMeas {
+  float u, v, un, vn;
+  int cam, slot;      // camera id, clone slot
+  int lc_clone;       // local column of the clone block
+  int lc_ext, lc_intr;  // local columns of its camera's calibration (-1 if absent)
+  int pad;
+};
+
+// A local variable of a feature: covariance id, canonical column, size, local column
+struct DVar {
+  int pid, canon, size, loc;
+};
+
+// One feature of an update batch
+struct DFeat {
+  int meas_off, nmeas;  // into the measurement array (reference iteration order)
+  int var_off, nvar;    // into the variable array
+  int nf;               // local Jacobian columns (sum of var sizes)
+  int row_off;          // first output row in H_all
+  int anchor_cam, anchor_slot;  // FeatureInitializer anchor (host-computed, FeatureInitializer.cpp:35-45)
+  int lc_anchor_clone, lc_anchor_ext;  // local cols of the anchor clone / anchor cam extrinsic (anchored reps)
+  int rep;              // LandmarkRepresentation
+  int mode;             // 0 MSCKF (triangulate+refine+nullspace), 1 SLAM update (landmark in state),
+                        // 2 delayed init (triangulate+refine, all rows), 3 delayed init at a given triangulation
+  double p_in[3];       // SLAM: landmark xyz (value); MSCKF: unused
+  double p_in_fej[3];   // SLAM: landmark xyz (fej)
+  int lm_pid, lm_loc;   // SLAM: landmark covariance id / local col
+  int pad[2];
+};
+
+// Per-feature result
+struct DFeatOut {
+  double p_FinA[3], p_FinG[3];
+  double chi2;
+  double HfR[9];  // delayed init: the 3x3 upper block of H_f after the reflections (H_finit)
+  int status;  // 0 accepted, 1 triangulation failed, 2 refine failed, 3 chi2 rejected
+  int rows;    // rows written (accepted)
+};
+
+// Parameters shared by one update batch
+struct DBatchParams {
+  int nfeat;
+  int n_canon;     // canonical columns n (residual column stored at index n)
+  int ldh;         // leading dimension of H_all (>= n+1)
+  int ldp;         // leading dimension of P
+  double sigma_pix_sq;
+  double chi2_mult;
+  int do_fej;
+  int calib_ext, calib_intr;
+  // FeatureInitializerOptions
+  int fi_max_runs, fi_refine, fi_tri1d;
+  double fi_init_lamda, fi_max_lamda, fi_min_dx, fi_min_dcost, fi_lam_mult;
+  double fi_min_dist, fi_max_dist, fi_max_baseline, fi_max_cond;
+};
+
+// ---- launch wrappers (all asynchronous on `s`) ----
+// EKFPropagation (StateHelper.cpp:36-114) for a contiguous new block [s0, s0+p) with old index list
+// iold (q entries, device), Phi (p x q) and Q (p x p) in device memory.  T is N x p scratch.
+void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
+                          const double *Phi, const double *Q, double *T);
+// StateHelper::clone of imu->pose() + augment_clone time-offset term (StateHelper.cpp:341-391,579-616)
+void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt);
+// StateHelper::marginalize (StateHelper.cpp:271-339): Pout <- P without rows/cols [m0, m0+ms)
+void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, int N, int m0, int ms);
+// diagonal check: writes count of negative diagonal entries to *neg (device int)
+void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg);
+
+// MSCKF / SLAM per-feature linearization: triangulation (+LM), Jacobian, nullspace, chi2, rows to H_all
+void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const DMeas *meas,
+                              const DVar *vars, const DClone *clones, const DCam *cams, const double *P,
+                              const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf);
+size_t feature_lds_bytes(int max_meas, int max_nf);
+
+// Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->
+// R_aug ((n+1) x (n+1) upper, ld = ldr).  Rank-deficient pivots produce zero rows.
+void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, double *partials, int *nchunks_out);
+int gram_num_chunks(int m);
+void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks, int ncol, double *R, int ldr);
+
+// EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j
+// maps to covariance index hidx[j] (device), residual res (r, device, stride res_stride), noise sigma2.
+// Scratch: M (N x r), W (N x r), S (3 r x r: Linv, global work, S_up), y (r), dx (N), neg (int).
+struct EkfScratch {
+  double *M, *W, *S, *y, *dx;
+  int *neg;
+};
+void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc);
+// the same update split at the innovation covariance: phase A leaves S_up = H P H^T + s2 I (r x r) at
+// sc.S + 2 r^2 (used by gated single-row updates such as UWB); phase B finishes the update.
+void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, double sigma2, EkfScratch &sc);
+void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
+                       EkfScratch &sc);
+// StateHelper::initialize_invertible for a 3-dof variable appended at N (StateHelper.cpp:484-577)
+void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
+                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc);
+double chi2_quantile95(int dof);
+
+}  // namespace uvhp

@@ -1,0 +1,474 @@
+// gfx950 kernels for the dense covariance P (HBM-resident, row-major, leading dimension ld):
+//   EKFPropagation         StateHelper.cpp:36-114
+//   clone / augment_clone  StateHelper.cpp:341-391, 579-616
+//   marginalize            StateHelper.cpp:271-339
+//   measurement compression (UpdaterHelper.cpp:456-487) as CholeskyQR of [H | r]:
+//     G = [H r]^T [H r] (tiled FP64, split over row chunks), then the upper Cholesky factor of G is
+//     the R factor of the QR of [H r] up to row signs: R = rows of the reference's Givens-compressed
+//     [H_x | res] (DESIGN.md "Compression").
+//   EKFUpdate              StateHelper.cpp:116-197 as M = P[:,I] H^T, S = H M[I,:] + s2 I = L L^T,
+//                          W = M L^-T, P -= W W^T (upper, mirrored), dx = W L^-1 r.
+#include "kernels.h"
+
+namespace uvhp {
+
+// ----------------------------------------------------------------------------------------------
+// EKFPropagation
+// T[i][a] = sum_b P[i][iold[b]] * Phi[a][b]    (Cov_PhiT, StateHelper.cpp:80-85)
+__global__ void k_prop_T(const double *__restrict__ P, int ld, int N, int p, const int *__restrict__ iold, int q,
+                         const double *__restrict__ Phi, double *__restrict__ T) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * p) return;
+  int i = idx / p, a = idx % p;
+  const double *Pi = P + (size_t)i * ld;
+  double acc = 0.0;
+  for (int b = 0; b < q; b++) acc += Pi[iold[b]] * Phi[a * q + b];
+  T[(size_t)i * p + a] = acc;
+}
+
+// rows/cols of the new block <- T, block <- Q(upper-sym) + Phi * T[iold,:]   (StateHelper.cpp:88-101)
+__global__ void k_prop_write(double *__restrict__ P, int ld, int N, int s0, int p, const int *__restrict__ iold, int q,
+                             const double *__restrict__ Phi, const double *__restrict__ Q, const double *__restrict__ T) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * p) return;
+  int i = idx / p, a = idx % p;
+  if (i >= s0 && i < s0 + p) {
+    int x = i - s0;
+    double acc = (x <= a) ? Q[x * p + a] : Q[a * p + x];
+    for (int c = 0; c < q; c++) acc += Phi[x * q + c] * T[(size_t)iold[c] * p + a];
+    P[(size_t)i * ld + s0 + a] = acc;
+  } else {
+    double v = T[(size_t)i * p + a];
+    P[(size_t)i * ld + s0 + a] = v;
+    P[(size_t)(s0 + a) * ld + i] = v;
+  }
+}
+
+void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
+                          const double *Phi, const double *Q, double *T) {
+  int n = N * p, bs = 256, gs = (n + bs - 1) / bs;
+  hipLaunchKernelGGL(k_prop_T, dim3(gs), dim3(bs), 0, s, P, ld, N, p, iold, q, Phi, T);
+  hipLaunchKernelGGL(k_prop_write, dim3(gs), dim3(bs), 0, s, P, ld, N, s0, p, iold, q, Phi, Q, T);
+}
+
+// ----------------------------------------------------------------------------------------------
+// clone of the 6-dof IMU pose (ids src0..src0+5) appended at N, plus the time-offset cross term
+__global__ void k_clone(double *__restrict__ P, int ld, int N, int src0, int dt_id, const double *__restrict__ dnc,
+                        int do_dt) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (N + 6) * 6) return;
+  int i = idx / 6, b = idx % 6;
+  double db = do_dt ? dnc[b] : 0.0;
+  if (i < N) {
+    double col = P[(size_t)i * ld + src0 + b];
+    double row = P[(size_t)(src0 + b) * ld + i];
+    if (do_dt) {
+      col += P[(size_t)i * ld + dt_id] * db;
+      row += db * P[(size_t)dt_id * ld + i];
+    }
+    P[(size_t)i * ld + N + b] = col;
+    P[(size_t)(N + b) * ld + i] = row;
+  } else {
+    int a = i - N;
+    double v = P[(size_t)(src0 + a) * ld + src0 + b];
+    if (do_dt) {
+      double da = dnc[a];
+      v += P[(size_t)(src0 + a) * ld + dt_id] * db;
+      v += da * (P[(size_t)dt_id * ld + src0 + b] + P[(size_t)dt_id * ld + dt_id] * db);
+    }
+    P[(size_t)i * ld + N + b] = v;
+  }
+}
+
+void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt) {
+  int n = (N + 6) * 6, bs = 256, gs = (n + bs - 1) / bs;
+  hipLaunchKernelGGL(k_clone, dim3(gs), dim3(bs), 0, s, P, ld, N, src0, dt_id, dnc_dev, do_dt);
+}
+
+// ----------------------------------------------------------------------------------------------
+__global__ void k_marginalize(const double *__restrict__ P, double *__restrict__ Po, int ld, int N, int m0, int ms) {
+  int Nn = N - ms;
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  int i = blockIdx.y;
+  if (j >= Nn || i >= Nn) return;
+  int mi = i < m0 ? i : i + ms, mj = j < m0 ? j : j + ms;
+  double v;
+  if (i >= m0 && j < m0)
+    v = P[(size_t)j * ld + mi];  // Cov_new(x2,x1) = Cov_new(x1,x2)^T (StateHelper.cpp:303-304)
+  else
+    v = P[(size_t)mi * ld + mj];
+  Po[(size_t)i * ld + j] = v;
+}
+
+void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, int N, int m0, int ms) {
+  int Nn = N - ms;
+  if (Nn <= 0) return;
+  hipLaunchKernelGGL(k_marginalize, dim3((Nn + 127) / 128, Nn), dim3(128), 0, s, P, Pout, ld, N, m0, ms);
+}
+
+__global__ void k_check_diag(const double *__restrict__ P, int ld, int N, int *neg) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N && P[(size_t)i * ld + i] < 0.0) atomicAdd(neg, 1);
+}
+void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg) {
+  hipLaunchKernelGGL(k_check_diag, dim3((N + 255) / 256), dim3(256), 0, s, P, ld, N, neg);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Compression: Gram partials.  Grid: (upper tile pairs, row chunks).  Tile 32x32, 256 threads,
+// each thread 2x2 outputs.  A is m x ncol, row-major, ld = ldh.
+constexpr int GT = 32;         // tile edge
+constexpr int GCHUNK = 512;    // rows per chunk
+
+int gram_num_chunks(int m) { return (m + GCHUNK - 1) / GCHUNK; }
+
+__global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int m, int ncol, int ldh,
+                                              double *__restrict__ partials) {
+  __shared__ double As[GT][GT + 1];
+  __shared__ double Bs[GT][GT + 1];
+  int nt = (ncol + GT - 1) / GT;
+  // decode upper tile pair (ti <= tj) from blockIdx.x
+  int pair = blockIdx.x, ti = 0;
+  while (pair >= nt - ti) {
+    pair -= nt - ti;
+    ti++;
+  }
+  int tj = ti + pair;
+  int chunk = blockIdx.y;
+  int r0 = chunk * GCHUNK, r1 = min(m, r0 + GCHUNK);
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  double acc[2][2] = {{0, 0}, {0, 0}};
+  for (int rb = r0; rb < r1; rb += GT) {
+    for (int e = threadIdx.x; e < GT * GT; e += 256) {
+      int rr = e / GT, cc = e % GT;
+      int row = rb + rr;
+      int ca = ti * GT + cc, cb = tj * GT + cc;
+      As[rr][cc] = (row < r1 && ca < ncol) ? A[(size_t)row * ldh + ca] : 0.0;
+      Bs[rr][cc] = (row < r1 && cb < ncol) ? A[(size_t)row * ldh + cb] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < GT; k++) {
+      double a0 = As[k][ty], a1 = As[k][ty + 16];
+      double b0 = Bs[k][tx], b1 = Bs[k][tx + 16];
+      acc[0][0] += a0 * b0;
+      acc[0][1] += a0 * b1;
+      acc[1][0] += a1 * b0;
+      acc[1][1] += a1 * b1;
+    }
+    __syncthreads();
+  }
+  double *out = partials + (size_t)chunk * ncol * ncol;
+  for (int u = 0; u < 2; u++)
+    for (int v = 0; v < 2; v++) {
+      int a = ti * GT + ty + 16 * u, b = tj * GT + tx + 16 * v;
+      if (a < ncol && b < ncol) out[(size_t)a * ncol + b] = acc[u][v];
+    }
+}
+
+void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, double *partials, int *nchunks_out) {
+  int nt = (ncol + GT - 1) / GT;
+  int pairs = nt * (nt + 1) / 2;
+  int nch = gram_num_chunks(m);
+  *nchunks_out = nch;
+  hipLaunchKernelGGL(k_gram, dim3(pairs, nch), dim3(256), 0, s, A, m, ncol, ldh, partials);
+}
+
+// Sum partials (fixed chunk order) into the upper triangle of G, then upper Cholesky G = R^T R.
+// G lives in `W` (LDS when it fits, else global scratch `gbuf`). Pivots <= tol*G_jj give zero rows.
+__global__ void __launch_bounds__(1024) k_gram_reduce_chol(const double *__restrict__ partials, int nch, int ncol,
+                                                           double *__restrict__ R, int ldr, double *gbuf, int use_lds) {
+  extern __shared__ double lds[];
+  double *G = use_lds ? lds : gbuf;
+  __shared__ double piv;
+  __shared__ int zero_row;
+  int n = ncol;
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    int a = e / n, b = e % n;
+    double acc = 0.0;
+    if (b >= a)
+      for (int c = 0; c < nch; c++) acc += partials[(size_t)c * n * n + e];
+    G[e] = acc;
+  }
+  __syncthreads();
+  // keep the original diagonal for the rank tolerance in the (unused) lower-left corner
+  for (int k = 0; k < n; k++) {
+    if (threadIdx.x == 0) {
+      double d = G[k * n + k];
+      double g0 = 0.0;
+      // original diagonal recomputed from partials (cheap: one entry)
+      for (int c = 0; c < nch; c++) g0 += partials[(size_t)c * n * n + k * n + k];
+      if (d > 1e-13 * g0 && d > 0.0) {
+        piv = sqrt(d);
+        zero_row = 0;
+      } else {
+        piv = 0.0;
+        zero_row = 1;
+      }
+      G[k * n + k] = piv;
+    }
+    __syncthreads();
+    // row k of R: R[k][j] = G[k][j] / piv
+    for (int j = k + 1 + threadIdx.x; j < n; j += blockDim.x) G[k * n + j] = zero_row ? 0.0 : G[k * n + j] / piv;
+    __syncthreads();
+    // trailing update G[i][j] -= R[k][i] R[k][j] for k < i <= j
+    int m = n - k - 1;
+    int tot = m * m;
+    for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+      int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j >= i) G[i * n + j] -= G[k * n + i] * G[k * n + j];
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    int a = e / n, b = e % n;
+    R[(size_t)a * ldr + b] = (b >= a) ? G[e] : 0.0;
+  }
+}
+
+void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks, int ncol, double *R, int ldr) {
+  size_t bytes = (size_t)ncol * ncol * sizeof(double);
+  int use_lds = bytes <= 150 * 1024;
+  // global scratch for large ncol lives right after R (caller sizes R for 2 * ncol^2)
+  double *gbuf = R + (size_t)ncol * ldr;
+  hipLaunchKernelGGL(k_gram_reduce_chol, dim3(1), dim3(1024), use_lds ? bytes : 0, s, partials, nchunks, ncol, R, ldr,
+                     gbuf, use_lds);
+}
+
+// ----------------------------------------------------------------------------------------------
+// EKF update
+// M[i][j] = sum_k P[i][hidx[k]] * H[j][k]   (N x r)   (M_a = P H^T, StateHelper.cpp:137-146)
+__global__ void __launch_bounds__(256) k_ekf_M(const double *__restrict__ P, int ldp, int N, const double *__restrict__ H,
+                                               int ldh, int r, int n, const int *__restrict__ hidx, double *__restrict__ M) {
+  __shared__ double Ps[16][17];
+  __shared__ double Hs[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  double acc = 0.0;
+  for (int k0 = 0; k0 < n; k0 += 16) {
+    int k = k0 + tx;
+    Ps[ty][tx] = (i0 + ty < N && k < n) ? P[(size_t)(i0 + ty) * ldp + hidx[k]] : 0.0;
+    Hs[ty][tx] = (j0 + ty < r && k < n) ? H[(size_t)(j0 + ty) * ldh + k] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += Ps[ty][kk] * Hs[tx][kk];
+    __syncthreads();
+  }
+  if (i0 + ty < N && j0 + tx < r) M[(size_t)(i0 + ty) * r + j0 + tx] = acc;
+}
+
+// S_up[a][b] = sum_k H[a][k] * M[hidx[k]][b] (+ s2 on the diagonal)   (r x r, multi-WG)
+__global__ void __launch_bounds__(256) k_ekf_S(const double *__restrict__ H, int ldh, int r, int n,
+                                               const int *__restrict__ hidx, const double *__restrict__ M, double s2,
+                                               double *__restrict__ Sout) {
+  __shared__ double Hs[16][17];
+  __shared__ double Ms[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int a0 = blockIdx.y * 16, b0 = blockIdx.x * 16;
+  double acc = 0.0;
+  for (int k0 = 0; k0 < n; k0 += 16) {
+    Hs[ty][tx] = (a0 + ty < r && k0 + tx < n) ? H[(size_t)(a0 + ty) * ldh + k0 + tx] : 0.0;
+    Ms[ty][tx] = (k0 + ty < n && b0 + tx < r) ? M[(size_t)hidx[k0 + ty] * r + b0 + tx] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += Hs[ty][kk] * Ms[kk][tx];
+    __syncthreads();
+  }
+  int a = a0 + ty, b = b0 + tx;
+  if (a < r && b < r) Sout[(size_t)a * r + b] = acc + (a == b ? s2 : 0.0);
+}
+
+// Single workgroup: S = L L^T on the upper triangle of S_up (selfadjointView<Upper>, StateHelper.cpp:160);
+// Linv in place; y = Linv res.  Work buffer: LDS when r*r*8 <= 150 KiB, else global `Sg`.
+__global__ void __launch_bounds__(1024) k_ekf_small(const double *__restrict__ Sup, int r,
+                                                    const double *__restrict__ res, int res_stride,
+                                                    double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
+                                                    int use_lds) {
+  extern __shared__ double lds[];
+  double *S = use_lds ? lds : Sg;
+  __shared__ double tmp[1024];
+  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
+    int a = e / r, b = e % r;
+    if (b <= a) S[e] = Sup[(size_t)b * r + a];
+  }
+  __syncthreads();
+  // right-looking lower Cholesky on the lower triangle
+  for (int k = 0; k < r; k++) {
+    if (threadIdx.x == 0) S[k * r + k] = sqrt(S[k * r + k]);
+    __syncthreads();
+    double d = S[k * r + k];
+    for (int i = k + 1 + threadIdx.x; i < r; i += blockDim.x) S[i * r + k] /= d;
+    __syncthreads();
+    int m = r - k - 1;
+    for (int e = threadIdx.x; e < m * m; e += blockDim.x) {
+      int i = k + 1 + e / m, j = k + 1 + e % m;
+      if (j <= i) S[i * r + j] -= S[i * r + k] * S[j * r + k];
+    }
+    __syncthreads();
+  }
+  // y = L^-1 res (forward substitution, one thread per step with a parallel dot)
+  for (int i = threadIdx.x; i < r; i += blockDim.x) tmp[i] = res[(size_t)i * res_stride];
+  __syncthreads();
+  for (int k = 0; k < r; k++) {
+    if (threadIdx.x == 0) tmp[k] /= S[k * r + k];
+    __syncthreads();
+    for (int i = k + 1 + threadIdx.x; i < r; i += blockDim.x) tmp[i] -= S[i * r + k] * tmp[k];
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < r; i += blockDim.x) y_out[i] = tmp[i];
+  // in-place inverse of lower-triangular L (LAPACK trti2, lower, backward over columns)
+  for (int j = r - 1; j >= 0; j--) {
+    if (threadIdx.x == 0) S[j * r + j] = 1.0 / S[j * r + j];
+    __syncthreads();
+    double ajj = -S[j * r + j];
+    // x = Linv[j+1:, j+1:] * L[j+1:, j]
+    for (int i = j + 1 + threadIdx.x; i < r; i += blockDim.x) {
+      double acc = 0.0;
+      for (int k = j + 1; k <= i; k++) acc += S[i * r + k] * S[k * r + j];
+      tmp[i] = acc;
+    }
+    __syncthreads();
+    for (int i = j + 1 + threadIdx.x; i < r; i += blockDim.x) S[i * r + j] = ajj * tmp[i];
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
+    int a = e / r, b = e % r;
+    Linv_out[e] = (b <= a) ? S[e] : 0.0;
+  }
+}
+
+// W = M Linv^T  (N x r): W[i][j] = sum_{k<=j} M[i][k] Linv[j][k]
+__global__ void __launch_bounds__(256) k_ekf_W(const double *__restrict__ M, int N, int r, const double *__restrict__ Linv,
+                                               double *__restrict__ W) {
+  __shared__ double Ms[16][17];
+  __shared__ double Ls[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  double acc = 0.0;
+  int kmax = min(r, j0 + 16);
+  for (int k0 = 0; k0 < kmax; k0 += 16) {
+    Ms[ty][tx] = (i0 + ty < N && k0 + tx < r) ? M[(size_t)(i0 + ty) * r + k0 + tx] : 0.0;
+    Ls[ty][tx] = (j0 + ty < r && k0 + tx < r) ? Linv[(size_t)(j0 + ty) * r + k0 + tx] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += Ms[ty][kk] * Ls[tx][kk];
+    __syncthreads();
+  }
+  if (i0 + ty < N && j0 + tx < r) W[(size_t)(i0 + ty) * r + j0 + tx] = acc;
+}
+
+// P[i][j] -= sum_k W[i][k] W[j][k] for j >= i, mirrored to (j,i); dx = W y; negative-diagonal count
+__global__ void __launch_bounds__(256) k_ekf_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ W,
+                                               int r, const double *__restrict__ y, double *__restrict__ dx, int *neg) {
+  __shared__ double Wi[16][17];
+  __shared__ double Wj[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int bi = blockIdx.y, bj = blockIdx.x;
+  if (bj < bi) return;  // upper tiles only (uniform per block)
+  int i0 = bi * 16, j0 = bj * 16;
+  double acc = 0.0;
+  for (int k0 = 0; k0 < r; k0 += 16) {
+    Wi[ty][tx] = (i0 + ty < N && k0 + tx < r) ? W[(size_t)(i0 + ty) * r + k0 + tx] : 0.0;
+    Wj[ty][tx] = (j0 + ty < N && k0 + tx < r) ? W[(size_t)(j0 + ty) * r + k0 + tx] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += Wi[ty][kk] * Wj[tx][kk];
+    __syncthreads();
+  }
+  int i = i0 + ty, j = j0 + tx;
+  if (i < N && j < N && j >= i) {
+    double v = P[(size_t)i * ldp + j] - acc;
+    P[(size_t)i * ldp + j] = v;
+    P[(size_t)j * ldp + i] = v;
+    if (i == j && v < 0.0) atomicAdd(neg, 1);
+  }
+  // dx by the diagonal blocks' first row of threads
+  if (bi == bj && ty == 0) {
+    int row = i0 + tx;
+    if (row < N) {
+      double a = 0.0;
+      for (int k = 0; k < r; k++) a += W[(size_t)row * r + k] * y[k];
+      dx[row] = a;
+    }
+  }
+}
+
+void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, double sigma2, EkfScratch &sc) {
+  dim3 gM((r + 15) / 16, (N + 15) / 16);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, H, ldh, r, n, hidx, sc.M);
+  double *Sup = sc.S + 2 * (size_t)r * r;
+  dim3 gS((r + 15) / 16, (r + 15) / 16);
+  hipLaunchKernelGGL(k_ekf_S, gS, dim3(256), 0, s, H, ldh, r, n, hidx, sc.M, sigma2, Sup);
+}
+
+void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
+                       EkfScratch &sc) {
+  size_t bytes = (size_t)r * r * sizeof(double);
+  int use_lds = bytes <= 150 * 1024;
+  double *Linv = sc.S;
+  double *Sg = sc.S + (size_t)r * r;
+  double *Sup = sc.S + 2 * (size_t)r * r;
+  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(1024), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
+                     use_lds);
+  dim3 gM((r + 15) / 16, (N + 15) / 16);
+  hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, r, Linv, sc.W);
+  int nb = (N + 15) / 16;
+  hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg);
+}
+
+void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc) {
+  launch_ekf_phaseA(s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc);
+  launch_ekf_phaseB(s, P, ldp, N, r, res, res_stride, sc);
+}
+
+// StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
+// M = P[:, hidx] Hx^T is in sc.M (N x 3, from k_ekf_M); Hx (3 x n, ld), HLinv (3x3, device), s2.
+__global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
+                                  const double *__restrict__ Hx, int ldh, int n, const int *__restrict__ hidx,
+                                  const double *__restrict__ HLinv, double s2) {
+  __shared__ double S3[9], PLL[9];
+  int t = threadIdx.x + blockIdx.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < 9) {
+    int a = threadIdx.x / 3, b = threadIdx.x % 3;
+    double acc = 0.0;
+    for (int k = 0; k < n; k++) acc += Hx[(size_t)a * ldh + k] * M[(size_t)hidx[k] * 3 + b];
+    // M.selfadjointView<Upper>(): use the upper element for both halves
+    S3[threadIdx.x] = acc + (a == b ? s2 : 0.0);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 9) {
+    int a = threadIdx.x / 3, b = threadIdx.x % 3;
+    double acc = 0.0;
+    for (int c = 0; c < 3; c++)
+      for (int e = 0; e < 3; e++) {
+        double sce = (c <= e) ? S3[c * 3 + e] : S3[e * 3 + c];
+        acc += HLinv[a * 3 + c] * sce * HLinv[b * 3 + e];
+      }
+    PLL[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  if (t < N * 3) {
+    int i = t / 3, a = t % 3;
+    double acc = 0.0;
+    for (int b = 0; b < 3; b++) acc += M[(size_t)i * 3 + b] * HLinv[a * 3 + b];
+    P[(size_t)i * ldp + N + a] = -acc;
+    P[(size_t)(N + a) * ldp + i] = -acc;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 9) {
+    int a = threadIdx.x / 3, b = threadIdx.x % 3;
+    P[(size_t)(N + a) * ldp + N + b] = PLL[threadIdx.x];
+  }
+}
+
+void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
+                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc) {
+  dim3 gM(1, (N + 15) / 16);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M);
+  int nt = N * 3;
+  hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
+                     HLinv, s2);
+}
+
+}  // namespace uvhp

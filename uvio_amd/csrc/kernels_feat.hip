@@ -1,0 +1,702 @@
+// Per-feature linearization kernel, one 256-thread workgroup (4 waves) per feature.
+//
+//   wave 0 : FeatureInitializer::single_triangulation  (FeatureInitializer.cpp:30-112)
+//            FeatureInitializer::single_gaussnewton    (FeatureInitializer.cpp:197-375, float residuals)
+//            one lane per measurement, 64-lane __shfl_xor reductions; every lane ends with the same
+//            reduced sums so the LM control flow is wave-uniform.
+//   all    : UpdaterHelper::get_feature_jacobian_full (UpdaterHelper.cpp:192-424), one thread per
+//            measurement, dense local Jacobian [H_x | res] (2m x (nf+1)) in LDS.
+//   all    : left-nullspace projection (UpdaterHelper.cpp:426-454) as 3 Householder reflections of H_f
+//            applied to [H_x | res] (any orthonormal basis of the left nullspace gives the same chi2,
+//            the same Gram matrix and hence the same EKF update as the reference's Givens sweep).
+//   all    : chi2 gate (UpdaterMSCKF.cpp:209-234): S = H P_marg H^T + s2 I built in row chunks with
+//            P_marg gathered from the HBM-resident P; Cholesky of [S | r] in LDS; chi2 = |L^-1 r|^2.
+//   all    : accepted rows are written to H_all in canonical dense columns (zeros when rejected).
+#include "kernels.h"
+
+namespace uvhp {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// colPivHouseholderQr().solve for 3x3 (A row-major), single right-hand side
+__device__ void colpiv_solve3(const double *Ain, const double *bin, double *x) {
+  double A[9], b[3];
+  for (int i = 0; i < 9; i++) A[i] = Ain[i];
+  for (int i = 0; i < 3; i++) b[i] = bin[i];
+  int perm[3] = {0, 1, 2};
+  double cn[3];
+  for (int j = 0; j < 3; j++) cn[j] = A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j];
+  int rank = 3;
+  double maxpivot = 0;
+  for (int k = 0; k < 3; k++) {
+    int best = k;
+    for (int j = k + 1; j < 3; j++)
+      if (cn[j] > cn[best]) best = j;
+    if (best != k) {
+      for (int i = 0; i < 3; i++) {
+        double t = A[3 * i + k];
+        A[3 * i + k] = A[3 * i + best];
+        A[3 * i + best] = t;
+      }
+      double t = cn[k];
+      cn[k] = cn[best];
+      cn[best] = t;
+      int tp = perm[k];
+      perm[k] = perm[best];
+      perm[best] = tp;
+    }
+    double alpha = 0;
+    for (int i = k; i < 3; i++) alpha += A[3 * i + k] * A[3 * i + k];
+    alpha = sqrt(alpha);
+    if (k == 0) maxpivot = alpha;
+    if (alpha <= maxpivot * 1e-15 || alpha == 0) {
+      rank = k;
+      break;
+    }
+    if (A[3 * k + k] > 0) alpha = -alpha;
+    double v[3] = {0, 0, 0};
+    for (int i = k; i < 3; i++) v[i] = A[3 * i + k];
+    v[k] -= alpha;
+    double vn = 0;
+    for (int i = k; i < 3; i++) vn += v[i] * v[i];
+    if (vn > 0) {
+      for (int j = k; j < 3; j++) {
+        double s = 0;
+        for (int i = k; i < 3; i++) s += v[i] * A[3 * i + j];
+        s = 2 * s / vn;
+        for (int i = k; i < 3; i++) A[3 * i + j] -= s * v[i];
+      }
+      double s = 0;
+      for (int i = k; i < 3; i++) s += v[i] * b[i];
+      s = 2 * s / vn;
+      for (int i = k; i < 3; i++) b[i] -= s * v[i];
+    }
+    for (int j = k + 1; j < 3; j++) {
+      double s = 0;
+      for (int i = k + 1; i < 3; i++) s += A[3 * i + j] * A[3 * i + j];
+      cn[j] = s;
+    }
+  }
+  double y[3] = {0, 0, 0};
+  for (int i = rank - 1; i >= 0; i--) {
+    double v = b[i];
+    for (int k = i + 1; k < rank; k++) v -= A[3 * i + k] * y[k];
+    y[i] = v / A[3 * i + i];
+  }
+  for (int i = 0; i < 3; i++) x[perm[i]] = y[i];
+}
+
+// singular values (descending) of 3x3 A via Jacobi eigenvalues of A^T A
+__device__ void singular_values3(const double *A, double *sv) {
+  double a[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) a[i][j] = A[i] * A[j] + A[3 + i] * A[3 + j] + A[6 + i] * A[6 + j];
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+    if (off < 1e-300) break;
+    for (int p = 0; p < 2; p++)
+      for (int q = p + 1; q < 3; q++) {
+        if (a[p][q] == 0) continue;
+        double theta = (a[q][q] - a[p][p]) / (2 * a[p][q]);
+        double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+        double c = 1 / sqrt(t * t + 1), s = t * c;
+        for (int k = 0; k < 3; k++) {
+          double akp = a[k][p], akq = a[k][q];
+          a[k][p] = c * akp - s * akq;
+          a[k][q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < 3; k++) {
+          double apk = a[p][k], aqk = a[q][k];
+          a[p][k] = c * apk - s * aqk;
+          a[q][k] = s * apk + c * aqk;
+        }
+      }
+  }
+  double e0 = fmax(a[0][0], 0.0), e1 = fmax(a[1][1], 0.0), e2 = fmax(a[2][2], 0.0);
+  // sort descending
+  double t;
+  if (e0 < e1) { t = e0; e0 = e1; e1 = t; }
+  if (e1 < e2) { t = e1; e1 = e2; e2 = t; }
+  if (e0 < e1) { t = e0; e0 = e1; e1 = t; }
+  sv[0] = sqrt(e0);
+  sv[1] = sqrt(e1);
+  sv[2] = sqrt(e2);
+}
+
+// camera pose of clone slot s in camera k (UpdaterMSCKF.cpp:98-115): R_GtoCi, p_CiinG
+__device__ __forceinline__ void clone_cam_pose(const DClone &c, const DCam &k, double *R_GtoCi, double *p_CiinG) {
+  m3_mul(k.R_ItoC, c.R, R_GtoCi);
+  double t[3];
+  m3t_vec(R_GtoCi, k.p_IinC, t);
+  for (int i = 0; i < 3; i++) p_CiinG[i] = c.p[i] - t[i];
+}
+
+// per-lane LM terms (FeatureInitializer.cpp:241-271): returns H (2x3) and float residual
+__device__ __forceinline__ void lm_terms(const double *R_AtoCi, const double *p_AinCi, double alpha, double beta,
+                                         double rho, float un, float vn, double *H, double *res) {
+  double hi1 = R_AtoCi[0] * alpha + R_AtoCi[1] * beta + R_AtoCi[2] + rho * p_AinCi[0];
+  double hi2 = R_AtoCi[3] * alpha + R_AtoCi[4] * beta + R_AtoCi[5] + rho * p_AinCi[1];
+  double hi3 = R_AtoCi[6] * alpha + R_AtoCi[7] * beta + R_AtoCi[8] + rho * p_AinCi[2];
+  double h3s = hi3 * hi3;
+  if (H) {
+    H[0] = (R_AtoCi[0] * hi3 - hi1 * R_AtoCi[6]) / h3s;
+    H[1] = (R_AtoCi[1] * hi3 - hi1 * R_AtoCi[7]) / h3s;
+    H[2] = (p_AinCi[0] * hi3 - hi1 * p_AinCi[2]) / h3s;
+    H[3] = (R_AtoCi[3] * hi3 - hi2 * R_AtoCi[6]) / h3s;
+    H[4] = (R_AtoCi[4] * hi3 - hi2 * R_AtoCi[7]) / h3s;
+    H[5] = (p_AinCi[1] * hi3 - hi2 * p_AinCi[2]) / h3s;
+  }
+  float z1 = (float)(hi1 / hi3), z2 = (float)(hi2 / hi3);
+  float r1 = un - z1, r2 = vn - z2;
+  res[0] = (double)r1;
+  res[1] = (double)r2;
+}
+__device__ __forceinline__ double lm_err(const double *R_AtoCi, const double *p_AinCi, double alpha, double beta,
+                                         double rho, float un, float vn) {
+  double hi1 = R_AtoCi[0] * alpha + R_AtoCi[1] * beta + R_AtoCi[2] + rho * p_AinCi[0];
+  double hi2 = R_AtoCi[3] * alpha + R_AtoCi[4] * beta + R_AtoCi[5] + rho * p_AinCi[1];
+  double hi3 = R_AtoCi[6] * alpha + R_AtoCi[7] * beta + R_AtoCi[8] + rho * p_AinCi[2];
+  float z1 = (float)(hi1 / hi3), z2 = (float)(hi2 / hi3);
+  float r1 = un - z1, r2 = vn - z2;
+  float nrm = sqrtf(r1 * r1 + r2 * r2);
+  double dn = (double)nrm;
+  return dn * dn;
+}
+
+struct FeatShared {
+  double p_FinA[3], p_FinG[3], p_FinA_fej[3], p_FinG_fej[3];
+  int status;
+  int nrows_out;
+  double beta[3];
+  double chi2;
+};
+
+// LDS layout helper (doubles)
+__host__ __device__ inline size_t feat_lds_doubles(int max_meas, int max_nf) {
+  int rows = 2 * max_meas;
+  size_t n = 0;
+  n += (size_t)rows * (max_nf + 1);  // Hl
+  n += (size_t)rows * 3;             // Hf
+  n += (size_t)rows * 3;             // V (Householder vectors)
+  n += (size_t)(rows + 1) * (rows + 1);  // S augmented
+  n += (size_t)16 * max_nf;          // T chunk
+  n += (size_t)max_nf;               // loc2pid (as double-size slots for alignment)
+  n += 64;                           // scratch
+  return n;
+}
+size_t feature_lds_bytes(int max_meas, int max_nf) { return feat_lds_doubles(max_meas, max_nf) * sizeof(double); }
+
+__global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *__restrict__ feats,
+                                                 const DMeas *__restrict__ meas, const DVar *__restrict__ vars,
+                                                 const DClone *__restrict__ clones, const DCam *__restrict__ cams,
+                                                 const double *__restrict__ P, const double *__restrict__ chi2_table,
+                                                 double *__restrict__ H_all, DFeatOut *__restrict__ out, int max_meas,
+                                                 int max_nf) {
+  extern __shared__ double lds[];
+  __shared__ FeatShared sh;
+  __shared__ int canon2loc[512];
+  const int f = blockIdx.x;
+  const DFeat F = feats[f];
+  const int m = F.nmeas, rows = 2 * m, nf = F.nf, ldl = nf + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const DMeas *Ms = meas + F.meas_off;
+
+  double *Hl = lds;
+  double *Hf = Hl + (size_t)2 * max_meas * (max_nf + 1);
+  double *V = Hf + 2 * max_meas * 3;
+  double *S = V + 2 * max_meas * 3;
+  double *Tc = S + (size_t)(2 * max_meas + 1) * (2 * max_meas + 1);
+  int *loc2pid = (int *)(Tc + 16 * max_nf);
+
+  // ---- setup: column maps, zero the local Jacobian ----
+  for (int j = tid; j <= bp.n_canon; j += 256) canon2loc[j] = -1;
+  for (int e = tid; e < rows * ldl; e += 256) Hl[e] = 0.0;
+  __syncthreads();
+  for (int v = 0; v < F.nvar; v++) {
+    DVar dv = vars[F.var_off + v];
+    for (int k = tid; k < dv.size; k += 256) {
+      loc2pid[dv.loc + k] = dv.pid + k;
+      if (dv.canon >= 0) canon2loc[dv.canon + k] = dv.loc + k;
+    }
+  }
+  if (tid == 0) {
+    sh.status = 0;
+    for (int k = 0; k < 3; k++) {
+      sh.p_FinA[k] = F.p_in[k];
+      sh.p_FinA_fej[k] = F.p_in_fej[k];
+      sh.p_FinG[k] = (F.mode == 3) ? F.p_in_fej[k] : F.p_in[k];
+      sh.p_FinG_fej[k] = F.p_in_fej[k];
+      if (F.mode == 3) sh.p_FinA_fej[k] = F.p_in[k];
+    }
+  }
+  __syncthreads();
+
+  // ---- geometry (wave 0): triangulation + Levenberg-Marquardt (MSCKF / delayed init only) ----
+  if ((F.mode == 0 || F.mode == 2) && wave == 0) {
+    const DClone &ca = clones[F.anchor_slot];
+    const DCam &ka = cams[F.anchor_cam];
+    double R_GtoA[9], p_AinG[3];
+    clone_cam_pose(ca, ka, R_GtoA, p_AinG);
+    double R_AtoCi[9] = {0}, p_CiinA[3] = {0, 0, 0}, p_AinCi[3] = {0, 0, 0};
+    float un = 0.f, vn = 0.f;
+    bool act = lane < m;
+    if (act) {
+      const DMeas &mm = Ms[lane];
+      double R_GtoCi[9], p_CiinG[3];
+      clone_cam_pose(clones[mm.slot], cams[mm.cam], R_GtoCi, p_CiinG);
+      m3_mul_bt(R_GtoCi, R_GtoA, R_AtoCi);
+      double d[3] = {p_CiinG[0] - p_AinG[0], p_CiinG[1] - p_AinG[1], p_CiinG[2] - p_AinG[2]};
+      m3_vec(R_GtoA, d, p_CiinA);
+      double t[3];
+      m3_vec(R_AtoCi, p_CiinA, t);
+      p_AinCi[0] = -t[0];
+      p_AinCi[1] = -t[1];
+      p_AinCi[2] = -t[2];
+      un = mm.un;
+      vn = mm.vn;
+    }
+    // linear triangulation
+    double Ai[6] = {0, 0, 0, 0, 0, 0}, bi[3] = {0, 0, 0};
+    if (act) {
+      double b0[3] = {(double)un, (double)vn, 1.0}, b[3];
+      m3t_vec(R_AtoCi, b0, b);
+      double nb = norm3(b);
+      b[0] /= nb; b[1] /= nb; b[2] /= nb;
+      double Bp[9], A9[9];
+      skew(b, Bp);
+      m3_mul_at(Bp, Bp, A9);
+      Ai[0] = A9[0]; Ai[1] = A9[1]; Ai[2] = A9[2]; Ai[3] = A9[4]; Ai[4] = A9[5]; Ai[5] = A9[8];
+      m3_vec(A9, p_CiinA, bi);
+    }
+    double A[9], bb[3];
+    {
+      double s0 = wave_sum(Ai[0]), s1 = wave_sum(Ai[1]), s2 = wave_sum(Ai[2]);
+      double s3 = wave_sum(Ai[3]), s4 = wave_sum(Ai[4]), s5 = wave_sum(Ai[5]);
+      A[0] = s0; A[1] = s1; A[2] = s2; A[3] = s1; A[4] = s3; A[5] = s4; A[6] = s2; A[7] = s4; A[8] = s5;
+      bb[0] = wave_sum(bi[0]);
+      bb[1] = wave_sum(bi[1]);
+      bb[2] = wave_sum(bi[2]);
+    }
+    double pf[3];
+    colpiv_solve3(A, bb, pf);
+    double sv[3];
+    singular_values3(A, sv);
+    double condA = sv[0] / sv[2];
+    int st = 0;
+    double npf = norm3(pf);
+    if (fabs(condA) > bp.fi_max_cond || pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || isnan(npf)) st = 1;
+    if (st == 0 && bp.fi_refine) {
+      double rho = 1 / pf[2], alpha = pf[0] / pf[2], beta = pf[1] / pf[2];
+      double lam = bp.fi_init_lamda, eps = 10000;
+      int runs = 0;
+      bool recompute = true;
+      double Hs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+      double cost_old = wave_sum(act ? lm_err(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn) : 0.0);
+      while (runs < bp.fi_max_runs && lam < bp.fi_max_lamda && eps > bp.fi_min_dx) {
+        if (recompute) {
+          double h[6] = {0, 0, 0, 0, 0, 0}, gg[3] = {0, 0, 0};
+          if (act) {
+            double H[6], r[2];
+            lm_terms(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn, H, r);
+            // H^T H (upper 6) and H^T r
+            h[0] = H[0] * H[0] + H[3] * H[3];
+            h[1] = H[0] * H[1] + H[3] * H[4];
+            h[2] = H[0] * H[2] + H[3] * H[5];
+            h[3] = H[1] * H[1] + H[4] * H[4];
+            h[4] = H[1] * H[2] + H[4] * H[5];
+            h[5] = H[2] * H[2] + H[5] * H[5];
+            gg[0] = H[0] * r[0] + H[3] * r[1];
+            gg[1] = H[1] * r[0] + H[4] * r[1];
+            gg[2] = H[2] * r[0] + H[5] * r[1];
+          }
+          for (int k = 0; k < 6; k++) Hs[k] = wave_sum(h[k]);
+          for (int k = 0; k < 3; k++) g[k] = wave_sum(gg[k]);
+        }
+        double Hl3[9] = {Hs[0], Hs[1], Hs[2], Hs[1], Hs[3], Hs[4], Hs[2], Hs[4], Hs[5]};
+        Hl3[0] *= (1.0 + lam);
+        Hl3[4] *= (1.0 + lam);
+        Hl3[8] *= (1.0 + lam);
+        double dx[3];
+        colpiv_solve3(Hl3, g, dx);
+        double cost = wave_sum(act ? lm_err(R_AtoCi, p_AinCi, alpha + dx[0], beta + dx[1], rho + dx[2], un, vn) : 0.0);
+        if (cost <= cost_old && (cost_old - cost) / cost_old < bp.fi_min_dcost) {
+          alpha += dx[0];
+          beta += dx[1];
+          rho += dx[2];
+          eps = 0;
+          break;
+        }
+        if (cost <= cost_old) {
+          recompute = true;
+          cost_old = cost;
+          alpha += dx[0];
+          beta += dx[1];
+          rho += dx[2];
+          runs++;
+          lam = lam / bp.fi_lam_mult;
+          eps = sqrt(dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2]);
+        } else {
+          recompute = false;
+          lam = lam * bp.fi_lam_mult;
+          continue;
+        }
+      }
+      pf[0] = alpha / rho;
+      pf[1] = beta / rho;
+      pf[2] = 1 / rho;
+      double np = norm3(pf);
+      double vh[3] = {pf[0] / np, pf[1] / np, pf[2] / np};
+      double bl = 0.0;
+      if (act) {
+        double dd = dot3(p_CiinA, vh);
+        double perp[3] = {p_CiinA[0] - dd * vh[0], p_CiinA[1] - dd * vh[1], p_CiinA[2] - dd * vh[2]};
+        bl = norm3(perp);
+      }
+      double base_line_max = wave_max(bl);
+      if (pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || (np / base_line_max) > bp.fi_max_baseline || isnan(np))
+        st = 2;
+    }
+    if (lane == 0) {
+      sh.status = st;
+      double pG[3];
+      m3t_vec(R_GtoA, pf, pG);
+      for (int k = 0; k < 3; k++) {
+        sh.p_FinA[k] = pf[k];
+        sh.p_FinA_fej[k] = pf[k];
+        sh.p_FinG[k] = pG[k] + p_AinG[k];
+        sh.p_FinG_fej[k] = sh.p_FinG[k];
+      }
+    }
+  }
+  __syncthreads();
+  const int status0 = sh.status;
+
+  // ---- Jacobians (one thread per measurement) ----
+  if (status0 == 0 && tid < m) {
+    const DMeas &mm = Ms[tid];
+    const DClone &cl = clones[mm.slot];
+    const DCam &ck = cams[mm.cam];
+    const bool rel = (F.rep == 2 || F.rep == 3 || F.rep == 4 || F.rep == 5);
+    double p_FinG[3], p_FinG_fej[3];
+    // representation Jacobian (UpdaterHelper.cpp:32-190) and anchor terms
+    double dl[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // dpfg_dlambda
+    double Hanc[18], Hcal[18];                   // 3x6 each
+    int ncolf = (F.rep == 5) ? 1 : 3;
+    if (!rel) {
+      for (int k = 0; k < 3; k++) {
+        p_FinG[k] = sh.p_FinG[k];
+        p_FinG_fej[k] = sh.p_FinG_fej[k];
+      }
+      if (F.rep == 1) {  // GLOBAL_FULL_INVERSE_DEPTH
+        const double *pg = bp.do_fej ? p_FinG_fej : p_FinG;
+        double g_rho = 1 / norm3(pg), g_phi = acos(g_rho * pg[2]), g_theta = atan2(pg[1], pg[0]);
+        double sth = sin(g_theta), cth = cos(g_theta), sph = sin(g_phi), cph = cos(g_phi), rho = g_rho;
+        dl[0] = -(1.0 / rho) * sth * sph; dl[1] = (1.0 / rho) * cth * cph; dl[2] = -(1.0 / (rho * rho)) * cth * sph;
+        dl[3] = (1.0 / rho) * cth * sph;  dl[4] = (1.0 / rho) * sth * cph; dl[5] = -(1.0 / (rho * rho)) * sth * sph;
+        dl[6] = 0.0; dl[7] = -(1.0 / rho) * sph; dl[8] = -(1.0 / (rho * rho)) * cph;
+      }
+    } else {
+      const DClone &an = clones[F.anchor_slot];
+      const DCam &ak = cams[F.anchor_cam];
+      const double *pA = sh.p_FinA;
+      // p_FinG = R_GtoI^T R_ItoC^T (p_FinA - p_IinC) + p_IinG (UpdaterHelper.cpp:271-283)
+      double d0[3] = {pA[0] - ak.p_IinC[0], pA[1] - ak.p_IinC[1], pA[2] - ak.p_IinC[2]}, t1[3], t2[3];
+      m3t_vec(ak.R_ItoC, d0, t1);
+      m3t_vec(an.R, t1, t2);
+      for (int k = 0; k < 3; k++) {
+        p_FinG[k] = t2[k] + an.p[k];
+        p_FinG_fej[k] = p_FinG[k];
+      }
+      double R_GtoI[9], p_IinG[3], pFA[3];
+      for (int k = 0; k < 9; k++) R_GtoI[k] = an.R[k];
+      for (int k = 0; k < 3; k++) {
+        p_IinG[k] = an.p[k];
+        pFA[k] = pA[k];
+      }
+      if (bp.do_fej) {
+        for (int k = 0; k < 9; k++) R_GtoI[k] = an.Rf[k];
+        for (int k = 0; k < 3; k++) p_IinG[k] = an.pf[k];
+        // p_FinA = (R_GtoI^T R_ItoC^T)^T (p_FinG_best - p_IinG) + p_IinC
+        double RCG[9], RCG_T[9], dd[3], tt[3];
+        double RIT[9], RCT[9];
+        m3_transpose(R_GtoI, RIT);
+        m3_transpose(ak.R_ItoC, RCT);
+        m3_mul(RIT, RCT, RCG);
+        m3_transpose(RCG, RCG_T);
+        for (int k = 0; k < 3; k++) dd[k] = p_FinG[k] - p_IinG[k];
+        m3_vec(RCG_T, dd, tt);
+        for (int k = 0; k < 3; k++) pFA[k] = tt[k] + ak.p_IinC[k];
+      }
+      double RIT[9], RCT[9], R_CtoG[9];
+      m3_transpose(R_GtoI, RIT);
+      m3_transpose(ak.R_ItoC, RCT);
+      m3_mul(RIT, RCT, R_CtoG);
+      // H_anc = [-R_GtoI^T skew(R_ItoC^T (p_FinA - p_IinC)), I]
+      double dd[3] = {pFA[0] - ak.p_IinC[0], pFA[1] - ak.p_IinC[1], pFA[2] - ak.p_IinC[2]}, w[3], Sk[9], Tm[9];
+      m3t_vec(ak.R_ItoC, dd, w);
+      skew(w, Sk);
+      m3_mul(RIT, Sk, Tm);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          Hanc[6 * i + j] = -Tm[3 * i + j];
+          Hanc[6 * i + 3 + j] = (i == j) ? 1.0 : 0.0;
+        }
+      // H_calib = [-R_CtoG skew(p_FinA - p_IinC), -R_CtoG]
+      skew(dd, Sk);
+      m3_mul(R_CtoG, Sk, Tm);
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          Hcal[6 * i + j] = -Tm[3 * i + j];
+          Hcal[6 * i + 3 + j] = -R_CtoG[3 * i + j];
+        }
+      if (F.rep == 2) {
+        for (int k = 0; k < 9; k++) dl[k] = R_CtoG[k];
+      } else if (F.rep == 4 || F.rep == 5) {
+        double alpha = pFA[0] / pFA[2], beta = pFA[1] / pFA[2], rho = 1 / pFA[2];
+        double d[9] = {1.0 / rho, 0.0, -(1.0 / (rho * rho)) * alpha, 0.0, 1.0 / rho, -(1.0 / (rho * rho)) * beta,
+                       0.0, 0.0, -(1.0 / (rho * rho))};
+        if (F.rep == 4) {
+          m3_mul(R_CtoG, d, dl);
+        } else {
+          double bear[3] = {rho * pFA[0], rho * pFA[1], rho * pFA[2]};
+          double dr[3] = {-(1.0 / (rho * rho)) * bear[0], -(1.0 / (rho * rho)) * bear[1], -(1.0 / (rho * rho)) * bear[2]};
+          double o[3];
+          m3_vec(R_CtoG, dr, o);
+          dl[0] = o[0]; dl[3] = o[1]; dl[6] = o[2];
+        }
+      } else if (F.rep == 3) {
+        double a_rho = 1 / norm3(pFA), a_phi = acos(a_rho * pFA[2]), a_theta = atan2(pFA[1], pFA[0]);
+        double sth = sin(a_theta), cth = cos(a_theta), sph = sin(a_phi), cph = cos(a_phi), rho = a_rho;
+        double d[9] = {-(1.0 / rho) * sth * sph, (1.0 / rho) * cth * cph, -(1.0 / (rho * rho)) * cth * sph,
+                       (1.0 / rho) * cth * sph,  (1.0 / rho) * sth * cph, -(1.0 / (rho * rho)) * sth * sph,
+                       0.0, -(1.0 / rho) * sph, -(1.0 / (rho * rho)) * cph};
+        m3_mul(R_CtoG, d, dl);
+      }
+    }
+    // measurement model (UpdaterHelper.cpp:310-404)
+    double R_GtoIi[9], p_IiinG[3];
+    for (int k = 0; k < 9; k++) R_GtoIi[k] = cl.R[k];
+    for (int k = 0; k < 3; k++) p_IiinG[k] = cl.p[k];
+    double d1[3] = {p_FinG[0] - p_IiinG[0], p_FinG[1] - p_IiinG[1], p_FinG[2] - p_IiinG[2]}, p_FinIi[3], p_FinCi[3];
+    m3_vec(R_GtoIi, d1, p_FinIi);
+    m3_vec(ck.R_ItoC, p_FinIi, p_FinCi);
+    for (int k = 0; k < 3; k++) p_FinCi[k] += ck.p_IinC[k];
+    double xn = p_FinCi[0] / p_FinCi[2], yn = p_FinCi[1] / p_FinCi[2];
+    float ud, vd;
+    cam_distort_f(ck.cam, (float)xn, (float)yn, ud, vd);
+    double res0 = (double)mm.u - (double)ud, res1 = (double)mm.v - (double)vd;
+    if (bp.do_fej) {
+      for (int k = 0; k < 9; k++) R_GtoIi[k] = cl.Rf[k];
+      for (int k = 0; k < 3; k++) p_IiinG[k] = cl.pf[k];
+      double d2[3] = {p_FinG_fej[0] - p_IiinG[0], p_FinG_fej[1] - p_IiinG[1], p_FinG_fej[2] - p_IiinG[2]};
+      m3_vec(R_GtoIi, d2, p_FinIi);
+      m3_vec(ck.R_ItoC, p_FinIi, p_FinCi);
+      for (int k = 0; k < 3; k++) p_FinCi[k] += ck.p_IinC[k];
+    }
+    double dzn[4], dzeta[16];
+    cam_distort_jac(ck.cam, xn, yn, dzn, dzeta);
+    double iz = 1 / p_FinCi[2];
+    double dzn_dpfc[6] = {iz, 0, -p_FinCi[0] / (p_FinCi[2] * p_FinCi[2]), 0, iz, -p_FinCi[1] / (p_FinCi[2] * p_FinCi[2])};
+    double dpfc_dpfg[9];
+    m3_mul(ck.R_ItoC, R_GtoIi, dpfc_dpfg);
+    double Sk[9], RS[9];
+    skew(p_FinIi, Sk);
+    m3_mul(ck.R_ItoC, Sk, RS);
+    double dz_dpfc[6];  // 2x3
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 3; j++) dz_dpfc[3 * i + j] = dzn[2 * i] * dzn_dpfc[j] + dzn[2 * i + 1] * dzn_dpfc[3 + j];
+    double dz_dpfg[6];
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 3; j++)
+        dz_dpfg[3 * i + j] = dz_dpfc[3 * i] * dpfc_dpfg[j] + dz_dpfc[3 * i + 1] * dpfc_dpfg[3 + j] +
+                             dz_dpfc[3 * i + 2] * dpfc_dpfg[6 + j];
+    for (int i = 0; i < 2; i++) {
+      double *row = Hl + (size_t)(2 * tid + i) * ldl;
+      double *hf = Hf + (2 * tid + i) * 3;
+      // H_f = dz_dpfg * dpfg_dlambda
+      for (int j = 0; j < ncolf; j++)
+        hf[j] = dz_dpfg[3 * i] * dl[j] + dz_dpfg[3 * i + 1] * dl[3 + j] + dz_dpfg[3 * i + 2] * dl[6 + j];
+      for (int j = ncolf; j < 3; j++) hf[j] = 0.0;
+      // clone block: dz_dpfc * [R_ItoC skew(p_FinIi), -dpfc_dpfg]
+      for (int j = 0; j < 3; j++) {
+        row[mm.lc_clone + j] =
+            dz_dpfc[3 * i] * RS[j] + dz_dpfc[3 * i + 1] * RS[3 + j] + dz_dpfc[3 * i + 2] * RS[6 + j];
+        row[mm.lc_clone + 3 + j] = -(dz_dpfc[3 * i] * dpfc_dpfg[j] + dz_dpfc[3 * i + 1] * dpfc_dpfg[3 + j] +
+                                     dz_dpfc[3 * i + 2] * dpfc_dpfg[6 + j]);
+      }
+      if (rel) {
+        for (int j = 0; j < 6; j++)
+          row[F.lc_anchor_clone + j] +=
+              dz_dpfg[3 * i] * Hanc[j] + dz_dpfg[3 * i + 1] * Hanc[6 + j] + dz_dpfg[3 * i + 2] * Hanc[12 + j];
+        if (bp.calib_ext)
+          for (int j = 0; j < 6; j++)
+            row[F.lc_anchor_ext + j] +=
+                dz_dpfg[3 * i] * Hcal[j] + dz_dpfg[3 * i + 1] * Hcal[6 + j] + dz_dpfg[3 * i + 2] * Hcal[12 + j];
+      }
+      if (bp.calib_ext && mm.lc_ext >= 0) {
+        double pc[3] = {p_FinCi[0] - ck.p_IinC[0], p_FinCi[1] - ck.p_IinC[1], p_FinCi[2] - ck.p_IinC[2]}, Sc[9];
+        skew(pc, Sc);
+        for (int j = 0; j < 3; j++) {
+          row[mm.lc_ext + j] += dz_dpfc[3 * i] * Sc[j] + dz_dpfc[3 * i + 1] * Sc[3 + j] + dz_dpfc[3 * i + 2] * Sc[6 + j];
+          row[mm.lc_ext + 3 + j] += dz_dpfc[3 * i + j];
+        }
+      }
+      if (bp.calib_intr && mm.lc_intr >= 0)
+        for (int j = 0; j < 8; j++) row[mm.lc_intr + j] = dzeta[8 * i + j];
+      row[nf] = (i == 0) ? res0 : res1;
+      // SLAM update: landmark columns hold H_f (UpdaterSLAM.cpp:355-358)
+      if (F.mode == 1)
+        for (int j = 0; j < ncolf; j++) row[F.lm_loc + j] = hf[j];
+    }
+  }
+  __syncthreads();
+
+  // ---- left-nullspace projection: 3 Householder reflections of H_f (MSCKF) ----
+  int r0 = 0;  // first output row in Hl
+  if (status0 == 0 && F.mode != 1) {
+    for (int c = 0; c < 3; c++) {
+      if (wave == 0) {
+        // v = x - alpha e_c over rows c..rows-1
+        double ss = 0.0;
+        for (int i = c + lane; i < rows; i += 64) {
+          double x = Hf[i * 3 + c];
+          ss += x * x;
+        }
+        ss = wave_sum(ss);
+        double x0 = Hf[c * 3 + c];
+        double alpha = (x0 > 0) ? -sqrt(ss) : sqrt(ss);
+        for (int i = c + lane; i < rows; i += 64) V[i * 3 + c] = (i == c) ? (x0 - alpha) : Hf[i * 3 + c];
+        double vn = ss - x0 * x0 + (x0 - alpha) * (x0 - alpha);
+        if (lane == 0) sh.beta[c] = (vn > 0) ? 2.0 / vn : 0.0;
+      }
+      __syncthreads();
+      double b = sh.beta[c];
+      // apply to Hf columns c+1..2 and all Hl columns
+      int ncols_tot = (3 - c - 1) + ldl;
+      for (int j = tid; j < ncols_tot; j += 256) {
+        bool isf = j < (3 - c - 1);
+        double *colp;
+        int stride;
+        if (isf) {
+          colp = Hf + (c + 1 + j);
+          stride = 3;
+        } else {
+          colp = Hl + (j - (3 - c - 1));
+          stride = ldl;
+        }
+        double s = 0.0;
+        for (int i = c; i < rows; i++) s += V[i * 3 + c] * colp[(size_t)i * stride];
+        s *= b;
+        for (int i = c; i < rows; i++) colp[(size_t)i * stride] -= s * V[i * 3 + c];
+      }
+      __syncthreads();
+    }
+    r0 = 3;
+  }
+  const int R = rows - r0;
+
+  // ---- chi2: S = Hhat P_marg Hhat^T + s2 I, augmented with the residual row ----
+  if (status0 == 0 && R > 0) {
+    const int ldS = R + 1;
+    for (int i0 = 0; i0 < R; i0 += 16) {
+      int nr = min(16, R - i0);
+      // Tc[ii][d] = sum_c Hhat[i0+ii][c] * P[pid(d)][pid(c)]
+      for (int e = tid; e < nr * nf; e += 256) {
+        int ii = e / nf, d = e % nf;
+        const double *hrow = Hl + (size_t)(r0 + i0 + ii) * ldl;
+        const double *Prow = P + (size_t)loc2pid[d] * bp.ldp;
+        double acc = 0.0;
+        for (int c = 0; c < nf; c++) acc += hrow[c] * Prow[loc2pid[c]];
+        Tc[ii * nf + d] = acc;
+      }
+      __syncthreads();
+      for (int e = tid; e < nr * R; e += 256) {
+        int ii = e / R, j = e % R;
+        const double *hrow = Hl + (size_t)(r0 + j) * ldl;
+        double acc = 0.0;
+        for (int d = 0; d < nf; d++) acc += Tc[ii * nf + d] * hrow[d];
+        if (i0 + ii == j) acc += bp.sigma_pix_sq;
+        S[(i0 + ii) * ldS + j] = acc;
+      }
+      __syncthreads();
+    }
+    // residual row
+    for (int j = tid; j < R; j += 256) S[R * ldS + j] = Hl[(size_t)(r0 + j) * ldl + nf];
+    __syncthreads();
+    // lower Cholesky of the augmented matrix; last row becomes y = L^-1 r
+    for (int k = 0; k < R; k++) {
+      if (tid == 0) S[k * ldS + k] = sqrt(S[k * ldS + k]);
+      __syncthreads();
+      double dkk = S[k * ldS + k];
+      for (int i = k + 1 + tid; i <= R; i += 256) S[i * ldS + k] /= dkk;
+      __syncthreads();
+      int mm2 = R - k;  // rows k+1..R
+      for (int e = tid; e < mm2 * mm2; e += 256) {
+        int i = k + 1 + e / mm2, j = k + 1 + e % mm2;
+        if (j <= i && j < R) S[i * ldS + j] -= S[i * ldS + k] * S[j * ldS + k];
+      }
+      __syncthreads();
+    }
+    if (wave == 0) {
+      double c2 = 0.0;
+      for (int k = lane; k < R; k += 64) {
+        double y = S[R * ldS + k];
+        c2 += y * y;
+      }
+      c2 = wave_sum(c2);
+      if (lane == 0) {
+        sh.chi2 = c2;
+        // delayed init tests the update rows against chi2(dof = all rows) (StateHelper.cpp:463-468)
+        double thr = chi2_table[min(F.mode >= 2 ? rows : R, 999)];
+        if (c2 > bp.chi2_mult * thr) sh.status = 3;
+      }
+    }
+    __syncthreads();
+  }
+  const int status = sh.status;
+
+  // ---- output rows (canonical dense columns; zeros when rejected) ----
+  const int out_r0 = (F.mode == 0) ? 3 : 0;
+  const int nrows_out = max(rows - out_r0, 0);
+  for (int e = tid; e < nrows_out * (bp.n_canon + 1); e += 256) {
+    int i = e / (bp.n_canon + 1), j = e % (bp.n_canon + 1);
+    double v = 0.0;
+    if (status == 0) {
+      int lc = (j == bp.n_canon) ? nf : canon2loc[j];
+      if (lc >= 0) v = Hl[(size_t)(out_r0 + i) * ldl + lc];
+    }
+    H_all[(size_t)(F.row_off + i) * bp.ldh + j] = v;
+  }
+  if (tid == 0) {
+    DFeatOut o;
+    for (int k = 0; k < 3; k++) {
+      o.p_FinA[k] = sh.p_FinA[k];
+      o.p_FinG[k] = sh.p_FinG[k];
+    }
+    o.chi2 = (status0 == 0) ? sh.chi2 : -1.0;
+    for (int k = 0; k < 9; k++) o.HfR[k] = (F.mode >= 2 && status0 == 0) ? Hf[(k / 3) * 3 + (k % 3)] : 0.0;
+    o.status = status;
+    o.rows = status == 0 ? nrows_out : 0;
+    out[f] = o;
+  }
+}
+
+void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const DMeas *meas,
+                              const DVar *vars, const DClone *clones, const DCam *cams, const double *P,
+                              const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf) {
+  if (bp.nfeat <= 0) return;
+  size_t bytes = feature_lds_bytes(max_meas, max_nf);
+  hipLaunchKernelGGL(k_feature, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, meas, vars, clones, cams, P,
+                     chi2_table, H_all, out, max_meas, max_nf);
+}
+
+}  // namespace uvhp

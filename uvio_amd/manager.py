@@ -1,0 +1,176 @@
+"""Python mirror of the reference manager surface (ov_msckf::VioManager / uvio::UVioManager).
+
+Method names follow the reference C++ API (VioManager.h:75-111, UVioManager.h:48-73):
+``feed_measurement_imu``, ``feed_measurement_simulation``, ``feed_measurement_uwb``,
+``try_to_initialize_uwb_anchors``, ``initialize_with_gt``, ``initialized``, ``get_state`` ...
+Every call goes through the C ABI of libuvio_hp.so (include/uvio_hp.h); the estimator state and the
+covariance live on the MI355X.  Errors the reference would turn into ``std::exit`` raise here.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+def load_options(yaml_path=None, **overrides):
+    """VioManagerOptions::print_and_load equivalent: defaults, then the YAML keys, then overrides."""
+    lib = N.load()
+    opts = N.Options()
+    N.check(lib.uvio_hp_options_default(C.byref(opts)), what="options_default")
+    if yaml_path is not None:
+        N.check(lib.uvio_hp_options_load(yaml_path.encode(), C.byref(opts)), what="options_load(%s)" % yaml_path)
+    apply_overrides(opts, overrides)
+    return opts
+
+
+def apply_overrides(opts, overrides):
+    for k, v in overrides.items():
+        if not hasattr(opts, k):
+            raise KeyError(k)
+        setattr(opts, k, v)
+    return opts
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class VioManager:
+    """Handle on one estimator instance (one MI355X device)."""
+
+    _prefix = "uvio_hp_"
+
+    def __init__(self, options, device=0):
+        self._lib = self._load()
+        self._h = C.c_void_p()
+        rc = self._call("create", C.byref(options), device, C.byref(self._h)) if self._prefix == "uvio_hp_" else \
+            self._call("create", C.byref(options), C.byref(self._h))
+        if rc != 0:
+            raise RuntimeError("%screate failed: %s" % (self._prefix, N.ERRNAMES.get(rc, rc)))
+        self.options = options
+
+    @classmethod
+    def _load(cls):
+        return N.load()
+
+    def _call(self, name, *args):
+        return getattr(self._lib, self._prefix + name)(*args)
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = ""
+            if self._prefix == "uvio_hp_":
+                msg = (self._lib.uvio_hp_last_error(self._h) or b"").decode()
+            raise RuntimeError("%s failed: %s %s" % (what, N.ERRNAMES.get(rc, rc), msg))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._call("destroy", self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ---- feeds ----
+    def initialize_with_gt(self, imustate17):
+        x = np.ascontiguousarray(imustate17, dtype=np.float64)
+        assert x.shape == (17,)
+        self._check(self._call("initialize_with_gt", self._h, _dp(x)), "initialize_with_gt")
+
+    def feed_measurement_imu(self, t, wm, am):
+        w = (C.c_double * 3)(*wm)
+        a = (C.c_double * 3)(*am)
+        self._check(self._call("feed_imu", self._h, C.c_double(t), w, a), "feed_measurement_imu")
+
+    def feed_measurement_simulation(self, t, camids, feats, allow_uninit=False):
+        """feats[i] = (ids uint64[n], uv float32[n,2]) for camera camids[i] (TrackSIM input)."""
+        ncam = len(camids)
+        cam = (C.c_int * ncam)(*camids)
+        cnt = (C.c_int * ncam)(*[len(f[0]) for f in feats])
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(f[0], dtype=np.uint64) for f in feats]))
+        uv = np.ascontiguousarray(np.concatenate([np.asarray(f[1], dtype=np.float32).reshape(-1, 2) for f in feats]))
+        rc = self._call("feed_simulation", self._h, C.c_double(t), ncam, cam, cnt,
+                        ids.ctypes.data_as(C.POINTER(C.c_uint64)), uv.ctypes.data_as(C.POINTER(C.c_float)))
+        if rc == N.E_STATE and allow_uninit:
+            return rc
+        self._check(rc, "feed_measurement_simulation")
+        return rc
+
+    def feed_measurement_uwb(self, t, anchor_ids, ranges):
+        n = len(anchor_ids)
+        ids = (C.c_uint64 * n)(*anchor_ids)
+        r = (C.c_double * n)(*ranges)
+        self._check(self._call("feed_uwb", self._h, C.c_double(t), n, ids, r), "feed_measurement_uwb")
+
+    def try_to_initialize_uwb_anchors(self, anchors):
+        n = len(anchors)
+        arr = (N.Anchor * max(n, 1))(*anchors)
+        self._check(self._call("init_anchors", self._h, n, arr), "try_to_initialize_uwb_anchors")
+
+    # ---- getters ----
+    def get_imu_state(self):
+        t = C.c_double()
+        out = np.zeros(16)
+        self._check(self._call("get_imu_state", self._h, C.byref(t), _dp(out)), "get_imu_state")
+        return t.value, out
+
+    def cov_dim(self):
+        n = C.c_int()
+        self._check(self._call("get_cov_dim", self._h, C.byref(n)), "get_cov_dim")
+        return n.value
+
+    def get_cov(self):
+        n = self.cov_dim()
+        P = np.zeros((n, n))
+        self._check(self._call("get_cov", self._h, _dp(P), n), "get_cov")
+        return P
+
+    def get_state_vector(self):
+        cap = 4096
+        out = np.zeros(cap)
+        meta = np.zeros(3 * 1024, dtype=np.int32)
+        ln, nv = C.c_int(), C.c_int()
+        self._check(self._call("get_state_vector", self._h, _dp(out), cap, C.byref(ln),
+                               meta.ctypes.data_as(C.POINTER(C.c_int)), meta.size, C.byref(nv)), "get_state_vector")
+        return out[:ln.value].copy(), meta[:3 * nv.value].reshape(-1, 3).copy()
+
+    def get_timing(self):
+        t = N.Timing()
+        self._check(self._call("get_timing", self._h, C.byref(t)), "get_timing")
+        return t.as_dict()
+
+    def get_clone_times(self):
+        out = np.zeros(256)
+        n = C.c_int()
+        self._check(self._call("get_clone_times", self._h, _dp(out), 256, C.byref(n)), "get_clone_times")
+        return out[:n.value].copy()
+
+
+def ekf_update(P, H_index, H, res, sigma2):
+    """StateHelper::EKFUpdate on a standalone covariance, on the device (returns P_new, dx)."""
+    lib = N.load()
+    P = np.array(P, dtype=np.float64, order="C", copy=True)
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    res = np.ascontiguousarray(res, dtype=np.float64)
+    idx = np.ascontiguousarray(H_index, dtype=np.int32)
+    Nn = P.shape[0]
+    r, n = H.shape
+    dx = np.zeros(Nn)
+    rc = lib.uvio_hp_ekf_update(_dp(P), Nn, idx.ctypes.data_as(C.POINTER(C.c_int)), n, _dp(H), r, _dp(res),
+                                float(sigma2), _dp(dx))
+    N.check(rc, what="uvio_hp_ekf_update")
+    return P, dx
+
+
+def compress(A):
+    """R factor of [H | res] (measurement_compress_inplace semantics), on the device."""
+    lib = N.load()
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    m, nc = A.shape
+    R = np.zeros((nc, nc))
+    N.check(lib.uvio_hp_compress(_dp(A), m, nc - 1, _dp(R)), what="uvio_hp_compress")
+    return R
