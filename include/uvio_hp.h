@@ -169,21 +169,34 @@ int uvio_hp_get_cov(uvio_hp_t *h, double *out, int ld);
  * *len receives the number of doubles written; meta (optional, 3 ints per variable:
  * kind, covariance id, covariance size) */
 int uvio_hp_get_state_vector(uvio_hp_t *h, double *out, int cap, int *len, int *meta, int meta_cap, int *nvars);
+/* the first-estimate (FEJ) values, same layout as uvio_hp_get_state_vector (Type::fej(), Type.h:87) */
+int uvio_hp_get_fej_vector(uvio_hp_t *h, double *out, int cap, int *len);
 /* timings of the last processed frame */
 int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out);
 /* number of clones and their timestamps (ascending) */
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
 
 /* ---- inner (kernel-level) boundary used by parity tests ---- */
+/* per-feature results of the last UpdaterMSCKF::update: feature id, triangulated p_FinG (3 per
+ * feature), status (0 accepted, 1 triangulation/refinement failed, 3 chi2 rejected) and chi2 */
+int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n);
 /* StateHelper::EKFUpdate (StateHelper.cpp:116) on a standalone covariance: P (N x N, row-major,
  * in/out, host memory), H (r x n, row-major) whose column j maps to covariance index H_index[j]
  * (the H_order blocks flattened), residual (r), isotropic noise sigma2.  dx_out (N) receives K*res.
  * The update runs on the device (same kernels as the manager). */
 int uvio_hp_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r,
                        const double *res, double sigma2, double *dx_out);
+/* UpdaterMSCKF.cpp:274-286: measurement_compress_inplace of the stacked [H | res] (m x n) followed by
+ * StateHelper::EKFUpdate on the compressed rows, on a standalone covariance (same arguments as
+ * uvio_hp_ekf_update).  When m > n the device runs the update in information form on H^T H, H^T res
+ * (the quantities the compressed system carries); otherwise it is uvio_hp_ekf_update. */
+int uvio_hp_msckf_compressed_update(double *P, int N, const int *H_index, int n, const double *H, int m,
+                                    const double *res, double sigma2, double *dx_out);
 /* UpdaterHelper::measurement_compress_inplace (UpdaterHelper.cpp:456) semantics: A = [H | res]
  * (m x (n+1), row-major) -> the (n+1) x (n+1) upper-triangular R factor of A (rows of the reference's
- * compressed [H|res] up to a per-row sign; the last row holds the residual norm not explained by H). */
+ * compressed [H|res] up to a per-row sign; the last row holds the residual norm not explained by H).
+ * Computed as the Cholesky factor of the Gram matrix: intended for full-column-rank A (the manager's
+ * update does not factor the Gram, see uvio_hp_msckf_compressed_update). */
 int uvio_hp_compress(const double *A, int m, int n, double *R_out);
 
 #ifdef __cplusplus

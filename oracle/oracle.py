@@ -24,7 +24,8 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 
 _ORC_NAMES = ["create", "destroy", "initialize_with_gt", "feed_imu", "feed_simulation", "feed_uwb", "init_anchors",
               "get_imu_state", "get_cov_dim", "get_cov", "get_state_vector", "get_timing", "get_clone_times",
-              "ekf_update", "compress"]
+              "ekf_update", "compress", "debug_last_msckf", "get_fej_vector",
+              "msckf_compressed_update"]
 
 _lib = None
 
@@ -42,6 +43,8 @@ def load():
         lib = C.CDLL(LIB_PATH)
         N.bind(lib, "orc_", _ORC_NAMES)
         lib.orc_create.argtypes = [C.POINTER(N.Options), C.POINTER(C.c_void_p)]
+        lib.orc_set_state.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int,
+                                      C.POINTER(C.c_double), C.c_int]
         lib.orc_chi2_quantile95.restype = C.c_double
         lib.orc_chi2_quantile95.argtypes = [C.c_int]
         lib.orc_camera_distort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -60,6 +63,15 @@ class OracleManager(VioManager):
     def _load(cls):
         return load()
 
+    def set_state(self, val, fej, P):
+        """Lock-step parity: adopt another implementation's mean / FEJ / covariance."""
+        val = np.ascontiguousarray(val, dtype=np.float64)
+        fej = np.ascontiguousarray(fej, dtype=np.float64)
+        P = np.ascontiguousarray(P, dtype=np.float64)
+        rc = self._lib.orc_set_state(self._h, _dp(val), _dp(fej), val.size, _dp(P), P.shape[0])
+        if rc != 0:
+            raise RuntimeError("orc_set_state: layout mismatch (%d)" % rc)
+
 
 def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
@@ -69,7 +81,7 @@ def chi2_quantile95(dof):
     return load().orc_chi2_quantile95(int(dof))
 
 
-def ekf_update(P, H_index, H, res, sigma2):
+def ekf_update(P, H_index, H, res, sigma2, compressed=False):
     lib = load()
     P = np.array(P, dtype=np.float64, order="C", copy=True)
     H = np.ascontiguousarray(H, dtype=np.float64)
@@ -78,8 +90,8 @@ def ekf_update(P, H_index, H, res, sigma2):
     n_ = P.shape[0]
     r, n = H.shape
     dx = np.zeros(n_)
-    rc = lib.orc_ekf_update(_dp(P), n_, idx.ctypes.data_as(C.POINTER(C.c_int)), n, _dp(H), r, _dp(res), float(sigma2),
-                            _dp(dx))
+    fn = lib.orc_msckf_compressed_update if compressed else lib.orc_ekf_update
+    rc = fn(_dp(P), n_, idx.ctypes.data_as(C.POINTER(C.c_int)), n, _dp(H), r, _dp(res), float(sigma2), _dp(dx))
     if rc != 0:
         raise RuntimeError("orc_ekf_update failed %d" % rc)
     return P, dx

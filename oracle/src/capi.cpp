@@ -84,6 +84,33 @@ int orc_get_state_vector(orc_handle *h, double *out, int cap, int *len, int *met
   if (nvars) *nvars = nv;
   return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
 }
+int orc_get_fej_vector(orc_handle *h, double *out, int cap, int *len) {
+  int k = 0;
+  for (auto &v : h->m.state.variables)
+    for (int i = 0; i < v->fej.r; i++, k++)
+      if (k < cap) out[k] = v->fej[i];
+  *len = k;
+  return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
+}
+// lock-step parity: overwrite the mean, the FEJ values and the covariance with another
+// implementation's (same variable layout required)
+int orc_set_state(orc_handle *h, const double *val, const double *fej, int len, const double *P, int n) {
+  int k = 0;
+  for (auto &v : h->m.state.variables) k += v->val.r;
+  if (k != len || n != h->m.state.Cov.r) return UVIO_HP_E_ARG;
+  k = 0;
+  for (auto &v : h->m.state.variables)
+    for (int i = 0; i < v->val.r; i++, k++) {
+      v->val[i] = val[k];
+      v->fej[i] = fej[k];
+    }
+  std::memcpy(h->m.state.Cov.d.data(), P, sizeof(double) * n * n);
+  // the camera models mirror the intrinsics after every update (StateHelper.cpp:190-195)
+  if (h->m.state.opt.do_calib_camera_intrinsics)
+    for (auto &c : h->m.state.cam_intrinsics)
+      for (int i = 0; i < 8; i++) h->m.state.cams.at(c.first).v[i] = c.second->val[i];
+  return 0;
+}
 int orc_get_timing(orc_handle *h, uvio_hp_timing_t *out) {
   *out = h->m.timing;
   return 0;
@@ -125,6 +152,20 @@ int orc_ekf_update(double *P, int N, const int *H_index, int n, const double *H,
   return ok ? 0 : UVIO_HP_E_NUMERIC;
 }
 
+// UpdaterMSCKF.cpp:274-286: measurement_compress_inplace then EKFUpdate on a standalone covariance
+int orc_msckf_compressed_update(double *P, int N, const int *H_index, int n, const double *H, int m, const double *res,
+                                double sigma2, double *dx_out) {
+  Mat Hm(m, n), rm(m, 1);
+  std::memcpy(Hm.d.data(), H, sizeof(double) * m * n);
+  std::memcpy(rm.d.data(), res, sizeof(double) * m);
+  UpdaterHelper::measurement_compress_inplace(Hm, rm);
+  if (Hm.r == 0) {
+    for (int i = 0; i < N; i++) dx_out[i] = 0.0;
+    return 0;
+  }
+  return orc_ekf_update(P, N, H_index, n, Hm.d.data(), Hm.r, rm.d.data(), sigma2, dx_out);
+}
+
 // UpdaterHelper::measurement_compress_inplace on [H | res]: returns R (n+1 x n+1) of the Givens
 // sweep applied to the augmented matrix (the reference applies it to H and res jointly).
 int orc_compress(const double *A, int m, int n, double *R_out) {
@@ -144,6 +185,23 @@ int orc_compress(const double *A, int m, int n, double *R_out) {
 }
 
 double orc_chi2_quantile95(int dof) { return chi2_quantile95(dof); }
+
+// per-feature results of the last MSCKF update (debug / parity tests)
+int orc_debug_last_msckf(orc_handle *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n) {
+  const auto &v = h->m.last_msckf.feats;
+  int k = 0;
+  for (const auto &d : v) {
+    if (k < cap) {
+      ids[k] = d.id;
+      for (int j = 0; j < 3; j++) pG[3 * k + j] = d.p_FinG[j];
+      status[k] = d.status;
+      chi2[k] = d.chi2;
+    }
+    k++;
+  }
+  *n = k;
+  return 0;
+}
 
 // Camera model entry points for fixture / finite-difference tests
 int orc_camera_distort(const uvio_hp_camera_t *c, int n, const double *xy, double *uv, double *dz_dzn, double *dz_dzeta) {

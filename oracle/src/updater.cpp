@@ -1,5 +1,7 @@
 // ORACLE — test infrastructure only (see la.h header).
 #include "updater.h"
+#include <cstdio>
+#include <cstdlib>
 
 #include <map>
 
@@ -182,6 +184,13 @@ void get_feature_jacobian_full(State &s, HelperFeature &feature, Mat &H_f, Mat &
       auto uvm = F.uvs.at(pair.first)[m];
       res[2 * c] = (double)uvm.first - ud;
       res[2 * c + 1] = (double)uvm.second - vd;
+      if (const char *md = std::getenv("ORC_MEAS_DUMP")) {  // debug only
+        FILE *fp = std::fopen(md, "ab");
+        double rec[9] = {(double)feature.featid, (double)pair.first, xn, yn, ud, vd, (double)uvm.first, (double)uvm.second,
+                         p_FinCi[2]};
+        std::fwrite(rec, sizeof(double), 9, fp);
+        std::fclose(fp);
+      }
       if (s.opt.do_fej) {
         R_GtoIi = clone_Ii->Rot_fej();
         p_IiinG = clone_Ii->pos_fej();
@@ -298,6 +307,7 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
     bool ok_ref = true;
     if (init.o.fi_refine_features) ok_ref = init.single_gaussnewton(**it1, clones_cam);
     if (!ok_tri || !ok_ref) {
+      if (st) st->feats.push_back(FeatDebug{(*it1)->featid, {0, 0, 0}, 1, -1.0});
       (*it1)->to_delete = true;
       it1 = feature_vec.erase(it1);
       continue;
@@ -334,6 +344,18 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
     std::vector<Ref> Hx_order;
     UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
     UpdaterHelper::nullspace_project_inplace(H_f, H_x, res);
+    if (const char *dump = std::getenv("ORC_DUMP")) {  // debug: projected rows per feature
+      FILE *fp = std::fopen(dump, "ab");
+      std::vector<double> hdr = {(double)feat.featid, (double)H_x.r, (double)H_x.c};
+      for (auto &rf : Hx_order)
+        for (int k = 0; k < rf.size; k++) hdr.push_back(rf.id() + k);
+      std::fwrite(hdr.data(), sizeof(double), hdr.size(), fp);
+      for (int i = 0; i < H_x.r; i++) {
+        for (int j = 0; j < H_x.c; j++) std::fwrite(&H_x(i, j), sizeof(double), 1, fp);
+        std::fwrite(&res[i], sizeof(double), 1, fp);
+      }
+      std::fclose(fp);
+    }
     Mat P_marg = StateHelper::get_marginal_covariance(s, Hx_order);
     Mat S = H_x * P_marg * H_x.T();
     for (int i = 0; i < S.r; i++) S(i, i) += sigma_pix_sq;
@@ -341,6 +363,11 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
     llt_solve(S, sol);
     double chi2 = dot(res, sol);
     double chi2_check = (res.r < 500) ? chi_squared_table[res.r] : chi2_quantile95(res.r);
+    if (st) {
+      FeatDebug d{(*it2)->featid, {(*it2)->p_FinG[0], (*it2)->p_FinG[1], (*it2)->p_FinG[2]}, 0, chi2};
+      if (chi2 > chi2_mult * chi2_check) d.status = 3;
+      st->feats.push_back(d);
+    }
     if (chi2 > chi2_mult * chi2_check) {
       (*it2)->to_delete = true;
       it2 = feature_vec.erase(it2);

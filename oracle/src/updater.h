@@ -23,8 +23,15 @@ void nullspace_project_inplace(Mat &H_f, Mat &H_x, Mat &res);
 void measurement_compress_inplace(Mat &H_x, Mat &res);
 }  // namespace UpdaterHelper
 
+struct FeatDebug {
+  size_t id;
+  double p_FinG[3];
+  int status;  // 0 accepted, 1 triangulation / refine failed, 3 chi2 rejected
+  double chi2;
+};
 struct UpdateStats {
   int rows_stacked = 0, cols = 0, accepted = 0, rows_compressed = 0;
+  std::vector<FeatDebug> feats;
 };
 
 struct UpdaterMSCKF {

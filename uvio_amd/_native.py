@@ -91,9 +91,12 @@ SIGNATURES = [
     ("get_cov_dim", _I, [C.c_void_p, _P(_I)]),
     ("get_cov", _I, [C.c_void_p, _P(_D), _I]),
     ("get_state_vector", _I, [C.c_void_p, _P(_D), _I, _P(_I), _P(_I), _I, _P(_I)]),
+    ("get_fej_vector", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
     ("get_timing", _I, [C.c_void_p, _P(Timing)]),
     ("get_clone_times", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
+    ("debug_last_msckf", _I, [C.c_void_p, _P(C.c_uint64), _P(_D), _P(_I), _P(_D), _I, _P(_I)]),
     ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
+    ("msckf_compressed_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("compress", _I, [_P(_D), _I, _I, _P(_D)]),
 ]
 

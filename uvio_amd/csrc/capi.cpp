@@ -134,6 +134,13 @@ int uvio_hp_get_state_vector(uvio_hp_t *h, double *out, int cap, int *len, int *
   return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
 }
 
+int uvio_hp_get_fej_vector(uvio_hp_t *h, double *out, int cap, int *len) {
+  if (!h || !out || !len) return UVIO_HP_E_ARG;
+  int k = h->e->state_vector(out, cap, nullptr, 0, nullptr, true);
+  *len = k;
+  return k <= cap ? 0 : UVIO_HP_E_CAPACITY;
+}
+
 int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out) {
   if (!h || !out) return UVIO_HP_E_ARG;
   *out = h->e->timing();
@@ -148,10 +155,38 @@ int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n) {
   return 0;
 }
 
+int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n) {
+  if (!h || !n) return UVIO_HP_E_ARG;
+  const auto &v = h->e->last_msckf_;
+  int k = 0;
+  for (const auto &d : v) {
+    if (k < cap) {
+      ids[k] = d.id;
+      for (int j = 0; j < 3; j++) pG[3 * k + j] = d.p_FinG[j];
+      status[k] = d.status;
+      chi2[k] = d.chi2;
+    }
+    k++;
+  }
+  *n = k;
+  return 0;
+}
+
 int uvio_hp_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
                        double sigma2, double *dx_out) {
   try {
     return Engine::ekf_update_standalone(P, N, H_index, n, H, r, res, sigma2, dx_out);
+  } catch (const HpError &ex) {
+    return ex.code;
+  } catch (...) {
+    return UVIO_HP_E_DEVICE;
+  }
+}
+
+int uvio_hp_msckf_compressed_update(double *P, int N, const int *H_index, int n, const double *H, int m,
+                                    const double *res, double sigma2, double *dx_out) {
+  try {
+    return Engine::ekf_update_standalone(P, N, H_index, n, H, m, res, sigma2, dx_out, true);
   } catch (const HpError &ex) {
     return ex.code;
   } catch (...) {

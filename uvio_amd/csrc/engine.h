@@ -111,13 +111,13 @@ class Engine {
   const Var &imu() const { return *imu_; }
   int cov_dim() const { return N_; }
   void get_cov(double *out, int ld);
-  int state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars);
+  int state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars, bool fej = false);
   uvio_hp_timing_t timing() const { return timing_; }
   std::vector<double> clone_times() const;
 
   // standalone kernel-level entry points (parity tests)
   static int ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
-                                   double sigma2, double *dx_out);
+                                   double sigma2, double *dx_out, bool compress = false);
   static int compress_standalone(const double *A, int m, int n, double *R_out);
 
  private:
@@ -150,6 +150,17 @@ class Engine {
   uvio_hp_timing_t timing_{};
   std::vector<double> chi2_table_;
 
+ public:
+  struct FeatDebug {
+    size_t id;
+    double p_FinG[3];
+    int status;
+    double chi2;
+  };
+  std::vector<FeatDebug> last_msckf_;
+
+ private:
+
   // covariance ops (device)
   void alloc_device();
   void upload_P_full(const std::vector<double> &Ph, int N);
@@ -159,6 +170,7 @@ class Engine {
   VarP clone_imu_pose(const double *dnc, bool do_dt);
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
+  void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2);
   void ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx, const double *resdev,
                        int res_stride, double sigma2);
   void apply_dx(const double *dx);

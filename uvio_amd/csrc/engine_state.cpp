@@ -379,6 +379,18 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
   apply_dx(d_.dx_host);
 }
 
+// EKF update from the Gram partials of a stacked batch (compressed path, m > n)
+void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2) {
+  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
+  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
+  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, d_.hidx, sigma2, d_.R, d_.ekf);
+  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+  apply_dx(d_.dx_host);
+}
+
 // StateHelper::set_initial_covariance (StateHelper.cpp:199-223).  Start-up only (initialize_with_gt,
 // anchor init): P is read back, the blocks are written, and P is re-uploaded.
 void Engine::set_initial_covariance(const std::vector<double> &cov, const std::vector<VarP> &order) {
@@ -476,7 +488,7 @@ void Engine::initialize_invertible_host(const VarP &v, const std::vector<std::pa
   upload_P_full(Pn, Nn);
 }
 
-int Engine::state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars) {
+int Engine::state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars, bool fej) {
   int k = 0, nv = 0;
   for (auto &v : vars_) {
     if (meta && 3 * nv + 2 < meta_cap) {
@@ -485,7 +497,7 @@ int Engine::state_vector(double *out, int cap, int *meta, int meta_cap, int *nva
       meta[3 * nv + 2] = v->size;
     }
     for (int i = 0; i < v->vlen; i++) {
-      if (k < cap) out[k] = v->val[i];
+      if (k < cap) out[k] = fej ? v->fej[i] : v->val[i];
       k++;
     }
     nv++;
@@ -507,7 +519,7 @@ namespace uvhp {
 // Standalone StateHelper::EKFUpdate on a caller-provided covariance (kernel-level parity entry):
 // the same device kernels the manager uses, on temporary device buffers.
 int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r,
-                                  const double *res, double sigma2, double *dx_out) {
+                                  const double *res, double sigma2, double *dx_out, bool compress) {
   if (!P || N <= 0 || n <= 0 || r <= 0 || !H || !res || !H_index || !dx_out) return UVIO_HP_E_ARG;
   for (int j = 0; j < n; j++)
     if (H_index[j] < 0 || H_index[j] >= N) return UVIO_HP_E_ARG;
@@ -516,14 +528,21 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   hipStream_t s;
   HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   int ldh = n + 1;
-  double *dP, *dH, *dM, *dW, *dS, *dy, *ddx;
+  bool info = compress && r > n;
+  int rw = std::max(r, n + 1);
+  int nch = gram_num_chunks(r);
+  double *dP, *dH, *dM, *dW, *dS, *dy, *ddx, *dPart = nullptr, *dG = nullptr;
   int *dI, *dneg;
   dalloc(&dP, (size_t)N * N);
   dalloc(&dH, (size_t)r * ldh);
-  dalloc(&dM, (size_t)N * r);
-  dalloc(&dW, (size_t)N * r);
-  dalloc(&dS, (size_t)3 * r * r);
-  dalloc(&dy, r);
+  dalloc(&dM, (size_t)N * rw);
+  dalloc(&dW, (size_t)N * rw);
+  dalloc(&dS, (size_t)3 * rw * rw);
+  dalloc(&dy, rw);
+  if (info) {
+    dalloc(&dPart, (size_t)nch * ldh * ldh);
+    dalloc(&dG, (size_t)ldh * ldh);
+  }
   dalloc(&ddx, N);
   dalloc(&dI, n);
   dalloc(&dneg, 1);
@@ -537,14 +556,21 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   HP_HIP(hipMemcpyAsync(dI, H_index, sizeof(int) * n, hipMemcpyHostToDevice, s));
   HP_HIP(hipMemsetAsync(dneg, 0, sizeof(int), s));
   EkfScratch sc{dM, dW, dS, dy, ddx, dneg};
-  launch_ekf_update(s, dP, N, N, dH, ldh, r, n, dI, dH + n, ldh, sigma2, sc);
+  if (info) {
+    int nc2 = 0;
+    launch_gram(s, dH, r, ldh, ldh, dPart, &nc2);
+    launch_ekf_info(s, dP, N, N, dPart, nc2, n, dI, sigma2, dG, sc);
+  } else {
+    launch_ekf_update(s, dP, N, N, dH, ldh, r, n, dI, dH + n, ldh, sigma2, sc);
+  }
   int neg = 0;
   HP_HIP(hipMemcpyAsync(P, dP, sizeof(double) * N * N, hipMemcpyDeviceToHost, s));
   HP_HIP(hipMemcpyAsync(dx_out, ddx, sizeof(double) * N, hipMemcpyDeviceToHost, s));
   HP_HIP(hipMemcpyAsync(&neg, dneg, sizeof(int), hipMemcpyDeviceToHost, s));
   HP_HIP(hipStreamSynchronize(s));
-  void *ptrs[] = {dP, dH, dM, dW, dS, dy, ddx, dI, dneg};
-  for (void *p : ptrs) hipFree(p);
+  void *ptrs[] = {dP, dH, dM, dW, dS, dy, ddx, dI, dneg, dPart, dG};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
   hipStreamDestroy(s);
   return neg > 0 ? UVIO_HP_E_NUMERIC : 0;
 }

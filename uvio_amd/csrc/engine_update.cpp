@@ -2,6 +2,8 @@
 // (FeatureDatabase.cpp:59-263) and the update orchestration (UpdaterMSCKF.cpp:58-295,
 // UpdaterSLAM.cpp:61-647, UpdaterUWB.cpp:53-90) over the device kernels.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine.h"
@@ -571,17 +573,35 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   bp.fi_max_dist = o_.fi_max_dist;
   bp.fi_max_baseline = o_.fi_max_baseline;
   bp.fi_max_cond = o_.fi_max_cond_number;
+  const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
+  if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.meas.size()));
   launch_feature_linearize(d_.stream, bp, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
   HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
   HP_HIP(hipStreamSynchronize(d_.stream));
   outs.assign(d_.fout_host, d_.fout_host + nf);
+  if (mdump) {
+    std::vector<double> h(8 * b.meas.size());
+    HP_HIP(hipMemcpy(h.data(), bp.dbg, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+    HP_HIP(hipFree(bp.dbg));
+    FILE *fp = std::fopen(mdump, "ab");
+    for (int i = 0; i < nf; i++) {
+      if (outs[i].status != 0) continue;
+      for (int k = 0; k < b.feats[i].nmeas; k++) {
+        double fid = (double)i;
+        std::fwrite(&fid, sizeof(double), 1, fp);
+        std::fwrite(h.data() + 8 * (size_t)(b.feats[i].meas_off + k), sizeof(double), 8, fp);
+      }
+    }
+    std::fclose(fp);
+  }
   (void)mode;
   return b.rows;
 }
 
 // UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295)
 int Engine::msckf_update(std::vector<FeatP> &fv) {
+  last_msckf_.clear();
   if (fv.empty()) return 0;
   std::vector<double> clonetimes;
   for (auto &c : clones_) clonetimes.push_back(c.first);
@@ -606,21 +626,39 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   int m = run_batch(b, 0, o_.msckf_sigma_pix * o_.msckf_sigma_pix, o_.msckf_chi2_multipler, true, outs);
   int acc = 0, acc_rows = 0;
   for (size_t i = 0; i < outs.size(); i++) {
+    last_msckf_.push_back(FeatDebug{fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
+                                    outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
     fv[i]->to_delete = true;
     for (int k = 0; k < 3; k++) fv[i]->p_FinG[k] = outs[i].p_FinG[k], fv[i]->p_FinA[k] = outs[i].p_FinA[k];
     if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
   }
   timing_.msckf_rows = acc_rows;
   timing_.msckf_cols = b.n_canon;
+  if (const char *dump = std::getenv("UVIO_HP_DUMP")) {  // debug: projected rows per feature
+    int nc = b.n_canon + 1;
+    std::vector<double> Hh((size_t)std::max(m, 1) * nc);
+    if (m > 0)
+      HP_HIP(hipMemcpy2D(Hh.data(), sizeof(double) * nc, d_.H, sizeof(double) * d_.ldh, sizeof(double) * nc, m,
+                         hipMemcpyDeviceToHost));
+    FILE *fp = std::fopen(dump, "ab");
+    for (size_t i = 0; i < outs.size(); i++) {
+      if (outs[i].status != 0) continue;
+      std::vector<double> hdr = {(double)fv[i]->featid, (double)outs[i].rows, (double)b.n_canon};
+      for (int j = 0; j < b.n_canon; j++) hdr.push_back(b.hidx[j]);
+      std::fwrite(hdr.data(), sizeof(double), hdr.size(), fp);
+      std::fwrite(Hh.data() + (size_t)b.feats[i].row_off * nc, sizeof(double), (size_t)outs[i].rows * nc, fp);
+    }
+    std::fclose(fp);
+  }
   if (acc == 0 || m < 1) return 0;
   int n = b.n_canon, ncol = n + 1;
   double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
   if (m > n) {
-    // measurement compression (UpdaterHelper.cpp:456-487) as CholeskyQR of [H | r]
+    // measurement compression (UpdaterHelper.cpp:456-487) + EKFUpdate on the compressed system, carried
+    // out in information form on G = [H r]^T [H r] (see launch_ekf_info)
     int nch = 0;
     launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
-    launch_gram_reduce_chol(d_.stream, d_.partials, nch, ncol, d_.R, d_.ldh);
-    ekf_update_rows(d_.R, d_.ldh, n, n, b.hidx, d_.R + n, d_.ldh, s2);
+    ekf_update_info(nch, n, b.hidx, s2);
   } else {
     ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
   }
@@ -674,8 +712,7 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
   if (m > n) {
     int nch = 0;
     launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
-    launch_gram_reduce_chol(d_.stream, d_.partials, nch, ncol, d_.R, d_.ldh);
-    ekf_update_rows(d_.R, d_.ldh, n, n, b.hidx, d_.R + n, d_.ldh, s2);
+    ekf_update_info(nch, n, b.hidx, s2);
   } else {
     ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
   }

@@ -88,6 +88,7 @@ struct DBatchParams {
   int fi_max_runs, fi_refine, fi_tri1d;
   double fi_init_lamda, fi_max_lamda, fi_min_dx, fi_min_dcost, fi_lam_mult;
   double fi_min_dist, fi_max_dist, fi_max_baseline, fi_max_cond;
+  double *dbg;  // optional per-measurement debug record (8 doubles each), nullptr in production
 };
 
 // ---- launch wrappers (all asynchronous on `s`) ----
@@ -123,6 +124,10 @@ struct EkfScratch {
 };
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
                        const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc);
+// information-form update for a compressed batch (m > n): G = [H r]^T [H r] from k_gram partials;
+// Gbuf holds (n+1)^2 doubles.  Same P / dx outputs as launch_ekf_update on the Givens R factor.
+void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
+                     const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc);
 // the same update split at the innovation covariance: phase A leaves S_up = H P H^T + s2 I (r x r) at
 // sc.S + 2 r^2 (used by gated single-row updates such as UWB); phase B finishes the update.
 void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,

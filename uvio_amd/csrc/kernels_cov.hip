@@ -12,6 +12,8 @@
 
 namespace uvhp {
 
+static void ensure_lds_attrs();  // large dynamic LDS (> 64 KiB) opt-in, defined at the end
+
 // ----------------------------------------------------------------------------------------------
 // EKFPropagation
 // T[i][a] = sum_b P[i][iold[b]] * Phi[a][b]    (Cov_PhiT, StateHelper.cpp:80-85)
@@ -231,6 +233,7 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
   int use_lds = bytes <= 150 * 1024;
   // global scratch for large ncol lives right after R (caller sizes R for 2 * ncol^2)
   double *gbuf = R + (size_t)ncol * ldr;
+  ensure_lds_attrs();
   hipLaunchKernelGGL(k_gram_reduce_chol, dim3(1), dim3(1024), use_lds ? bytes : 0, s, partials, nchunks, ncol, R, ldr,
                      gbuf, use_lds);
 }
@@ -409,6 +412,7 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   double *Linv = sc.S;
   double *Sg = sc.S + (size_t)r * r;
   double *Sup = sc.S + 2 * (size_t)r * r;
+  ensure_lds_attrs();
   hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(1024), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
                      use_lds);
   dim3 gM((r + 15) / 16, (N + 15) / 16);
@@ -421,6 +425,188 @@ void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H
                        const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc) {
   launch_ekf_phaseA(s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc);
   launch_ekf_phaseB(s, P, ldp, N, r, res, res_stride, sc);
+}
+
+// ----------------------------------------------------------------------------------------------
+// Information-form EKF update for compressed (m > n) batches.
+//
+// The reference compresses [H | r] with Givens (UpdaterHelper.cpp:456-487) and runs EKFUpdate on the
+// n x n R factor.  EKFUpdate depends on R only through G = R^T R = H^T H and b = R^T z = H^T r:
+//   P+ = P - P[:,I] (G P_II + s2 I)^-1 G P[I,:],   dx = P[:,I] (G P_II + s2 I)^-1 b
+// (push-through identity on K = P H^T (H P H^T + s2 I)^-1).  G is the fixed-order Gram of the stacked
+// rows; no factor of G is formed, so the gauge directions in which H is exactly singular (cond ~1e17 on
+// real MSCKF batches) stay at rounding level instead of picking up sqrt(eps)-sized rows the way a
+// Cholesky factor of a singular Gram does.  The eigenvalues of G P_II + s2 I are >= s2, so the LU solve
+// below is well conditioned.
+
+// full symmetric G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk order)
+__global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ partials, int nch, int ncol,
+                                                     double *__restrict__ G) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ncol * ncol) return;
+  int a = e / ncol, b = e % ncol;
+  int u = (a <= b) ? a * ncol + b : b * ncol + a;
+  double acc = 0.0;
+  for (int c = 0; c < nch; c++) acc += partials[(size_t)c * ncol * ncol + u];
+  G[e] = acc;
+}
+
+// Single workgroup: K = G_nn P_II + s2 I, LU with partial pivoting, [Q | y] = K^-1 [G_nn | b];
+// Q is symmetrised.  K and the right-hand sides live in LDS when 2 n (n+1) doubles fit, else in `gbuf`.
+__global__ void __launch_bounds__(1024) k_info_small(const double *__restrict__ G, int n, const double *__restrict__ P,
+                                                     int ldp, const int *__restrict__ hidx, double s2,
+                                                     double *__restrict__ Q, double *__restrict__ y, double *gbuf,
+                                                     int use_lds) {
+  extern __shared__ double lds[];
+  double *K = use_lds ? lds : gbuf;      // n x n
+  double *B = K + (size_t)n * n;         // n x (n+1)
+  __shared__ double rv[1024];
+  __shared__ int ri[1024];
+  __shared__ int piv_row;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int nc = n + 1, ldg = n + 1;
+  // K[a][b] = sum_c G[a][c] P[hidx[c]][hidx[b]] (+ s2 on the diagonal)
+  for (int e = tid; e < n * n; e += nt) {
+    int a = e / n, b = e % n;
+    const double *Pb = P + (size_t)hidx[b];
+    double acc = 0.0;
+    for (int c = 0; c < n; c++) acc += G[(size_t)a * ldg + c] * Pb[(size_t)hidx[c] * ldp];
+    K[e] = acc + (a == b ? s2 : 0.0);
+  }
+  for (int e = tid; e < n * nc; e += nt) {
+    int a = e / nc, b = e % nc;
+    B[e] = G[(size_t)a * ldg + b];
+  }
+  __syncthreads();
+  for (int k = 0; k < n; k++) {
+    // pivot: largest |K[i][k]|, i >= k (lowest index on ties)
+    double best = -1.0;
+    int bi = k;
+    for (int i = k + tid; i < n; i += nt) {
+      double v = fabs(K[(size_t)i * n + k]);
+      if (v > best) best = v, bi = i;
+    }
+    rv[tid] = best;
+    ri[tid] = bi;
+    __syncthreads();
+    for (int w = nt / 2; w > 0; w >>= 1) {
+      if (tid < w) {
+        double o = rv[tid + w];
+        int oi = ri[tid + w];
+        if (o > rv[tid] || (o == rv[tid] && oi < ri[tid])) rv[tid] = o, ri[tid] = oi;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) piv_row = ri[0];
+    __syncthreads();
+    int p = piv_row;
+    if (p != k) {
+      for (int j = tid; j < n; j += nt) {
+        double t = K[(size_t)k * n + j];
+        K[(size_t)k * n + j] = K[(size_t)p * n + j];
+        K[(size_t)p * n + j] = t;
+      }
+      for (int j = tid; j < nc; j += nt) {
+        double t = B[(size_t)k * nc + j];
+        B[(size_t)k * nc + j] = B[(size_t)p * nc + j];
+        B[(size_t)p * nc + j] = t;
+      }
+      __syncthreads();
+    }
+    double dkk = K[(size_t)k * n + k];
+    for (int i = k + 1 + tid; i < n; i += nt) K[(size_t)i * n + k] /= dkk;
+    __syncthreads();
+    int m = n - k - 1;
+    for (int e = tid; e < m * m; e += nt) {
+      int i = k + 1 + e / m, j = k + 1 + e % m;
+      K[(size_t)i * n + j] -= K[(size_t)i * n + k] * K[(size_t)k * n + j];
+    }
+    for (int e = tid; e < m * nc; e += nt) {
+      int i = k + 1 + e / nc, j = e % nc;
+      B[(size_t)i * nc + j] -= K[(size_t)i * n + k] * B[(size_t)k * nc + j];
+    }
+    __syncthreads();
+  }
+  // back substitution U X = B
+  for (int k = n - 1; k >= 0; k--) {
+    double ukk = K[(size_t)k * n + k];
+    for (int j = tid; j < nc; j += nt) B[(size_t)k * nc + j] /= ukk;
+    __syncthreads();
+    for (int e = tid; e < k * nc; e += nt) {
+      int i = e / nc, j = e % nc;
+      B[(size_t)i * nc + j] -= K[(size_t)i * n + k] * B[(size_t)k * nc + j];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < n * n; e += nt) {
+    int a = e / n, b = e % n;
+    Q[e] = 0.5 * (B[(size_t)a * nc + b] + B[(size_t)b * nc + a]);
+  }
+  for (int a = tid; a < n; a += nt) y[a] = B[(size_t)a * nc + n];
+}
+
+// M = P[:, hidx]  (N x n)
+__global__ void k_gather_cols(const double *__restrict__ P, int ldp, int N, const int *__restrict__ hidx, int n,
+                              double *__restrict__ M) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * n) return;
+  int i = e / n, k = e % n;
+  M[e] = P[(size_t)i * ldp + hidx[k]];
+}
+
+// P[i][j] -= sum_k W[i][k] M[j][k] for j >= i, mirrored; dx = M y; negative-diagonal count
+__global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ W,
+                                                const double *__restrict__ M, int n, const double *__restrict__ y,
+                                                double *__restrict__ dx, int *neg) {
+  __shared__ double Wi[16][17];
+  __shared__ double Mj[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int bi = blockIdx.y, bj = blockIdx.x;
+  if (bj < bi) return;
+  int i0 = bi * 16, j0 = bj * 16;
+  double acc = 0.0;
+  for (int k0 = 0; k0 < n; k0 += 16) {
+    Wi[ty][tx] = (i0 + ty < N && k0 + tx < n) ? W[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
+    Mj[ty][tx] = (j0 + ty < N && k0 + tx < n) ? M[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += Wi[ty][kk] * Mj[tx][kk];
+    __syncthreads();
+  }
+  int i = i0 + ty, j = j0 + tx;
+  if (i < N && j < N && j >= i) {
+    double v = P[(size_t)i * ldp + j] - acc;
+    P[(size_t)i * ldp + j] = v;
+    P[(size_t)j * ldp + i] = v;
+    if (i == j && v < 0.0) atomicAdd(neg, 1);
+  }
+  if (bi == bj && ty == 0) {
+    int row = i0 + tx;
+    if (row < N) {
+      double a = 0.0;
+      for (int k = 0; k < n; k++) a += M[(size_t)row * n + k] * y[k];
+      dx[row] = a;
+    }
+  }
+}
+
+void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
+                     const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc) {
+  int ncol = n + 1;
+  hipLaunchKernelGGL(k_gram_reduce, dim3((ncol * ncol + 255) / 256), dim3(256), 0, s, partials, nch, ncol, Gbuf);
+  size_t bytes = (size_t)2 * n * ncol * sizeof(double);
+  int use_lds = bytes <= 150 * 1024;
+  double *Q = sc.S;                          // n x n
+  double *work = sc.S + (size_t)n * n;       // 2 n (n+1) when not in LDS
+  ensure_lds_attrs();
+  hipLaunchKernelGGL(k_info_small, dim3(1), dim3(1024), use_lds ? bytes : 0, s, Gbuf, n, P, ldp, hidx, sigma2, Q, sc.y,
+                     work, use_lds);
+  // W = P[:, I] Q (Q symmetric, so the k_ekf_M "H^T" operand is Q itself)
+  dim3 gM((n + 15) / 16, (N + 15) / 16);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Q, n, n, n, hidx, sc.W);
+  hipLaunchKernelGGL(k_gather_cols, dim3((N * n + 255) / 256), dim3(256), 0, s, P, ldp, N, hidx, n, sc.M);
+  int nb = (N + 15) / 16;
+  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, sc.M, n, sc.y, sc.dx, sc.neg);
 }
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
@@ -469,6 +655,15 @@ void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const doub
   int nt = N * 3;
   hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
                      HLinv, s2);
+}
+
+static void ensure_lds_attrs() {
+  static bool done = false;
+  if (done) return;
+  hipFuncSetAttribute((const void *)k_gram_reduce_chol, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  hipFuncSetAttribute((const void *)k_ekf_small, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  hipFuncSetAttribute((const void *)k_info_small, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  done = true;
 }
 
 }  // namespace uvhp

@@ -21,6 +21,27 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Sum over the first m lanes in lane (= measurement) order, the order the reference accumulates
+// (FeatureInitializer.cpp:76-82, 268-270, 413-416), so the LM accept/stop decisions see the same
+// bits.  Values go through LDS; every lane reads them back in the same order -> identical sums.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int NV>
+__device__ __forceinline__ void ordered_sum(double *red, const double *v, int lane, int m, double *out) {
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < NV; k++) red[k * 64 + lane] = v[k];
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    double s = 0.0;
+    for (int j = 0; j < m; j++) s += red[k * 64 + j];
+    out[k] = s;
+  }
+}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -204,6 +225,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   extern __shared__ double lds[];
   __shared__ FeatShared sh;
   __shared__ int canon2loc[512];
+  __shared__ double red[9 * 64];
   const int f = blockIdx.x;
   const DFeat F = feats[f];
   const int m = F.nmeas, rows = 2 * m, nf = F.nf, ldl = nf + 1;
@@ -279,12 +301,13 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
     }
     double A[9], bb[3];
     {
-      double s0 = wave_sum(Ai[0]), s1 = wave_sum(Ai[1]), s2 = wave_sum(Ai[2]);
-      double s3 = wave_sum(Ai[3]), s4 = wave_sum(Ai[4]), s5 = wave_sum(Ai[5]);
-      A[0] = s0; A[1] = s1; A[2] = s2; A[3] = s1; A[4] = s3; A[5] = s4; A[6] = s2; A[7] = s4; A[8] = s5;
-      bb[0] = wave_sum(bi[0]);
-      bb[1] = wave_sum(bi[1]);
-      bb[2] = wave_sum(bi[2]);
+      double v9[9] = {Ai[0], Ai[1], Ai[2], Ai[3], Ai[4], Ai[5], bi[0], bi[1], bi[2]}, s9[9];
+      ordered_sum<9>(red, v9, lane, m, s9);
+      A[0] = s9[0]; A[1] = s9[1]; A[2] = s9[2]; A[3] = s9[1]; A[4] = s9[3]; A[5] = s9[4];
+      A[6] = s9[2]; A[7] = s9[4]; A[8] = s9[5];
+      bb[0] = s9[6];
+      bb[1] = s9[7];
+      bb[2] = s9[8];
     }
     double pf[3];
     colpiv_solve3(A, bb, pf);
@@ -300,7 +323,11 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       int runs = 0;
       bool recompute = true;
       double Hs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-      double cost_old = wave_sum(act ? lm_err(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn) : 0.0);
+      double cost_old;
+      {
+        double e1 = act ? lm_err(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn) : 0.0;
+        ordered_sum<1>(red, &e1, lane, m, &cost_old);
+      }
       while (runs < bp.fi_max_runs && lam < bp.fi_max_lamda && eps > bp.fi_min_dx) {
         if (recompute) {
           double h[6] = {0, 0, 0, 0, 0, 0}, gg[3] = {0, 0, 0};
@@ -318,8 +345,10 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
             gg[1] = H[1] * r[0] + H[4] * r[1];
             gg[2] = H[2] * r[0] + H[5] * r[1];
           }
-          for (int k = 0; k < 6; k++) Hs[k] = wave_sum(h[k]);
-          for (int k = 0; k < 3; k++) g[k] = wave_sum(gg[k]);
+          double v9[9] = {h[0], h[1], h[2], h[3], h[4], h[5], gg[0], gg[1], gg[2]}, s9[9];
+          ordered_sum<9>(red, v9, lane, m, s9);
+          for (int k = 0; k < 6; k++) Hs[k] = s9[k];
+          for (int k = 0; k < 3; k++) g[k] = s9[6 + k];
         }
         double Hl3[9] = {Hs[0], Hs[1], Hs[2], Hs[1], Hs[3], Hs[4], Hs[2], Hs[4], Hs[5]};
         Hl3[0] *= (1.0 + lam);
@@ -327,7 +356,11 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
         Hl3[8] *= (1.0 + lam);
         double dx[3];
         colpiv_solve3(Hl3, g, dx);
-        double cost = wave_sum(act ? lm_err(R_AtoCi, p_AinCi, alpha + dx[0], beta + dx[1], rho + dx[2], un, vn) : 0.0);
+        double cost;
+        {
+          double e1 = act ? lm_err(R_AtoCi, p_AinCi, alpha + dx[0], beta + dx[1], rho + dx[2], un, vn) : 0.0;
+          ordered_sum<1>(red, &e1, lane, m, &cost);
+        }
         if (cost <= cost_old && (cost_old - cost) / cost_old < bp.fi_min_dcost) {
           alpha += dx[0];
           beta += dx[1];
@@ -494,6 +527,10 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
     float ud, vd;
     cam_distort_f(ck.cam, (float)xn, (float)yn, ud, vd);
     double res0 = (double)mm.u - (double)ud, res1 = (double)mm.v - (double)vd;
+    if (bp.dbg) {
+      double *d = bp.dbg + (size_t)(F.meas_off + tid) * 8;
+      d[0] = mm.cam; d[1] = xn; d[2] = yn; d[3] = ud; d[4] = vd; d[5] = mm.u; d[6] = mm.v; d[7] = p_FinCi[2];
+    }
     if (bp.do_fej) {
       for (int k = 0; k < 9; k++) R_GtoIi[k] = cl.Rf[k];
       for (int k = 0; k < 3; k++) p_IiinG[k] = cl.pf[k];
@@ -574,7 +611,11 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
         ss = wave_sum(ss);
         double x0 = Hf[c * 3 + c];
         double alpha = (x0 > 0) ? -sqrt(ss) : sqrt(ss);
-        for (int i = c + lane; i < rows; i += 64) V[i * 3 + c] = (i == c) ? (x0 - alpha) : Hf[i * 3 + c];
+        for (int i = c + lane; i < rows; i += 64) {
+          V[i * 3 + c] = (i == c) ? (x0 - alpha) : Hf[i * 3 + c];
+          // the reflected column c is alpha e_c (H_finit = the upper 3x3 of the reflected H_f)
+          Hf[i * 3 + c] = (i == c) ? alpha : 0.0;
+        }
         double vn = ss - x0 * x0 + (x0 - alpha) * (x0 - alpha);
         if (lane == 0) sh.beta[c] = (vn > 0) ? 2.0 / vn : 0.0;
       }
@@ -695,6 +736,11 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf) {
   if (bp.nfeat <= 0) return;
   size_t bytes = feature_lds_bytes(max_meas, max_nf);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void *)k_feature, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+    attr = true;
+  }
   hipLaunchKernelGGL(k_feature, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, meas, vars, clones, cams, P,
                      chi2_table, H_all, out, max_meas, max_nf);
 }

@@ -138,10 +138,28 @@ class VioManager:
                                meta.ctypes.data_as(C.POINTER(C.c_int)), meta.size, C.byref(nv)), "get_state_vector")
         return out[:ln.value].copy(), meta[:3 * nv.value].reshape(-1, 3).copy()
 
+    def get_fej_vector(self):
+        out = np.zeros(4096)
+        ln = C.c_int()
+        self._check(self._call("get_fej_vector", self._h, _dp(out), out.size, C.byref(ln)), "get_fej_vector")
+        return out[:ln.value].copy()
+
     def get_timing(self):
         t = N.Timing()
         self._check(self._call("get_timing", self._h, C.byref(t)), "get_timing")
         return t.as_dict()
+
+    def debug_last_msckf(self):
+        cap = 8192
+        ids = np.zeros(cap, dtype=np.uint64)
+        pG = np.zeros((cap, 3))
+        st = np.zeros(cap, dtype=np.int32)
+        c2 = np.zeros(cap)
+        n = C.c_int()
+        self._check(self._call("debug_last_msckf", self._h, ids.ctypes.data_as(C.POINTER(C.c_uint64)), _dp(pG),
+                               st.ctypes.data_as(C.POINTER(C.c_int)), _dp(c2), cap, C.byref(n)), "debug_last_msckf")
+        k = n.value
+        return ids[:k].copy(), pG[:k].copy(), st[:k].copy(), c2[:k].copy()
 
     def get_clone_times(self):
         out = np.zeros(256)
@@ -150,8 +168,9 @@ class VioManager:
         return out[:n.value].copy()
 
 
-def ekf_update(P, H_index, H, res, sigma2):
-    """StateHelper::EKFUpdate on a standalone covariance, on the device (returns P_new, dx)."""
+def ekf_update(P, H_index, H, res, sigma2, compressed=False):
+    """StateHelper::EKFUpdate on a standalone covariance, on the device (returns P_new, dx).
+    compressed=True: measurement compression + EKFUpdate as UpdaterMSCKF.cpp:274-286 does it."""
     lib = N.load()
     P = np.array(P, dtype=np.float64, order="C", copy=True)
     H = np.ascontiguousarray(H, dtype=np.float64)
@@ -160,8 +179,8 @@ def ekf_update(P, H_index, H, res, sigma2):
     Nn = P.shape[0]
     r, n = H.shape
     dx = np.zeros(Nn)
-    rc = lib.uvio_hp_ekf_update(_dp(P), Nn, idx.ctypes.data_as(C.POINTER(C.c_int)), n, _dp(H), r, _dp(res),
-                                float(sigma2), _dp(dx))
+    fn = lib.uvio_hp_msckf_compressed_update if compressed else lib.uvio_hp_ekf_update
+    rc = fn(_dp(P), Nn, idx.ctypes.data_as(C.POINTER(C.c_int)), n, _dp(H), r, _dp(res), float(sigma2), _dp(dx))
     N.check(rc, what="uvio_hp_ekf_update")
     return P, dx
 

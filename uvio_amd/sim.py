@@ -248,23 +248,30 @@ class SimStream:
         ev.sort(key=lambda e: (e[1] + (0.0 if e[0] == "imu" else lag), order[e[0]]))
         return ev
 
-    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0):
-        """Drive a manager: initialize from ground truth at t0, then feed IMU / UWB / camera in time order."""
-        mgr.initialize_with_gt(self.gt_state(self.t0))
+    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None):
+        """Drive one manager (or a list of managers in lock-step): initialize from ground truth at t0, then
+        feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed."""
+        mgrs = mgr if isinstance(mgr, (list, tuple)) else [mgr]
+        for m in mgrs:
+            m.initialize_with_gt(self.gt_state(self.t0))
         nf = 0
         for kind, t, i in self.events():
             if t < self.t0 - 0.4:
                 continue
             if kind == "imu":
-                mgr.feed_measurement_imu(t, self.wm[i], self.am[i])
+                for m in mgrs:
+                    m.feed_measurement_imu(t, self.wm[i], self.am[i])
             elif kind == "uwb":
-                mgr.feed_measurement_uwb(t, self.uwb[i][1], self.uwb[i][2])
+                for m in mgrs:
+                    m.feed_measurement_uwb(t, self.uwb[i][1], self.uwb[i][2])
             else:
                 if t <= self.t0:
                     continue
-                # the manager needs IMU past the camera time before it can propagate
                 fr = self.frames[i]
-                mgr.feed_measurement_simulation(t, list(range(self.K)), fr)
+                if before_frame is not None:
+                    before_frame(nf + 1, t)
+                for m in mgrs:
+                    m.feed_measurement_simulation(t, list(range(self.K)), fr)
                 nf += 1
                 if on_frame is not None:
                     on_frame(nf, t)
