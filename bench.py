@@ -1,0 +1,194 @@
+"""Headline benchmark: VIO frames/s of the per-frame propagate -> MSCKF/SLAM update loop.
+
+Workload (BASELINE.json configs[1], SURVEY.md §8 cfg 2): EuRoC V1_02-shaped stereo 752x480 rig from
+configs/euroc_mav (radtan, 2 cameras, 20 Hz), 11 clones (+1 at update time), up to 200 MSCKF features
+per update and 50 SLAM landmarks, 200 Hz IMU, on a synthetic EuRoC-shaped stream (uvio_amd/sim.py:
+seeded smooth trajectory, IMU from analytic derivatives + the config's noise densities, feature
+tracks projected through each camera with 1 px noise).  One step = one camera frame: the IMU samples
+since the last frame, then VioManager::feed_measurement_simulation (TrackSIM front-end: undistort +
+feature database) -> propagate + clone -> MSCKF update -> SLAM update / delayed init -> marginalize.
+
+The image tracker (TrackKLT) is not on this path yet: the front-end is the reference's TrackSIM
+(DESIGN.md "Scope").  Frames/s is whole-job throughput: every rank runs its own estimator on its own
+stream (independent replicas, weak scaling), value = total frames / max-over-ranks wall time.
+
+roofline: the dominant device kernel (the per-feature linearize kernel: triangulation + LM,
+Jacobians, left-nullspace reflections, chi2 Cholesky), timed with HIP events on the library's stream;
+achieved = the algorithmic FP64 FLOPs of its launches (SURVEY.md §8(d) F_feat formula on the actual
+feature shapes) / their event time.  cpu_baseline: the oracle/ CPU restatement (single-threaded, as
+the reference estimator is) on a bounded sample of the same stream, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+EUROC = os.path.join(ROOT, "configs", "euroc_mav", "estimator_config.yaml")
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (vector = matrix on gfx950)
+
+
+def cfg2_options(U):
+    return U.load_options(EUROC, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
+                          dt_slam_delay=1.0, record_timing=1)
+
+
+def make_stream(opts, n_frames, seed):
+    from uvio_amd.sim import SimStream
+    # 200 tracks reach the full window every frame (max-track MSCKF features), 10 % are lost early,
+    # 3 % live 3-5 windows (SLAM candidates)
+    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, spawn=200, frac_lost=0.10,
+                     frac_long=0.03)
+
+
+class Driver:
+    """Feeds one stream into one manager frame by frame (events precomputed)."""
+
+    def __init__(self, sim, mgr):
+        self.sim, self.mgr = sim, mgr
+        self.ev = [e for e in sim.events() if e[1] >= sim.t0 - 0.4]
+        self.k = 0
+        mgr.initialize_with_gt(sim.gt_state(sim.t0))
+
+    def step(self):
+        """Feed events up to and including the next camera frame; returns its timestamp."""
+        sim, mgr = self.sim, self.mgr
+        while True:
+            kind, t, i = self.ev[self.k]
+            self.k += 1
+            if kind == "imu":
+                mgr.feed_measurement_imu(t, sim.wm[i], sim.am[i])
+            elif kind == "uwb":
+                mgr.feed_measurement_uwb(t, sim.uwb[i][1], sim.uwb[i][2])
+            elif t > sim.t0:
+                mgr.feed_measurement_simulation(t, list(range(sim.K)), sim.frames[i])
+                return t
+
+
+def feat_flops(t):
+    return t["k_feat_flops"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--cpu-frames", type=int, default=60, help="timed oracle frames for cpu_baseline (0 = skip)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import uvio_amd as U
+
+    opts = cfg2_options(U)
+    n_frames = args.warmup + args.steps
+    sim = make_stream(opts, n_frames + 2, seed=5 + rank)
+    mgr = U.VioManager(opts, device=local)
+    drv = Driver(sim, mgr)
+    for _ in range(args.warmup):
+        drv.step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    acc = {"k_feat_s": 0.0, "k_feat_flops": 0.0, "k_feat_launches": 0, "rows": 0, "n_msckf": 0, "n_slam": 0,
+           "cols": 0, "cov_dim": 0}
+    pos_err = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t = drv.step()
+        tm = mgr.get_timing()
+        acc["k_feat_s"] += tm["k_feat_s"]
+        acc["k_feat_flops"] += tm["k_feat_flops"]
+        acc["k_feat_launches"] += tm["k_feat_launches"]
+        acc["rows"] += tm["msckf_rows"]
+        acc["n_msckf"] += tm["n_msckf"]
+        acc["n_slam"] += tm["n_slam"]
+        acc["cols"] = max(acc["cols"], tm["msckf_cols"])
+        acc["cov_dim"] = max(acc["cov_dim"], tm["cov_dim"])
+        _, x = mgr.get_imu_state()
+        pos_err.append(x[4:7] - sim.traj.pos(t))
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ate = float(np.sqrt(np.mean(np.sum(np.array(pos_err) ** 2, axis=1))))
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        launches = max(acc["k_feat_launches"], 1)
+        avg_s = acc["k_feat_s"] / launches
+        flops_per_launch = acc["k_feat_flops"] / launches
+        achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
+        cpu = None
+        if args.cpu_frames > 0:
+            cpu = cpu_baseline(opts, args.warmup, args.cpu_frames)
+        out = {
+            "metric": "VIO frames/sec (track+propagate+update) at clones x feats",
+            "value": value,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic EuRoC-shaped stream (uvio_amd/sim.py, seed 5+rank), TrackSIM front-end",
+            "config": {"workload": "cfg2 EuRoC V1_02-shaped stereo 752x480, 11 clones, <=200 MSCKF + 50 SLAM",
+                       "clones": int(opts.max_clone_size), "cameras": int(opts.num_cameras),
+                       "max_msckf_in_update": int(opts.max_msckf_in_update),
+                       "max_slam_features": int(opts.max_slam_features),
+                       "mean_msckf_feats": acc["n_msckf"] / args.steps, "mean_slam_feats": acc["n_slam"] / args.steps,
+                       "mean_msckf_rows": acc["rows"] / args.steps, "H_cols": acc["cols"],
+                       "state_dim": acc["cov_dim"], "parallelism": "replicas%d" % world},
+            "ate_rmse_m": ate,
+            "roofline": {"kernel": "k_feature (per-feature linearize, FP64)", "bound": "mfma",
+                         "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops_per_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(opts, warmup, frames):
+    """oracle/ (the CPU restatement) on the same stream, one thread, bounded sample."""
+    from oracle import oracle as O
+    sim = make_stream(opts, warmup + frames + 2, seed=5)
+    mgr = O.OracleManager(opts)
+    drv = Driver(sim, mgr)
+    for _ in range(warmup):
+        drv.step()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        drv.step()
+    dt = time.perf_counter() - t0
+    return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "%d frames of the cfg2 stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
+                      (frames, warmup)}
+
+
+if __name__ == "__main__":
+    main()

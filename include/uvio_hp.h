@@ -121,6 +121,12 @@ typedef struct {
   int n_msckf, n_slam, n_slam_delayed, n_clones, cov_dim;
   int msckf_rows;   /* stacked rows m before compression */
   int msckf_cols;   /* H columns n */
+  /* device-side measurement of the per-feature linearize kernel over this frame (HIP events on the
+   * library's stream): launches, summed kernel seconds, and algorithmic FP64 FLOPs of those launches
+   * (3 Householder reflections 12*(2m_f)*(n_f+4) + chi2 2 r n^2 + 2 r^2 n + r^3/3 per feature) */
+  int k_feat_launches;
+  double k_feat_s;
+  double k_feat_flops;
 } uvio_hp_timing_t;
 
 typedef struct uvio_hp uvio_hp_t;

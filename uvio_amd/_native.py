@@ -63,7 +63,8 @@ class Timing(C.Structure):
                 ("msckf_update", C.c_double), ("slam_update", C.c_double), ("slam_delayed", C.c_double),
                 ("marg", C.c_double), ("total", C.c_double), ("n_msckf", C.c_int), ("n_slam", C.c_int),
                 ("n_slam_delayed", C.c_int), ("n_clones", C.c_int), ("cov_dim", C.c_int),
-                ("msckf_rows", C.c_int), ("msckf_cols", C.c_int)]
+                ("msckf_rows", C.c_int), ("msckf_cols", C.c_int), ("k_feat_launches", C.c_int),
+                ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -92,6 +92,7 @@ struct DeviceBufs {
   double *dx_host = nullptr;
   int *neg_host = nullptr;
   DFeatOut *fout_host = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // feature-kernel timing
 };
 
 class Engine {

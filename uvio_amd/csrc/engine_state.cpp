@@ -218,6 +218,8 @@ Engine::~Engine() {
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
+  if (d_.ev0) hipEventDestroy(d_.ev0);
+  if (d_.ev1) hipEventDestroy(d_.ev1);
   if (d_.stream) hipStreamDestroy(d_.stream);
 }
 
@@ -235,6 +237,8 @@ void Engine::alloc_device() {
     throw HpError(UVIO_HP_E_DEVICE, "no HIP device " + std::to_string(device_));
   HP_HIP(hipSetDevice(device_));
   HP_HIP(hipStreamCreateWithFlags(&d_.stream, hipStreamNonBlocking));
+  HP_HIP(hipEventCreate(&d_.ev0));
+  HP_HIP(hipEventCreate(&d_.ev1));
   int C = o_.max_clone_size + 2;
   int K = o_.num_cameras;
   int cap = N_ + 6 * C + 3 * std::max(o_.max_slam_features, 0) + 5 * UVIO_HP_MAX_ANCHORS + 3 + 8;
@@ -271,13 +275,13 @@ void Engine::alloc_device() {
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
   dalloc(&d_.hidx, d_.max_ncol + d_.max_rows);
-  int rmax = std::max(d_.max_ncol, 2 * 64 * 25);
+  int rmax = std::max(d_.max_ncol, kMaxEkfRows);
   dalloc(&d_.ekf.M, (size_t)cap * rmax);
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
-  dalloc(&d_.ekf.S, (size_t)3 * rmax * rmax);
+  dalloc(&d_.ekf.S, (size_t)4 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.dx, cap);
-  dalloc(&d_.ekf.neg, 4);
+  dalloc(&d_.ekf.neg, 4 + d_.max_ncol);  // [0] negative-diagonal count, [1..] pivots
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
   for (int i = 1; i < 1000; i++) chi2_table_[i] = chi2_quantile95(i);
   HP_HIP(hipMemcpy(d_.chi2, chi2_table_.data(), 1000 * sizeof(double), hipMemcpyHostToDevice));
@@ -369,6 +373,7 @@ void Engine::apply_dx(const double *dx) {
 void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx,
                              const double *resdev, int res_stride, double sigma2) {
   if (r <= 0) return;
+  if (r > kMaxEkfRows) throw HpError(UVIO_HP_E_CAPACITY, "direct EKF update with more than 256 rows");
   HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
   HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
   launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, d_.hidx, resdev, res_stride, sigma2, d_.ekf);
@@ -529,6 +534,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   int ldh = n + 1;
   bool info = compress && r > n;
+  if (!info && r > kMaxEkfRows) return UVIO_HP_E_CAPACITY;
   int rw = std::max(r, n + 1);
   int nch = gram_num_chunks(r);
   double *dP, *dH, *dM, *dW, *dS, *dy, *ddx, *dPart = nullptr, *dG = nullptr;
@@ -537,7 +543,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   dalloc(&dH, (size_t)r * ldh);
   dalloc(&dM, (size_t)N * rw);
   dalloc(&dW, (size_t)N * rw);
-  dalloc(&dS, (size_t)3 * rw * rw);
+  dalloc(&dS, (size_t)4 * rw * rw);
   dalloc(&dy, rw);
   if (info) {
     dalloc(&dPart, (size_t)nch * ldh * ldh);
@@ -545,7 +551,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   }
   dalloc(&ddx, N);
   dalloc(&dI, n);
-  dalloc(&dneg, 1);
+  dalloc(&dneg, 2 + n);
   std::vector<double> Ha((size_t)r * ldh);
   for (int i = 0; i < r; i++) {
     std::memcpy(&Ha[(size_t)i * ldh], H + (size_t)i * n, sizeof(double) * n);

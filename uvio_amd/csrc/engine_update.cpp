@@ -575,11 +575,27 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   bp.fi_max_cond = o_.fi_max_cond_number;
   const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
   if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.meas.size()));
+  if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
   launch_feature_linearize(d_.stream, bp, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
+  if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
   HP_HIP(hipStreamSynchronize(d_.stream));
   outs.assign(d_.fout_host, d_.fout_host + nf);
+  if (o_.record_timing) {
+    float ms = 0.f;
+    HP_HIP(hipEventElapsedTime(&ms, d_.ev0, d_.ev1));
+    timing_.k_feat_launches += 1;
+    timing_.k_feat_s += 1e-3 * ms;
+    // algorithmic FP64 FLOPs (SURVEY.md §8(d) F_feat) of the features that reached the projection
+    for (int i = 0; i < nf; i++) {
+      if (outs[i].status == 1 || outs[i].status == 2) continue;
+      double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
+      double r = (mode == 1) ? rows : rows - 3.0;
+      double refl = (mode == 1) ? 0.0 : 12.0 * rows * (nfc + 4.0);
+      timing_.k_feat_flops += refl + 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
+    }
+  }
   if (mdump) {
     std::vector<double> h(8 * b.meas.size());
     HP_HIP(hipMemcpy(h.data(), bp.dbg, sizeof(double) * h.size(), hipMemcpyDeviceToHost));

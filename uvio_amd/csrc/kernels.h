@@ -118,6 +118,8 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 // EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j
 // maps to covariance index hidx[j] (device), residual res (r, device, stride res_stride), noise sigma2.
 // Scratch: M (N x r), W (N x r), S (3 r x r: Linv, global work, S_up), y (r), dx (N), neg (int).
+constexpr int kMaxEkfRows = 256;  // rows of one direct (uncompressed) EKF update
+// S holds 4 r^2 doubles for r rows
 struct EkfScratch {
   double *M, *W, *S, *y, *dx;
   int *neg;

@@ -648,20 +648,43 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   // ---- chi2: S = Hhat P_marg Hhat^T + s2 I, augmented with the residual row ----
   if (status0 == 0 && R > 0) {
     const int ldS = R + 1;
+    // T = Hhat P_f in 16-row chunks: thread d owns column d of the chunk (16 accumulators) and reads
+    // P[pid(d)][pid(c)] once per chunk (HBM/L2-resident P, unrolled for memory-level parallelism)
     for (int i0 = 0; i0 < R; i0 += 16) {
-      int nr = min(16, R - i0);
-      // Tc[ii][d] = sum_c Hhat[i0+ii][c] * P[pid(d)][pid(c)]
-      for (int e = tid; e < nr * nf; e += 256) {
-        int ii = e / nf, d = e % nf;
-        const double *hrow = Hl + (size_t)(r0 + i0 + ii) * ldl;
+      const int nr = min(16, R - i0);
+      for (int d = tid; d < nf; d += 256) {
         const double *Prow = P + (size_t)loc2pid[d] * bp.ldp;
-        double acc = 0.0;
-        for (int c = 0; c < nf; c++) acc += hrow[c] * Prow[loc2pid[c]];
-        Tc[ii * nf + d] = acc;
+        double acc[16];
+#pragma unroll
+        for (int ii = 0; ii < 16; ii++) acc[ii] = 0.0;
+        int c = 0;
+        for (; c + 4 <= nf; c += 4) {
+          double p0 = Prow[loc2pid[c]], p1 = Prow[loc2pid[c + 1]], p2 = Prow[loc2pid[c + 2]], p3 = Prow[loc2pid[c + 3]];
+#pragma unroll
+          for (int ii = 0; ii < 16; ii++) {
+            if (ii < nr) {
+              const double *h = Hl + (size_t)(r0 + i0 + ii) * ldl + c;
+              acc[ii] += h[0] * p0;
+              acc[ii] += h[1] * p1;
+              acc[ii] += h[2] * p2;
+              acc[ii] += h[3] * p3;
+            }
+          }
+        }
+        for (; c < nf; c++) {
+          double p0 = Prow[loc2pid[c]];
+#pragma unroll
+          for (int ii = 0; ii < 16; ii++)
+            if (ii < nr) acc[ii] += Hl[(size_t)(r0 + i0 + ii) * ldl + c] * p0;
+        }
+#pragma unroll
+        for (int ii = 0; ii < 16; ii++)
+          if (ii < nr) Tc[ii * nf + d] = acc[ii];
       }
       __syncthreads();
       for (int e = tid; e < nr * R; e += 256) {
         int ii = e / R, j = e % R;
+        if (j > i0 + ii) continue;  // lower triangle is all the Cholesky reads
         const double *hrow = Hl + (size_t)(r0 + j) * ldl;
         double acc = 0.0;
         for (int d = 0; d < nf; d++) acc += Tc[ii * nf + d] * hrow[d];
@@ -673,21 +696,22 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
     // residual row
     for (int j = tid; j < R; j += 256) S[R * ldS + j] = Hl[(size_t)(r0 + j) * ldl + nf];
     __syncthreads();
-    // lower Cholesky of the augmented matrix; last row becomes y = L^-1 r
-    for (int k = 0; k < R; k++) {
-      if (tid == 0) S[k * ldS + k] = sqrt(S[k * ldS + k]);
-      __syncthreads();
-      double dkk = S[k * ldS + k];
-      for (int i = k + 1 + tid; i <= R; i += 256) S[i * ldS + k] /= dkk;
-      __syncthreads();
-      int mm2 = R - k;  // rows k+1..R
-      for (int e = tid; e < mm2 * mm2; e += 256) {
-        int i = k + 1 + e / mm2, j = k + 1 + e % mm2;
-        if (j <= i && j < R) S[i * ldS + j] -= S[i * ldS + k] * S[j * ldS + k];
-      }
-      __syncthreads();
-    }
+    // lower Cholesky of the augmented matrix by wave 0 (lane i owns rows i, i+64, ...; no block
+    // barriers); the last row becomes y = L^-1 r and chi2 = |y|^2
     if (wave == 0) {
+      for (int k = 0; k < R; k++) {
+        wave_sync();
+        const double dkk = sqrt(S[k * ldS + k]);
+        for (int i = k + 1 + lane; i <= R; i += 64) S[i * ldS + k] /= dkk;
+        if (lane == 0) S[k * ldS + k] = dkk;
+        wave_sync();
+        for (int i = k + 1 + lane; i <= R; i += 64) {
+          const double lik = S[i * ldS + k];
+          const int jmax = min(i, R - 1);
+          for (int j = k + 1; j <= jmax; j++) S[i * ldS + j] -= lik * S[j * ldS + k];
+        }
+      }
+      wave_sync();
       double c2 = 0.0;
       for (int k = lane; k < R; k += 64) {
         double y = S[R * ldS + k];
