@@ -70,8 +70,15 @@ class Driver:
                 return t
 
 
-def feat_flops(t):
-    return t["k_feat_flops"]
+def max_over_ranks(x, device="cuda"):
+    """Whole-job wall time: the slowest rank's (one all-reduce, outside the timed region)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -125,11 +132,7 @@ def main():
         pos_err.append(x[4:7] - sim.traj.pos(t))
     barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(t1 - t0)
     ate = float(np.sqrt(np.mean(np.sum(np.array(pos_err) ** 2, axis=1))))
 
     if rank == 0:
