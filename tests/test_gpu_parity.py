@@ -210,3 +210,54 @@ def test_free_run_slam_parity(euroc_yaml):
     assert _rel(G[-1]["x"], Ov[-1]["x"]) < 1e-5
     dth, dp = _pose_err(G[-1], Ov[-1])
     assert dth < 1e-5 and dp < 1e-5, (dth, dp)
+
+
+def make_anchors(N):
+    """6 anchors at room corners / mid-walls, 2 fixed (uwb_config.yaml:6 n_anchors_to_fix 2)."""
+    pos = [(6, 6, 0.5), (-6, 6, 2.5), (-6, -6, 0.5), (6, -6, 2.5), (0, 7, 1.5), (7, 0, 1.0)]
+    out = []
+    for i, p in enumerate(pos):
+        a = N.Anchor()
+        a.id = 100 + i
+        a.fix = 1 if i < 2 else 0
+        for k in range(3):
+            a.p_AinG[k] = p[k]
+        a.const_bias, a.dist_bias = 0.0, 0.0
+        for k, v in enumerate([0.1, 0.1, 0.1, 0.01, 0.001]):
+            a.cov_diag[k] = v
+        out.append(a)
+    return out
+
+
+def test_lockstep_uwb_parity(euroc_yaml):
+    """UpdaterUWB::update_single (UpdaterUWB.cpp:53-90) + UVioPropagator + anchor init, lock-step."""
+    import uvio_amd as U
+    from uvio_amd import _native as N
+    from uvio_amd.sim import SimStream
+    from oracle import oracle as O
+    opts = U.load_options(euroc_yaml, max_msckf_in_update=60, max_slam_features=0, use_uwb=1,
+                          do_calib_uwb_extrinsics=1, min_dist_to_use_uwb=0.05)
+    for k, v in enumerate([0.05, -0.02, 0.03]):
+        opts.p_IinU[k] = v
+    anchors = make_anchors(N)
+    n = 30
+    sim = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=60, anchors=anchors, uwb_rate=10.0,
+                    uwb_sigma=0.1)
+    g, o = U.VioManager(opts), O.OracleManager(opts)
+    steps = []
+
+    def init(m):
+        m.try_to_initialize_uwb_anchors(anchors)
+
+    def before(nf, t):
+        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
+
+    def after(nf, t):
+        steps.append((_snap(g), _snap(o)))
+
+    sim.run([g, o], n_frames=n, before_frame=before, on_frame=after, after_init=init)
+    # 4 non-fixed anchors x 5 + p_IinU 3 extra state dims
+    assert steps[-1][0]["P"].shape[0] >= 15 + 1 + 28 + 6 * 12 + 20 + 3 - 6
+    worst_x = max(_rel(a["x"], b["x"]) for a, b in steps)
+    worst_P = max(_rel(a["P"], b["P"]) for a, b in steps)
+    assert worst_x < 1e-10 and worst_P < 1e-10, (worst_x, worst_P)

@@ -248,12 +248,15 @@ class SimStream:
         ev.sort(key=lambda e: (e[1] + (0.0 if e[0] == "imu" else lag), order[e[0]]))
         return ev
 
-    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None):
+    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None):
         """Drive one manager (or a list of managers in lock-step): initialize from ground truth at t0, then
-        feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed."""
+        feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed,
+        after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init)."""
         mgrs = mgr if isinstance(mgr, (list, tuple)) else [mgr]
         for m in mgrs:
             m.initialize_with_gt(self.gt_state(self.t0))
+            if after_init is not None:
+                after_init(m)
         nf = 0
         for kind, t, i in self.events():
             if t < self.t0 - 0.4:
