@@ -1,0 +1,32 @@
+"""Per-phase cycle counts of the feature kernel (UVIO_HP_FEAT_TS debug dump) on the bench stream."""
+import os, sys
+sys.path.insert(0, '.')
+import numpy as np
+os.makedirs("gpurun_out", exist_ok=True)
+path = "gpurun_out/feat_ts.bin"
+if os.path.exists(path):
+    os.remove(path)
+import bench, uvio_amd as U
+opts = bench.cfg2_options(U)
+sim = bench.make_stream(opts, 80, seed=5)
+mgr = U.VioManager(opts)
+drv = bench.Driver(sim, mgr)
+for _ in range(60):
+    drv.step()
+os.environ["UVIO_HP_FEAT_TS"] = path
+for _ in range(10):
+    drv.step()
+os.environ.pop("UVIO_HP_FEAT_TS")
+a = np.fromfile(path, dtype=np.int64).reshape(-1, 12)
+names = ["setup", "geom", "jacob", "nullsp", "T/S", "chol", "output"]
+for mode in sorted(set(a[:, 0])):
+    for big in (False, True):
+        sel = a[(a[:, 0] == mode) & ((a[:, 1] > 1) == big)]
+        if len(sel) == 0:
+            continue
+        ts = sel[:, 4:12].astype(float)
+        d = np.diff(ts, axis=1)
+        d[d < 0] = np.nan
+        print("mode %d %s launches-feats %d  meas %.1f nf %.1f | " % (mode, "batch" if big else "single", len(sel),
+              sel[:, 2].mean(), sel[:, 3].mean()) + "  ".join("%s %.0f" % (n, v) for n, v in zip(names, np.nanmean(d, axis=0))),
+              " total %.0f cyc" % np.nanmean(ts[:, 7] - ts[:, 0]))

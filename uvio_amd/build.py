@@ -23,6 +23,7 @@ SOURCES = [
     "capi.cpp",
     "kernels_cov.hip",
     "kernels_feat.hip",
+    "kernels_chi2.hip",
 ]
 
 

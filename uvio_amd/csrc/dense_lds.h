@@ -1,0 +1,84 @@
+// Small dense factorizations for ONE workgroup, matrices resident in LDS.
+//
+// The estimator's dense solves are small (r, n <= ~256) and sequential by nature, so they are
+// latency bound: the cost is (number of sequential steps) x (latency of one step).  Long dependent
+// chains inside a step (a single lane walking a row through LDS, or a wave-level 16x16 factor with
+// v_readlane hops) cost far more than the barrier itself, so both routines take ONE barrier per
+// column and make every step a flat parallel update whose only latency is one LDS round trip:
+//   ldl_inplace      : right-looking LDL^T with unnormalized columns (no intra-step race); extra rows
+//                      below n are right-hand sides (an appended residual row yields L_unit^-1 r, so
+//                      chi2 = sum_k z_k^2 / d_k without a triangular solve);
+//   ldl_to_chol      : L D^1/2 (the LLT factor StateHelper.cpp:160 uses) in one parallel pass;
+//   trtri_gj_inplace : L^-1 by in-place Gauss-Jordan, one thread per row, one barrier per column.
+// Measured on MI355X (tools/bench_dense.hip): see DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace uvhp {
+
+// LDS bytes for an (nrows x n) factorization: A with an odd row stride (ld = n | 1)
+__host__ __device__ inline size_t dense_lds_bytes(int nrows, int n) { return (size_t)nrows * (n | 1) * sizeof(double); }
+
+// In-place LDL^T of the n x n lower triangle of A (right-looking, ONE barrier per column): after
+// it, A[k][k] = d_k and A[i][k] = d_k L[i][k] for i > k (columns are left unnormalized, so step k
+// only reads column k and writes columns > k -- no intra-step race).  Rows n .. nrows-1 are extra
+// right-hand-side rows: they leave as z = L_unit^-1 b (unnormalized, z_k = d_k (row)_k).
+// Thread mapping: 8 consecutive lanes share a row and stride its columns by 8 (rows never straddle
+// a wavefront, no integer division in the loop).
+constexpr int kRowLanes = 8;
+__device__ void ldl_inplace(double *A, int ld, int n, int nrows) {
+  const int c0 = threadIdx.x % kRowLanes, rstep = blockDim.x / kRowLanes;
+  for (int k = 0; k < n; k++) {
+    const double dinv = 1.0 / A[k * ld + k];
+    const double *__restrict__ colk = A + k;
+    for (int i = k + 1 + threadIdx.x / kRowLanes; i < nrows; i += rstep) {
+      double *__restrict__ Ai = A + i * ld;
+      const double aik = Ai[k] * dinv;
+      const int jmax = min(i, n - 1);
+      for (int j = k + 1 + c0; j <= jmax; j += kRowLanes) Ai[j] -= aik * colk[j * ld];
+    }
+    __syncthreads();
+  }
+}
+
+// LDL^T (as left by ldl_inplace) -> Cholesky factor L D^1/2 in place; extra rows -> b L^-T.
+__device__ void ldl_to_chol(double *A, int ld, int n, int nrows) {
+  const int c0 = threadIdx.x % kRowLanes, rstep = blockDim.x / kRowLanes;
+  for (int i = threadIdx.x / kRowLanes; i < nrows; i += rstep) {
+    const int jmax = min(i - 1, n - 1);
+    for (int k = c0; k <= jmax; k += kRowLanes) A[i * ld + k] *= 1.0 / sqrt(A[k * ld + k]);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += blockDim.x) A[k * ld + k] = sqrt(A[k * ld + k]);
+  __syncthreads();
+}
+
+// In-place inverse of a lower-triangular L by Gauss-Jordan elimination (ONE barrier per column).
+// Row i keeps its not-yet-eliminated L entries at columns >= k and the inverse's entries at columns
+// < k; the final pass divides by the pivots.  8 lanes per row as in ldl_inplace; the lanes of a row
+// read A[i][k] before the row's first lane overwrites it (same wavefront, in-order LDS).
+__device__ void trtri_gj_inplace(double *A, int ld, int n) {
+  const int c0 = threadIdx.x % kRowLanes, rstep = blockDim.x / kRowLanes;
+  for (int k = 0; k < n; k++) {
+    const double pinv = 1.0 / A[k * ld + k];
+    const double *__restrict__ Rk = A + k * ld;
+    for (int i = k + 1 + threadIdx.x / kRowLanes; i < n; i += rstep) {
+      double *__restrict__ Ri = A + i * ld;
+      const double f = Ri[k] * pinv;
+      for (int j = c0; j < k; j += kRowLanes) Ri[j] -= f * Rk[j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (c0 == 0) Ri[k] = -f;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x / kRowLanes; i < n; i += rstep) {
+    const double s = 1.0 / A[i * ld + i];
+    for (int j = c0; j < i; j += kRowLanes) A[i * ld + j] *= s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) A[i * ld + i] = 1.0 / A[i * ld + i];
+  __syncthreads();
+}
+
+}  // namespace uvhp

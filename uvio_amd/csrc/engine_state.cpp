@@ -213,7 +213,7 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
 Engine::~Engine() {
   hipSetDevice(device_);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
-                  d_.fout, d_.chi2, d_.H, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
+                  d_.fout, d_.chi2, d_.H, d_.Tall, d_.Pc, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
                   d_.ekf.dx, d_.ekf.neg};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -271,6 +271,8 @@ void Engine::alloc_device() {
   dalloc(&d_.fout, maxf);
   dalloc(&d_.chi2, 1000);
   dalloc(&d_.H, (size_t)d_.max_rows * d_.ldh);
+  dalloc(&d_.Tall, (size_t)d_.max_rows * d_.ldh);
+  dalloc(&d_.Pc, (size_t)d_.max_ncol * d_.max_ncol);
   int maxch = (d_.max_rows + 511) / 512 + 1;
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
@@ -278,7 +280,7 @@ void Engine::alloc_device() {
   int rmax = std::max(d_.max_ncol, kMaxEkfRows);
   dalloc(&d_.ekf.M, (size_t)cap * rmax);
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
-  dalloc(&d_.ekf.S, (size_t)4 * rmax * rmax);
+  dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.dx, cap);
   dalloc(&d_.ekf.neg, 4 + d_.max_ncol);  // [0] negative-diagonal count, [1..] pivots
@@ -543,7 +545,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   dalloc(&dH, (size_t)r * ldh);
   dalloc(&dM, (size_t)N * rw);
   dalloc(&dW, (size_t)N * rw);
-  dalloc(&dS, (size_t)4 * rw * rw);
+  dalloc(&dS, (size_t)5 * rw * rw);
   dalloc(&dy, rw);
   if (info) {
     dalloc(&dPart, (size_t)nch * ldh * ldh);

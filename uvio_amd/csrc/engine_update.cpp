@@ -575,9 +575,20 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   bp.fi_max_cond = o_.fi_max_cond_number;
   const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
   if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.meas.size()));
+  const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
+  if (tsdump) HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 8 * nf));
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
   launch_feature_linearize(d_.stream, bp, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
+  {
+    int max_rows_f = 0;
+    for (auto &F : b.feats) {
+      int rows_out = (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
+      max_rows_f = std::max(max_rows_f, rows_out - (mode >= 2 ? 3 : 0));
+    }
+    launch_chi2_batch(d_.stream, bp, d_.feats, d_.P, d_.hidx, d_.H, b.rows, d_.Tall, d_.Pc, d_.chi2, d_.fout,
+                      max_rows_f);
+  }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
   HP_HIP(hipStreamSynchronize(d_.stream));
@@ -595,6 +606,18 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
       double refl = (mode == 1) ? 0.0 : 12.0 * rows * (nfc + 4.0);
       timing_.k_feat_flops += refl + 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
     }
+  }
+  if (tsdump) {
+    std::vector<long long> h(8 * (size_t)nf);
+    HP_HIP(hipMemcpy(h.data(), bp.dbg_ts, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+    HP_HIP(hipFree(bp.dbg_ts));
+    FILE *fp = std::fopen(tsdump, "ab");
+    for (int i = 0; i < nf; i++) {
+      long long rec[12] = {mode, nf, b.feats[i].nmeas, b.feats[i].nf};
+      for (int k = 0; k < 8; k++) rec[4 + k] = h[8 * (size_t)i + k];
+      std::fwrite(rec, sizeof(long long), 12, fp);
+    }
+    std::fclose(fp);
   }
   if (mdump) {
     std::vector<double> h(8 * b.meas.size());

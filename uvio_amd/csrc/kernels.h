@@ -88,7 +88,8 @@ struct DBatchParams {
   int fi_max_runs, fi_refine, fi_tri1d;
   double fi_init_lamda, fi_max_lamda, fi_min_dx, fi_min_dcost, fi_lam_mult;
   double fi_min_dist, fi_max_dist, fi_max_baseline, fi_max_cond;
-  double *dbg;  // optional per-measurement debug record (8 doubles each), nullptr in production
+  double *dbg;         // optional per-measurement debug record (8 doubles each), nullptr in production
+  long long *dbg_ts;   // optional per-feature phase timestamps (8 per feature), nullptr in production
 };
 
 // ---- launch wrappers (all asynchronous on `s`) ----
@@ -107,6 +108,11 @@ void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg);
 void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const DMeas *meas,
                               const DVar *vars, const DClone *clones, const DCam *cams, const double *P,
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf);
+// batched chi2 gate (kernels_chi2.hip): P_can gather, T = H_all P_can, per-feature S / LDL^T / chi2;
+// rejected MSCKF / SLAM features get zero rows.  Pc: n^2, T_all: like H_all.
+void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
+                       double *H_all, int m, double *T_all, double *Pc, const double *chi2_table, DFeatOut *out,
+                       int max_rows_f);
 size_t feature_lds_bytes(int max_meas, int max_nf);
 
 // Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->
@@ -118,8 +124,9 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 // EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j
 // maps to covariance index hidx[j] (device), residual res (r, device, stride res_stride), noise sigma2.
 // Scratch: M (N x r), W (N x r), S (3 r x r: Linv, global work, S_up), y (r), dx (N), neg (int).
-constexpr int kMaxEkfRows = 256;  // rows of one direct (uncompressed) EKF update
-// S holds 4 r^2 doubles for r rows
+constexpr int kMaxEkfRows = 256;
+constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-workgroup solvers  // rows of one direct (uncompressed) EKF update
+// S holds 5 r^2 doubles for r rows
 struct EkfScratch {
   double *M, *W, *S, *y, *dx;
   int *neg;

@@ -1,0 +1,189 @@
+// Batched chi2 gate for a linearized update batch (UpdaterMSCKF.cpp:209-234, UpdaterSLAM.cpp:207-226
+// and :370-391, StateHelper::initialize :451-470).
+//
+// Every feature's projected rows [Hhat_f | r_f] sit in H_all over the batch's canonical columns, and
+// every feature's P_marg is a principal block of the same canonical covariance P_can = P[hidx, hidx]
+// (zero columns of Hhat_f drop out).  So
+//     T = H_all P_can                    one FP64 GEMM over the whole batch (m x n x n),
+//     S_f = T_f Hhat_f^T + s2 I          per feature, R_f x R_f,
+// and the per-feature work is only the small S_f and its factorization.  One workgroup per feature
+// stages T_f and Hhat_f in LDS, forms the lower triangle of [S_f ; r_f^T], runs the one-barrier-per-
+// column LDL^T of dense_lds.h (the appended residual row becomes z = L_unit^-1 r), and
+// chi2 = sum_k z_k^2 / d_k = r^T S^-1 r.  Rejected MSCKF / SLAM features get their rows zeroed so the
+// batch Gram (compression) and the direct EKF see only accepted rows.
+#include "dense_lds.h"
+#include "kernels.h"
+
+namespace uvhp {
+
+// P_can[a][b] = P[hidx[a]][hidx[b]]   (n x n)
+__global__ void k_gather_can(const double *__restrict__ P, int ldp, const int *__restrict__ hidx, int n,
+                             double *__restrict__ Pc) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * n) return;
+  int a = e / n, b = e - a * n;
+  Pc[e] = P[(size_t)hidx[a] * ldp + hidx[b]];
+}
+
+// T (m x n, ld ldt) = H (m x n, ld ldh) * Pc (n x n).  64x64 block tiles, 256 threads with 4x4
+// register tiles, K in steps of 16 through LDS.
+constexpr int GB = 64, GK = 16;
+__global__ void __launch_bounds__(256) k_gemm_HP(const double *__restrict__ H, int m, int n, int ldh,
+                                                 const double *__restrict__ Pc, double *__restrict__ T, int ldt) {
+  __shared__ double As[GK][GB + 1];  // As[k][row]
+  __shared__ double Bs[GK][GB + 1];  // Bs[k][col]
+  const int tid = threadIdx.x, tr = tid / 16, tc = tid % 16;
+  const int i0 = blockIdx.y * GB, j0 = blockIdx.x * GB;
+  double acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
+  for (int k0 = 0; k0 < n; k0 += GK) {
+    for (int e = tid; e < GB * GK; e += 256) {
+      int r = e / GK, k = e % GK;  // H tile: coalesced along k
+      int gi = i0 + r, gk = k0 + k;
+      As[k][r] = (gi < m && gk < n) ? H[(size_t)gi * ldh + gk] : 0.0;
+      int kk = e / GB, c = e % GB;  // Pc tile: coalesced along columns
+      int gkk = k0 + kk, gj = j0 + c;
+      Bs[kk][c] = (gkk < n && gj < n) ? Pc[(size_t)gkk * n + gj] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < GK; k++) {
+      double a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        a[q] = As[k][tr + 16 * q];
+        b[q] = Bs[k][tc + 16 * q];
+      }
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] += a[x] * b[y];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int x = 0; x < 4; x++)
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+      int gi = i0 + tr + 16 * x, gj = j0 + tc + 16 * y;
+      if (gi < m && gj < n) T[(size_t)gi * ldt + gj] = acc[x][y];
+    }
+}
+
+size_t chi2_lds_bytes(int max_rows_f, int n) {
+  size_t R = max_rows_f;
+  return (2 * R * (size_t)n + (R + 1) * (R | 1)) * sizeof(double);
+}
+
+// One workgroup per feature.  out[f] carries the feature kernel's status / rows; chi2 rows are the
+// feature's H_all rows from c0 = (mode >= 2 ? 3 : 0) on (delayed init tests the update rows against
+// chi2(dof = all rows), StateHelper.cpp:463-468).
+__global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
+                                              const double *__restrict__ T_all, const double *__restrict__ chi2_table,
+                                              DFeatOut *__restrict__ out, int use_lds) {
+  extern __shared__ double lds[];
+  __shared__ double red[256];
+  __shared__ int st;
+  const int f = blockIdx.x;
+  const DFeat F = feats[f];
+  const DFeatOut o = out[f];
+  if (o.status != 0 || o.rows <= 0) return;
+  const int n = bp.n_canon, ldh = bp.ldh;
+  const int c0 = (F.mode >= 2) ? 3 : 0;
+  const int R = o.rows - c0;
+  const int tid = threadIdx.x;
+  if (R <= 0) {
+    if (tid == 0) out[f].chi2 = 0.0;
+    return;
+  }
+  const double *Hg = H_all + (size_t)(F.row_off + c0) * ldh;
+  const double *Tg = T_all + (size_t)(F.row_off + c0) * ldh;
+  const double *Hs = Hg, *Ts = Tg;
+  int ldx = ldh;
+  double *S = lds;
+  const int ldS = R | 1;
+  if (use_lds) {
+    double *Hl = lds + (size_t)(R + 1) * ldS;
+    double *Tl = Hl + (size_t)R * n;
+    for (int e = tid; e < R * n; e += blockDim.x) {
+      int i = e / n, j = e - i * n;
+      Hl[e] = Hg[(size_t)i * ldh + j];
+      Tl[e] = Tg[(size_t)i * ldh + j];
+    }
+    Hs = Hl;
+    Ts = Tl;
+    ldx = n;
+    __syncthreads();
+  }
+  // lower triangle of S = T Hhat^T + s2 I, and the residual row
+  for (int e = tid; e < R * R; e += blockDim.x) {
+    int i = e / R, j = e - i * R;
+    if (j > i) continue;
+    const double *ti = Ts + (size_t)i * ldx, *hj = Hs + (size_t)j * ldx;
+    double a0 = 0.0, a1 = 0.0;
+    int k = 0;
+    for (; k + 2 <= n; k += 2) {
+      a0 += ti[k] * hj[k];
+      a1 += ti[k + 1] * hj[k + 1];
+    }
+    if (k < n) a0 += ti[k] * hj[k];
+    S[i * ldS + j] = a0 + a1 + (i == j ? bp.sigma_pix_sq : 0.0);
+  }
+  for (int j = tid; j < R; j += blockDim.x) S[R * ldS + j] = Hg[(size_t)j * ldh + n];
+  __syncthreads();
+  ldl_inplace(S, ldS, R, R + 1);
+  double c2 = 0.0;
+  for (int k = tid; k < R; k += blockDim.x) {
+    double z = S[R * ldS + k];
+    c2 += z * z / S[k * ldS + k];
+  }
+  red[tid] = c2;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double chi2 = red[0];
+    double thr = chi2_table[min(F.mode >= 2 ? o.rows : R, 999)];
+    int reject = chi2 > bp.chi2_mult * thr;
+    out[f].chi2 = chi2;
+    if (reject) {
+      out[f].status = 3;
+      out[f].rows = 0;
+    }
+    st = reject;
+  }
+  __syncthreads();
+  if (st && F.mode <= 1) {
+    double *rows = H_all + (size_t)F.row_off * ldh;
+    for (int e = tid; e < o.rows * (n + 1); e += blockDim.x) {
+      int i = e / (n + 1), j = e - i * (n + 1);
+      rows[(size_t)i * ldh + j] = 0.0;
+    }
+  }
+}
+
+void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
+                       double *H_all, int m, double *T_all, double *Pc, const double *chi2_table, DFeatOut *out,
+                       int max_rows_f) {
+  if (bp.nfeat <= 0 || m <= 0) return;
+  const int n = bp.n_canon;
+  hipLaunchKernelGGL(k_gather_can, dim3((n * n + 255) / 256), dim3(256), 0, s, P, bp.ldp, hidx, n, Pc);
+  dim3 g((n + GB - 1) / GB, (m + GB - 1) / GB);
+  hipLaunchKernelGGL(k_gemm_HP, g, dim3(256), 0, s, H_all, m, n, bp.ldh, Pc, T_all, bp.ldh);
+  size_t bytes = chi2_lds_bytes(max_rows_f, n);
+  int use_lds = bytes <= kMaxDynLds;
+  if (!use_lds) bytes = (size_t)(max_rows_f + 1) * (max_rows_f | 1) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_chi2, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds);
+}
+
+}  // namespace uvhp

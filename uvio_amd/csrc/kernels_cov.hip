@@ -9,6 +9,7 @@
 //   EKFUpdate              StateHelper.cpp:116-197 as M = P[:,I] H^T, S = H M[I,:] + s2 I = L L^T,
 //                          W = M L^-T, P -= W W^T (upper, mirrored), dx = W L^-1 r.
 #include "kernels.h"
+#include "dense_lds.h"
 
 namespace uvhp {
 
@@ -281,62 +282,29 @@ __global__ void __launch_bounds__(256) k_ekf_S(const double *__restrict__ H, int
   if (a < r && b < r) Sout[(size_t)a * r + b] = acc + (a == b ? s2 : 0.0);
 }
 
-// Single workgroup: S = L L^T on the upper triangle of S_up (selfadjointView<Upper>, StateHelper.cpp:160);
-// Linv in place; y = Linv res.  Work buffer: LDS when r*r*8 <= 150 KiB, else global `Sg`.
-__global__ void __launch_bounds__(1024) k_ekf_small(const double *__restrict__ Sup, int r,
-                                                    const double *__restrict__ res, int res_stride,
-                                                    double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
-                                                    int use_lds) {
+// Single workgroup (512 threads): LDL^T-based Cholesky of the augmented [S ; res^T] (S from the upper
+// triangle of S_up = selfadjointView<Upper>, StateHelper.cpp:160) -> L and y = L^-1 res, then L^-1 in
+// place (dense_lds.h).  LDS when (r+1) r + 16 r doubles fit, else the global scratch `Sg`.
+__global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Sup, int r,
+                                                   const double *__restrict__ res, int res_stride,
+                                                   double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
+                                                   int use_lds) {
   extern __shared__ double lds[];
-  double *S = use_lds ? lds : Sg;
-  __shared__ double tmp[1024];
+  double *A = use_lds ? lds : Sg;
+  const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
   for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
     int a = e / r, b = e % r;
-    if (b <= a) S[e] = Sup[(size_t)b * r + a];
+    if (b <= a) A[(size_t)a * ld + b] = Sup[(size_t)b * r + a];
   }
+  for (int j = threadIdx.x; j < r; j += blockDim.x) A[(size_t)r * ld + j] = res[(size_t)j * res_stride];
   __syncthreads();
-  // right-looking lower Cholesky on the lower triangle
-  for (int k = 0; k < r; k++) {
-    if (threadIdx.x == 0) S[k * r + k] = sqrt(S[k * r + k]);
-    __syncthreads();
-    double d = S[k * r + k];
-    for (int i = k + 1 + threadIdx.x; i < r; i += blockDim.x) S[i * r + k] /= d;
-    __syncthreads();
-    int m = r - k - 1;
-    for (int e = threadIdx.x; e < m * m; e += blockDim.x) {
-      int i = k + 1 + e / m, j = k + 1 + e % m;
-      if (j <= i) S[i * r + j] -= S[i * r + k] * S[j * r + k];
-    }
-    __syncthreads();
-  }
-  // y = L^-1 res (forward substitution, one thread per step with a parallel dot)
-  for (int i = threadIdx.x; i < r; i += blockDim.x) tmp[i] = res[(size_t)i * res_stride];
-  __syncthreads();
-  for (int k = 0; k < r; k++) {
-    if (threadIdx.x == 0) tmp[k] /= S[k * r + k];
-    __syncthreads();
-    for (int i = k + 1 + threadIdx.x; i < r; i += blockDim.x) tmp[i] -= S[i * r + k] * tmp[k];
-    __syncthreads();
-  }
-  for (int i = threadIdx.x; i < r; i += blockDim.x) y_out[i] = tmp[i];
-  // in-place inverse of lower-triangular L (LAPACK trti2, lower, backward over columns)
-  for (int j = r - 1; j >= 0; j--) {
-    if (threadIdx.x == 0) S[j * r + j] = 1.0 / S[j * r + j];
-    __syncthreads();
-    double ajj = -S[j * r + j];
-    // x = Linv[j+1:, j+1:] * L[j+1:, j]
-    for (int i = j + 1 + threadIdx.x; i < r; i += blockDim.x) {
-      double acc = 0.0;
-      for (int k = j + 1; k <= i; k++) acc += S[i * r + k] * S[k * r + j];
-      tmp[i] = acc;
-    }
-    __syncthreads();
-    for (int i = j + 1 + threadIdx.x; i < r; i += blockDim.x) S[i * r + j] = ajj * tmp[i];
-    __syncthreads();
-  }
+  ldl_inplace(A, ld, r, r + 1);
+  ldl_to_chol(A, ld, r, r + 1);
+  for (int j = threadIdx.x; j < r; j += blockDim.x) y_out[j] = A[(size_t)r * ld + j];
+  trtri_gj_inplace(A, ld, r);
   for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
     int a = e / r, b = e % r;
-    Linv_out[e] = (b <= a) ? S[e] : 0.0;
+    Linv_out[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
   }
 }
 
@@ -407,13 +375,13 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
 
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc) {
-  size_t bytes = (size_t)r * r * sizeof(double);
-  int use_lds = bytes <= 150 * 1024;
+  size_t bytes = dense_lds_bytes(r + 1, r);
+  int use_lds = bytes <= kMaxDynLds;
   double *Linv = sc.S;
-  double *Sg = sc.S + (size_t)r * r;
   double *Sup = sc.S + 2 * (size_t)r * r;
+  double *Sg = sc.S + 3 * (size_t)r * r;  // dense_lds_bytes(r+1, r) <= 2 r^2 doubles once r >= 40 (else LDS)
   ensure_lds_attrs();
-  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(1024), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
+  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
                      use_lds);
   dim3 gM((r + 15) / 16, (N + 15) / 16);
   hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, r, Linv, sc.W);
@@ -451,131 +419,112 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ 
   G[e] = acc;
 }
 
-// Single workgroup: K = G_nn P_II + s2 I, LU with partial pivoting, [Q | y] = K^-1 [G_nn | b];
-// Q is symmetrised.  K and the right-hand sides live in LDS when 2 n (n+1) doubles fit, else in `gbuf`.
-__global__ void __launch_bounds__(1024) k_info_small(const double *__restrict__ G, int n, const double *__restrict__ P,
-                                                     int ldp, const int *__restrict__ hidx, double s2,
-                                                     double *__restrict__ Q, double *__restrict__ y, double *gbuf,
-                                                     int use_lds) {
-  extern __shared__ double lds[];
-  double *K = use_lds ? lds : gbuf;      // n x n
-  double *B = K + (size_t)n * n;         // n x (n+1)
-  __shared__ double rv[1024];
-  __shared__ int ri[1024];
-  __shared__ int piv_row;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int nc = n + 1, ldg = n + 1;
-  // K[a][b] = sum_c G[a][c] P[hidx[c]][hidx[b]] (+ s2 on the diagonal)
-  for (int e = tid; e < n * n; e += nt) {
-    int a = e / n, b = e % n;
-    const double *Pb = P + (size_t)hidx[b];
-    double acc = 0.0;
-    for (int c = 0; c < n; c++) acc += G[(size_t)a * ldg + c] * Pb[(size_t)hidx[c] * ldp];
-    K[e] = acc + (a == b ? s2 : 0.0);
+// C (m x n) = op(A) op(B), 16x16 tiles; op(X) = X or X^T.  Small dense products of the info path.
+__global__ void __launch_bounds__(256) k_gemm(int ta, int tb, int m, int n, int k, const double *__restrict__ A,
+                                              int lda, const double *__restrict__ B, int ldb, double *__restrict__ C,
+                                              int ldc) {
+  __shared__ double As[16][17];
+  __shared__ double Bs[16][17];
+  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  double acc = 0.0;
+  for (int k0 = 0; k0 < k; k0 += 16) {
+    int ai = i0 + ty, ak = k0 + tx;
+    As[ty][tx] = (ai < m && ak < k) ? (ta ? A[(size_t)ak * lda + ai] : A[(size_t)ai * lda + ak]) : 0.0;
+    int bk = k0 + ty, bj = j0 + tx;
+    Bs[ty][tx] = (bk < k && bj < n) ? (tb ? B[(size_t)bj * ldb + bk] : B[(size_t)bk * ldb + bj]) : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) acc += As[ty][kk] * Bs[kk][tx];
+    __syncthreads();
   }
-  for (int e = tid; e < n * nc; e += nt) {
-    int a = e / nc, b = e % nc;
-    B[e] = G[(size_t)a * ldg + b];
+  if (i0 + ty < m && j0 + tx < n) C[(size_t)(i0 + ty) * ldc + j0 + tx] = acc;
+}
+
+// Single workgroup: P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1),
+// zero upper) and L_P^-1 (n x n).
+__global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
+                                                    int n, double *__restrict__ Laug, double *__restrict__ Linv,
+                                                    double *gbuf, int use_lds) {
+  extern __shared__ double lds[];
+  double *A = use_lds ? lds : gbuf;
+  const int ld = n | 1;
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    int a = e / n, b = e % n;
+    if (b <= a) A[(size_t)a * ld + b] = P[(size_t)hidx[a] * ldp + hidx[b]];
   }
   __syncthreads();
-  for (int k = 0; k < n; k++) {
-    // pivot: largest |K[i][k]|, i >= k (lowest index on ties)
-    double best = -1.0;
-    int bi = k;
-    for (int i = k + tid; i < n; i += nt) {
-      double v = fabs(K[(size_t)i * n + k]);
-      if (v > best) best = v, bi = i;
-    }
-    rv[tid] = best;
-    ri[tid] = bi;
-    __syncthreads();
-    for (int w = nt / 2; w > 0; w >>= 1) {
-      if (tid < w) {
-        double o = rv[tid + w];
-        int oi = ri[tid + w];
-        if (o > rv[tid] || (o == rv[tid] && oi < ri[tid])) rv[tid] = o, ri[tid] = oi;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) piv_row = ri[0];
-    __syncthreads();
-    int p = piv_row;
-    if (p != k) {
-      for (int j = tid; j < n; j += nt) {
-        double t = K[(size_t)k * n + j];
-        K[(size_t)k * n + j] = K[(size_t)p * n + j];
-        K[(size_t)p * n + j] = t;
-      }
-      for (int j = tid; j < nc; j += nt) {
-        double t = B[(size_t)k * nc + j];
-        B[(size_t)k * nc + j] = B[(size_t)p * nc + j];
-        B[(size_t)p * nc + j] = t;
-      }
-      __syncthreads();
-    }
-    double dkk = K[(size_t)k * n + k];
-    for (int i = k + 1 + tid; i < n; i += nt) K[(size_t)i * n + k] /= dkk;
-    __syncthreads();
-    int m = n - k - 1;
-    for (int e = tid; e < m * m; e += nt) {
-      int i = k + 1 + e / m, j = k + 1 + e % m;
-      K[(size_t)i * n + j] -= K[(size_t)i * n + k] * K[(size_t)k * n + j];
-    }
-    for (int e = tid; e < m * nc; e += nt) {
-      int i = k + 1 + e / nc, j = e % nc;
-      B[(size_t)i * nc + j] -= K[(size_t)i * n + k] * B[(size_t)k * nc + j];
-    }
-    __syncthreads();
+  ldl_inplace(A, ld, n, n);
+  ldl_to_chol(A, ld, n, n);
+  const int na = n + 1;
+  for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
+    int a = e / na, b = e % na;
+    double v = 0.0;
+    if (a < n && b < n) v = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    else if (a == n && b == n) v = 1.0;
+    Laug[e] = v;
   }
-  // back substitution U X = B
-  for (int k = n - 1; k >= 0; k--) {
-    double ukk = K[(size_t)k * n + k];
-    for (int j = tid; j < nc; j += nt) B[(size_t)k * nc + j] /= ukk;
-    __syncthreads();
-    for (int e = tid; e < k * nc; e += nt) {
-      int i = e / nc, j = e % nc;
-      B[(size_t)i * nc + j] -= K[(size_t)i * n + k] * B[(size_t)k * nc + j];
-    }
-    __syncthreads();
-  }
-  for (int e = tid; e < n * n; e += nt) {
+  __syncthreads();
+  trtri_gj_inplace(A, ld, n);
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
     int a = e / n, b = e % n;
-    Q[e] = 0.5 * (B[(size_t)a * nc + b] + B[(size_t)b * nc + a]);
+    Linv[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
   }
-  for (int a = tid; a < n; a += nt) y[a] = B[(size_t)a * nc + n];
 }
 
-// M = P[:, hidx]  (N x n)
-__global__ void k_gather_cols(const double *__restrict__ P, int ldp, int N, const int *__restrict__ hidx, int n,
-                              double *__restrict__ M) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= N * n) return;
-  int i = e / n, k = e % n;
-  M[e] = P[(size_t)i * ldp + hidx[k]];
+// Single workgroup: [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T
+// -> w = U^-1 c; then U^-1 in place.  Writes U^-1 (n x n) and w (n).
+__global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
+                                                    double *__restrict__ Uinv, double *__restrict__ w, double *gbuf,
+                                                    int use_lds) {
+  extern __shared__ double lds[];
+  double *A = use_lds ? lds : gbuf;
+  const int ld = n | 1;
+  const int na = n + 1;
+  for (int e = threadIdx.x; e < (n + 1) * n; e += blockDim.x) {
+    int a = e / n, b = e % n;
+    if (b <= a) A[(size_t)a * ld + b] = E[(size_t)a * na + b] + ((a == b) ? s2 : 0.0);
+  }
+  __syncthreads();
+  ldl_inplace(A, ld, n, n + 1);
+  ldl_to_chol(A, ld, n, n + 1);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[(size_t)n * ld + j];
+  trtri_gj_inplace(A, ld, n);
+  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+    int a = e / n, b = e % n;
+    Uinv[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+  }
 }
 
-// P[i][j] -= sum_k W[i][k] M[j][k] for j >= i, mirrored; dx = M y; negative-diagonal count
-__global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ W,
-                                                const double *__restrict__ M, int n, const double *__restrict__ y,
-                                                double *__restrict__ dx, int *neg) {
-  __shared__ double Wi[16][17];
-  __shared__ double Mj[16][17];
+
+// P[i][j] -= sum_k V[i][k] V[j][k] - s2 sum_k X[i][k] X[j][k]  for j >= i, mirrored;  dx = X w;
+// negative-diagonal count.   (P+ = P - V (I - s2 Z^-1) V^T, see launch_ekf_info)
+__global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ V,
+                                                const double *__restrict__ X, int n, double s2,
+                                                const double *__restrict__ w, double *__restrict__ dx, int *neg) {
+  __shared__ double Vi[16][17], Vj[16][17], Xi[16][17], Xj[16][17];
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   int bi = blockIdx.y, bj = blockIdx.x;
   if (bj < bi) return;
   int i0 = bi * 16, j0 = bj * 16;
-  double acc = 0.0;
+  double av = 0.0, ax = 0.0;
   for (int k0 = 0; k0 < n; k0 += 16) {
-    Wi[ty][tx] = (i0 + ty < N && k0 + tx < n) ? W[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
-    Mj[ty][tx] = (j0 + ty < N && k0 + tx < n) ? M[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
+    bool kin = k0 + tx < n;
+    Vi[ty][tx] = (i0 + ty < N && kin) ? V[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
+    Vj[ty][tx] = (j0 + ty < N && kin) ? V[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
+    Xi[ty][tx] = (i0 + ty < N && kin) ? X[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
+    Xj[ty][tx] = (j0 + ty < N && kin) ? X[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += Wi[ty][kk] * Mj[tx][kk];
+    for (int kk = 0; kk < 16; kk++) {
+      av += Vi[ty][kk] * Vj[tx][kk];
+      ax += Xi[ty][kk] * Xj[tx][kk];
+    }
     __syncthreads();
   }
   int i = i0 + ty, j = j0 + tx;
   if (i < N && j < N && j >= i) {
-    double v = P[(size_t)i * ldp + j] - acc;
+    double v = P[(size_t)i * ldp + j] - (av - s2 * ax);
     P[(size_t)i * ldp + j] = v;
     P[(size_t)j * ldp + i] = v;
     if (i == j && v < 0.0) atomicAdd(neg, 1);
@@ -584,29 +533,43 @@ __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp,
     int row = i0 + tx;
     if (row < N) {
       double a = 0.0;
-      for (int k = 0; k < n; k++) a += M[(size_t)row * n + k] * y[k];
+      for (int k = 0; k < n; k++) a += X[(size_t)row * n + k] * w[k];
       dx[row] = a;
     }
   }
 }
 
+// Compressed update in information form on the Gram G = [H r]^T [H r]:
+//   P_II = L L^T,  E = L^T G_nn L,  c = L^T b,  Z = E + s2 I = U U^T,  V = P[:,I] L^-T,  X = V U^-T
+//   P+ = P - V V^T + s2 X X^T  (= P - P[:,I] (G P_II + s2 I)^-1 G P[I,:]),   dx = X U^-1 c.
+// Z has eigenvalues >= s2, so both Cholesky factors are of SPD matrices and G itself is never
+// factored (it is exactly singular in the gauge directions of an MSCKF stack).
 void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
                      const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc) {
-  int ncol = n + 1;
-  hipLaunchKernelGGL(k_gram_reduce, dim3((ncol * ncol + 255) / 256), dim3(256), 0, s, partials, nch, ncol, Gbuf);
-  size_t bytes = (size_t)2 * n * ncol * sizeof(double);
-  int use_lds = bytes <= 150 * 1024;
-  double *Q = sc.S;                          // n x n
-  double *work = sc.S + (size_t)n * n;       // 2 n (n+1) when not in LDS
+  const int na = n + 1;
+  hipLaunchKernelGGL(k_gram_reduce, dim3((na * na + 255) / 256), dim3(256), 0, s, partials, nch, na, Gbuf);
+  double *Laug = sc.S;                            // (n+1)^2
+  double *Linv = Laug + (size_t)na * na;          // n^2
+  double *T1 = Linv + (size_t)n * n;              // (n+1)^2
+  double *E = T1 + (size_t)na * na;               // (n+1)^2
+  double *Uinv = E + (size_t)na * na;             // n^2   (5 (n+1)^2 in total)
+  double *w = sc.y;
+  double *gbuf = sc.M;                            // global fallback work buffer (N rmax >= dense_lds_bytes)
   ensure_lds_attrs();
-  hipLaunchKernelGGL(k_info_small, dim3(1), dim3(1024), use_lds ? bytes : 0, s, Gbuf, n, P, ldp, hidx, sigma2, Q, sc.y,
-                     work, use_lds);
-  // W = P[:, I] Q (Q symmetric, so the k_ekf_M "H^T" operand is Q itself)
+  size_t b1 = dense_lds_bytes(n, n);
+  int l1 = b1 <= kMaxDynLds;
+  hipLaunchKernelGGL(k_info_cholP, dim3(1), dim3(512), l1 ? b1 : 0, s, P, ldp, hidx, n, Laug, Linv, gbuf, l1);
+  dim3 g((na + 15) / 16, (na + 15) / 16);
+  hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 0, 0, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug
+  hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 1, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
+  size_t b2 = dense_lds_bytes(n + 1, n);
+  int l2 = b2 <= kMaxDynLds;
+  hipLaunchKernelGGL(k_info_cholZ, dim3(1), dim3(512), l2 ? b2 : 0, s, E, n, sigma2, Uinv, w, gbuf, l2);
   dim3 gM((n + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Q, n, n, n, hidx, sc.W);
-  hipLaunchKernelGGL(k_gather_cols, dim3((N * n + 255) / 256), dim3(256), 0, s, P, ldp, N, hidx, n, sc.M);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Linv, n, n, n, hidx, sc.M);  // V = P[:,I] L^-T
+  hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, n, Uinv, sc.W);               // X = V U^-T
   int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, sc.M, n, sc.y, sc.dx, sc.neg);
+  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg);
 }
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
@@ -661,8 +624,9 @@ static void ensure_lds_attrs() {
   static bool done = false;
   if (done) return;
   hipFuncSetAttribute((const void *)k_gram_reduce_chol, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-  hipFuncSetAttribute((const void *)k_ekf_small, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-  hipFuncSetAttribute((const void *)k_info_small, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  hipFuncSetAttribute((const void *)k_ekf_small, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
+  hipFuncSetAttribute((const void *)k_info_cholP, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
+  hipFuncSetAttribute((const void *)k_info_cholZ, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
   done = true;
 }
 

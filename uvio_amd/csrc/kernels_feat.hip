@@ -9,9 +9,11 @@
 //   all    : left-nullspace projection (UpdaterHelper.cpp:426-454) as 3 Householder reflections of H_f
 //            applied to [H_x | res] (any orthonormal basis of the left nullspace gives the same chi2,
 //            the same Gram matrix and hence the same EKF update as the reference's Givens sweep).
-//   all    : chi2 gate (UpdaterMSCKF.cpp:209-234): S = H P_marg H^T + s2 I built in row chunks with
-//            P_marg gathered from the HBM-resident P; Cholesky of [S | r] in LDS; chi2 = |L^-1 r|^2.
-//   all    : accepted rows are written to H_all in canonical dense columns (zeros when rejected).
+//   all    : the projected rows [Hhat | rhat] are written to H_all in canonical dense columns (zeros
+//            when triangulation / refinement failed).
+// The chi2 gate (UpdaterMSCKF.cpp:209-234) runs afterwards for the whole batch (kernels_chi2.hip):
+// T = H_all P_can as one GEMM over the shared canonical covariance block, then one workgroup per
+// feature forms S = T Hhat^T + s2 I, factors [S | r] and zeroes the rows of rejected features.
 #include "kernels.h"
 
 namespace uvhp {
@@ -208,8 +210,6 @@ __host__ __device__ inline size_t feat_lds_doubles(int max_meas, int max_nf) {
   n += (size_t)rows * (max_nf + 1);  // Hl
   n += (size_t)rows * 3;             // Hf
   n += (size_t)rows * 3;             // V (Householder vectors)
-  n += (size_t)(rows + 1) * (rows + 1);  // S augmented
-  n += (size_t)16 * max_nf;          // T chunk
   n += (size_t)max_nf;               // loc2pid (as double-size slots for alignment)
   n += 64;                           // scratch
   return n;
@@ -224,6 +224,9 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
                                                  int max_nf) {
   extern __shared__ double lds[];
   __shared__ FeatShared sh;
+  long long *tsp = bp.dbg_ts ? bp.dbg_ts + (size_t)blockIdx.x * 8 : nullptr;
+#define FEAT_TS(k) \
+  if (tsp && threadIdx.x == 0) tsp[k] = clock64();
   __shared__ int canon2loc[512];
   __shared__ double red[9 * 64];
   const int f = blockIdx.x;
@@ -235,10 +238,9 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   double *Hl = lds;
   double *Hf = Hl + (size_t)2 * max_meas * (max_nf + 1);
   double *V = Hf + 2 * max_meas * 3;
-  double *S = V + 2 * max_meas * 3;
-  double *Tc = S + (size_t)(2 * max_meas + 1) * (2 * max_meas + 1);
-  int *loc2pid = (int *)(Tc + 16 * max_nf);
+  int *loc2pid = (int *)(V + 2 * max_meas * 3);
 
+  FEAT_TS(0)
   // ---- setup: column maps, zero the local Jacobian ----
   for (int j = tid; j <= bp.n_canon; j += 256) canon2loc[j] = -1;
   for (int e = tid; e < rows * ldl; e += 256) Hl[e] = 0.0;
@@ -262,6 +264,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   }
   __syncthreads();
 
+  FEAT_TS(1)
   // ---- geometry (wave 0): triangulation + Levenberg-Marquardt (MSCKF / delayed init only) ----
   if ((F.mode == 0 || F.mode == 2) && wave == 0) {
     const DClone &ca = clones[F.anchor_slot];
@@ -413,6 +416,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   __syncthreads();
   const int status0 = sh.status;
 
+  FEAT_TS(2)
   // ---- Jacobians (one thread per measurement) ----
   if (status0 == 0 && tid < m) {
     const DMeas &mm = Ms[tid];
@@ -597,6 +601,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   }
   __syncthreads();
 
+  FEAT_TS(3)
   // ---- left-nullspace projection: 3 Householder reflections of H_f (MSCKF) ----
   int r0 = 0;  // first output row in Hl
   if (status0 == 0 && F.mode != 1) {
@@ -645,90 +650,10 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   }
   const int R = rows - r0;
 
-  // ---- chi2: S = Hhat P_marg Hhat^T + s2 I, augmented with the residual row ----
-  if (status0 == 0 && R > 0) {
-    const int ldS = R + 1;
-    // T = Hhat P_f in 16-row chunks: thread d owns column d of the chunk (16 accumulators) and reads
-    // P[pid(d)][pid(c)] once per chunk (HBM/L2-resident P, unrolled for memory-level parallelism)
-    for (int i0 = 0; i0 < R; i0 += 16) {
-      const int nr = min(16, R - i0);
-      for (int d = tid; d < nf; d += 256) {
-        const double *Prow = P + (size_t)loc2pid[d] * bp.ldp;
-        double acc[16];
-#pragma unroll
-        for (int ii = 0; ii < 16; ii++) acc[ii] = 0.0;
-        int c = 0;
-        for (; c + 4 <= nf; c += 4) {
-          double p0 = Prow[loc2pid[c]], p1 = Prow[loc2pid[c + 1]], p2 = Prow[loc2pid[c + 2]], p3 = Prow[loc2pid[c + 3]];
-#pragma unroll
-          for (int ii = 0; ii < 16; ii++) {
-            if (ii < nr) {
-              const double *h = Hl + (size_t)(r0 + i0 + ii) * ldl + c;
-              acc[ii] += h[0] * p0;
-              acc[ii] += h[1] * p1;
-              acc[ii] += h[2] * p2;
-              acc[ii] += h[3] * p3;
-            }
-          }
-        }
-        for (; c < nf; c++) {
-          double p0 = Prow[loc2pid[c]];
-#pragma unroll
-          for (int ii = 0; ii < 16; ii++)
-            if (ii < nr) acc[ii] += Hl[(size_t)(r0 + i0 + ii) * ldl + c] * p0;
-        }
-#pragma unroll
-        for (int ii = 0; ii < 16; ii++)
-          if (ii < nr) Tc[ii * nf + d] = acc[ii];
-      }
-      __syncthreads();
-      for (int e = tid; e < nr * R; e += 256) {
-        int ii = e / R, j = e % R;
-        if (j > i0 + ii) continue;  // lower triangle is all the Cholesky reads
-        const double *hrow = Hl + (size_t)(r0 + j) * ldl;
-        double acc = 0.0;
-        for (int d = 0; d < nf; d++) acc += Tc[ii * nf + d] * hrow[d];
-        if (i0 + ii == j) acc += bp.sigma_pix_sq;
-        S[(i0 + ii) * ldS + j] = acc;
-      }
-      __syncthreads();
-    }
-    // residual row
-    for (int j = tid; j < R; j += 256) S[R * ldS + j] = Hl[(size_t)(r0 + j) * ldl + nf];
-    __syncthreads();
-    // lower Cholesky of the augmented matrix by wave 0 (lane i owns rows i, i+64, ...; no block
-    // barriers); the last row becomes y = L^-1 r and chi2 = |y|^2
-    if (wave == 0) {
-      for (int k = 0; k < R; k++) {
-        wave_sync();
-        const double dkk = sqrt(S[k * ldS + k]);
-        for (int i = k + 1 + lane; i <= R; i += 64) S[i * ldS + k] /= dkk;
-        if (lane == 0) S[k * ldS + k] = dkk;
-        wave_sync();
-        for (int i = k + 1 + lane; i <= R; i += 64) {
-          const double lik = S[i * ldS + k];
-          const int jmax = min(i, R - 1);
-          for (int j = k + 1; j <= jmax; j++) S[i * ldS + j] -= lik * S[j * ldS + k];
-        }
-      }
-      wave_sync();
-      double c2 = 0.0;
-      for (int k = lane; k < R; k += 64) {
-        double y = S[R * ldS + k];
-        c2 += y * y;
-      }
-      c2 = wave_sum(c2);
-      if (lane == 0) {
-        sh.chi2 = c2;
-        // delayed init tests the update rows against chi2(dof = all rows) (StateHelper.cpp:463-468)
-        double thr = chi2_table[min(F.mode >= 2 ? rows : R, 999)];
-        if (c2 > bp.chi2_mult * thr) sh.status = 3;
-      }
-    }
-    __syncthreads();
-  }
-  const int status = sh.status;
-
+  FEAT_TS(4)
+  FEAT_TS(5)
+  const int status = sh.status;  // 0 or a triangulation / refinement failure; chi2 is k_chi2's
+  FEAT_TS(6)
   // ---- output rows (canonical dense columns; zeros when rejected) ----
   const int out_r0 = (F.mode == 0) ? 3 : 0;
   const int nrows_out = max(rows - out_r0, 0);
@@ -747,12 +672,14 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       o.p_FinA[k] = sh.p_FinA[k];
       o.p_FinG[k] = sh.p_FinG[k];
     }
-    o.chi2 = (status0 == 0) ? sh.chi2 : -1.0;
+    o.chi2 = -1.0;
     for (int k = 0; k < 9; k++) o.HfR[k] = (F.mode >= 2 && status0 == 0) ? Hf[(k / 3) * 3 + (k % 3)] : 0.0;
     o.status = status;
     o.rows = status == 0 ? nrows_out : 0;
     out[f] = o;
   }
+  FEAT_TS(7)
+#undef FEAT_TS
 }
 
 void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const DMeas *meas,
