@@ -12,10 +12,10 @@ The image tracker (TrackKLT) is not on this path yet: the front-end is the refer
 (DESIGN.md "Scope").  Frames/s is whole-job throughput: every rank runs its own estimator on its own
 stream (independent replicas, weak scaling), value = total frames / max-over-ranks wall time.
 
-roofline: the dominant device kernel (the per-feature linearize kernel: triangulation + LM,
-Jacobians, left-nullspace reflections, chi2 Cholesky), timed with HIP events on the library's stream;
-achieved = the algorithmic FP64 FLOPs of its launches (SURVEY.md §8(d) F_feat formula on the actual
-feature shapes) / their event time.  cpu_baseline: the oracle/ CPU restatement (single-threaded, as
+roofline: the dominant device work, the feature launch group (k_feature: triangulation + LM,
+Jacobians, left-nullspace reflections; then k_gather_can + k_gemm_HP + k_chi2: the batched chi2
+gate), timed with HIP events on the library's stream around the group; achieved = the algorithmic
+FP64 FLOPs of the group (SURVEY.md §8(d) F_feat formula on the actual feature shapes) / event time.  cpu_baseline: the oracle/ CPU restatement (single-threaded, as
 the reference estimator is) on a bounded sample of the same stream, rank 0 only.
 """
 import argparse
@@ -165,7 +165,8 @@ def main():
                        "mean_msckf_rows": acc["rows"] / args.steps, "H_cols": acc["cols"],
                        "state_dim": acc["cov_dim"], "parallelism": "replicas%d" % world},
             "ate_rmse_m": ate,
-            "roofline": {"kernel": "k_feature (per-feature linearize, FP64)", "bound": "mfma",
+            "roofline": {"kernel": "feature linearize + chi2 launch group (k_feature, k_gather_can, k_gemm_HP, k_chi2)",
+                         "bound": "mfma",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                          "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops_per_launch},
