@@ -110,6 +110,10 @@ typedef struct {
   uvio_hp_anchor_t anchors[UVIO_HP_MAX_ANCHORS];
   /* runtime */
   int record_timing;          /* keep per-frame stage timings (VioManager.cpp:631-644 schema) */
+  /* InertialInitializerOptions::init_max_features (InertialInitializerOptions.h:73): the KLT tracker
+   * keeps floor(init_max_features / num_cameras) tracks per camera until an initializer succeeds
+   * (VioManager.cpp:131; initialize_with_gt does not raise it to num_pts, VioManagerHelper.cpp:40) */
+  int init_max_features;
 } uvio_hp_options_t;
 
 /* Per-frame stage timings in seconds, the reference CSV schema

@@ -42,6 +42,25 @@ int orc_feed_simulation(orc_handle *h, double t, int ncam, const int *cam_ids, c
     for (int j = 0; j < counts[i]; j++, k++) feats[i].push_back({(size_t)ids[k], {uv[2 * k], uv[2 * k + 1]}});
   return h->m.feed_simulation(t, camids, feats);
 }
+int orc_feed_camera(orc_handle *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
+                    const uint8_t *const *masks) {
+  std::vector<int> camids(cam_ids, cam_ids + ncam);
+  std::vector<GrayImg> im(ncam), mk(ncam);
+  for (int i = 0; i < ncam; i++) {
+    const uvio_hp_camera_t &c = h->m.o.cams[cam_ids[i]];
+    im[i].w = c.width;
+    im[i].h = c.height;
+    im[i].d.resize((size_t)c.width * c.height);
+    for (int y = 0; y < c.height; y++)
+      std::memcpy(&im[i].d[(size_t)y * c.width], imgs[i] + (size_t)y * strides[i], c.width);
+    if (masks && masks[i]) {
+      mk[i] = im[i];
+      for (int y = 0; y < c.height; y++)
+        std::memcpy(&mk[i].d[(size_t)y * c.width], masks[i] + (size_t)y * strides[i], c.width);
+    }
+  }
+  return h->m.feed_camera(t, camids, im, mk);
+}
 int orc_feed_uwb(orc_handle *h, double t, int n, const uint64_t *anchor_ids, const double *ranges) {
   std::vector<std::pair<size_t, double>> r;
   for (int i = 0; i < n; i++) r.push_back({(size_t)anchor_ids[i], ranges[i]});

@@ -1,6 +1,8 @@
 // ORACLE — test infrastructure only (see la.h header).
 #include "manager.h"
 
+#include <cmath>
+
 #include <algorithm>
 
 namespace orc {
@@ -10,6 +12,15 @@ static double secs(clk::time_point a, clk::time_point b) { return std::chrono::d
 
 Manager::Manager(const uvio_hp_options_t &opt)
     : o(opt), state(opt), prop(opt), msckf(opt), slam(opt), uwb(opt), currid(4 * (size_t)opt.max_aruco_features + 1) {
+  tracker.num_features = (int)std::floor((double)opt.init_max_features / (double)opt.num_cameras);
+  tracker.threshold = opt.fast_threshold;
+  tracker.grid_x = opt.grid_x;
+  tracker.grid_y = opt.grid_y;
+  tracker.min_px_dist = opt.min_px_dist;
+  tracker.histogram_method = opt.histogram_method;
+  tracker.use_stereo = opt.use_stereo != 0;
+  tracker.currid = 4 * (size_t)opt.max_aruco_features + 1;
+  tracker.cams = &state.cams;
   // UVioManager ctor (UVioManager.cpp:33-58)
   if (o.use_uwb) {
     if (o.do_calib_uwb_extrinsics) {
@@ -140,6 +151,29 @@ int Manager::feed_simulation(double t, const std::vector<int> &camids,
   int rc = do_feature_propagate_update(t, camids);
   auto rT7 = clk::now();
   timing.total = secs(rT1, rT7);
+  return rc;
+}
+
+// VioManager.cpp:255-321 (track_image_and_update, no ZUPT / ArUco / downsampling)
+int Manager::feed_camera(double t, const std::vector<int> &camids, const std::vector<GrayImg> &imgs,
+                         const std::vector<GrayImg> &masks) {
+  auto rT1 = clk::now();
+  tracker.feed(t, camids, imgs, masks, db);
+  auto rT2 = clk::now();
+  timing = uvio_hp_timing_t{};
+  timing.tracking = secs(rT1, rT2);
+  if (!is_initialized) return UVIO_HP_E_STATE;
+  if (!past_uwb.empty()) {
+    for (auto it = past_uwb.begin(); it != past_uwb.lower_bound(t); it++) {
+      if (it->first < t && it->first > state.timestamp) {
+        int rc = do_uwb_propagate_update(it->second);
+        if (rc < 0) return rc;
+      }
+    }
+    past_uwb.erase(past_uwb.begin(), past_uwb.upper_bound(t));
+  }
+  int rc = do_feature_propagate_update(t, camids);
+  timing.total = secs(rT1, clk::now());
   return rc;
 }
 

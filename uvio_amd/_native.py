@@ -54,7 +54,7 @@ class Options(C.Structure):
         ("uwb_sigma_range", C.c_double), ("uwb_chi2_multipler", C.c_double), ("min_dist_to_use_uwb", C.c_double),
         ("p_IinU", C.c_double * 3), ("n_anchors_to_fix", C.c_int), ("n_anchors", C.c_int),
         ("anchors", Anchor * MAX_ANCHORS),
-        ("record_timing", C.c_int),
+        ("record_timing", C.c_int), ("init_max_features", C.c_int),
     ]
 
 

@@ -316,6 +316,7 @@ void options_default(uvio_hp_options_t *o) {
   o->uwb_chi2_multipler = 1.0;
   o->min_dist_to_use_uwb = 0.5;
   o->record_timing = 1;
+  o->init_max_features = 50;
 }
 
 int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
@@ -367,6 +368,7 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
   // tracker
   est.get({"num_pts"}, o->num_pts);
   est.get({"fast_threshold"}, o->fast_threshold);
+  est.get({"init_max_features"}, o->init_max_features);
   est.get({"grid_x"}, o->grid_x);
   est.get({"grid_y"}, o->grid_y);
   est.get({"min_px_dist"}, o->min_px_dist);

@@ -100,6 +100,23 @@ class VioManager:
         self._check(rc, "feed_measurement_simulation")
         return rc
 
+    def feed_measurement_camera(self, t, camids, images, masks=None, allow_uninit=False):
+        """VioManager::feed_measurement_camera: images[i] is a u8 (H, W) array for camera camids[i]."""
+        ncam = len(camids)
+        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        cam = (C.c_int * ncam)(*camids)
+        ptrs = (C.POINTER(C.c_uint8) * ncam)(*[im.ctypes.data_as(C.POINTER(C.c_uint8)) for im in imgs])
+        strides = (C.c_int * ncam)(*[im.strides[0] for im in imgs])
+        mptr = None
+        if masks is not None:
+            mk = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
+            mptr = (C.POINTER(C.c_uint8) * ncam)(*[m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in mk])
+        rc = self._call("feed_camera", self._h, C.c_double(t), ncam, cam, ptrs, strides, mptr)
+        if rc == N.E_STATE and allow_uninit:
+            return rc
+        self._check(rc, "feed_measurement_camera")
+        return rc
+
     def feed_measurement_uwb(self, t, anchor_ids, ranges):
         n = len(anchor_ids)
         ids = (C.c_uint64 * n)(*anchor_ids)

@@ -230,6 +230,14 @@ class SimStream:
                 self.uwb.append((t, ids, rs))
                 t += 1.0 / uwb_rate
 
+    def camera_pose(self, i, k):
+        """(R_GtoC, p_CinG) of camera k at camera frame i (ground truth)."""
+        t = self.cam_t[i]
+        R_ItoG = self.traj.R_ItoG(t)
+        p_IinG = self.traj.pos(t)
+        R_GtoC = self.R_ItoC[k] @ R_ItoG.T
+        return R_GtoC, p_IinG - R_GtoC.T @ self.p_IinC[k]
+
     def gt_state(self, t):
         """[t, q_GtoI, p_IinG, v_IinG, bg, ba] (initialize_with_gt input, VioManagerHelper.cpp:40)."""
         R_ItoG = self.traj.R_ItoG(t)
@@ -248,10 +256,12 @@ class SimStream:
         ev.sort(key=lambda e: (e[1] + (0.0 if e[0] == "imu" else lag), order[e[0]]))
         return ev
 
-    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None):
+    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None, renderer=None):
         """Drive one manager (or a list of managers in lock-step): initialize from ground truth at t0, then
         feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed,
-        after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init)."""
+        after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init).  With a
+        renderer (uvio_amd.render.SceneRenderer) the managers get images (feed_measurement_camera)
+        instead of the simulated tracks."""
         mgrs = mgr if isinstance(mgr, (list, tuple)) else [mgr]
         for m in mgrs:
             m.initialize_with_gt(self.gt_state(self.t0))
@@ -270,11 +280,16 @@ class SimStream:
             else:
                 if t <= self.t0:
                     continue
-                fr = self.frames[i]
                 if before_frame is not None:
                     before_frame(nf + 1, t)
-                for m in mgrs:
-                    m.feed_measurement_simulation(t, list(range(self.K)), fr)
+                if renderer is not None:
+                    imgs = [renderer.render(k, *self.camera_pose(i, k), frame_seed=i).cpu().numpy() for k in range(self.K)]
+                    for m in mgrs:
+                        m.feed_measurement_camera(t, list(range(self.K)), imgs)
+                else:
+                    fr = self.frames[i]
+                    for m in mgrs:
+                        m.feed_measurement_simulation(t, list(range(self.K)), fr)
                 nf += 1
                 if on_frame is not None:
                     on_frame(nf, t)
