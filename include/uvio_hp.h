@@ -162,6 +162,11 @@ int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids
  * imgs[i] is a u8 W x H image with row stride strides[i]; masks may be NULL. */
 int uvio_hp_feed_camera(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
                         const int *strides, const uint8_t *const *masks);
+/* The same with imgs[i] in device memory (HBM-resident input, e.g. a camera DMA buffer or a torch
+ * tensor); the images must be complete (their producer synchronized) before the call.  masks stay
+ * host pointers. */
+int uvio_hp_feed_camera_device(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
+                               const int *strides, const uint8_t *const *masks);
 /* UVioManager::feed_measurement_uwb (UVioManager.cpp:61): one UwbData message */
 int uvio_hp_feed_uwb(uvio_hp_t *h, double t, int n, const uint64_t *anchor_ids, const double *ranges);
 /* UVioManager::try_to_initialize_uwb_anchors (UVioManager.cpp:81) */
@@ -185,6 +190,13 @@ int uvio_hp_get_fej_vector(uvio_hp_t *h, double *out, int cap, int *len);
 int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out);
 /* number of clones and their timestamps (ascending) */
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
+/* TrackBase::get_last_obs / get_last_ids (TrackBase.h:107-122) for one camera: ids and raw (u, v) of
+ * the KLT tracks after the last camera feed; *n receives the count (E_CAPACITY if > cap) */
+int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap, int *n);
+/* the last image pyramid of one camera (TrackKLT::img_pyramid_last, TrackKLT.h:130): level size,
+ * the (equalized) u8 image (w*h) and interleaved Scharr (dx, dy) int16 derivatives (w*h*2); img / der
+ * may be NULL, cap = pixels available */
+int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap);
 
 /* ---- inner (kernel-level) boundary used by parity tests ---- */
 /* per-feature results of the last UpdaterMSCKF::update: feature id, triangulated p_FinG (3 per

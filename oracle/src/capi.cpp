@@ -222,6 +222,40 @@ int orc_debug_last_msckf(orc_handle *h, uint64_t *ids, double *pG, int *status, 
   return 0;
 }
 
+// TrackKLT state after the last camera feed (parity tests)
+int orc_get_tracks(orc_handle *h, int cam, uint64_t *ids, float *uv, int cap, int *n) {
+  auto &tr = h->m.tracker;
+  auto it = tr.pts_last.find((size_t)cam);
+  *n = 0;
+  if (it == tr.pts_last.end()) return 0;
+  const auto &pts = it->second;
+  const auto &id = tr.ids_last[(size_t)cam];
+  *n = (int)pts.size();
+  if ((int)pts.size() > cap) return UVIO_HP_E_CAPACITY;
+  for (size_t i = 0; i < pts.size(); i++) {
+    if (ids) ids[i] = (uint64_t)id[i];
+    if (uv) {
+      uv[2 * i] = pts[i].x;
+      uv[2 * i + 1] = pts[i].y;
+    }
+  }
+  return 0;
+}
+int orc_get_pyramid(orc_handle *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap) {
+  auto &tr = h->m.tracker;
+  auto it = tr.pyr_last.find((size_t)cam);
+  if (it == tr.pyr_last.end() || level < 0 || level >= it->second.levels()) return UVIO_HP_E_STATE;
+  const GrayImg &g = it->second.img[level];
+  *w = g.w;
+  *hgt = g.h;
+  size_t px = (size_t)g.w * g.h;
+  if (!img && !der) return 0;
+  if (px > cap) return UVIO_HP_E_CAPACITY;
+  if (img) std::memcpy(img, g.d.data(), px);
+  if (der) std::memcpy(der, it->second.deriv[level].data(), px * 2 * sizeof(int16_t));
+  return 0;
+}
+
 // Camera model entry points for fixture / finite-difference tests
 int orc_camera_distort(const uvio_hp_camera_t *c, int n, const double *xy, double *uv, double *dz_dzn, double *dz_dzeta) {
   Camera cam;

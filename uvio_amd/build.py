@@ -20,10 +20,12 @@ SOURCES = [
     "engine_state.cpp",
     "engine_prop.cpp",
     "engine_update.cpp",
+    "engine_track.cpp",
     "capi.cpp",
     "kernels_cov.hip",
     "kernels_feat.hip",
     "kernels_chi2.hip",
+    "kernels_track.hip",
 ]
 
 

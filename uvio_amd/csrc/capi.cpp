@@ -82,15 +82,48 @@ int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids
 
 int uvio_hp_feed_camera(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
                         const int *strides, const uint8_t *const *masks) {
-  (void)t;
-  (void)ncam;
-  (void)cam_ids;
-  (void)imgs;
-  (void)strides;
-  (void)masks;
-  if (!h) return UVIO_HP_E_ARG;
-  h->err = "image front-end (TrackKLT) not built in this version";
-  return UVIO_HP_E_STATE;
+  if (!h || ncam <= 0 || !cam_ids || !imgs || !strides) return UVIO_HP_E_ARG;
+  HP_GUARD(h, return h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, false);)
+}
+
+int uvio_hp_feed_camera_device(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
+                               const int *strides, const uint8_t *const *masks) {
+  if (!h || ncam <= 0 || !cam_ids || !imgs || !strides) return UVIO_HP_E_ARG;
+  HP_GUARD(h, return h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, true);)
+}
+
+int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap, int *n) {
+  if (!h || !n) return UVIO_HP_E_ARG;
+  HP_GUARD(h, {
+    std::vector<uvhp::KeyPt> pts;
+    std::vector<size_t> id;
+    if (h->e->tracker()) h->e->tracker()->last_tracks(cam, pts, id);
+    *n = (int)pts.size();
+    if ((int)pts.size() > cap) return UVIO_HP_E_CAPACITY;
+    for (size_t i = 0; i < pts.size(); i++) {
+      if (ids) ids[i] = (uint64_t)id[i];
+      if (uv) {
+        uv[2 * i] = pts[i].x;
+        uv[2 * i + 1] = pts[i].y;
+      }
+    }
+    return 0;
+  })
+}
+
+int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap) {
+  if (!h || !w || !hgt) return UVIO_HP_E_ARG;
+  HP_GUARD(h, {
+    std::vector<uint8_t> im;
+    std::vector<int16_t> d;
+    if (!h->e->tracker() || !h->e->tracker()->last_pyramid(cam, level, w, hgt, img ? &im : nullptr, der ? &d : nullptr))
+      return UVIO_HP_E_STATE;
+    size_t px = (size_t)*w * *hgt;
+    if ((img || der) && px > cap) return UVIO_HP_E_CAPACITY;
+    if (img) std::memcpy(img, im.data(), px);
+    if (der) std::memcpy(der, d.data(), px * 2 * sizeof(int16_t));
+    return 0;
+  })
 }
 
 int uvio_hp_feed_uwb(uvio_hp_t *h, double t, int n, const uint64_t *ids, const double *ranges) {

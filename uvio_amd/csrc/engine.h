@@ -16,6 +16,7 @@
 
 #include "hp_common.h"
 #include "kernels.h"
+#include "tracker.h"
 
 namespace uvhp {
 
@@ -105,7 +106,10 @@ class Engine {
   void initialize_with_gt(const double x[17]);
   void feed_imu(double t, const double wm[3], const double am[3]);
   int feed_simulation(double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids, const float *uv);
+  int feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
+                  const uint8_t *const *masks, bool device_imgs);
   int feed_uwb(double t, int n, const uint64_t *ids, const double *ranges);
+  Tracker *tracker() { return tracker_.get(); }
   int init_anchors(int n, const uvio_hp_anchor_t *a);
 
   // getters
@@ -142,7 +146,9 @@ class Engine {
   std::vector<ImuSample> imu_data_;
   bool have_last_prop_time_offset_ = false;
   double last_prop_time_offset_ = 0;
-  // ---- feature database (TrackSIM's) ----
+  // ---- KLT front-end (created on the first camera feed) ----
+  std::unique_ptr<Tracker> tracker_;
+  // ---- feature database (TrackSIM's / TrackKLT's) ----
   std::unordered_map<size_t, FeatP> db_;
   size_t currid_;
   // ---- manager ----
@@ -192,6 +198,7 @@ class Engine {
   int propagate_uwb(double t);
 
   // updates
+  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1);
   int do_feature_propagate_update(double t, const std::vector<int> &camids);
   int msckf_update(std::vector<FeatP> &feats);
   int slam_update(std::vector<FeatP> &feats);

@@ -212,6 +212,7 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
 
 Engine::~Engine() {
   hipSetDevice(device_);
+  tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.fout, d_.chi2, d_.H, d_.Tall, d_.Pc, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
                   d_.ekf.dx, d_.ekf.neg};

@@ -1,0 +1,751 @@
+// KLT front-end host orchestration — see tracker.h.  Reference: ov_core TrackKLT.cpp:34-886,
+// Grider_GRID.h:74-180 (restated for the checker in oracle/src/tracker_klt.cpp).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "tracker.h"
+
+namespace uvhp {
+
+namespace {
+constexpr int kRansacIters = 1000;      // findFundamentalMat(FM_RANSAC, thr, 0.999) default maxIters
+constexpr double kRansacConf = 0.999;   // TrackKLT.cpp:878
+constexpr int kLkIters = 30;            // TermCriteria(COUNT + EPS, 30, 0.01), TrackKLT.cpp:641 / 852
+constexpr float kLkEps = 0.01f;
+constexpr int kSubpixWin = 5, kSubpixIters = 20;  // Grider_GRID.h:170-175: Size(5,5), (20, 0.001)
+constexpr double kSubpixEps = 0.001;
+constexpr double kMinFeatPercent = 0.50;        // TrackKLT.cpp:466 / 590
+
+// cv::RNG((uint64)-1): multiply-with-carry, coefficient 4164903690 (CV_RNG_COEFF)
+struct MwcRng {
+  uint64_t s;
+  unsigned next() {
+    s = (uint64_t)(unsigned)s * 4164903690U + (unsigned)(s >> 32);
+    return (unsigned)s;
+  }
+};
+
+uint8_t mask_px(const std::vector<uint8_t> &m, int w, int x, int y) { return m.empty() ? 0 : m[(size_t)y * w + x]; }
+// cv::resize(mask, Size(GX, GY), INTER_NEAREST) sampled at grid cell (gx, gy)
+uint8_t mask_cell(const std::vector<uint8_t> &m, int w, int h, int gx, int gy, int GX, int GY) {
+  if (m.empty()) return 0;
+  int sx = std::min((int)std::floor(gx * ((double)w / GX)), w - 1);
+  int sy = std::min((int)std::floor(gy * ((double)h / GY)), h - 1);
+  return m[(size_t)sy * w + sx];
+}
+// the min-distance boxes TrackKLT draws into mask0_updated (cv::rectangle FILLED, inclusive corners)
+bool in_boxes(const std::vector<int> &boxes, int d, int x, int y) {
+  for (size_t k = 0; k + 1 < boxes.size(); k += 2)
+    if (std::abs(x - boxes[k]) <= d && std::abs(y - boxes[k + 1]) <= d) return true;
+  return false;
+}
+struct Occupancy {  // cv::Mat grid_2d_close / grid_2d_grid (CV_8UC1)
+  int w, h;
+  std::vector<uint8_t> d;
+  Occupancy(int w_, int h_) : w(w_), h(h_), d((size_t)std::max(w_, 0) * std::max(h_, 0), 0) {}
+  uint8_t &at(int x, int y) { return d[(size_t)y * w + x]; }
+};
+}  // namespace
+
+struct Tracker::Bufs {
+  int cap = 0, maxcells = 0, kmax = 0;
+  void *dmem = nullptr, *hmem = nullptr;
+  // device
+  float *p0[2], *p1[2], *p0n[2], *p1n[2];
+  uint8_t *st[2], *mask[2];
+  int *sub[2], *nm[2], *good[2];
+  double *F[2];
+  int *cells, *fastn;
+  float *fast, *det, *det1, *spmask;
+  uint8_t *detst;
+  // pinned host mirrors
+  float *h_p0[2], *h_p1[2];
+  uint8_t *h_st[2], *h_mask[2];
+  int *h_sub[2], *h_cells, *h_fastn;
+  float *h_fast, *h_det, *h_det1;
+  uint8_t *h_detst;
+};
+
+namespace {
+struct Arena {
+  size_t off = 0;
+  char *base = nullptr;
+  template <class T>
+  T *take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T *p = (T *)(base ? base + off : nullptr);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+}  // namespace
+
+Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s) : cams_(cams), s_(s) {
+  // TrackKLT construction in VioManager.cpp:98-107: num_pts per camera = init_max_features / ncam
+  num_features_ = (int)std::floor((double)o.init_max_features / (double)o.num_cameras);
+  threshold_ = o.fast_threshold;
+  grid_x_ = o.grid_x;
+  grid_y_ = o.grid_y;
+  min_px_dist_ = o.min_px_dist;
+  histogram_method_ = o.histogram_method;
+  use_stereo_ = o.use_stereo != 0;
+  currid = 4 * (size_t)o.max_aruco_features + 1;
+  if (num_features_ <= 0 || grid_x_ <= 0 || grid_y_ <= 0 || min_px_dist_ <= 0)
+    throw HpError(UVIO_HP_E_CONFIG, "tracker: num features / grid / min_px_dist must be positive");
+  // cornerSubPix window weights (cornersubpix.cpp: exp(-x^2) exp(-y^2), x, y in [-1, 1])
+  const int ww = 2 * kSubpixWin + 1;
+  spmask_host_.resize((size_t)ww * ww);
+  for (int i = 0; i < ww; i++) {
+    float y = (float)(i - kSubpixWin) / kSubpixWin;
+    float vy = std::exp(-y * y);
+    for (int j = 0; j < ww; j++) {
+      float x = (float)(j - kSubpixWin) / kSubpixWin;
+      spmask_host_[(size_t)i * ww + j] = (float)(vy * std::exp(-x * x));
+    }
+  }
+  b_ = new Bufs();
+  b_->maxcells = grid_x_ * grid_y_;
+  int gx = grid_x_, gy = grid_y_;
+  if (num_features_ < gx * gy) {
+    double ratio = (double)gx / (double)gy;
+    gy = (int)std::ceil(std::sqrt(num_features_ / ratio));
+    gx = (int)std::ceil(gy * ratio);
+  }
+  b_->kmax = (int)((double)num_features_ / (double)(gx * gy)) + 1;
+  ensure_cap(std::max(1024, 8 * num_features_));
+}
+
+Tracker::~Tracker() {
+  for (auto &kv : cs_) {
+    for (int k = 0; k < 2; k++)
+      if (kv.second.pyr_mem[k]) (void)hipFree(kv.second.pyr_mem[k]);
+    if (kv.second.d_raw) (void)hipFree(kv.second.d_raw);
+    if (kv.second.d_hist) (void)hipFree(kv.second.d_hist);
+  }
+  if (b_) {
+    if (b_->dmem) (void)hipFree(b_->dmem);
+    if (b_->hmem) (void)hipHostFree(b_->hmem);
+    delete b_;
+  }
+}
+
+void Tracker::sync() {
+  HP_HIP(hipStreamSynchronize(s_));
+  device_syncs++;
+}
+
+void Tracker::ensure_cap(int n) {
+  Bufs &b = *b_;
+  if (n <= b.cap) return;
+  if (b.dmem) {
+    sync();
+    HP_HIP(hipFree(b.dmem));
+    HP_HIP(hipHostFree(b.hmem));
+    b.dmem = b.hmem = nullptr;
+  }
+  int cap = std::max(n, 2 * b.cap);
+  size_t ncell = (size_t)b.maxcells;
+  for (int pass = 0; pass < 2; pass++) {
+    Arena d, h;
+    if (pass == 1) {
+      d.base = (char *)b.dmem;
+      h.base = (char *)b.hmem;
+    }
+    for (int k = 0; k < 2; k++) {
+      b.p0[k] = d.take<float>(2 * cap);
+      b.p1[k] = d.take<float>(2 * cap);
+      b.p0n[k] = d.take<float>(2 * cap);
+      b.p1n[k] = d.take<float>(2 * cap);
+      b.st[k] = d.take<uint8_t>(cap);
+      b.mask[k] = d.take<uint8_t>(cap);
+      b.sub[k] = d.take<int>(7 * kRansacIters);
+      b.nm[k] = d.take<int>(kRansacIters);
+      b.good[k] = d.take<int>(3 * kRansacIters);
+      b.F[k] = d.take<double>(27 * kRansacIters);
+      b.h_p0[k] = h.take<float>(2 * cap);
+      b.h_p1[k] = h.take<float>(2 * cap);
+      b.h_st[k] = h.take<uint8_t>(cap);
+      b.h_mask[k] = h.take<uint8_t>(cap);
+      b.h_sub[k] = h.take<int>(7 * kRansacIters);
+    }
+    b.cells = d.take<int>(2 * ncell);
+    b.fastn = d.take<int>(ncell);
+    b.fast = d.take<float>(3 * ncell * b.kmax);
+    b.det = d.take<float>(2 * cap);
+    b.det1 = d.take<float>(2 * cap);
+    b.detst = d.take<uint8_t>(cap);
+    b.spmask = d.take<float>(spmask_host_.size());
+    b.h_cells = h.take<int>(2 * ncell);
+    b.h_fastn = h.take<int>(ncell);
+    b.h_fast = h.take<float>(3 * ncell * b.kmax);
+    b.h_det = h.take<float>(2 * cap);
+    b.h_det1 = h.take<float>(2 * cap);
+    b.h_detst = h.take<uint8_t>(cap);
+    if (pass == 0) {
+      HP_HIP(hipMalloc(&b.dmem, d.off + 256));
+      HP_HIP(hipHostMalloc(&b.hmem, h.off + 256, hipHostMallocDefault));
+    }
+  }
+  b.cap = cap;
+  HP_HIP(hipMemcpy(b.spmask, spmask_host_.data(), spmask_host_.size() * sizeof(float), hipMemcpyHostToDevice));
+}
+
+Tracker::CamState &Tracker::cam_state(int cid) {
+  auto it = cs_.find(cid);
+  if (it != cs_.end()) return it->second;
+  CamState &c = cs_[cid];
+  alloc_pyr(c, cams_[cid].w, cams_[cid].h);
+  return c;
+}
+
+// buildOpticalFlowPyramid level sizes (stops once the next side would be <= win) for both slots
+void Tracker::alloc_pyr(CamState &c, int w, int h) {
+  DPyr p{};
+  int lw = w, lh = h;
+  size_t bytes = 0;
+  std::vector<size_t> img_off, der_off;
+  for (int level = 0; level <= pyr_levels_ && level < kMaxPyrLevels; level++) {
+    p.w[level] = lw;
+    p.h[level] = lh;
+    p.levels = level + 1;
+    img_off.push_back(bytes);
+    bytes += ((size_t)lw * lh + 255) & ~(size_t)255;
+    der_off.push_back(bytes);
+    bytes += ((size_t)lw * lh * 4 + 255) & ~(size_t)255;
+    lw = (lw + 1) / 2;
+    lh = (lh + 1) / 2;
+    if (lw <= win_ || lh <= win_) break;
+  }
+  for (int k = 0; k < 2; k++) {
+    HP_HIP(hipMalloc(&c.pyr_mem[k], bytes));
+    c.pyr[k] = p;
+    for (int l = 0; l < p.levels; l++) {
+      c.pyr[k].img[l] = (const uint8_t *)((char *)c.pyr_mem[k] + img_off[l]);
+      c.pyr[k].der[l] = (const int16_t *)((char *)c.pyr_mem[k] + der_off[l]);
+    }
+  }
+  HP_HIP(hipMalloc(&c.d_raw, (size_t)w * h));
+  HP_HIP(hipMalloc(&c.d_hist, 256 * sizeof(unsigned)));
+}
+
+// RANSACPointSetRegistrator::getSubset draws (ptsetreg.cpp), one rng per findFundamentalMat call
+const std::vector<int> &Tracker::subsets(int count) {
+  auto it = subset_cache_.find(count);
+  if (it != subset_cache_.end()) return it->second;
+  std::vector<int> &idx = subset_cache_[count];
+  idx.assign((size_t)kRansacIters * 7, 0);
+  MwcRng rng{~(uint64_t)0};
+  for (int it2 = 0; it2 < kRansacIters; it2++) {
+    int *s = &idx[(size_t)it2 * 7];
+    for (int i = 0; i < 7; i++) {
+      for (;;) {
+        int v = (int)(rng.next() % (unsigned)count);
+        bool dup = false;
+        for (int j = 0; j < i; j++) dup |= (s[j] == v);
+        if (!dup) {
+          s[i] = v;
+          break;
+        }
+      }
+    }
+  }
+  return idx;
+}
+
+void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
+                   const uint8_t *const *masks, bool device_imgs, const DbSink &db) {
+  device_syncs = 0;
+  if (histogram_method_ == 2)
+    throw HpError(UVIO_HP_E_CONFIG, "histogram_method 2 (CLAHE) is not implemented by the KLT front-end");
+  for (int k = 0; k < ncam; k++) {
+    const int cid = cam_ids[k];
+    const int w = cams_[cid].w, h = cams_[cid].h;
+    if (strides[k] < w) throw HpError(UVIO_HP_E_ARG, "image stride smaller than the configured width");
+    CamState &c = cam_state(cid);
+    const int nw = 1 - c.last;
+    const uint8_t *src = imgs[k];
+    int stride = strides[k];
+    if (!device_imgs) {
+      HP_HIP(hipMemcpy2DAsync(c.d_raw, w, imgs[k], strides[k], w, h, hipMemcpyHostToDevice, s_));
+      src = c.d_raw;
+      stride = w;
+    }
+    launch_equalize(s_, src, w, h, stride, histogram_method_ == 1, c.d_hist, (uint8_t *)c.pyr[nw].img[0]);
+    launch_pyramid(s_, c.pyr[nw]);
+    c.mask_new.clear();
+    if (masks && masks[k]) {
+      c.mask_new.resize((size_t)w * h);
+      for (int y = 0; y < h; y++) std::memcpy(&c.mask_new[(size_t)y * w], masks[k] + (size_t)y * strides[k], w);
+    }
+  }
+  if (ncam == 1) {
+    feed_monocular(t, cam_ids[0], db);
+  } else if (ncam == 2 && use_stereo_) {
+    feed_stereo(t, cam_ids[0], cam_ids[1], db);
+  } else {
+    for (int k = 0; k < ncam; k++) feed_monocular(t, cam_ids[k], db);
+  }
+  // pyr_last / mask_last <- this frame's (every TrackKLT path ends this way)
+  for (int k = 0; k < ncam; k++) {
+    CamState &c = cs_[cam_ids[k]];
+    c.last = 1 - c.last;
+    c.have_last = true;
+    c.mask_last.swap(c.mask_new);
+  }
+}
+
+// ---------------------------------------------------------------- detection
+void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &boxes,
+                      const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
+                      std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st) {
+  (void)cam;
+  out.clear();
+  if (valid.empty()) return;
+  Bufs &b = *b_;
+  const int W = p.w[0], H = p.h[0];
+  int gx = grid_x_, gy = grid_y_;
+  if (num_features_ < gx * gy) {
+    double ratio = (double)gx / (double)gy;
+    gy = (int)std::ceil(std::sqrt(num_features_ / ratio));
+    gx = (int)std::ceil(gy * ratio);
+  }
+  const int nfg = b.kmax;
+  const int size_x = W / gx, size_y = H / gy;
+  int nc = 0;
+  for (auto &g : valid) {
+    int x = g.first * size_x, y = g.second * size_y;
+    if (x + size_x > W || y + size_y > H) continue;
+    b.h_cells[2 * nc] = x;
+    b.h_cells[2 * nc + 1] = y;
+    nc++;
+  }
+  if (nc == 0) return;
+  HP_HIP(hipMemcpyAsync(b.cells, b.h_cells, 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
+  launch_fast_cells(s_, p.img[0], W, H, b.cells, nc, size_x, size_y, threshold_, nfg, b.fast, b.fastn);
+  HP_HIP(hipMemcpyAsync(b.h_fastn, b.fastn, nc * sizeof(int), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.h_fast, b.fast, (size_t)3 * nc * nfg * sizeof(float), hipMemcpyDeviceToHost, s_));
+  sync();
+  const int d = min_px_dist_;
+  for (int c = 0; c < nc; c++)
+    for (int i = 0; i < b.h_fastn[c]; i++) {
+      const float *f = b.h_fast + ((size_t)c * nfg + i) * 3;
+      KeyPt k{f[0], f[1], f[2]};
+      if ((int)k.x < 0 || (int)k.x > W || (int)k.y < 0 || (int)k.y > H) continue;
+      if (mask_px(user_mask, W, (int)k.x, (int)k.y) > 127 || in_boxes(boxes, d, (int)k.x, (int)k.y)) continue;
+      out.push_back(k);
+    }
+  if (out.empty()) return;
+  const int n = (int)out.size();
+  ensure_cap(n);
+  for (int i = 0; i < n; i++) {
+    b.h_det[2 * i] = out[i].x;
+    b.h_det[2 * i + 1] = out[i].y;
+  }
+  HP_HIP(hipMemcpyAsync(b.det, b.h_det, 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
+  launch_subpix(s_, p.img[0], W, H, b.det, n, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
+  if (lk_to) {
+    HP_HIP(hipMemcpyAsync(b.det1, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToDevice, s_));
+    launch_lk(s_, p, *lk_to, b.det, b.det1, b.detst, n, win_, pyr_levels_, kLkIters, kLkEps);
+    HP_HIP(hipMemcpyAsync(b.h_det1, b.det1, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
+    HP_HIP(hipMemcpyAsync(b.h_detst, b.detst, n, hipMemcpyDeviceToHost, s_));
+  }
+  HP_HIP(hipMemcpyAsync(b.h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
+  sync();
+  for (int i = 0; i < n; i++) {
+    out[i].x = b.h_det[2 * i];
+    out[i].y = b.h_det[2 * i + 1];
+  }
+  if (lk_to) {
+    lk_pts->resize(n);
+    lk_st->resize(n);
+    for (int i = 0; i < n; i++) {
+      (*lk_pts)[i] = KeyPt{b.h_det1[2 * i], b.h_det1[2 * i + 1], out[i].response};
+      (*lk_st)[i] = b.h_detst[i];
+    }
+  }
+}
+
+// TrackKLT::perform_detection_monocular (TrackKLT.cpp:395-528)
+void Tracker::detect_monocular(int cam, const DPyr &p, const std::vector<uint8_t> &mask0, std::vector<KeyPt> &pts0,
+                               std::vector<size_t> &ids0) {
+  const int W = p.w[0], H = p.h[0], d = min_px_dist_;
+  const int scw = (int)((float)W / (float)d), sch = (int)((float)H / (float)d);
+  Occupancy close(scw, sch), grid(grid_x_, grid_y_);
+  const float size_x = (float)W / (float)grid_x_, size_y = (float)H / (float)grid_y_;
+  std::vector<int> boxes;
+  std::vector<KeyPt> kp;
+  std::vector<size_t> kid;
+  for (size_t i = 0; i < pts0.size(); i++) {
+    const KeyPt &k = pts0[i];
+    const int x = (int)k.x, y = (int)k.y, edge = 10;
+    if (x < edge || x >= W - edge || y < edge || y >= H - edge) continue;
+    const int xc = (int)(k.x / (float)d), yc = (int)(k.y / (float)d);
+    if (xc < 0 || xc >= scw || yc < 0 || yc >= sch) continue;
+    const int xg = (int)std::floor(k.x / size_x), yg = (int)std::floor(k.y / size_y);
+    if (xg < 0 || xg >= grid_x_ || yg < 0 || yg >= grid_y_) continue;
+    if (close.at(xc, yc) > 127) continue;
+    if (mask_px(mask0, W, x, y) > 127) continue;
+    close.at(xc, yc) = 255;
+    if (grid.at(xg, yg) < 255) grid.at(xg, yg) += 1;
+    if (x - d >= 0 && x + d < W && y - d >= 0 && y + d < H) {
+      boxes.push_back(x);
+      boxes.push_back(y);
+    }
+    kp.push_back(k);
+    kid.push_back(ids0[i]);
+  }
+  pts0.swap(kp);
+  ids0.swap(kid);
+  const int needed = num_features_ - (int)pts0.size();
+  if (needed < std::min(20, (int)(kMinFeatPercent * num_features_))) return;
+  const int nfg = (int)((double)num_features_ / (double)(grid_x_ * grid_y_)) + 1;
+  const int nfg_req = std::max(1, (int)(kMinFeatPercent * nfg));
+  std::vector<std::pair<int, int>> valid;
+  for (int x = 0; x < grid_x_; x++)
+    for (int y = 0; y < grid_y_; y++)
+      if ((int)grid.at(x, y) < nfg_req && (int)mask_cell(mask0, W, H, x, y, grid_x_, grid_y_) != 255) valid.emplace_back(x, y);
+  std::vector<KeyPt> ext;
+  griding(cam, p, mask0, boxes, valid, ext, nullptr, nullptr, nullptr);
+  for (auto &k : ext) {
+    const int xg = (int)(k.x / (float)d), yg = (int)(k.y / (float)d);
+    if (xg < 0 || xg >= scw || yg < 0 || yg >= sch) continue;
+    if (close.at(xg, yg) > 127) continue;
+    close.at(xg, yg) = 255;
+    pts0.push_back(k);
+    ids0.push_back(++currid);
+  }
+}
+
+// TrackKLT::perform_detection_stereo (TrackKLT.cpp:530-827)
+void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, const std::vector<uint8_t> &mask0,
+                            const std::vector<uint8_t> &mask1, std::vector<KeyPt> &pts0, std::vector<KeyPt> &pts1,
+                            std::vector<size_t> &ids0, std::vector<size_t> &ids1) {
+  const int d = min_px_dist_;
+  // ---- left: keep, then detect and track the new points into the right image
+  {
+    const int W = p0.w[0], H = p0.h[0];
+    const int scw = (int)((float)W / (float)d), sch = (int)((float)H / (float)d);
+    Occupancy close(scw, sch), grid(grid_x_, grid_y_);
+    const float size_x = (float)W / (float)grid_x_, size_y = (float)H / (float)grid_y_;
+    std::vector<int> boxes;
+    std::vector<KeyPt> kp;
+    std::vector<size_t> kid;
+    for (size_t i = 0; i < pts0.size(); i++) {
+      const KeyPt &k = pts0[i];
+      const int x = (int)k.x, y = (int)k.y, edge = 10;
+      if (x < edge || x >= W - edge || y < edge || y >= H - edge) continue;
+      const int xc = (int)(k.x / (float)d), yc = (int)(k.y / (float)d);
+      if (xc < 0 || xc >= scw || yc < 0 || yc >= sch) continue;
+      const int xg = (int)std::floor(k.x / size_x), yg = (int)std::floor(k.y / size_y);
+      if (xg < 0 || xg >= grid_x_ || yg < 0 || yg >= grid_y_) continue;
+      if (close.at(xc, yc) > 127) continue;
+      if (mask_px(mask0, W, x, y) > 127) continue;
+      close.at(xc, yc) = 255;
+      if (grid.at(xg, yg) < 255) grid.at(xg, yg) += 1;
+      if (x - d >= 0 && x + d < W && y - d >= 0 && y + d < H) {
+        boxes.push_back(x);
+        boxes.push_back(y);
+      }
+      kp.push_back(k);
+      kid.push_back(ids0[i]);
+    }
+    pts0.swap(kp);
+    ids0.swap(kid);
+    const int needed = num_features_ - (int)pts0.size();
+    if (needed > std::min(20, (int)(kMinFeatPercent * num_features_))) {
+      const int nfg = (int)((double)num_features_ / (double)(grid_x_ * grid_y_)) + 1;
+      const int nfg_req = std::max(1, (int)(kMinFeatPercent * nfg));
+      std::vector<std::pair<int, int>> valid;
+      for (int x = 0; x < grid_x_; x++)
+        for (int y = 0; y < grid_y_; y++)
+          if ((int)grid.at(x, y) < nfg_req && (int)mask_cell(mask0, W, H, x, y, grid_x_, grid_y_) != 255)
+            valid.emplace_back(x, y);
+      // LK into the right image runs on every detected point in the same device pass; the
+      // min-distance filter below then selects the subset the reference tracks (per-point
+      // independent, so the results are the same)
+      std::vector<KeyPt> ext, lk_pts;
+      std::vector<uint8_t> lk_st;
+      griding(cl, p0, mask0, boxes, valid, ext, &p1, &lk_pts, &lk_st);
+      const int W1 = p1.w[0], H1 = p1.h[0];
+      for (size_t e = 0; e < ext.size(); e++) {
+        const KeyPt &k = ext[e];
+        const int xg = (int)(k.x / (float)d), yg = (int)(k.y / (float)d);
+        if (xg < 0 || xg >= scw || yg < 0 || yg >= sch) continue;
+        if (close.at(xg, yg) > 127) continue;
+        close.at(xg, yg) = 255;
+        const KeyPt &k1 = lk_pts[e];
+        const bool oobl = ((int)k.x < 0 || (int)k.x >= W || (int)k.y < 0 || (int)k.y >= H);
+        const bool oobr = ((int)k1.x < 0 || (int)k1.x >= W1 || (int)k1.y < 0 || (int)k1.y >= H1);
+        if (!oobl && !oobr && lk_st[e] == 1) {
+          pts0.push_back(k);
+          pts1.push_back(k1);
+          const size_t id = ++currid;
+          ids0.push_back(id);
+          ids1.push_back(id);
+        } else if (!oobl) {
+          pts0.push_back(k);
+          ids0.push_back(++currid);
+        }
+      }
+    }
+  }
+  // ---- right
+  {
+    const int W = p1.w[0], H = p1.h[0];
+    const int scw = (int)((float)W / (float)d), sch = (int)((float)H / (float)d);
+    Occupancy close(scw, sch), grid(grid_x_, grid_y_);
+    const float size_x = (float)W / (float)grid_x_, size_y = (float)H / (float)grid_y_;
+    std::vector<int> boxes;  // drawn into a clone of the LEFT mask (TrackKLT.cpp:713)
+    std::vector<KeyPt> kp;
+    std::vector<size_t> kid;
+    for (size_t i = 0; i < pts1.size(); i++) {
+      const KeyPt &k = pts1[i];
+      const int x = (int)k.x, y = (int)k.y, edge = 10;
+      if (x < edge || x >= W - edge || y < edge || y >= H - edge) continue;
+      const int xc = (int)(k.x / (float)d), yc = (int)(k.y / (float)d);
+      if (xc < 0 || xc >= scw || yc < 0 || yc >= sch) continue;
+      const int xg = (int)std::floor(k.x / size_x), yg = (int)std::floor(k.y / size_y);
+      if (xg < 0 || xg >= grid_x_ || yg < 0 || yg >= grid_y_) continue;
+      const bool is_stereo = std::find(ids0.begin(), ids0.end(), ids1[i]) != ids0.end();
+      if (close.at(xc, yc) > 127 && !is_stereo) continue;
+      if (mask_px(mask1, W, x, y) > 127) continue;
+      close.at(xc, yc) = 255;
+      if (grid.at(xg, yg) < 255) grid.at(xg, yg) += 1;
+      if (x - d >= 0 && x + d < W && y - d >= 0 && y + d < H) {
+        boxes.push_back(x);
+        boxes.push_back(y);
+      }
+      kp.push_back(k);
+      kid.push_back(ids1[i]);
+    }
+    pts1.swap(kp);
+    ids1.swap(kid);
+    const int needed = num_features_ - (int)pts1.size();
+    if (needed > std::min(20, (int)(kMinFeatPercent * num_features_))) {
+      const int nfg = (int)((double)num_features_ / (double)(grid_x_ * grid_y_)) + 1;
+      const int nfg_req = std::max(1, (int)(kMinFeatPercent * nfg));
+      std::vector<std::pair<int, int>> valid;
+      for (int x = 0; x < grid_x_; x++)
+        for (int y = 0; y < grid_y_; y++)
+          if ((int)grid.at(x, y) < nfg_req && (int)mask_cell(mask1, W, H, x, y, grid_x_, grid_y_) != 255)
+            valid.emplace_back(x, y);
+      std::vector<KeyPt> ext;
+      griding(cr, p1, mask0, boxes, valid, ext, nullptr, nullptr, nullptr);
+      for (auto &k : ext) {
+        const int xg = (int)(k.x / (float)d), yg = (int)(k.y / (float)d);
+        if (xg < 0 || xg >= scw || yg < 0 || yg >= sch) continue;
+        if (close.at(xg, yg) > 127) continue;
+        pts1.push_back(k);
+        ids1.push_back(++currid);
+        close.at(xg, yg) = 255;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- temporal matching
+// TrackKLT::perform_matching (TrackKLT.cpp:829-886): LK from the last pyramid, then
+// findFundamentalMat(FM_RANSAC, 2 / max focal, 0.999) on undistorted points, all on the device
+void Tracker::match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
+                           MatchJob &j) {
+  j.n = (int)k0.size();
+  j.run = j.n >= 10;
+  if (!j.run) return;
+  const int n = j.n;
+  ensure_cap(n);
+  Bufs &b = *b_;
+  for (int i = 0; i < n; i++) {
+    b.h_p0[slot][2 * i] = k0[i].x;
+    b.h_p0[slot][2 * i + 1] = k0[i].y;
+  }
+  const std::vector<int> &sub = subsets(n);
+  std::memcpy(b.h_sub[slot], sub.data(), sub.size() * sizeof(int));
+  HP_HIP(hipMemcpyAsync(b.p0[slot], b.h_p0[slot], 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
+  HP_HIP(hipMemcpyAsync(b.p1[slot], b.h_p0[slot], 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
+  HP_HIP(hipMemcpyAsync(b.sub[slot], b.h_sub[slot], sub.size() * sizeof(int), hipMemcpyHostToDevice, s_));
+  launch_lk(s_, p0, p1, b.p0[slot], b.p1[slot], b.st[slot], n, win_, pyr_levels_, kLkIters, kLkEps);
+  const CamParams &c0 = cams_[cam0], &c1 = cams_[cam1];
+  const double fmax = std::max(std::max(c0.v[0], c0.v[1]), std::max(c1.v[0], c1.v[1]));
+  launch_ransac(s_, c0, c1, b.p0[slot], b.p1[slot], n, b.p0n[slot], b.p1n[slot], b.sub[slot], kRansacIters, 2.0 / fmax,
+                kRansacConf, b.F[slot], b.nm[slot], b.good[slot], b.mask[slot]);
+  HP_HIP(hipMemcpyAsync(b.h_p1[slot], b.p1[slot], 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.h_st[slot], b.st[slot], n, hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.h_mask[slot], b.mask[slot], n, hipMemcpyDeviceToHost, s_));
+}
+
+void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out) {
+  mask_out.clear();
+  if (j.n == 0) return;
+  if (!j.run) {
+    mask_out.assign(j.n, 0);
+    return;
+  }
+  Bufs &b = *b_;
+  mask_out.resize(j.n);
+  for (int i = 0; i < j.n; i++) {
+    k1[i].x = b.h_p1[slot][2 * i];
+    k1[i].y = b.h_p1[slot][2 * i + 1];
+    mask_out[i] = (b.h_st[slot][i] && b.h_mask[slot][i]) ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------- per-frame logic
+// TrackKLT::feed_monocular (TrackKLT.cpp:96-200)
+void Tracker::feed_monocular(double t, int cam, const DbSink &db) {
+  CamState &c = cs_[cam];
+  const DPyr &pn = c.pyr[1 - c.last], &pl = c.pyr[c.last];
+  if (c.pts_last.empty()) {
+    std::vector<KeyPt> good;
+    std::vector<size_t> gid;
+    detect_monocular(cam, pn, c.mask_new, good, gid);
+    c.pts_last = good;
+    c.ids_last = gid;
+    return;
+  }
+  std::vector<KeyPt> pts_old = c.pts_last;
+  std::vector<size_t> ids_old = c.ids_last;
+  detect_monocular(cam, pl, c.mask_last, pts_old, ids_old);
+  MatchJob j;
+  match_launch(0, pl, pn, cam, cam, pts_old, j);
+  if (j.run) sync();
+  std::vector<KeyPt> pts_new = pts_old;
+  std::vector<uint8_t> mask_ll;
+  match_collect(0, j, pts_new, mask_ll);
+  if (mask_ll.empty()) {
+    c.pts_last.clear();
+    c.ids_last.clear();
+    return;
+  }
+  const int W = pn.w[0], H = pn.h[0];
+  std::vector<KeyPt> good;
+  std::vector<size_t> gid;
+  for (size_t i = 0; i < pts_new.size(); i++) {
+    if (pts_new[i].x < 0 || pts_new[i].y < 0 || (int)pts_new[i].x >= W || (int)pts_new[i].y >= H) continue;
+    if (mask_px(c.mask_new, W, (int)pts_new[i].x, (int)pts_new[i].y) > 127) continue;
+    if (mask_ll[i]) {
+      good.push_back(pts_new[i]);
+      gid.push_back(ids_old[i]);
+    }
+  }
+  for (size_t i = 0; i < good.size(); i++) {
+    float un, vn;
+    cam_undistort_f(cams_[cam], good[i].x, good[i].y, un, vn);
+    db(gid[i], t, cam, good[i].x, good[i].y, un, vn);
+  }
+  c.pts_last.swap(good);
+  c.ids_last.swap(gid);
+}
+
+// TrackKLT::feed_stereo (TrackKLT.cpp:202-393)
+void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
+  CamState &A = cs_[cl], &B = cs_[cr];
+  const DPyr &nl = A.pyr[1 - A.last], &nr = B.pyr[1 - B.last];
+  const DPyr &ll = A.pyr[A.last], &lr = B.pyr[B.last];
+  if (A.pts_last.empty() && B.pts_last.empty()) {
+    std::vector<KeyPt> gl, gr;
+    std::vector<size_t> il, ir;
+    detect_stereo(cl, cr, nl, nr, A.mask_new, B.mask_new, gl, gr, il, ir);
+    A.pts_last = gl;
+    B.pts_last = gr;
+    A.ids_last = il;
+    B.ids_last = ir;
+    return;
+  }
+  std::vector<KeyPt> pl_old = A.pts_last, pr_old = B.pts_last;
+  std::vector<size_t> il_old = A.ids_last, ir_old = B.ids_last;
+  detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
+  MatchJob jl, jr;
+  ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two launches
+  match_launch(0, ll, nl, cl, cl, pl_old, jl);
+  match_launch(1, lr, nr, cr, cr, pr_old, jr);
+  if (jl.run || jr.run) sync();
+  std::vector<KeyPt> pl_new = pl_old, pr_new = pr_old;
+  std::vector<uint8_t> mask_ll, mask_rr;
+  match_collect(0, jl, pl_new, mask_ll);
+  match_collect(1, jr, pr_new, mask_rr);
+  if (mask_ll.empty() && mask_rr.empty()) {
+    A.pts_last.clear();
+    B.pts_last.clear();
+    A.ids_last.clear();
+    B.ids_last.clear();
+    return;
+  }
+  const int Wl = nl.w[0], Hl = nl.h[0], Wr = nr.w[0], Hr = nr.h[0];
+  std::vector<KeyPt> gl, gr;
+  std::vector<size_t> gil, gir;
+  for (size_t i = 0; i < pl_new.size(); i++) {
+    if (pl_new[i].x < 0 || pl_new[i].y < 0 || (int)pl_new[i].x > Wl || (int)pl_new[i].y > Hl) continue;
+    bool found = false;
+    size_t ir = 0;
+    for (size_t n = 0; n < ir_old.size(); n++)
+      if (il_old[i] == ir_old[n]) {
+        found = true;
+        ir = n;
+        break;
+      }
+    if (mask_ll[i] && found && mask_rr[ir]) {
+      if (pr_new[ir].x < 0 || pr_new[ir].y < 0 || (int)pr_new[ir].x >= Wr || (int)pr_new[ir].y >= Hr) continue;
+      gl.push_back(pl_new[i]);
+      gr.push_back(pr_new[ir]);
+      gil.push_back(il_old[i]);
+      gir.push_back(ir_old[ir]);
+    } else if (mask_ll[i]) {
+      gl.push_back(pl_new[i]);
+      gil.push_back(il_old[i]);
+    }
+  }
+  for (size_t i = 0; i < pr_new.size(); i++) {
+    if (pr_new[i].x < 0 || pr_new[i].y < 0 || (int)pr_new[i].x >= Wr || (int)pr_new[i].y >= Hr) continue;
+    const bool added = std::find(gir.begin(), gir.end(), ir_old[i]) != gir.end();
+    if (mask_rr[i] && !added) {
+      gr.push_back(pr_new[i]);
+      gir.push_back(ir_old[i]);
+    }
+  }
+  for (size_t i = 0; i < gl.size(); i++) {
+    float un, vn;
+    cam_undistort_f(cams_[cl], gl[i].x, gl[i].y, un, vn);
+    db(gil[i], t, cl, gl[i].x, gl[i].y, un, vn);
+  }
+  for (size_t i = 0; i < gr.size(); i++) {
+    float un, vn;
+    cam_undistort_f(cams_[cr], gr[i].x, gr[i].y, un, vn);
+    db(gir[i], t, cr, gr[i].x, gr[i].y, un, vn);
+  }
+  A.pts_last.swap(gl);
+  B.pts_last.swap(gr);
+  A.ids_last.swap(gil);
+  B.ids_last.swap(gir);
+}
+
+// ---------------------------------------------------------------- inspection
+void Tracker::last_tracks(int cam, std::vector<KeyPt> &pts, std::vector<size_t> &ids) const {
+  pts.clear();
+  ids.clear();
+  auto it = cs_.find(cam);
+  if (it == cs_.end()) return;
+  pts = it->second.pts_last;
+  ids = it->second.ids_last;
+}
+
+bool Tracker::last_pyramid(int cam, int level, int *w, int *h, std::vector<uint8_t> *img, std::vector<int16_t> *der) {
+  auto it = cs_.find(cam);
+  if (it == cs_.end() || !it->second.have_last) return false;
+  const DPyr &p = it->second.pyr[it->second.last];
+  if (level < 0 || level >= p.levels) return false;
+  *w = p.w[level];
+  *h = p.h[level];
+  sync();
+  if (img) {
+    img->resize((size_t)*w * *h);
+    HP_HIP(hipMemcpy(img->data(), p.img[level], img->size(), hipMemcpyDeviceToHost));
+  }
+  if (der) {
+    der->resize((size_t)*w * *h * 2);
+    HP_HIP(hipMemcpy(der->data(), p.der[level], der->size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+  }
+  return true;
+}
+
+}  // namespace uvhp

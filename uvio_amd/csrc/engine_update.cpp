@@ -172,6 +172,29 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
       db_update((size_t)ids[k] + currid_, t, cid, uv[2 * k], uv[2 * k + 1], un, vn);
     }
   }
+  return after_tracking(t, camids, rT1);
+}
+
+// VioManager::feed_measurement_camera -> TrackKLT::feed_new_camera (TrackKLT.cpp:34-94), then the
+// same propagate / update sequence as the simulated feed
+int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
+                        const uint8_t *const *masks, bool device_imgs) {
+  auto rT1 = clk::now();
+  std::vector<int> camids;
+  for (int i = 0; i < ncam; i++) {
+    int cid = cam_ids[i];
+    if (cid < 0 || cid >= o_.num_cameras || !imgs[i]) return UVIO_HP_E_ARG;
+    camids.push_back(cid);
+  }
+  if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream));
+  tracker_->feed(t, ncam, cam_ids, imgs, strides, masks, device_imgs,
+                 [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
+                   db_update(id, tt, (size_t)cam, u, v, un, vn);
+                 });
+  return after_tracking(t, camids, rT1);
+}
+
+int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1) {
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
   timing_.tracking = secs(rT1, rT2);

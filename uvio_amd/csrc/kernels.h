@@ -124,8 +124,8 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 // EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j
 // maps to covariance index hidx[j] (device), residual res (r, device, stride res_stride), noise sigma2.
 // Scratch: M (N x r), W (N x r), S (3 r x r: Linv, global work, S_up), y (r), dx (N), neg (int).
-constexpr int kMaxEkfRows = 256;
-constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-workgroup solvers  // rows of one direct (uncompressed) EKF update
+constexpr int kMaxEkfRows = 256;        // rows of one direct (uncompressed) EKF update
+constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-workgroup solvers
 // S holds 5 r^2 doubles for r rows
 struct EkfScratch {
   double *M, *W, *S, *y, *dx;
@@ -147,5 +147,51 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc);
 double chi2_quantile95(int dof);
+
+// Raise a kernel's dynamic-LDS limit to `want` bytes, capped so static + dynamic LDS fits the CU's
+// 160 KiB.  Returns the granted bytes (0 on failure); a failed call's sticky runtime error is cleared so
+// it cannot surface in another library (torch) on this thread.
+inline int set_dyn_lds(const void *fn, int want) {
+  hipFuncAttributes a{};
+  int stat = 0;
+  if (hipFuncGetAttributes(&a, fn) == hipSuccess)
+    stat = (int)a.sharedSizeBytes;
+  else
+    (void)hipGetLastError();
+  int v = want < 160 * 1024 - stat ? want : 160 * 1024 - stat;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, v) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return v;
+}
+
+// ---- KLT front-end (kernels_track.hip) ----
+constexpr int kMaxPyrLevels = 8;
+// one image pyramid in HBM: level l image (w x h u8, packed) and Scharr derivatives (w x h x 2 int16)
+struct DPyr {
+  const uint8_t *img[kMaxPyrLevels];
+  const int16_t *der[kMaxPyrLevels];
+  int w[kMaxPyrLevels], h[kMaxPyrLevels];
+  int levels;
+};
+// equalizeHist (or copy when !equalize) of src (row stride `stride`) into dst (packed); hist: 256 u32
+void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride, int equalize, unsigned *hist,
+                     uint8_t *dst);
+// pyrDown + Scharr for every level of p (level 0 image already written)
+void launch_pyramid(hipStream_t s, DPyr &p);
+// FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell
+void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
+                       int kmax, float *out, int *out_n);
+// cornerSubPix in place on n points (x, y); mask: (2 win + 1)^2 weights
+void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
+                   int max_iters, double eps2);
+// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW: p1 holds the initial guess, is overwritten
+void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
+               int max_level, int max_iters, float eps);
+// undistort both point sets, then findFundamentalMat(FM_RANSAC) mask over host-drawn subsets
+void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
+                   float *p0n, float *p1n, const int *subsets, int max_iters, double thr, double conf, double *Fs,
+                   int *nmodels, int *good, uint8_t *mask);
 
 }  // namespace uvhp

@@ -12,6 +12,9 @@
 // chi2 = sum_k z_k^2 / d_k = r^T S^-1 r.  Rejected MSCKF / SLAM features get their rows zeroed so the
 // batch Gram (compression) and the direct EKF see only accepted rows.
 #include "dense_lds.h"
+#include <stdexcept>
+#include <string>
+
 #include "kernels.h"
 
 namespace uvhp {
@@ -178,11 +181,10 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = (size_t)(max_rows_f + 1) * (max_rows_f | 1) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_chi2, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
-    attr = true;
-  }
+  static int granted = -1;
+  if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
+  if (bytes > 64 * 1024 && (int)bytes > granted)
+    throw std::runtime_error("k_chi2 needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
   hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds);
 }
 

@@ -8,6 +8,9 @@
 //     [H_x | res] (DESIGN.md "Compression").
 //   EKFUpdate              StateHelper.cpp:116-197 as M = P[:,I] H^T, S = H M[I,:] + s2 I = L L^T,
 //                          W = M L^-T, P -= W W^T (upper, mirrored), dx = W L^-1 r.
+#include <stdexcept>
+#include <string>
+
 #include "kernels.h"
 #include "dense_lds.h"
 
@@ -623,10 +626,12 @@ void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const doub
 static void ensure_lds_attrs() {
   static bool done = false;
   if (done) return;
-  hipFuncSetAttribute((const void *)k_gram_reduce_chol, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-  hipFuncSetAttribute((const void *)k_ekf_small, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
-  hipFuncSetAttribute((const void *)k_info_cholP, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
-  hipFuncSetAttribute((const void *)k_info_cholZ, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxDynLds);
+  const void *fns[4] = {(const void *)k_gram_reduce_chol, (const void *)k_ekf_small, (const void *)k_info_cholP,
+                        (const void *)k_info_cholZ};
+  const int want[4] = {150 * 1024, kMaxDynLds, kMaxDynLds, kMaxDynLds};
+  for (int k = 0; k < 4; k++)
+    if (set_dyn_lds(fns[k], want[k]) < want[k])
+      throw std::runtime_error("dynamic LDS limit not granted for a covariance kernel (" + std::to_string(k) + ")");
   done = true;
 }
 

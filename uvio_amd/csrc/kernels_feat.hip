@@ -14,6 +14,9 @@
 // The chi2 gate (UpdaterMSCKF.cpp:209-234) runs afterwards for the whole batch (kernels_chi2.hip):
 // T = H_all P_can as one GEMM over the shared canonical covariance block, then one workgroup per
 // feature forms S = T Hhat^T + s2 I, factors [S | r] and zeroes the rows of rejected features.
+#include <stdexcept>
+#include <string>
+
 #include "kernels.h"
 
 namespace uvhp {
@@ -687,11 +690,10 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf) {
   if (bp.nfeat <= 0) return;
   size_t bytes = feature_lds_bytes(max_meas, max_nf);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void *)k_feature, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
-    attr = true;
-  }
+  static int granted = -1;
+  if (granted < 0) granted = set_dyn_lds((const void *)k_feature, 156 * 1024);
+  if (bytes > 64 * 1024 && (int)bytes > granted)
+    throw std::runtime_error("k_feature needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
   hipLaunchKernelGGL(k_feature, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, meas, vars, clones, cams, P,
                      chi2_table, H_all, out, max_meas, max_nf);
 }

@@ -1,0 +1,721 @@
+// KLT front-end kernels (TrackKLT.cpp:34-886, Grider_GRID.h:74-180 over the OpenCV primitives they
+// call; restated in oracle/src/tracker.cpp).  Byte / integer work throughout
+// except cornerSubPix (double) and the LK float tail; every result is bit-identical to the oracle:
+//   k_hist + k_equalize      equalizeHist: LDS histogram, LUT per workgroup from the global counts
+//   k_pyrdown                pyrDown 5x5 (sum + 128) >> 8, reflect-101
+//   k_scharr                 Scharr dx/dy int16, reflect-101 (calcSharrDeriv)
+//   k_fast_cells             FAST-9 + 3x3 NMS + top-k per grid cell (one workgroup per valid cell)
+//   k_subpix                 cornerSubPix, one thread per point (sequential sums = oracle order)
+//   k_lk                     pyramidal LK, one wavefront per point, exact integer window sums
+//   k_undistort              cv::undistortPoints restatement (hp_math.h)
+//   k_ransac_hyp / _select   7-point RANSAC: all hypotheses in parallel, then the sequential
+//                            adaptive-iteration scan of RANSACPointSetRegistrator::run on one lane
+#include <stdexcept>
+
+#include "kernels.h"
+
+namespace uvhp {
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = (p < 0) ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+// ---------------------------------------------------------------- equalizeHist
+__global__ void __launch_bounds__(256) k_hist(const uint8_t *__restrict__ img, int w, int h, int stride,
+                                              unsigned *__restrict__ hist) {
+  __shared__ unsigned hs[256];
+  hs[threadIdx.x] = 0;
+  __syncthreads();
+  const int n = w * h;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    int y = e / w, x = e - y * w;
+    atomicAdd(&hs[img[(size_t)y * stride + x]], 1u);
+  }
+  __syncthreads();
+  if (hs[threadIdx.x]) atomicAdd(&hist[threadIdx.x], hs[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) k_equalize(const uint8_t *__restrict__ src, int w, int h, int stride,
+                                                  const unsigned *__restrict__ hist, int equalize,
+                                                  uint8_t *__restrict__ dst) {
+  // LUT of EqualizeHistLut_Invoker from an inclusive LDS scan of the counts (blockDim == 256)
+  __shared__ uint8_t lut[256];
+  __shared__ int scan[256];
+  __shared__ int first;
+  const int t = threadIdx.x;
+  if (!equalize) {
+    lut[t] = (uint8_t)t;
+  } else {
+    const int hv = (int)hist[t];
+    scan[t] = hv;
+    if (t == 0) first = 256;
+    __syncthreads();
+    if (hv) atomicMin(&first, t);
+    for (int o = 1; o < 256; o <<= 1) {
+      int v = (t >= o) ? scan[t - o] : 0;
+      __syncthreads();
+      scan[t] += v;
+      __syncthreads();
+    }
+    const int i0 = first, total = w * h, h0 = (int)hist[i0];
+    if (h0 == total) {
+      lut[t] = (uint8_t)i0;
+    } else if (t <= i0) {
+      lut[t] = 0;
+    } else {
+      float scale = __fdiv_rn(256 - 1.f, (float)(total - h0));
+      int sum = scan[t] - scan[i0];
+      int r = (int)rintf(__fmul_rn((float)sum, scale));
+      lut[t] = (uint8_t)min(255, max(0, r));
+    }
+  }
+  __syncthreads();
+  const int n = w * h;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    int y = e / w, x = e - y * w;
+    dst[e] = lut[src[(size_t)y * stride + x]];
+  }
+}
+
+// ---------------------------------------------------------------- pyramid
+__global__ void k_pyrdown(const uint8_t *__restrict__ src, int sw, int sh, uint8_t *__restrict__ dst, int dw, int dh) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const int k[5] = {1, 4, 6, 4, 1};
+  int xs[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
+  int acc = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * sw;
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) r += k[j] * row[xs[j]];
+    acc += k[i] * r;
+  }
+  dst[(size_t)y * dw + x] = (uint8_t)((acc + 128) >> 8);
+}
+
+__global__ void k_scharr(const uint8_t *__restrict__ s, int w, int h, int16_t *__restrict__ d) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= w || y >= h) return;
+  const uint8_t *r0 = s + (size_t)reflect101(y - 1, h) * w, *r1 = s + (size_t)y * w, *r2 = s + (size_t)reflect101(y + 1, h) * w;
+  int xm = reflect101(x - 1, w), xp = reflect101(x + 1, w);
+  int t0m = (r0[xm] + r2[xm]) * 3 + r1[xm] * 10, t0p = (r0[xp] + r2[xp]) * 3 + r1[xp] * 10;
+  int t1m = r2[xm] - r0[xm], t1p = r2[xp] - r0[xp], t1 = r2[x] - r0[x];
+  d[((size_t)y * w + x) * 2] = (int16_t)(t0p - t0m);
+  d[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1p + t1m) * 3 + t1 * 10);
+}
+
+// ---------------------------------------------------------------- FAST-9 on grid cells
+__constant__ int c_fast_off[16][2] = {{0, 3},  {1, 3},  {2, 2},  {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                                      {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+__device__ int fast_corner_score(const uint8_t *img, int w, int x, int y, int thr) {
+  const int v = img[(size_t)y * w + x];
+  int ring[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) ring[k] = img[(size_t)(y + c_fast_off[k][1]) * w + x + c_fast_off[k][0]];
+  bool corner = false;
+  for (int pass = 0; pass < 2 && !corner; pass++) {
+    int count = 0;
+    for (int k = 0; k < 25; k++) {
+      int p = ring[k & 15];
+      bool ok = (pass == 0) ? (p < v - thr) : (p > v + thr);
+      if (ok) {
+        if (++count > 8) {
+          corner = true;
+          break;
+        }
+      } else {
+        count = 0;
+      }
+    }
+  }
+  if (!corner) return 0;
+  int d[25];
+#pragma unroll
+  for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
+  int a0 = thr;
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    if (a <= a0) continue;
+    a = min(a, d[k + 4]);
+    a = min(a, d[k + 5]);
+    a = min(a, d[k + 6]);
+    a = min(a, d[k + 7]);
+    a = min(a, d[k + 8]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+    b = max(b, d[k + 3]);
+    b = max(b, d[k + 4]);
+    b = max(b, d[k + 5]);
+    if (b >= b0) continue;
+    b = max(b, d[k + 6]);
+    b = max(b, d[k + 7]);
+    b = max(b, d[k + 8]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// one workgroup per cell; LDS holds the cell's score map (u8) and the NMS survivors.  Output per cell:
+// up to kmax keypoints (x, y, response) in (response desc, raster asc) order, image coordinates.
+// Strict 3x3 NMS leaves no two adjacent survivors, so a cell has at most ceil(sw/2) ceil(sh/2).
+__host__ __device__ inline int fast_max_cand(int sw, int sh) { return ((sw + 1) / 2) * ((sh + 1) / 2); }
+__host__ __device__ inline size_t fast_lds_bytes(int sw, int sh) {
+  return (size_t)fast_max_cand(sw, sh) * 8 + (((size_t)sw * sh + 15) & ~(size_t)15);
+}
+__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t *__restrict__ img, int w, int h,
+                                                    const int *__restrict__ cells, int sw, int sh, int thr, int kmax,
+                                                    float *__restrict__ out, int *__restrict__ out_n) {
+  extern __shared__ int lds_fast[];
+  const int kFastMaxCand = fast_max_cand(sw, sh);
+  int *cand_idx = lds_fast, *cand_s = lds_fast + kFastMaxCand;
+  uint8_t *score = (uint8_t *)(cand_s + kFastMaxCand);  // sw * sh
+  __shared__ int ncand;
+  const int c = blockIdx.x;
+  const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
+  if (threadIdx.x == 0) ncand = 0;
+  for (int e = threadIdx.x; e < sw * sh; e += blockDim.x) {
+    int i = e / sw, j = e - i * sw;
+    int s = 0;
+    if (i >= 3 && i < sh - 3 && j >= 3 && j < sw - 3) s = fast_corner_score(img, w, x0 + j, y0 + i, thr);
+    score[e] = (uint8_t)s;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < sw * sh; e += blockDim.x) {
+    int s = score[e];
+    if (s == 0) continue;
+    int i = e / sw, j = e - i * sw;
+    bool keep = true;
+    for (int di = -1; di <= 1 && keep; di++)
+      for (int dj = -1; dj <= 1; dj++) {
+        if (!di && !dj) continue;
+        if (s <= score[(i + di) * sw + j + dj]) {
+          keep = false;
+          break;
+        }
+      }
+    if (keep) {
+      int slot = atomicAdd(&ncand, 1);
+      if (slot < kFastMaxCand) {
+        cand_idx[slot] = e;
+        cand_s[slot] = s;
+      }
+    }
+  }
+  __syncthreads();
+  const int n = min(ncand, kFastMaxCand);
+  // rank = #candidates ordered before this one (response desc, raster asc): the stable sort order
+  for (int a = threadIdx.x; a < n; a += blockDim.x) {
+    int sa = cand_s[a], ia = cand_idx[a], rank = 0;
+    for (int b = 0; b < n; b++) {
+      int sb = cand_s[b];
+      rank += (sb > sa) || (sb == sa && cand_idx[b] < ia);
+    }
+    if (rank < kmax) {
+      float *o = out + ((size_t)c * kmax + rank) * 3;
+      o[0] = (float)(x0 + ia % sw);
+      o[1] = (float)(y0 + ia / sw);
+      o[2] = (float)sa;
+    }
+  }
+  if (threadIdx.x == 0) out_n[c] = min(n, kmax);
+}
+
+// ---------------------------------------------------------------- cornerSubPix
+__device__ __forceinline__ float px_clamped(const uint8_t *img, int w, int h, int x, int y) {
+  x = min(max(x, 0), w - 1);
+  y = min(max(y, 0), h - 1);
+  return (float)img[(size_t)y * w + x];
+}
+
+// one thread per point: the sums run in the oracle's raster order, so results are bit-identical
+__global__ void k_subpix(const uint8_t *__restrict__ img, int w, int h, float *__restrict__ pts, int n,
+                         const float *__restrict__ mask, int win, int max_iters, double eps2) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int win_w = 2 * win + 1, bw = win_w + 2;  // bilinear buffer (win_w + 2)^2, <= 13 x 13 for win 5
+  float buf[13 * 13];
+  const float cTx = pts[2 * p], cTy = pts[2 * p + 1];
+  float cIx = cTx, cIy = cTy;
+  int iter = 0;
+  double err = 0;
+  do {
+    float cx = cIx - (bw - 1) * 0.5f, cy = cIy - (bw - 1) * 0.5f;
+    int ix = (int)floorf(cx), iy = (int)floorf(cy);
+    float a = cx - ix, b = cy - iy;
+    float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+    for (int i = 0; i < bw; i++)
+      for (int j = 0; j < bw; j++) {
+        int x = ix + j, y = iy + i;
+        buf[i * bw + j] = px_clamped(img, w, h, x, y) * a11 + px_clamped(img, w, h, x + 1, y) * a12 +
+                          px_clamped(img, w, h, x, y + 1) * a21 + px_clamped(img, w, h, x + 1, y + 1) * a22;
+      }
+    double sa = 0, sb = 0, sc = 0, bb1 = 0, bb2 = 0;
+    const float *sp = buf + bw + 1;
+    for (int i = 0, k = 0; i < win_w; i++, sp += bw) {
+      double py = i - win;
+      for (int j = 0; j < win_w; j++, k++) {
+        double m = mask[k];
+        double tgx = sp[j + 1] - sp[j - 1];
+        double tgy = sp[j + bw] - sp[j - bw];
+        double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+        double pxv = j - win;
+        sa += gxx;
+        sb += gxy;
+        sc += gyy;
+        bb1 += gxx * pxv + gxy * py;
+        bb2 += gxy * pxv + gyy * py;
+      }
+    }
+    double det = sa * sc - sb * sb;
+    if (fabs(det) <= 4.930380657631324e-32) break;  // DBL_EPSILON^2
+    double scale = 1.0 / det;
+    float nx = (float)(cIx + sc * scale * bb1 - sb * scale * bb2);
+    float ny = (float)(cIy - sb * scale * bb1 + sa * scale * bb2);
+    err = (double)(nx - cIx) * (nx - cIx) + (double)(ny - cIy) * (ny - cIy);
+    cIx = nx;
+    cIy = ny;
+    if (cIx < 0 || cIx >= w || cIy < 0 || cIy >= h) break;
+  } while (++iter < max_iters && err > eps2);
+  if (fabsf(cIx - cTx) > win || fabsf(cIy - cTy) > win) {
+    cIx = cTx;
+    cIy = cTy;
+  }
+  pts[2 * p] = cIx;
+  pts[2 * p + 1] = cIy;
+}
+
+// ---------------------------------------------------------------- pyramidal LK
+__device__ __forceinline__ int img_px(const uint8_t *g, int w, int h, int x, int y) {
+  return g[(size_t)reflect101(y, h) * w + reflect101(x, w)];
+}
+__device__ __forceinline__ int der_px(const int16_t *d, int w, int h, int x, int y, int c) {
+  if (x < 0 || y < 0 || x >= w || y >= h) return 0;
+  return d[((size_t)y * w + x) * 2 + c];
+}
+__device__ __forceinline__ int descale(long long x, int n) { return (int)((x + (1ll << (n - 1))) >> n); }
+__device__ __forceinline__ long long wave_sum_ll(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one 64-lane workgroup per point; lanes own window pixels lane, lane+64, ... (225 for win 15).
+// (qx, qy) is nextPts[ptidx] of LKTrackerInvoker: it carries the result between levels, and an
+// early exit leaves it at its last written value, exactly as the oracle's p1[pi].
+__device__ __forceinline__ int bilin_img(const uint8_t *g, int w, int h, int X, int Y, int i00, int i01, int i10, int i11) {
+  return descale((long long)img_px(g, w, h, X, Y) * i00 + img_px(g, w, h, X + 1, Y) * i01 + img_px(g, w, h, X, Y + 1) * i10 +
+                     img_px(g, w, h, X + 1, Y + 1) * i11,
+                 14 - 5);
+}
+__device__ __forceinline__ int bilin_der(const int16_t *d, int w, int h, int X, int Y, int c, int i00, int i01, int i10,
+                                         int i11) {
+  return descale((long long)der_px(d, w, h, X, Y, c) * i00 + der_px(d, w, h, X + 1, Y, c) * i01 +
+                     der_px(d, w, h, X, Y + 1, c) * i10 + der_px(d, w, h, X + 1, Y + 1, c) * i11,
+                 14);
+}
+
+__global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__restrict__ p0, float *__restrict__ p1,
+                                           uint8_t *__restrict__ status, int n, int win, int max_level, int max_iters,
+                                           float crit_eps) {
+  const int pi = blockIdx.x;
+  if (pi >= n) return;
+  const int lane = threadIdx.x;
+  const int maxL = min(max_level, min(prev.levels, next.levels) - 1);
+  const float halfw = (win - 1) * 0.5f;
+  const float FLT_SCALE = 1.f / (1 << 20);
+  const float WSCALE = (float)(1 << 14);
+  const int area = win * win;
+  constexpr int kPer = 4;  // ceil(225 / 64)
+  int Iw[kPer], dIx[kPer], dIy[kPer];
+  float qx = p1[2 * pi], qy = p1[2 * pi + 1];
+  uint8_t st = 1;
+  for (int level = maxL; level >= 0; level--) {
+    const uint8_t *I = prev.img[level], *J = next.img[level];
+    const int16_t *dI = prev.der[level];
+    const int Iw_ = prev.w[level], Ih_ = prev.h[level], Jw_ = next.w[level], Jh_ = next.h[level];
+    const float sc = (float)(1. / (1 << level));
+    float prx = p0[2 * pi] * sc, pry = p0[2 * pi + 1] * sc;
+    if (level == maxL) {
+      qx = qx * sc;
+      qy = qy * sc;
+    } else {
+      qx = qx * 2.f;
+      qy = qy * 2.f;
+    }
+    prx -= halfw;
+    pry -= halfw;
+    const int ipx = (int)floorf(prx), ipy = (int)floorf(pry);
+    if (ipx < -win || ipx >= Iw_ || ipy < -win || ipy >= Ih_) {
+      if (level == 0) st = 0;
+      continue;
+    }
+    float a = prx - ipx, b = pry - ipy;
+    int iw00 = (int)rintf((1.f - a) * (1.f - b) * WSCALE);
+    int iw01 = (int)rintf(a * (1.f - b) * WSCALE);
+    int iw10 = (int)rintf((1.f - a) * b * WSCALE);
+    int iw11 = (1 << 14) - iw00 - iw01 - iw10;
+    long long sA11 = 0, sA12 = 0, sA22 = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int e = lane + 64 * q;
+      Iw[q] = dIx[q] = dIy[q] = 0;
+      if (e < area) {
+        const int y = e / win, x = e - y * win, X = ipx + x, Y = ipy + y;
+        const int ival = bilin_img(I, Iw_, Ih_, X, Y, iw00, iw01, iw10, iw11);
+        const int ixv = bilin_der(dI, Iw_, Ih_, X, Y, 0, iw00, iw01, iw10, iw11);
+        const int iyv = bilin_der(dI, Iw_, Ih_, X, Y, 1, iw00, iw01, iw10, iw11);
+        Iw[q] = (int16_t)ival;
+        dIx[q] = (int16_t)ixv;
+        dIy[q] = (int16_t)iyv;
+        sA11 += (long long)ixv * ixv;
+        sA12 += (long long)ixv * iyv;
+        sA22 += (long long)iyv * iyv;
+      }
+    }
+    sA11 = wave_sum_ll(sA11);
+    sA12 = wave_sum_ll(sA12);
+    sA22 = wave_sum_ll(sA22);
+    const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+    float D = A11 * A22 - A12 * A12;
+    const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
+    if (minEig < 1e-4f || D < 1.19209290e-07f) {
+      if (level == 0) st = 0;
+      continue;
+    }
+    D = 1.f / D;
+    float nx = qx - halfw, ny = qy - halfw;
+    float pdx = 0.f, pdy = 0.f;
+    for (int j = 0; j < max_iters; j++) {
+      const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+      if (inx < -win || inx >= Jw_ || iny < -win || iny >= Jh_) {
+        if (level == 0) st = 0;
+        break;
+      }
+      a = nx - inx;
+      b = ny - iny;
+      iw00 = (int)rintf((1.f - a) * (1.f - b) * WSCALE);
+      iw01 = (int)rintf(a * (1.f - b) * WSCALE);
+      iw10 = (int)rintf((1.f - a) * b * WSCALE);
+      iw11 = (1 << 14) - iw00 - iw01 - iw10;
+      long long ib1 = 0, ib2 = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; q++) {
+        const int e = lane + 64 * q;
+        if (e < area) {
+          const int y = e / win, x = e - y * win;
+          const int diff = bilin_img(J, Jw_, Jh_, inx + x, iny + y, iw00, iw01, iw10, iw11) - Iw[q];
+          ib1 += (long long)diff * dIx[q];
+          ib2 += (long long)diff * dIy[q];
+        }
+      }
+      ib1 = wave_sum_ll(ib1);
+      ib2 = wave_sum_ll(ib2);
+      const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+      const float dx = (A12 * b2 - A22 * b1) * D;
+      const float dy = (A12 * b1 - A11 * b2) * D;
+      nx += dx;
+      ny += dy;
+      qx = nx + halfw;
+      qy = ny + halfw;
+      if ((double)dx * dx + (double)dy * dy <= (double)crit_eps) break;
+      if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
+        qx -= dx * 0.5f;
+        qy -= dy * 0.5f;
+        break;
+      }
+      pdx = dx;
+      pdy = dy;
+    }
+  }
+  if (lane == 0) {
+    p1[2 * pi] = qx;
+    p1[2 * pi + 1] = qy;
+    status[pi] = st;
+  }
+}
+
+// ---------------------------------------------------------------- undistort + RANSAC
+__global__ void k_undistort(CamParams cam, const float *__restrict__ pts, float *__restrict__ out, int n) {
+  int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  float x, y;
+  cam_undistort_f(cam, pts[2 * p], pts[2 * p + 1], x, y);
+  out[2 * p] = x;
+  out[2 * p + 1] = y;
+}
+
+__device__ int solve_cubic_d(const double *co, double *x) {
+  double a = co[0], b = co[1], c = co[2], d = co[3];
+  if (a == 0) {
+    if (b == 0) {
+      if (c == 0) return d == 0 ? -1 : 0;
+      x[0] = -d / c;
+      return 1;
+    }
+    double D = c * c - 4 * b * d;
+    if (D >= 0) {
+      D = sqrt(D);
+      x[0] = (-c - D) / (2 * b);
+      x[1] = (-c + D) / (2 * b);
+      return 2;
+    }
+    return 0;
+  }
+  a = 1. / a;
+  b *= a;
+  c *= a;
+  d *= a;
+  double Q = (b * b - c * 3) * (1. / 9);
+  double R = (b * b * b * 2 - b * c * 9 + d * 27) * (1. / 54);
+  double Qcubed = Q * Q * Q;
+  double dd = Qcubed - R * R;
+  if (dd > 0) {
+    double theta = acos(R / sqrt(Qcubed));
+    double sqrtQ = sqrt(Q);
+    double t0 = -2 * sqrtQ, t1 = theta * (1. / 3), t2 = b * (1. / 3);
+    x[0] = t0 * cos(t1) - t2;
+    x[1] = t0 * cos(t1 + (2. * M_PI / 3)) - t2;
+    x[2] = t0 * cos(t1 + (4. * M_PI / 3)) - t2;
+    return 3;
+  } else if (dd == 0) {
+    if (R >= 0) {
+      x[0] = -2 * pow(R, 1. / 3) - a / 3;
+      x[1] = pow(R, 1. / 3) - a / 3;
+    } else {
+      x[0] = 2 * pow(-R, 1. / 3) - a / 3;
+      x[1] = -pow(-R, 1. / 3) - a / 3;
+    }
+    return x[0] == x[1] ? 1 : 2;
+  }
+  dd = sqrt(-dd);
+  double e = pow(dd + fabs(R), 1. / 3);
+  if (R > 0) e = -e;
+  x[0] = (e + Q / e) - b * (1. / 3);
+  return 1;
+}
+
+// 7-point fundamental matrices (oracle fundamental_7pt: Householder QR null space + run7Point cubic)
+__device__ int fundamental_7pt_d(const double *x0, const double *y0, const double *x1, const double *y1, double *F) {
+  double At[9][7];
+  for (int i = 0; i < 7; i++) {
+    double a[9] = {x1[i] * x0[i], x1[i] * y0[i], x1[i], y1[i] * x0[i], y1[i] * y0[i], y1[i], x0[i], y0[i], 1.0};
+    for (int k = 0; k < 9; k++) At[k][i] = a[k];
+  }
+  double Vh[7][9], beta[7];
+  for (int c = 0; c < 7; c++) {
+    double ss = 0;
+    for (int r = c; r < 9; r++) ss += At[r][c] * At[r][c];
+    double x0v = At[c][c], alpha = (x0v > 0) ? -sqrt(ss) : sqrt(ss);
+    for (int r = 0; r < 9; r++) Vh[c][r] = (r < c) ? 0.0 : (r == c ? x0v - alpha : At[r][c]);
+    double vn = ss - x0v * x0v + (x0v - alpha) * (x0v - alpha);
+    beta[c] = vn > 0 ? 2.0 / vn : 0.0;
+    for (int j = c; j < 7; j++) {
+      double s = 0;
+      for (int r = c; r < 9; r++) s += Vh[c][r] * At[r][j];
+      s *= beta[c];
+      for (int r = c; r < 9; r++) At[r][j] -= s * Vh[c][r];
+    }
+  }
+  double f[2][9];
+  for (int q = 0; q < 2; q++) {
+    double e[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    e[7 + q] = 1.0;
+    for (int c = 6; c >= 0; c--) {
+      double s = 0;
+      for (int r = c; r < 9; r++) s += Vh[c][r] * e[r];
+      s *= beta[c];
+      for (int r = c; r < 9; r++) e[r] -= s * Vh[c][r];
+    }
+    for (int k = 0; k < 9; k++) f[q][k] = e[k];
+  }
+  double *f1 = f[0], *f2 = f[1];
+  for (int i = 0; i < 9; i++) f1[i] -= f2[i];
+  double t0, t1, t2, c[4], r[3] = {0, 0, 0};
+  t0 = f2[4] * f2[8] - f2[5] * f2[7];
+  t1 = f2[3] * f2[8] - f2[5] * f2[6];
+  t2 = f2[3] * f2[7] - f2[4] * f2[6];
+  c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+  c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+         f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+         f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+         f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+  t0 = f1[4] * f1[8] - f1[5] * f1[7];
+  t1 = f1[3] * f1[8] - f1[5] * f1[6];
+  t2 = f1[3] * f1[7] - f1[4] * f1[6];
+  c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+         f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+         f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+         f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+  c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+  int nr = solve_cubic_d(c, r);
+  if (nr < 1 || nr > 3) return 0;
+  for (int k = 0; k < nr; k++) {
+    double lambda = r[k], mu = 1.;
+    double s = f1[8] * r[k] + f2[8];
+    double *Fm = F + 9 * k;
+    if (fabs(s) > 2.220446049250313e-16) {
+      mu = 1. / s;
+      lambda *= mu;
+      Fm[8] = 1.;
+    } else {
+      Fm[8] = 0.;
+    }
+    for (int i = 0; i < 8; i++) Fm[i] = f1[i] * lambda + f2[i] * mu;
+  }
+  return nr;
+}
+
+__device__ __forceinline__ bool epipolar_inlier(const double *f, float x0, float y0, float x1, float y1, float t) {
+  double a = f[0] * x0 + f[1] * y0 + f[2];
+  double b = f[3] * x0 + f[4] * y0 + f[5];
+  double c = f[6] * x0 + f[7] * y0 + f[8];
+  double s2 = 1. / (a * a + b * b);
+  double d2 = x1 * a + y1 * b + c;
+  a = f[0] * x1 + f[3] * y1 + f[6];
+  b = f[1] * x1 + f[4] * y1 + f[7];
+  c = f[2] * x1 + f[5] * y1 + f[8];
+  double s1 = 1. / (a * a + b * b);
+  double d1 = x0 * a + y0 * b + c;
+  float err = (float)fmax(d1 * d1 * s1, d2 * d2 * s2);
+  return err <= t;
+}
+
+// one thread per hypothesis: models and their inlier counts
+__global__ void __launch_bounds__(256) k_ransac_hyp(const float *__restrict__ p0n, const float *__restrict__ p1n, int n,
+                                                    const int *__restrict__ subsets, int max_iters, float t,
+                                                    double *__restrict__ Fout, int *__restrict__ nmodels,
+                                                    int *__restrict__ good) {
+  const int it = blockIdx.x * blockDim.x + threadIdx.x;
+  if (it >= max_iters) return;
+  double x0[7], y0[7], x1[7], y1[7];
+  for (int i = 0; i < 7; i++) {
+    int k = subsets[it * 7 + i];
+    x0[i] = p0n[2 * k];
+    y0[i] = p0n[2 * k + 1];
+    x1[i] = p1n[2 * k];
+    y1[i] = p1n[2 * k + 1];
+  }
+  double F[27];
+  int nm = fundamental_7pt_d(x0, y0, x1, y1, F);
+  nmodels[it] = nm;
+  for (int m = 0; m < nm; m++) {
+    int g = 0;
+    for (int i = 0; i < n; i++) g += epipolar_inlier(F + 9 * m, p0n[2 * i], p0n[2 * i + 1], p1n[2 * i], p1n[2 * i + 1], t);
+    good[it * 3 + m] = g;
+    for (int k = 0; k < 9; k++) Fout[(size_t)it * 27 + 9 * m + k] = F[9 * m + k];
+  }
+}
+
+__device__ int ransac_update_iters_d(double p, double ep, int model_points, int max_iters) {
+  p = fmin(fmax(p, 0.), 1.);
+  ep = fmin(fmax(ep, 0.), 1.);
+  double num = fmax(1. - p, 2.2250738585072014e-308);
+  double denom = 1. - pow(1. - ep, model_points);
+  if (denom < 2.2250738585072014e-308) return 0;
+  num = log(num);
+  denom = log(denom);
+  return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
+}
+
+// sequential adaptive scan (RANSACPointSetRegistrator::run) on thread 0, then the winner's mask
+__global__ void __launch_bounds__(256) k_ransac_select(const float *__restrict__ p0n, const float *__restrict__ p1n, int n,
+                                                       int max_iters, float t, double conf,
+                                                       const double *__restrict__ Fs, const int *__restrict__ nmodels,
+                                                       const int *__restrict__ good, uint8_t *__restrict__ mask) {
+  __shared__ int best_it, best_m;
+  if (threadIdx.x == 0) {
+    int niters = max_iters, best = 0, bi = -1, bm = -1;
+    for (int it = 0; it < niters && it < max_iters; it++)
+      for (int m = 0; m < nmodels[it]; m++) {
+        int g = good[it * 3 + m];
+        if (g > max(best, 6)) {
+          best = g;
+          bi = it;
+          bm = m;
+          niters = ransac_update_iters_d(conf, (double)(n - g) / n, 7, niters);
+        }
+      }
+    best_it = bi;
+    best_m = bm;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    uint8_t v = 0;
+    if (best_it >= 0) v = epipolar_inlier(Fs + (size_t)best_it * 27 + 9 * best_m, p0n[2 * i], p0n[2 * i + 1], p1n[2 * i],
+                                          p1n[2 * i + 1], t);
+    mask[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- launch wrappers
+void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride, int equalize, unsigned *hist,
+                     uint8_t *dst) {
+  int blocks = min(256, (w * h + 4095) / 4096);
+  if (equalize) {
+    if (hipMemsetAsync(hist, 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
+    hipLaunchKernelGGL(k_hist, dim3(blocks), dim3(256), 0, s, src, w, h, stride, hist);
+  }
+  hipLaunchKernelGGL(k_equalize, dim3(blocks), dim3(256), 0, s, src, w, h, stride, hist, equalize, dst);
+}
+
+void launch_pyramid(hipStream_t s, DPyr &p) {
+  for (int l = 0; l < p.levels; l++) {
+    dim3 b(32, 8), g((p.w[l] + 31) / 32, (p.h[l] + 7) / 8);
+    if (l > 0)
+      hipLaunchKernelGGL(k_pyrdown, g, b, 0, s, p.img[l - 1], p.w[l - 1], p.h[l - 1], (uint8_t *)p.img[l], p.w[l], p.h[l]);
+    hipLaunchKernelGGL(k_scharr, g, b, 0, s, p.img[l], p.w[l], p.h[l], (int16_t *)p.der[l]);
+  }
+}
+
+void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
+                       int kmax, float *out, int *out_n) {
+  if (ncell <= 0) return;
+  const size_t lds = fast_lds_bytes(sw, sh);
+  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_cells, (int)lds) < (int)lds)
+    throw std::runtime_error("FAST cell too large for LDS");
+  hipLaunchKernelGGL(k_fast_cells, dim3(ncell), dim3(256), fast_lds_bytes(sw, sh), s, img, w, h, cells, sw, sh, thr, kmax,
+                     out, out_n);
+}
+
+void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
+                   int max_iters, double eps2) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_subpix, dim3((n + 63) / 64), dim3(64), 0, s, img, w, h, pts, n, mask, win, max_iters, eps2);
+}
+
+void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
+               int max_level, int max_iters, float eps) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_lk, dim3(n), dim3(64), 0, s, prev, next, p0, p1, status, n, win, max_level, max_iters, eps * eps);
+}
+
+void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
+                   float *p0n, float *p1n, const int *subsets, int max_iters, double thr, double conf, double *Fs,
+                   int *nmodels, int *good, uint8_t *mask) {
+  if (n <= 0) return;
+  if (n < 7) {  // findFundamentalMat needs 7 points: no inliers
+    if (hipMemsetAsync(mask, 0, n, s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
+    return;
+  }
+  hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c0, p0, p0n, n);
+  hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c1, p1, p1n, n);
+  float t = (float)(thr * thr);
+  hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 255) / 256), dim3(256), 0, s, p0n, p1n, n, subsets, max_iters, t, Fs,
+                     nmodels, good);
+  hipLaunchKernelGGL(k_ransac_select, dim3(1), dim3(256), 0, s, p0n, p1n, n, max_iters, t, conf, Fs, nmodels, good, mask);
+}
+
+}  // namespace uvhp

@@ -1,0 +1,97 @@
+// KLT front-end host orchestration (ov_core::TrackKLT, TrackKLT.cpp:34-886; Grider_GRID.h:74-180).
+//
+// The per-pixel and per-point work runs on the device (kernels_track.hip); the host keeps what the
+// reference keeps in TrackKLT's maps — the last points / ids / mask per camera — and makes the
+// same decisions in the same order (grid occupancy, min-distance grid, id assignment, stereo
+// bookkeeping), so the feature ids and their order in the database are the reference's.
+// Pyramids stay in HBM: two slots per camera (last, new), swapped every frame.
+#pragma once
+#include <functional>
+#include <unordered_map>
+#include <vector>
+
+#include "hp_common.h"
+#include "kernels.h"
+
+namespace uvhp {
+
+struct KeyPt {
+  float x, y, response;
+};
+
+using DbSink = std::function<void(size_t id, double t, int cam, float u, float v, float un, float vn)>;
+
+class Tracker {
+ public:
+  Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s);
+  ~Tracker();
+  Tracker(const Tracker &) = delete;
+  Tracker &operator=(const Tracker &) = delete;
+
+  // TrackKLT::feed_new_camera.  imgs: host (device_imgs false) or device u8 images of the
+  // configured size with row stride strides[k]; masks: host u8, same stride, may be null.
+  void feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
+            const uint8_t *const *masks, bool device_imgs, const DbSink &db);
+
+  // TrackBase::get_last_obs / get_last_ids for one camera
+  void last_tracks(int cam, std::vector<KeyPt> &pts, std::vector<size_t> &ids) const;
+  // last pyramid level of one camera (img: w*h, der: w*h*2); returns false if absent
+  bool last_pyramid(int cam, int level, int *w, int *h, std::vector<uint8_t> *img, std::vector<int16_t> *der);
+
+  size_t currid;
+  int device_syncs = 0;  // host waits in the last feed
+
+ private:
+  struct CamState {
+    DPyr pyr[2]{};
+    void *pyr_mem[2] = {nullptr, nullptr};
+    int last = 0;            // slot of pyr_last
+    bool have_last = false;
+    uint8_t *d_raw = nullptr;  // staging of a host image
+    unsigned *d_hist = nullptr;
+    std::vector<uint8_t> mask_last, mask_new;  // host masks (empty = none)
+    std::vector<KeyPt> pts_last;
+    std::vector<size_t> ids_last;
+  };
+  // one perform_matching in flight (slot 0 / 1)
+  struct MatchJob {
+    int n = 0;
+    bool run = false;   // LK + RANSAC launched
+  };
+  struct Bufs;
+
+  const CamParams *cams_;
+  hipStream_t s_;
+  int num_features_, threshold_, grid_x_, grid_y_, min_px_dist_, histogram_method_;
+  bool use_stereo_;
+  const int pyr_levels_ = 5, win_ = 15;
+  std::unordered_map<int, CamState> cs_;
+  std::vector<float> spmask_host_;
+  Bufs *b_ = nullptr;
+  std::unordered_map<int, std::vector<int>> subset_cache_;
+
+  CamState &cam_state(int cid);
+  void alloc_pyr(CamState &c, int w, int h);
+  void ensure_cap(int n);
+  void sync();
+  const std::vector<int> &subsets(int count);
+
+  void feed_monocular(double t, int cam, const DbSink &db);
+  void feed_stereo(double t, int cl, int cr, const DbSink &db);
+  // detection on pyramid `p` of camera `cam` (user mask `mask`); kept / new points in pts / ids
+  void detect_monocular(int cam, const DPyr &p, const std::vector<uint8_t> &mask, std::vector<KeyPt> &pts,
+                        std::vector<size_t> &ids);
+  void detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, const std::vector<uint8_t> &m0,
+                     const std::vector<uint8_t> &m1, std::vector<KeyPt> &pts0, std::vector<KeyPt> &pts1,
+                     std::vector<size_t> &ids0, std::vector<size_t> &ids1);
+  // Grider_GRID::perform_griding + cornerSubPix; when lk_to is set also tracks the new points into
+  // that pyramid (TrackKLT.cpp:640-655) and returns the results in lk_pts / lk_st.
+  void griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &rects,
+               const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
+               std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st);
+  void match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
+                    MatchJob &j);
+  void match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out);
+};
+
+}  // namespace uvhp

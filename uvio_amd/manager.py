@@ -117,6 +117,50 @@ class VioManager:
         self._check(rc, "feed_measurement_camera")
         return rc
 
+    def feed_measurement_camera_device(self, t, camids, images, masks=None, allow_uninit=False):
+        """feed_measurement_camera with images already in HBM: images[i] is a uint8 (H, W) CUDA tensor
+        (row stride = tensor stride).  The producer stream is synchronized before the call."""
+        import torch
+        ncam = len(camids)
+        for im in images:
+            if not (im.is_cuda and im.dtype == torch.uint8 and im.dim() == 2 and im.stride(1) == 1):
+                raise ValueError("images must be 2-D uint8 CUDA tensors with unit column stride")
+        torch.cuda.current_stream(images[0].device).synchronize()
+        cam = (C.c_int * ncam)(*camids)
+        ptrs = (C.c_void_p * ncam)(*[im.data_ptr() for im in images])
+        strides = (C.c_int * ncam)(*[im.stride(0) for im in images])
+        mptr = None
+        if masks is not None:
+            mk = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
+            mptr = (C.POINTER(C.c_uint8) * ncam)(*[m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in mk])
+        rc = self._call("feed_camera_device", self._h, C.c_double(t), ncam, cam, ptrs, strides, mptr)
+        if rc == N.E_STATE and allow_uninit:
+            return rc
+        self._check(rc, "feed_measurement_camera_device")
+        return rc
+
+    def get_tracks(self, cam):
+        """(ids uint64[n], uv float32[n, 2]) of the KLT tracks of camera `cam` after the last feed."""
+        n = C.c_int()
+        cap = 4096
+        ids = np.zeros(cap, dtype=np.uint64)
+        uv = np.zeros((cap, 2), dtype=np.float32)
+        self._check(self._call("get_tracks", self._h, cam, ids.ctypes.data_as(C.POINTER(C.c_uint64)),
+                               uv.ctypes.data_as(C.POINTER(C.c_float)), cap, C.byref(n)), "get_tracks")
+        return ids[:n.value].copy(), uv[:n.value].copy()
+
+    def get_pyramid(self, cam, level):
+        """(img u8 (h, w), der int16 (h, w, 2)) of the last pyramid level of camera `cam`."""
+        w, h = C.c_int(), C.c_int()
+        self._check(self._call("get_pyramid", self._h, cam, level, C.byref(w), C.byref(h), None, None, 0),
+                    "get_pyramid")
+        img = np.zeros((h.value, w.value), dtype=np.uint8)
+        der = np.zeros((h.value, w.value, 2), dtype=np.int16)
+        self._check(self._call("get_pyramid", self._h, cam, level, C.byref(w), C.byref(h),
+                               img.ctypes.data_as(C.POINTER(C.c_uint8)), der.ctypes.data_as(C.POINTER(C.c_int16)),
+                               img.size), "get_pyramid")
+        return img, der
+
     def feed_measurement_uwb(self, t, anchor_ids, ranges):
         n = len(anchor_ids)
         ids = (C.c_uint64 * n)(*anchor_ids)

@@ -88,7 +88,10 @@ class SceneRenderer:
         """u8 image (H, W) of camera k at pose (R_GtoC, p_CinG)."""
         R = torch.tensor(np.asarray(R_GtoC).T, dtype=torch.float32, device=self.device)  # C -> G
         o = torch.tensor(np.asarray(p_CinG), dtype=torch.float32, device=self.device)
-        d = self.rays[k] @ R.T  # (H, W, 3) in G
+        # (H, W, 3) in G; elementwise instead of a 3x3 matmul (keeps the harness off the BLAS
+        # libraries, whose kernel lookup has failed for this shape on the box)
+        rk = self.rays[k]
+        d = rk[..., 0:1] * R[:, 0] + rk[..., 1:2] * R[:, 1] + rk[..., 2:3] * R[:, 2]
         inv = 1.0 / torch.where(d.abs() < 1e-9, torch.full_like(d, 1e-9), d)
         t1 = (self.lo - o) * inv
         t2 = (self.hi - o) * inv
