@@ -1,22 +1,25 @@
-"""Headline benchmark: VIO frames/s of the per-frame propagate -> MSCKF/SLAM update loop.
+"""Headline benchmark: VIO frames/s of the full per-frame track -> propagate -> update loop.
 
 Workload (BASELINE.json configs[1], SURVEY.md §8 cfg 2): EuRoC V1_02-shaped stereo 752x480 rig from
-configs/euroc_mav (radtan, 2 cameras, 20 Hz), 11 clones (+1 at update time), up to 200 MSCKF features
-per update and 50 SLAM landmarks, 200 Hz IMU, on a synthetic EuRoC-shaped stream (uvio_amd/sim.py:
-seeded smooth trajectory, IMU from analytic derivatives + the config's noise densities, feature
-tracks projected through each camera with 1 px noise).  One step = one camera frame: the IMU samples
-since the last frame, then VioManager::feed_measurement_simulation (TrackSIM front-end: undistort +
-feature database) -> propagate + clone -> MSCKF update -> SLAM update / delayed init -> marginalize.
+configs/euroc_mav (radtan, 2 cameras, 20 Hz, 200 Hz IMU), 11 clones (+1 at update time), up to 200
+MSCKF features per update and 50 SLAM landmarks.  Input: a synthetic EuRoC-shaped stream
+(uvio_amd/sim.py: seeded smooth trajectory, IMU from analytic derivatives + the config's noise
+densities) whose camera images are ray-cast from a textured room (uvio_amd/render.py) and are
+resident in HBM before the timed region.  One step = one camera frame: the IMU samples since the
+last frame, then VioManager::feed_measurement_camera (TrackKLT on the device: equalizeHist, pyramid,
+FAST grid detection, cornerSubPix, stereo + temporal pyramidal LK, RANSAC) -> propagate + clone ->
+MSCKF update -> SLAM update / delayed init -> marginalize.  The tracker keeps 200 features per
+camera (init_max_features 400: initialize_with_gt keeps the initializer's count, VioManager.cpp:131).
 
-The image tracker (TrackKLT) is not on this path yet: the front-end is the reference's TrackSIM
-(DESIGN.md "Scope").  Frames/s is whole-job throughput: every rank runs its own estimator on its own
-stream (independent replicas, weak scaling), value = total frames / max-over-ranks wall time.
+Frames/s is whole-job throughput: every rank runs its own estimator on its own stream (independent
+replicas, weak scaling), value = total frames / max-over-ranks wall time.
 
-roofline: the dominant device work, the feature launch group (k_feature: triangulation + LM,
-Jacobians, left-nullspace reflections; then k_gather_can + k_gemm_HP + k_chi2: the batched chi2
-gate), timed with HIP events on the library's stream around the group; achieved = the algorithmic
-FP64 FLOPs of the group (SURVEY.md §8(d) F_feat formula on the actual feature shapes) / event time.  cpu_baseline: the oracle/ CPU restatement (single-threaded, as
-the reference estimator is) on a bounded sample of the same stream, rank 0 only.
+roofline: the feature launch group (k_feature: triangulation + LM, Jacobians, left-nullspace
+reflections; then k_gather_can + k_gemm_HP + k_chi2: the batched chi2 gate), timed with HIP events on
+the library's stream around the group; achieved = the algorithmic FP64 FLOPs of the group
+(SURVEY.md §8(d) F_feat formula on the actual feature shapes) / event time.  cpu_baseline: the oracle/
+CPU restatement (single-threaded, as the reference estimator is) on a bounded sample of the same
+image stream, rank 0 only.
 """
 import argparse
 import json
@@ -34,23 +37,33 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (vector = matrix on gfx950)
 
 
 def cfg2_options(U):
-    return U.load_options(EUROC, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
-                          dt_slam_delay=1.0, record_timing=1)
+    return U.load_options(EUROC, init_max_features=400, max_msckf_in_update=200, max_slam_features=50,
+                          max_slam_in_update=25, dt_slam_delay=1.0, record_timing=1)
 
 
 def make_stream(opts, n_frames, seed):
     from uvio_amd.sim import SimStream
-    # 200 tracks reach the full window every frame (max-track MSCKF features), 10 % are lost early,
-    # 3 % live 3-5 windows (SLAM candidates)
-    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, spawn=200, frac_lost=0.10,
-                     frac_long=0.03)
+    # the simulated tracks are not used (the images are); keep their generation small
+    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, spawn=4)
+
+
+def render_frames(sim, n_frames, device):
+    """All camera images of the first n_frames frames, resident in HBM (u8 tensors)."""
+    import torch
+    from uvio_amd.render import SceneRenderer
+    r = SceneRenderer(sim.opts, device=device)
+    frames = [[r.render(k, *sim.camera_pose(i, k), frame_seed=i) for k in range(sim.K)]
+              for i in range(min(n_frames, len(sim.cam_t)))]
+    torch.cuda.synchronize(device)
+    return frames
 
 
 class Driver:
-    """Feeds one stream into one manager frame by frame (events precomputed)."""
+    """Feeds one stream into one manager frame by frame (events precomputed).  frames: per camera frame
+    the list of device images (feed_measurement_camera_device) or of host arrays (feed_measurement_camera)."""
 
-    def __init__(self, sim, mgr):
-        self.sim, self.mgr = sim, mgr
+    def __init__(self, sim, mgr, frames, device_imgs=True):
+        self.sim, self.mgr, self.frames, self.device_imgs = sim, mgr, frames, device_imgs
         self.ev = [e for e in sim.events() if e[1] >= sim.t0 - 0.4]
         self.k = 0
         mgr.initialize_with_gt(sim.gt_state(sim.t0))
@@ -66,7 +79,11 @@ class Driver:
             elif kind == "uwb":
                 mgr.feed_measurement_uwb(t, sim.uwb[i][1], sim.uwb[i][2])
             elif t > sim.t0:
-                mgr.feed_measurement_simulation(t, list(range(sim.K)), sim.frames[i])
+                cams = list(range(sim.K))
+                if self.device_imgs:
+                    mgr.feed_measurement_camera_device(t, cams, self.frames[i])
+                else:
+                    mgr.feed_measurement_camera(t, cams, self.frames[i])
                 return t
 
 
@@ -86,7 +103,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--cpu-frames", type=int, default=60, help="timed oracle frames for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=120, help="timed oracle frames for cpu_baseline (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -102,8 +119,9 @@ def main():
     opts = cfg2_options(U)
     n_frames = args.warmup + args.steps
     sim = make_stream(opts, n_frames + 2, seed=5 + rank)
+    frames = render_frames(sim, n_frames + 2, torch.device("cuda", local))
     mgr = U.VioManager(opts, device=local)
-    drv = Driver(sim, mgr)
+    drv = Driver(sim, mgr, frames)
     for _ in range(args.warmup):
         drv.step()
 
@@ -113,7 +131,7 @@ def main():
         torch.cuda.synchronize()
 
     acc = {"k_feat_s": 0.0, "k_feat_flops": 0.0, "k_feat_launches": 0, "rows": 0, "n_msckf": 0, "n_slam": 0,
-           "cols": 0, "cov_dim": 0}
+           "cols": 0, "cov_dim": 0, "tracks": 0, "tracking_s": 0.0}
     pos_err = []
     barrier()
     t0 = time.perf_counter()
@@ -128,6 +146,7 @@ def main():
         acc["n_slam"] += tm["n_slam"]
         acc["cols"] = max(acc["cols"], tm["msckf_cols"])
         acc["cov_dim"] = max(acc["cov_dim"], tm["cov_dim"])
+        acc["tracking_s"] += tm["tracking"]
         _, x = mgr.get_imu_state()
         pos_err.append(x[4:7] - sim.traj.pos(t))
     barrier()
@@ -141,9 +160,10 @@ def main():
         avg_s = acc["k_feat_s"] / launches
         flops_per_launch = acc["k_feat_flops"] / launches
         achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
+        ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras))
         cpu = None
         if args.cpu_frames > 0:
-            cpu = cpu_baseline(opts, args.warmup, args.cpu_frames)
+            cpu = cpu_baseline(opts, args.warmup, args.cpu_frames, frames)
         out = {
             "metric": "VIO frames/sec (track+propagate+update) at clones x feats",
             "value": value,
@@ -156,8 +176,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic EuRoC-shaped stream (uvio_amd/sim.py, seed 5+rank), TrackSIM front-end",
-            "config": {"workload": "cfg2 EuRoC V1_02-shaped stereo 752x480, 11 clones, <=200 MSCKF + 50 SLAM",
+            "data": "synthetic EuRoC-shaped stream (uvio_amd/sim.py, seed 5+rank) with ray-cast images "
+                    "(uvio_amd/render.py) resident in HBM, TrackKLT front-end",
+            "config": {"workload": "cfg2 EuRoC V1_02-shaped stereo 752x480 images, 11 clones, <=200 MSCKF + 50 SLAM",
+                       "track_features_per_cam": int(opts.init_max_features) // int(opts.num_cameras),
+                       "tracks_last_frame": ntr, "mean_tracking_ms": 1e3 * acc["tracking_s"] / args.steps,
                        "clones": int(opts.max_clone_size), "cameras": int(opts.num_cameras),
                        "max_msckf_in_update": int(opts.max_msckf_in_update),
                        "max_slam_features": int(opts.max_slam_features),
@@ -177,12 +200,14 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(opts, warmup, frames):
-    """oracle/ (the CPU restatement) on the same stream, one thread, bounded sample."""
+def cpu_baseline(opts, warmup, frames, dev_frames):
+    """oracle/ (the CPU restatement) on the same image stream (rank 0's), one thread, bounded sample."""
     from oracle import oracle as O
+    frames = max(1, min(frames, len(dev_frames) - warmup - 2))
     sim = make_stream(opts, warmup + frames + 2, seed=5)
+    host = [[im.cpu().numpy() for im in fr] for fr in dev_frames[:warmup + frames + 2]]
     mgr = O.OracleManager(opts)
-    drv = Driver(sim, mgr)
+    drv = Driver(sim, mgr, host, device_imgs=False)
     for _ in range(warmup):
         drv.step()
     t0 = time.perf_counter()
@@ -190,7 +215,7 @@ def cpu_baseline(opts, warmup, frames):
         drv.step()
     dt = time.perf_counter() - t0
     return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "%d frames of the cfg2 stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
+            "sample": "%d frames of the cfg2 image stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
                       (frames, warmup)}
 
 

@@ -190,10 +190,10 @@ int uvio_hp_get_fej_vector(uvio_hp_t *h, double *out, int cap, int *len);
 int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out);
 /* number of clones and their timestamps (ascending) */
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
-/* TrackBase::get_last_obs / get_last_ids (TrackBase.h:107-122) for one camera: ids and raw (u, v) of
+/* TrackBase::get_last_obs / get_last_ids (TrackBase.h:137-148) for one camera: ids and raw (u, v) of
  * the KLT tracks after the last camera feed; *n receives the count (E_CAPACITY if > cap) */
 int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap, int *n);
-/* the last image pyramid of one camera (TrackKLT::img_pyramid_last, TrackKLT.h:130): level size,
+/* the last image pyramid of one camera (TrackKLT::img_pyramid_last, TrackKLT.h:147): level size,
  * the (equalized) u8 image (w*h) and interleaved Scharr (dx, dy) int16 derivatives (w*h*2); img / der
  * may be NULL, cap = pixels available */
 int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap);
