@@ -122,6 +122,7 @@ Tracker::~Tracker() {
       if (kv.second.pyr_mem[k]) (void)hipFree(kv.second.pyr_mem[k]);
     if (kv.second.d_raw) (void)hipFree(kv.second.d_raw);
     if (kv.second.d_hist) (void)hipFree(kv.second.d_hist);
+    if (kv.second.d_score) (void)hipFree(kv.second.d_score);
   }
   if (b_) {
     if (b_->dmem) (void)hipFree(b_->dmem);
@@ -227,6 +228,7 @@ void Tracker::alloc_pyr(CamState &c, int w, int h) {
   }
   HP_HIP(hipMalloc(&c.d_raw, (size_t)w * h));
   HP_HIP(hipMalloc(&c.d_hist, 256 * sizeof(unsigned)));
+  HP_HIP(hipMalloc(&c.d_score, (size_t)w * h));
 }
 
 // RANSACPointSetRegistrator::getSubset draws (ptsetreg.cpp), one rng per findFundamentalMat call
@@ -299,7 +301,6 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
 void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &boxes,
                       const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
                       std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st) {
-  (void)cam;
   out.clear();
   if (valid.empty()) return;
   Bufs &b = *b_;
@@ -322,7 +323,7 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
   }
   if (nc == 0) return;
   HP_HIP(hipMemcpyAsync(b.cells, b.h_cells, 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
-  launch_fast_cells(s_, p.img[0], W, H, b.cells, nc, size_x, size_y, threshold_, nfg, b.fast, b.fastn);
+  launch_fast_cells(s_, p.img[0], W, H, b.cells, nc, size_x, size_y, threshold_, nfg, b.fast, b.fastn, cs_[cam].d_score);
   HP_HIP(hipMemcpyAsync(b.h_fastn, b.fastn, nc * sizeof(int), hipMemcpyDeviceToHost, s_));
   HP_HIP(hipMemcpyAsync(b.h_fast, b.fast, (size_t)3 * nc * nfg * sizeof(float), hipMemcpyDeviceToHost, s_));
   sync();

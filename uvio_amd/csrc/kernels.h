@@ -180,9 +180,10 @@ void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride
                      uint8_t *dst);
 // pyrDown + Scharr for every level of p (level 0 image already written)
 void launch_pyramid(hipStream_t s, DPyr &p);
-// FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell
+// FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell;
+// score_map: w x h u8 scratch
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
-                       int kmax, float *out, int *out_n);
+                       int kmax, float *out, int *out_n, uint8_t *score_map);
 // cornerSubPix in place on n points (x, y); mask: (2 win + 1)^2 weights
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2);

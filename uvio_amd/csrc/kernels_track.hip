@@ -111,35 +111,39 @@ __global__ void k_scharr(const uint8_t *__restrict__ s, int w, int h, int16_t *_
 }
 
 // ---------------------------------------------------------------- FAST-9 on grid cells
+// ring offsets (dx, dy) of cv::makeOffsets(pattern 16)
 __constant__ int c_fast_off[16][2] = {{0, 3},  {1, 3},  {2, 2},  {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
                                       {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
 
-__device__ int fast_corner_score(const uint8_t *img, int w, int x, int y, int thr) {
-  const int v = img[(size_t)y * w + x];
+// true iff the 16-bit circular mask holds a run of >= 9 set bits (FAST_t's consecutive count over the
+// 25-long ring walk): bit i of r is set iff bits i..i+8 of the doubled mask all are
+__device__ __forceinline__ bool has_arc9(unsigned m) {
+  m |= m << 16;
+  unsigned r = m & (m >> 1);
+  r &= r >> 2;  // 4 consecutive
+  r &= r >> 4;  // 8 consecutive
+  r &= m >> 8;  // 9 consecutive
+  return (r & 0xFFFFu) != 0;
+}
+
+// FAST-9 test + cornerScore<16> of the pixel at p (row stride `ld`); 0 = not a corner
+__device__ int fast_corner_score(const uint8_t *p, int ld, int thr) {
+  const int v = p[0];
   int ring[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) ring[k] = img[(size_t)(y + c_fast_off[k][1]) * w + x + c_fast_off[k][0]];
-  bool corner = false;
-  for (int pass = 0; pass < 2 && !corner; pass++) {
-    int count = 0;
-    for (int k = 0; k < 25; k++) {
-      int p = ring[k & 15];
-      bool ok = (pass == 0) ? (p < v - thr) : (p > v + thr);
-      if (ok) {
-        if (++count > 8) {
-          corner = true;
-          break;
-        }
-      } else {
-        count = 0;
-      }
-    }
+  for (int k = 0; k < 16; k++) ring[k] = p[c_fast_off[k][1] * ld + c_fast_off[k][0]];
+  unsigned dk = 0, br = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    dk |= (unsigned)(ring[k] < v - thr) << k;
+    br |= (unsigned)(ring[k] > v + thr) << k;
   }
-  if (!corner) return 0;
+  if (!has_arc9(dk) && !has_arc9(br)) return 0;
   int d[25];
 #pragma unroll
   for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
   int a0 = thr;
+#pragma unroll
   for (int k = 0; k < 16; k += 2) {
     int a = min(d[k + 1], d[k + 2]);
     a = min(a, d[k + 3]);
@@ -153,6 +157,7 @@ __device__ int fast_corner_score(const uint8_t *img, int w, int x, int y, int th
     a0 = max(a0, min(a, d[k + 9]));
   }
   int b0 = -a0;
+#pragma unroll
   for (int k = 0; k < 16; k += 2) {
     int b = max(d[k + 1], d[k + 2]);
     b = max(b, d[k + 3]);
@@ -168,66 +173,125 @@ __device__ int fast_corner_score(const uint8_t *img, int w, int x, int y, int th
   return -b0 - 1;
 }
 
-// one workgroup per cell; LDS holds the cell's score map (u8) and the NMS survivors.  Output per cell:
-// up to kmax keypoints (x, y, response) in (response desc, raster asc) order, image coordinates.
-// Strict 3x3 NMS leaves no two adjacent survivors, so a cell has at most ceil(sw/2) ceil(sh/2).
+// Phase 1: scores of every interior pixel of every cell (cv::FAST on the cell ROI: ring reads of an
+// interior pixel stay inside the cell) into an image-sized u8 map.  Grid (cell, band of kFastBand rows)
+// so a few cells still spread over many CUs.
+constexpr int kFastBand = 8;
+__global__ void __launch_bounds__(256) k_fast_score(const uint8_t *__restrict__ img, int w, const int *__restrict__ cells,
+                                                    int sw, int sh, int thr, uint8_t *__restrict__ score) {
+  const int c = blockIdx.x, i0 = blockIdx.y * kFastBand;
+  const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
+  const int rows = min(kFastBand, sh - i0);
+  for (int e = threadIdx.x; e < rows * sw; e += blockDim.x) {
+    const int i = i0 + e / sw, j = e % sw;
+    int sc = 0;
+    if (i >= 3 && i < sh - 3 && j >= 3 && j < sw - 3) sc = fast_corner_score(img + (size_t)(y0 + i) * w + x0 + j, w, thr);
+    score[(size_t)(y0 + i) * w + x0 + j] = (uint8_t)sc;
+  }
+}
+
+// Phase 2: one workgroup per cell stages the cell's scores in LDS, keeps strict 3x3 maxima and
+// writes the top kmax by (response desc, raster asc) — the stable sort of Grider_GRID — as
+// (x, y, response) in image coordinates.  Strict NMS leaves no two adjacent survivors, so a cell
+// has at most ceil(sw/2) ceil(sh/2) candidates.
+constexpr int kFastThreads = 1024, kFastMaxK = 64;
 __host__ __device__ inline int fast_max_cand(int sw, int sh) { return ((sw + 1) / 2) * ((sh + 1) / 2); }
 __host__ __device__ inline size_t fast_lds_bytes(int sw, int sh) {
   return (size_t)fast_max_cand(sw, sh) * 8 + (((size_t)sw * sh + 15) & ~(size_t)15);
 }
-__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t *__restrict__ img, int w, int h,
-                                                    const int *__restrict__ cells, int sw, int sh, int thr, int kmax,
-                                                    float *__restrict__ out, int *__restrict__ out_n) {
+__global__ void __launch_bounds__(kFastThreads) k_fast_select(const uint8_t *__restrict__ scmap, int w,
+                                                              const int *__restrict__ cells, int sw, int sh, int kmax,
+                                                              float *__restrict__ out, int *__restrict__ out_n) {
   extern __shared__ int lds_fast[];
   const int kFastMaxCand = fast_max_cand(sw, sh);
+  const int area = sw * sh;
   int *cand_idx = lds_fast, *cand_s = lds_fast + kFastMaxCand;
-  uint8_t *score = (uint8_t *)(cand_s + kFastMaxCand);  // sw * sh
+  uint8_t *score = (uint8_t *)(cand_s + kFastMaxCand);
   __shared__ int ncand;
   const int c = blockIdx.x;
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
   if (threadIdx.x == 0) ncand = 0;
-  for (int e = threadIdx.x; e < sw * sh; e += blockDim.x) {
-    int i = e / sw, j = e - i * sw;
-    int s = 0;
-    if (i >= 3 && i < sh - 3 && j >= 3 && j < sw - 3) s = fast_corner_score(img, w, x0 + j, y0 + i, thr);
-    score[e] = (uint8_t)s;
+  for (int e = threadIdx.x; e < area; e += blockDim.x) {
+    const int i = e / sw, j = e - i * sw;
+    score[e] = scmap[(size_t)(y0 + i) * w + x0 + j];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < sw * sh; e += blockDim.x) {
-    int s = score[e];
-    if (s == 0) continue;
-    int i = e / sw, j = e - i * sw;
-    bool keep = true;
-    for (int di = -1; di <= 1 && keep; di++)
-      for (int dj = -1; dj <= 1; dj++) {
-        if (!di && !dj) continue;
-        if (s <= score[(i + di) * sw + j + dj]) {
-          keep = false;
-          break;
-        }
-      }
+  // survivors are appended with one LDS atomic per wavefront (ballot + prefix popcount): a per-thread
+  // atomic on one counter serializes thousands of candidates
+  const int lane = threadIdx.x & 63;
+  for (int e0 = 0; e0 < area; e0 += blockDim.x) {
+    const int e = e0 + threadIdx.x;
+    const int sc = (e < area) ? score[e] : 0;
+    bool keep = sc != 0;
     if (keep) {
-      int slot = atomicAdd(&ncand, 1);
+      const int i = e / sw, j = e - i * sw;
+      for (int di = -1; di <= 1 && keep; di++)
+        for (int dj = -1; dj <= 1; dj++) {
+          if (!di && !dj) continue;
+          if (sc <= score[(i + di) * sw + j + dj]) {
+            keep = false;
+            break;
+          }
+        }
+    }
+    const unsigned long long bal = __ballot(keep);
+    int base = 0;
+    if (lane == 0 && bal) base = atomicAdd(&ncand, __popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
       if (slot < kFastMaxCand) {
         cand_idx[slot] = e;
-        cand_s[slot] = s;
+        cand_s[slot] = sc;
       }
     }
   }
   __syncthreads();
+  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order):
+  // kmax rounds of a wavefront min over each wave's strided share of the candidates, then the same
+  // over the waves' winners on wave 0
   const int n = min(ncand, kFastMaxCand);
-  // rank = #candidates ordered before this one (response desc, raster asc): the stable sort order
-  for (int a = threadIdx.x; a < n; a += blockDim.x) {
-    int sa = cand_s[a], ia = cand_idx[a], rank = 0;
-    for (int b = 0; b < n; b++) {
-      int sb = cand_s[b];
-      rank += (sb > sa) || (sb == sa && cand_idx[b] < ia);
-    }
-    if (rank < kmax) {
-      float *o = out + ((size_t)c * kmax + rank) * 3;
-      o[0] = (float)(x0 + ia % sw);
-      o[1] = (float)(y0 + ia / sw);
-      o[2] = (float)sa;
+  unsigned *ckey = (unsigned *)cand_s;
+  for (int a = threadIdx.x; a < n; a += blockDim.x) ckey[a] = ((unsigned)(255 - cand_s[a]) << 16) | (unsigned)cand_idx[a];
+  __shared__ unsigned wtop[(kFastThreads / 64) * kFastMaxK];
+  const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  for (int r = 0; r < kmax; r++) {
+    unsigned m = 0xFFFFFFFFu;
+    int at = -1;
+    for (int a = wid * 64 + lane; a < n; a += blockDim.x)
+      if (ckey[a] < m) {
+        m = ckey[a];
+        at = a;
+      }
+    unsigned wm = m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wm = min(wm, (unsigned)__shfl_xor((int)wm, o, 64));
+    if (at >= 0 && m == wm) ckey[at] = 0xFFFFFFFFu;
+    if (lane == 0) wtop[wid * kmax + r] = wm;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    const int nt = nw * kmax;
+    for (int r = 0; r < kmax; r++) {
+      unsigned m = 0xFFFFFFFFu;
+      int at = -1;
+      for (int a = lane; a < nt; a += 64)
+        if (wtop[a] < m) {
+          m = wtop[a];
+          at = a;
+        }
+      unsigned wm = m;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wm = min(wm, (unsigned)__shfl_xor((int)wm, o, 64));
+      if (at >= 0 && m == wm) wtop[at] = 0xFFFFFFFFu;
+      if (lane == 0 && wm != 0xFFFFFFFFu) {
+        const int ia = (int)(wm & 0xFFFFu);
+        float *o = out + ((size_t)c * kmax + r) * 3;
+        o[0] = (float)(x0 + ia % sw);
+        o[1] = (float)(y0 + ia / sw);
+        o[2] = (float)(255 - (int)(wm >> 16));
+      }
     }
   }
   if (threadIdx.x == 0) out_n[c] = min(n, kmax);
@@ -240,61 +304,101 @@ __device__ __forceinline__ float px_clamped(const uint8_t *img, int w, int h, in
   return (float)img[(size_t)y * w + x];
 }
 
-// one thread per point: the sums run in the oracle's raster order, so results are bit-identical
-__global__ void k_subpix(const uint8_t *__restrict__ img, int w, int h, float *__restrict__ pts, int n,
-                         const float *__restrict__ mask, int win, int max_iters, double eps2) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// One 64-lane workgroup per point.  Lanes build the (win_w + 2)^2 bilinear patch and the 121 per-pixel
+// terms in LDS; lane 0 then accumulates them in the oracle's raster order (the double sums are
+// order-sensitive), so the result is bit-identical to the sequential cornerSubPix.
+constexpr int kSubpixMaxWin = 5, kSubpixMargin = 3;
+__global__ void __launch_bounds__(64) k_subpix(const uint8_t *__restrict__ img, int w, int h, float *__restrict__ pts,
+                                               int n, const float *__restrict__ mask, int win, int max_iters,
+                                               double eps2) {
+  constexpr int kBw = 2 * kSubpixMaxWin + 3, kT = (2 * kSubpixMaxWin + 1) * (2 * kSubpixMaxWin + 1);
+  constexpr int kTile = kBw + 1 + 2 * kSubpixMargin;
+  __shared__ float tile[kTile * kTile];  // clamped image neighbourhood (u8 as float)
+  __shared__ float buf[kBw * kBw];
+  __shared__ double tg[5][kT];
+  __shared__ double sums[5];
+  __shared__ float cur[2];
+  __shared__ int done;
+  const int p = blockIdx.x, lane = threadIdx.x;
   if (p >= n) return;
-  const int win_w = 2 * win + 1, bw = win_w + 2;  // bilinear buffer (win_w + 2)^2, <= 13 x 13 for win 5
-  float buf[13 * 13];
+  const int win_w = 2 * win + 1, bw = win_w + 2, nt = win_w * win_w, S = bw + 1 + 2 * kSubpixMargin;
   const float cTx = pts[2 * p], cTy = pts[2 * p + 1];
-  float cIx = cTx, cIy = cTy;
-  int iter = 0;
-  double err = 0;
-  do {
-    float cx = cIx - (bw - 1) * 0.5f, cy = cIy - (bw - 1) * 0.5f;
-    int ix = (int)floorf(cx), iy = (int)floorf(cy);
-    float a = cx - ix, b = cy - iy;
-    float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
-    for (int i = 0; i < bw; i++)
-      for (int j = 0; j < bw; j++) {
-        int x = ix + j, y = iy + i;
-        buf[i * bw + j] = px_clamped(img, w, h, x, y) * a11 + px_clamped(img, w, h, x + 1, y) * a12 +
-                          px_clamped(img, w, h, x, y + 1) * a21 + px_clamped(img, w, h, x + 1, y + 1) * a22;
+  if (lane == 0) {
+    cur[0] = cTx;
+    cur[1] = cTy;
+    done = 0;
+  }
+  __syncthreads();
+  int ox = -(1 << 28), oy = -(1 << 28);
+  for (int iter = 0; iter < max_iters; iter++) {
+    const float cIx = cur[0], cIy = cur[1];
+    const float cx = cIx - (bw - 1) * 0.5f, cy = cIy - (bw - 1) * 0.5f;
+    const int ix = (int)floorf(cx), iy = (int)floorf(cy);
+    const float a = cx - ix, b = cy - iy;
+    const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+    if (ix - ox < 0 || ix - ox > 2 * kSubpixMargin || iy - oy < 0 || iy - oy > 2 * kSubpixMargin) {
+      ox = ix - kSubpixMargin;
+      oy = iy - kSubpixMargin;
+      for (int e = lane; e < S * S; e += 64) {
+        const int ty = e / S;
+        tile[e] = px_clamped(img, w, h, ox + e - ty * S, oy + ty);
       }
-    double sa = 0, sb = 0, sc = 0, bb1 = 0, bb2 = 0;
-    const float *sp = buf + bw + 1;
-    for (int i = 0, k = 0; i < win_w; i++, sp += bw) {
-      double py = i - win;
-      for (int j = 0; j < win_w; j++, k++) {
-        double m = mask[k];
-        double tgx = sp[j + 1] - sp[j - 1];
-        double tgy = sp[j + bw] - sp[j - bw];
-        double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-        double pxv = j - win;
-        sa += gxx;
-        sb += gxy;
-        sc += gyy;
-        bb1 += gxx * pxv + gxy * py;
-        bb2 += gxy * pxv + gyy * py;
+      __syncthreads();
+    }
+    for (int e = lane; e < bw * bw; e += 64) {
+      const int i = e / bw, j = e - i * bw;
+      const float *t = tile + (iy - oy + i) * S + (ix - ox + j);
+      buf[e] = t[0] * a11 + t[1] * a12 + t[S] * a21 + t[S + 1] * a22;
+    }
+    __syncthreads();
+    for (int k = lane; k < nt; k += 64) {
+      const int i = k / win_w, j = k - i * win_w;
+      const float *sp = buf + (i + 1) * bw + 1;
+      const double m = mask[k];
+      const double tgx = sp[j + 1] - sp[j - 1];
+      const double tgy = sp[j + bw] - sp[j - bw];
+      const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+      const double pxv = j - win, py = i - win;
+      tg[0][k] = gxx;
+      tg[1][k] = gxy;
+      tg[2][k] = gyy;
+      tg[3][k] = gxx * pxv + gxy * py;
+      tg[4][k] = gxy * pxv + gyy * py;
+    }
+    __syncthreads();
+    if (lane < 5) {  // one series per lane, each in raster order
+      double acc = 0;
+      for (int k = 0; k < nt; k++) acc += tg[lane][k];
+      sums[lane] = acc;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      const double sa = sums[0], sb = sums[1], sc = sums[2], bb1 = sums[3], bb2 = sums[4];
+      const double det = sa * sc - sb * sb;
+      if (fabs(det) <= 4.930380657631324e-32) {  // DBL_EPSILON^2
+        done = 1;
+      } else {
+        const double scale = 1.0 / det;
+        const float nx = (float)(cIx + sc * scale * bb1 - sb * scale * bb2);
+        const float ny = (float)(cIy - sb * scale * bb1 + sa * scale * bb2);
+        const double err = (double)(nx - cIx) * (nx - cIx) + (double)(ny - cIy) * (ny - cIy);
+        cur[0] = nx;
+        cur[1] = ny;
+        if (nx < 0 || nx >= w || ny < 0 || ny >= h || !(err > eps2)) done = 1;
       }
     }
-    double det = sa * sc - sb * sb;
-    if (fabs(det) <= 4.930380657631324e-32) break;  // DBL_EPSILON^2
-    double scale = 1.0 / det;
-    float nx = (float)(cIx + sc * scale * bb1 - sb * scale * bb2);
-    float ny = (float)(cIy - sb * scale * bb1 + sa * scale * bb2);
-    err = (double)(nx - cIx) * (nx - cIx) + (double)(ny - cIy) * (ny - cIy);
-    cIx = nx;
-    cIy = ny;
-    if (cIx < 0 || cIx >= w || cIy < 0 || cIy >= h) break;
-  } while (++iter < max_iters && err > eps2);
-  if (fabsf(cIx - cTx) > win || fabsf(cIy - cTy) > win) {
-    cIx = cTx;
-    cIy = cTy;
+    __syncthreads();
+    if (done) break;
   }
-  pts[2 * p] = cIx;
-  pts[2 * p + 1] = cIy;
+  if (lane == 0) {
+    float cIx = cur[0], cIy = cur[1];
+    if (fabsf(cIx - cTx) > win || fabsf(cIy - cTy) > win) {
+      cIx = cTx;
+      cIy = cTy;
+    }
+    pts[2 * p] = cIx;
+    pts[2 * p + 1] = cIy;
+  }
 }
 
 // ---------------------------------------------------------------- pyramidal LK
@@ -312,6 +416,7 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
   return v;
 }
 
+constexpr int kLkMargin = 4, kLkMaxWin = 16, kLkMaxTile = kLkMaxWin + 1 + 2 * kLkMargin;
 // one 64-lane workgroup per point; lanes own window pixels lane, lane+64, ... (225 for win 15).
 // (qx, qy) is nextPts[ptidx] of LKTrackerInvoker: it carries the result between levels, and an
 // early exit leaves it at its last written value, exactly as the oracle's p1[pi].
@@ -340,6 +445,10 @@ __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__
   const int area = win * win;
   constexpr int kPer = 4;  // ceil(225 / 64)
   int Iw[kPer], dIx[kPer], dIy[kPer];
+  // J neighbourhood of the window staged in LDS (reflect-101 applied while staging); restaged only when
+  // an iteration moves the window more than kLkMargin pixels from where it was staged
+  __shared__ uint8_t Jt[kLkMaxTile * kLkMaxTile];
+  const int S = win + 1 + 2 * kLkMargin;
   float qx = p1[2 * pi], qy = p1[2 * pi + 1];
   uint8_t st = 1;
   for (int level = maxL; level >= 0; level--) {
@@ -398,11 +507,22 @@ __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__
     D = 1.f / D;
     float nx = qx - halfw, ny = qy - halfw;
     float pdx = 0.f, pdy = 0.f;
+    int ox = -(1 << 28), oy = -(1 << 28);
     for (int j = 0; j < max_iters; j++) {
       const int inx = (int)floorf(nx), iny = (int)floorf(ny);
       if (inx < -win || inx >= Jw_ || iny < -win || iny >= Jh_) {
         if (level == 0) st = 0;
         break;
+      }
+      if (inx - ox < 0 || inx - ox > 2 * kLkMargin || iny - oy < 0 || iny - oy > 2 * kLkMargin) {
+        __syncthreads();
+        ox = inx - kLkMargin;
+        oy = iny - kLkMargin;
+        for (int e = lane; e < S * S; e += 64) {
+          const int ty = e / S;
+          Jt[e] = (uint8_t)img_px(J, Jw_, Jh_, ox + e - ty * S, oy + ty);
+        }
+        __syncthreads();
       }
       a = nx - inx;
       b = ny - iny;
@@ -416,7 +536,8 @@ __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__
         const int e = lane + 64 * q;
         if (e < area) {
           const int y = e / win, x = e - y * win;
-          const int diff = bilin_img(J, Jw_, Jh_, inx + x, iny + y, iw00, iw01, iw10, iw11) - Iw[q];
+          const uint8_t *t = Jt + (iny - oy + y) * S + (inx - ox + x);
+          const int diff = descale((long long)t[0] * iw00 + t[1] * iw01 + t[S] * iw10 + t[S + 1] * iw11, 14 - 5) - Iw[q];
           ib1 += (long long)diff * dIx[q];
           ib2 += (long long)diff * dIy[q];
         }
@@ -593,12 +714,13 @@ __device__ __forceinline__ bool epipolar_inlier(const double *f, float x0, float
   return err <= t;
 }
 
-// one thread per hypothesis: models and their inlier counts
+// one wavefront per hypothesis: every lane solves the (tiny) 7-point system redundantly, so the
+// model is wave-uniform, then the lanes split the inlier count over the points
 __global__ void __launch_bounds__(256) k_ransac_hyp(const float *__restrict__ p0n, const float *__restrict__ p1n, int n,
                                                     const int *__restrict__ subsets, int max_iters, float t,
                                                     double *__restrict__ Fout, int *__restrict__ nmodels,
                                                     int *__restrict__ good) {
-  const int it = blockIdx.x * blockDim.x + threadIdx.x;
+  const int it = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
   if (it >= max_iters) return;
   double x0[7], y0[7], x1[7], y1[7];
   for (int i = 0; i < 7; i++) {
@@ -609,13 +731,17 @@ __global__ void __launch_bounds__(256) k_ransac_hyp(const float *__restrict__ p0
     y1[i] = p1n[2 * k + 1];
   }
   double F[27];
-  int nm = fundamental_7pt_d(x0, y0, x1, y1, F);
-  nmodels[it] = nm;
+  const int nm = fundamental_7pt_d(x0, y0, x1, y1, F);
+  if (lane == 0) nmodels[it] = nm;
   for (int m = 0; m < nm; m++) {
     int g = 0;
-    for (int i = 0; i < n; i++) g += epipolar_inlier(F + 9 * m, p0n[2 * i], p0n[2 * i + 1], p1n[2 * i], p1n[2 * i + 1], t);
-    good[it * 3 + m] = g;
-    for (int k = 0; k < 9; k++) Fout[(size_t)it * 27 + 9 * m + k] = F[9 * m + k];
+    for (int i = lane; i < n; i += 64)
+      g += epipolar_inlier(F + 9 * m, p0n[2 * i], p0n[2 * i + 1], p1n[2 * i], p1n[2 * i + 1], t);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o, 64);
+    if (lane == 0) good[it * 3 + m] = g;
+    if (lane == 0)
+      for (int k = 0; k < 9; k++) Fout[(size_t)it * 27 + 9 * m + k] = F[9 * m + k];
   }
 }
 
@@ -681,24 +807,30 @@ void launch_pyramid(hipStream_t s, DPyr &p) {
 }
 
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
-                       int kmax, float *out, int *out_n) {
+                       int kmax, float *out, int *out_n, uint8_t *score_map) {
+  (void)h;
   if (ncell <= 0) return;
   const size_t lds = fast_lds_bytes(sw, sh);
-  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_cells, (int)lds) < (int)lds)
+  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_select, (int)lds) < (int)lds)
     throw std::runtime_error("FAST cell too large for LDS");
-  hipLaunchKernelGGL(k_fast_cells, dim3(ncell), dim3(256), fast_lds_bytes(sw, sh), s, img, w, h, cells, sw, sh, thr, kmax,
-                     out, out_n);
+  if (kmax > kFastMaxK || sw * sh > 65536) throw std::runtime_error("FAST cell / per-cell count beyond the kernel's limits");
+  hipLaunchKernelGGL(k_fast_score, dim3(ncell, (sh + kFastBand - 1) / kFastBand), dim3(256), 0, s, img, w, cells, sw, sh,
+                     thr, score_map);
+  hipLaunchKernelGGL(k_fast_select, dim3(ncell), dim3(kFastThreads), lds, s, score_map, w, cells, sw, sh, kmax, out,
+                     out_n);
 }
 
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_subpix, dim3((n + 63) / 64), dim3(64), 0, s, img, w, h, pts, n, mask, win, max_iters, eps2);
+  if (win > kSubpixMaxWin) throw std::runtime_error("cornerSubPix window larger than the kernel's LDS patch");
+  hipLaunchKernelGGL(k_subpix, dim3(n), dim3(64), 0, s, img, w, h, pts, n, mask, win, max_iters, eps2);
 }
 
 void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
                int max_level, int max_iters, float eps) {
   if (n <= 0) return;
+  if (win > kLkMaxWin) throw std::runtime_error("LK window larger than the kernel supports");
   hipLaunchKernelGGL(k_lk, dim3(n), dim3(64), 0, s, prev, next, p0, p1, status, n, win, max_level, max_iters, eps * eps);
 }
 
@@ -713,7 +845,7 @@ void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, cons
   hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c0, p0, p0n, n);
   hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c1, p1, p1n, n);
   float t = (float)(thr * thr);
-  hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 255) / 256), dim3(256), 0, s, p0n, p1n, n, subsets, max_iters, t, Fs,
+  hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 3) / 4), dim3(256), 0, s, p0n, p1n, n, subsets, max_iters, t, Fs,
                      nmodels, good);
   hipLaunchKernelGGL(k_ransac_select, dim3(1), dim3(256), 0, s, p0n, p1n, n, max_iters, t, conf, Fs, nmodels, good, mask);
 }

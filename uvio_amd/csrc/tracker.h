@@ -49,6 +49,7 @@ class Tracker {
     bool have_last = false;
     uint8_t *d_raw = nullptr;  // staging of a host image
     unsigned *d_hist = nullptr;
+    uint8_t *d_score = nullptr;  // FAST score map (w x h)
     std::vector<uint8_t> mask_last, mask_new;  // host masks (empty = none)
     std::vector<KeyPt> pts_last;
     std::vector<size_t> ids_last;
