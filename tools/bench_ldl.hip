@@ -1,0 +1,83 @@
+// chol_inv_regs (register-resident) vs ldl_inplace + ldl_to_chol + trtri_gj_inplace: agreement and
+// single-workgroup time on MI355X.
+// Build: hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I uvio_amd/csrc tools/bench_ldl.hip -o build/bench_ldl
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "dense_lds.h"
+using namespace uvhp;
+
+__global__ void __launch_bounds__(512) k_test(const double *Ain, int n, int nrows, int which, int mode, double *out,
+                                              long long *ts) {
+  extern __shared__ double lds[];
+  const int ld = n | 1;
+  double *A = lds, *wsp = lds + (size_t)nrows * ld;
+  for (int e = threadIdx.x; e < nrows * n; e += blockDim.x) A[(e / n) * ld + e % n] = Ain[e];
+  __syncthreads();
+  long long t0 = clock64();
+  if (which) {
+    chol_inv_regs(A, ld, n, nrows, wsp, mode);
+  } else {
+    ldl_inplace(A, ld, n, nrows);
+    if (mode & kRB_CHOL) ldl_to_chol(A, ld, n, nrows);
+    if (mode & kRB_INV) trtri_gj_inplace(A, ld, n);
+  }
+  __syncthreads();
+  long long t1 = clock64();
+  for (int e = threadIdx.x; e < nrows * n; e += blockDim.x) out[e] = A[(e / n) * ld + e % n];
+  if (threadIdx.x == 0) ts[0] = t1 - t0;
+}
+
+int main(int argc, char **argv) {
+  int n = argc > 1 ? atoi(argv[1]) : 100;
+  int nt = argc > 2 ? atoi(argv[2]) : 512;
+  int mode = argc > 3 ? atoi(argv[3]) : 3;
+  int nrows = n + 1;
+  std::vector<double> A(nrows * n), B(n * n);
+  srand(n);
+  for (auto &x : B) x = (double)rand() / RAND_MAX - 0.5;
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) {
+      double s = (i == j) ? 0.1 : 0;
+      for (int k = 0; k < n; k++) s += B[i * n + k] * B[j * n + k];
+      A[i * n + j] = s;
+    }
+  for (int j = 0; j < n; j++) A[n * n + j] = (double)rand() / RAND_MAX - 0.5;
+  double *dA, *dO0, *dO1;
+  long long *dts;
+  (void)hipMalloc(&dA, 8 * nrows * n);
+  (void)hipMalloc(&dO0, 8 * nrows * n);
+  (void)hipMalloc(&dO1, 8 * nrows * n);
+  (void)hipMalloc(&dts, 16);
+  (void)hipMemcpy(dA, A.data(), 8 * nrows * n, hipMemcpyHostToDevice);
+  size_t bytes = (size_t)nrows * (n | 1) * 8 + (size_t)rb_wsp_doubles(nrows) * 8;
+  (void)hipFuncSetAttribute((const void *)k_test, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int which = 0; which < 2; which++)
+    for (int it = 0; it < 3; it++) {
+      (void)hipEventRecord(e0);
+      hipLaunchKernelGGL(k_test, dim3(1), dim3(nt), bytes, 0, dA, n, nrows, which, mode, which ? dO1 : dO0, dts);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      long long ts;
+      (void)hipMemcpy(&ts, dts, 8, hipMemcpyDeviceToHost);
+      if (it == 2) printf("%s n=%d nt=%d mode=%d kernel %.1f us  %lld cyc\n", which ? "regs " : "lds  ", n, nt, mode, ms * 1e3, ts);
+    }
+  std::vector<double> o0(nrows * n), o1(nrows * n);
+  (void)hipMemcpy(o0.data(), dO0, 8 * nrows * n, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(o1.data(), dO1, 8 * nrows * n, hipMemcpyDeviceToHost);
+  double err = 0, mx = 0;
+  for (int i = 0; i < nrows; i++)
+    for (int j = 0; j < n && j <= i; j++) {
+      err = fmax(err, fabs(o0[i * n + j] - o1[i * n + j]));
+      mx = fmax(mx, fabs(o0[i * n + j]));
+    }
+  printf("max |regs - lds| = %.3e (max %.3e)\n", err, mx);
+  return 0;
+}

@@ -159,8 +159,7 @@ int main(int argc, char **argv) {
   }
   CK(hipMemcpy(dp, g.data(), g.size() * 4, hipMemcpyHostToDevice));
   timeit("lk 200 pts", [&] {
-    CK(hipMemcpyAsync(dq, dp, 1600, hipMemcpyDeviceToDevice, s));
-    launch_lk(s, A.p, B.p, dp, dq, st, 200, 15, 5, 30, 0.01f);
+    launch_lk(s, A.p, B.p, dp, dq, st, 200, 15, 5, 30, 0.01f, true);
   });
   std::vector<float> q(400);
   std::vector<uint8_t> sv(200);

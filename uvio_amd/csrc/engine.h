@@ -8,6 +8,7 @@
 // UpdaterUWB (UpdaterUWB.cpp), FeatureDatabase (FeatureDatabase.cpp).
 #pragma once
 #include <chrono>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -96,6 +97,11 @@ struct DeviceBufs {
   int *neg_host = nullptr;
   DFeatOut *fout_host = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // feature-kernel timing
+  // upload staging ring: small host tables of one launch group are packed into pinned memory and sent
+  // with ONE copy (stage / stage_flush); the kernels read the device copy directly
+  char *stg_h = nullptr, *stg_d = nullptr;
+  size_t stg_cap = 0, stg_used = 0, stg_flushed = 0;
+  double *dxneg = nullptr;  // [negative-diagonal count (8 B) | dx (ldp)]: one readback per update
 };
 
 class Engine {
@@ -180,9 +186,21 @@ class Engine {
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
   void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2);
+  // hidx_dev: the batch's column map already on the device (staged), or nullptr to stage `hidx`;
+  // pre_apply runs after the readback, before dx is applied (initialize_invertible's landmark step)
   void ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx, const double *resdev,
-                       int res_stride, double sigma2);
+                       int res_stride, double sigma2, const int *hidx_dev = nullptr,
+                       const std::function<void()> &pre_apply = nullptr);
   void apply_dx(const double *dx);
+  // staging (see DeviceBufs): returns the device address the table will have after stage_flush()
+  void *stage_bytes(const void *src, size_t bytes);
+  template <class T>
+  T *stage(const T *src, size_t n) {
+    return (T *)stage_bytes(src, sizeof(T) * n);
+  }
+  void stage_flush();
+  // dx + negative-diagonal count back to the host (one copy + sync); throws on a negative diagonal
+  void read_dx(const char *who);
   void initialize_invertible_host(const VarP &v, const std::vector<std::pair<int, int>> &H_order,
                                   const std::vector<double> &H_R, const std::vector<double> &H_L,
                                   const std::vector<double> &R, const std::vector<double> &res);
@@ -223,6 +241,7 @@ class Engine {
     std::vector<DClone> clones;
     std::vector<DCam> cams;
     std::vector<int> hidx;     // canonical column -> covariance id
+    const int *hidx_dev = nullptr;  // its staged device copy
     std::vector<FeatP> fptrs;
     int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;
     std::map<double, int> slot_of_time;

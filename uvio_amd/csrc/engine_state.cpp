@@ -215,10 +215,11 @@ Engine::~Engine() {
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.fout, d_.chi2, d_.H, d_.Tall, d_.Pc, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.dx, d_.ekf.neg};
+                  d_.dxneg, d_.stg_d};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
+  if (d_.stg_h) hipHostFree(d_.stg_h);
   if (d_.ev0) hipEventDestroy(d_.ev0);
   if (d_.ev1) hipEventDestroy(d_.ev1);
   if (d_.stream) hipStreamDestroy(d_.stream);
@@ -283,8 +284,9 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
-  dalloc(&d_.ekf.dx, cap);
-  dalloc(&d_.ekf.neg, 4 + d_.max_ncol);  // [0] negative-diagonal count, [1..] pivots
+  dalloc(&d_.dxneg, cap + 2);
+  d_.ekf.neg = (int *)d_.dxneg;
+  d_.ekf.dx = d_.dxneg + 1;
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
   for (int i = 1; i < 1000; i++) chi2_table_[i] = chi2_quantile95(i);
   HP_HIP(hipMemcpy(d_.chi2, chi2_table_.data(), 1000 * sizeof(double), hipMemcpyHostToDevice));
@@ -294,9 +296,13 @@ void Engine::alloc_device() {
                  sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 4096;
   HP_HIP(hipHostMalloc(&d_.pin, d_.pin_bytes, hipHostMallocDefault));
   char *pb = (char *)d_.pin + d_.pin_bytes - (sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 64);
-  d_.dx_host = (double *)pb;
-  d_.neg_host = (int *)(pb + sizeof(double) * (cap + 8));
+  d_.neg_host = (int *)pb;  // same layout as dxneg
+  d_.dx_host = (double *)(pb + sizeof(double));
   d_.fout_host = (DFeatOut *)(pb + sizeof(double) * (cap + 16));
+  // upload staging (batch tables, Phi / Q, column maps)
+  d_.stg_cap = d_.pin_bytes + 2 * 64 * 64 * sizeof(double) + 64 * 1024;
+  HP_HIP(hipHostMalloc(&d_.stg_h, d_.stg_cap, hipHostMallocDefault));
+  HP_HIP(hipMalloc(&d_.stg_d, d_.stg_cap));
 }
 
 void Engine::upload_P_full(const std::vector<double> &Ph, int N) {
@@ -317,15 +323,45 @@ void Engine::get_cov(double *out, int ld) {
   HP_HIP(hipStreamSynchronize(d_.stream));
 }
 
+// A ring: tables are appended after the last flushed one and the ring restarts only when full (after
+// a stream sync), so a staged table stays valid on the device until many later launch groups.
+void *Engine::stage_bytes(const void *src, size_t bytes) {
+  const size_t need = (bytes + 255) / 256 * 256;
+  if (need > d_.stg_cap) throw HpError(UVIO_HP_E_CAPACITY, "upload staging exhausted");
+  if (d_.stg_used + need > d_.stg_cap) {
+    stage_flush();
+    HP_HIP(hipStreamSynchronize(d_.stream));
+    d_.stg_used = d_.stg_flushed = 0;
+  }
+  if (bytes) std::memcpy(d_.stg_h + d_.stg_used, src, bytes);
+  void *dev = d_.stg_d + d_.stg_used;
+  d_.stg_used += need;
+  return dev;
+}
+
+void Engine::stage_flush() {
+  if (d_.stg_used == d_.stg_flushed) return;
+  HP_HIP(hipMemcpyAsync(d_.stg_d + d_.stg_flushed, d_.stg_h + d_.stg_flushed, d_.stg_used - d_.stg_flushed,
+                        hipMemcpyHostToDevice, d_.stream));
+  d_.stg_flushed = d_.stg_used;
+}
+
+void Engine::read_dx(const char *who) {
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (1 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
+}
+
 // StateHelper::EKFPropagation on the device (StateHelper.cpp:36-114)
 void Engine::cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                            const std::vector<double> &Q) {
   int q = (int)iold.size();
   if (p > 64 || q > 256) throw HpError(UVIO_HP_E_CAPACITY, "propagation block too large");
-  HP_HIP(hipMemcpyAsync(d_.Phi, Phi.data(), sizeof(double) * p * q, hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.Q, Q.data(), sizeof(double) * p * p, hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.iold, iold.data(), sizeof(int) * q, hipMemcpyHostToDevice, d_.stream));
-  launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, d_.iold, q, d_.Phi, d_.Q, d_.T);
+  const double *dPhi = stage(Phi.data(), (size_t)p * q);
+  const double *dQ = stage(Q.data(), (size_t)p * p);
+  const int *diold = stage(iold.data(), (size_t)q);
+  stage_flush();
+  launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, diold, q, dPhi, dQ, d_.T);
 }
 
 void Engine::check_neg_diag(const char *who) {
@@ -339,8 +375,12 @@ void Engine::check_neg_diag(const char *who) {
 // StateHelper::clone(imu->pose()) + augment_clone (StateHelper.cpp:341-391, 579-616)
 VarP Engine::clone_imu_pose(const double *dnc, bool do_dt) {
   if (N_ + 6 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
-  if (do_dt) HP_HIP(hipMemcpyAsync(d_.dnc, dnc, sizeof(double) * 6, hipMemcpyHostToDevice, d_.stream));
-  launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, d_.dnc, do_dt ? 1 : 0);
+  const double *ddnc = d_.dnc;
+  if (do_dt) {
+    ddnc = stage(dnc, 6);
+    stage_flush();
+  }
+  launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, ddnc, do_dt ? 1 : 0);
   VarP pose = mk(V_POSE, 6, 7);
   for (int k = 0; k < 7; k++) pose->val[k] = imu_->val[k], pose->fej[k] = imu_->fej[k];
   pose->id = N_;
@@ -374,28 +414,29 @@ void Engine::apply_dx(const double *dx) {
 
 // EKF update of P on the device with rows H (r x n, ld) / residual; dx applied to the host mean
 void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx,
-                             const double *resdev, int res_stride, double sigma2) {
-  if (r <= 0) return;
+                             const double *resdev, int res_stride, double sigma2, const int *hidx_dev,
+                             const std::function<void()> &pre_apply) {
+  if (r <= 0) {
+    if (pre_apply) pre_apply();
+    return;
+  }
   if (r > kMaxEkfRows) throw HpError(UVIO_HP_E_CAPACITY, "direct EKF update with more than 256 rows");
-  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
-  launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, d_.hidx, resdev, res_stride, sigma2, d_.ekf);
-  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
-  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+  if (!hidx_dev) {
+    hidx_dev = stage(hidx.data(), (size_t)n);
+    stage_flush();
+  }
+  launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
+  read_dx("EKFUpdate");
+  if (pre_apply) pre_apply();
   apply_dx(d_.dx_host);
 }
 
 // EKF update from the Gram partials of a stacked batch (compressed path, m > n)
 void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2) {
-  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
-  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, d_.hidx, sigma2, d_.R, d_.ekf);
-  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
-  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+  const int *dh = stage(hidx.data(), (size_t)n);
+  stage_flush();
+  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
+  read_dx("EKFUpdate");
   apply_dx(d_.dx_host);
 }
 

@@ -50,8 +50,10 @@ struct Occupancy {  // cv::Mat grid_2d_close / grid_2d_grid (CV_8UC1)
 
 struct Tracker::Bufs {
   int cap = 0, maxcells = 0, kmax = 0;
-  void *dmem = nullptr, *hmem = nullptr;
-  // device
+  char *dmem = nullptr, *hmem = nullptr;
+  size_t mirror = 0;  // bytes [0, mirror) of the device block are mirrored in pinned host memory
+  // device (host mirror: hp(x)); per matching slot the inputs [p0 | sub] and outputs [p1 | st | mask]
+  // are contiguous so each direction is one copy
   float *p0[2], *p1[2], *p0n[2], *p1n[2];
   uint8_t *st[2], *mask[2];
   int *sub[2], *nm[2], *good[2];
@@ -59,12 +61,10 @@ struct Tracker::Bufs {
   int *cells, *fastn;
   float *fast, *det, *det1, *spmask;
   uint8_t *detst;
-  // pinned host mirrors
-  float *h_p0[2], *h_p1[2];
-  uint8_t *h_st[2], *h_mask[2];
-  int *h_sub[2], *h_cells, *h_fastn;
-  float *h_fast, *h_det, *h_det1;
-  uint8_t *h_detst;
+  template <class T>
+  T *hp(T *dev) const {
+    return (T *)(hmem + ((char *)dev - dmem));
+  }
 };
 
 namespace {
@@ -79,6 +79,7 @@ struct Arena {
     return p;
   }
 };
+size_t span(const void *a, const void *b_end) { return (size_t)((const char *)b_end - (const char *)a); }
 }  // namespace
 
 Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s) : cams_(cams), s_(s) {
@@ -148,27 +149,14 @@ void Tracker::ensure_cap(int n) {
   int cap = std::max(n, 2 * b.cap);
   size_t ncell = (size_t)b.maxcells;
   for (int pass = 0; pass < 2; pass++) {
-    Arena d, h;
-    if (pass == 1) {
-      d.base = (char *)b.dmem;
-      h.base = (char *)b.hmem;
-    }
+    Arena d;
+    if (pass == 1) d.base = b.dmem;
     for (int k = 0; k < 2; k++) {
       b.p0[k] = d.take<float>(2 * cap);
+      b.sub[k] = d.take<int>(7 * kRansacIters);
       b.p1[k] = d.take<float>(2 * cap);
-      b.p0n[k] = d.take<float>(2 * cap);
-      b.p1n[k] = d.take<float>(2 * cap);
       b.st[k] = d.take<uint8_t>(cap);
       b.mask[k] = d.take<uint8_t>(cap);
-      b.sub[k] = d.take<int>(7 * kRansacIters);
-      b.nm[k] = d.take<int>(kRansacIters);
-      b.good[k] = d.take<int>(3 * kRansacIters);
-      b.F[k] = d.take<double>(27 * kRansacIters);
-      b.h_p0[k] = h.take<float>(2 * cap);
-      b.h_p1[k] = h.take<float>(2 * cap);
-      b.h_st[k] = h.take<uint8_t>(cap);
-      b.h_mask[k] = h.take<uint8_t>(cap);
-      b.h_sub[k] = h.take<int>(7 * kRansacIters);
     }
     b.cells = d.take<int>(2 * ncell);
     b.fastn = d.take<int>(ncell);
@@ -176,16 +164,19 @@ void Tracker::ensure_cap(int n) {
     b.det = d.take<float>(2 * cap);
     b.det1 = d.take<float>(2 * cap);
     b.detst = d.take<uint8_t>(cap);
+    const size_t mirror = d.off;
+    for (int k = 0; k < 2; k++) {
+      b.p0n[k] = d.take<float>(2 * cap);
+      b.p1n[k] = d.take<float>(2 * cap);
+      b.nm[k] = d.take<int>(kRansacIters);
+      b.good[k] = d.take<int>(3 * kRansacIters);
+      b.F[k] = d.take<double>(27 * kRansacIters);
+    }
     b.spmask = d.take<float>(spmask_host_.size());
-    b.h_cells = h.take<int>(2 * ncell);
-    b.h_fastn = h.take<int>(ncell);
-    b.h_fast = h.take<float>(3 * ncell * b.kmax);
-    b.h_det = h.take<float>(2 * cap);
-    b.h_det1 = h.take<float>(2 * cap);
-    b.h_detst = h.take<uint8_t>(cap);
     if (pass == 0) {
+      b.mirror = mirror;
       HP_HIP(hipMalloc(&b.dmem, d.off + 256));
-      HP_HIP(hipHostMalloc(&b.hmem, h.off + 256, hipHostMallocDefault));
+      HP_HIP(hipHostMalloc(&b.hmem, mirror + 256, hipHostMallocDefault));
     }
   }
   b.cap = cap;
@@ -317,20 +308,21 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
   for (auto &g : valid) {
     int x = g.first * size_x, y = g.second * size_y;
     if (x + size_x > W || y + size_y > H) continue;
-    b.h_cells[2 * nc] = x;
-    b.h_cells[2 * nc + 1] = y;
+    b.hp(b.cells)[2 * nc] = x;
+    b.hp(b.cells)[2 * nc + 1] = y;
     nc++;
   }
   if (nc == 0) return;
-  HP_HIP(hipMemcpyAsync(b.cells, b.h_cells, 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
+  HP_HIP(hipMemcpyAsync(b.cells, b.hp(b.cells), 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
   launch_fast_cells(s_, p.img[0], W, H, b.cells, nc, size_x, size_y, threshold_, nfg, b.fast, b.fastn, cs_[cam].d_score);
-  HP_HIP(hipMemcpyAsync(b.h_fastn, b.fastn, nc * sizeof(int), hipMemcpyDeviceToHost, s_));
-  HP_HIP(hipMemcpyAsync(b.h_fast, b.fast, (size_t)3 * nc * nfg * sizeof(float), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, s_));
   sync();
+  const int *h_fastn = b.hp(b.fastn);
+  const float *h_fast = b.hp(b.fast);
   const int d = min_px_dist_;
   for (int c = 0; c < nc; c++)
-    for (int i = 0; i < b.h_fastn[c]; i++) {
-      const float *f = b.h_fast + ((size_t)c * nfg + i) * 3;
+    for (int i = 0; i < h_fastn[c]; i++) {
+      const float *f = h_fast + ((size_t)c * nfg + i) * 3;
       KeyPt k{f[0], f[1], f[2]};
       if ((int)k.x < 0 || (int)k.x > W || (int)k.y < 0 || (int)k.y > H) continue;
       if (mask_px(user_mask, W, (int)k.x, (int)k.y) > 127 || in_boxes(boxes, d, (int)k.x, (int)k.y)) continue;
@@ -339,30 +331,31 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
   if (out.empty()) return;
   const int n = (int)out.size();
   ensure_cap(n);
+  float *h_det = b.hp(b.det), *h_det1 = b.hp(b.det1);
+  const uint8_t *h_detst = b.hp(b.detst);
   for (int i = 0; i < n; i++) {
-    b.h_det[2 * i] = out[i].x;
-    b.h_det[2 * i + 1] = out[i].y;
+    h_det[2 * i] = out[i].x;
+    h_det[2 * i + 1] = out[i].y;
   }
-  HP_HIP(hipMemcpyAsync(b.det, b.h_det, 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
+  HP_HIP(hipMemcpyAsync(b.det, h_det, 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
   launch_subpix(s_, p.img[0], W, H, b.det, n, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
   if (lk_to) {
-    HP_HIP(hipMemcpyAsync(b.det1, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToDevice, s_));
-    launch_lk(s_, p, *lk_to, b.det, b.det1, b.detst, n, win_, pyr_levels_, kLkIters, kLkEps);
-    HP_HIP(hipMemcpyAsync(b.h_det1, b.det1, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
-    HP_HIP(hipMemcpyAsync(b.h_detst, b.detst, n, hipMemcpyDeviceToHost, s_));
+    launch_lk(s_, p, *lk_to, b.det, b.det1, b.detst, n, win_, pyr_levels_, kLkIters, kLkEps, true);
+    HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + n), hipMemcpyDeviceToHost, s_));
+  } else {
+    HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
   }
-  HP_HIP(hipMemcpyAsync(b.h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
   sync();
   for (int i = 0; i < n; i++) {
-    out[i].x = b.h_det[2 * i];
-    out[i].y = b.h_det[2 * i + 1];
+    out[i].x = h_det[2 * i];
+    out[i].y = h_det[2 * i + 1];
   }
   if (lk_to) {
     lk_pts->resize(n);
     lk_st->resize(n);
     for (int i = 0; i < n; i++) {
-      (*lk_pts)[i] = KeyPt{b.h_det1[2 * i], b.h_det1[2 * i + 1], out[i].response};
-      (*lk_st)[i] = b.h_detst[i];
+      (*lk_pts)[i] = KeyPt{h_det1[2 * i], h_det1[2 * i + 1], out[i].response};
+      (*lk_st)[i] = h_detst[i];
     }
   }
 }
@@ -556,23 +549,20 @@ void Tracker::match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, i
   const int n = j.n;
   ensure_cap(n);
   Bufs &b = *b_;
+  float *h_p0 = b.hp(b.p0[slot]);
   for (int i = 0; i < n; i++) {
-    b.h_p0[slot][2 * i] = k0[i].x;
-    b.h_p0[slot][2 * i + 1] = k0[i].y;
+    h_p0[2 * i] = k0[i].x;
+    h_p0[2 * i + 1] = k0[i].y;
   }
   const std::vector<int> &sub = subsets(n);
-  std::memcpy(b.h_sub[slot], sub.data(), sub.size() * sizeof(int));
-  HP_HIP(hipMemcpyAsync(b.p0[slot], b.h_p0[slot], 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
-  HP_HIP(hipMemcpyAsync(b.p1[slot], b.h_p0[slot], 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
-  HP_HIP(hipMemcpyAsync(b.sub[slot], b.h_sub[slot], sub.size() * sizeof(int), hipMemcpyHostToDevice, s_));
-  launch_lk(s_, p0, p1, b.p0[slot], b.p1[slot], b.st[slot], n, win_, pyr_levels_, kLkIters, kLkEps);
+  std::memcpy(b.hp(b.sub[slot]), sub.data(), sub.size() * sizeof(int));
+  HP_HIP(hipMemcpyAsync(b.p0[slot], h_p0, span(b.p0[slot], b.sub[slot] + sub.size()), hipMemcpyHostToDevice, s_));
+  launch_lk(s_, p0, p1, b.p0[slot], b.p1[slot], b.st[slot], n, win_, pyr_levels_, kLkIters, kLkEps, true);
   const CamParams &c0 = cams_[cam0], &c1 = cams_[cam1];
   const double fmax = std::max(std::max(c0.v[0], c0.v[1]), std::max(c1.v[0], c1.v[1]));
   launch_ransac(s_, c0, c1, b.p0[slot], b.p1[slot], n, b.p0n[slot], b.p1n[slot], b.sub[slot], kRansacIters, 2.0 / fmax,
                 kRansacConf, b.F[slot], b.nm[slot], b.good[slot], b.mask[slot]);
-  HP_HIP(hipMemcpyAsync(b.h_p1[slot], b.p1[slot], 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
-  HP_HIP(hipMemcpyAsync(b.h_st[slot], b.st[slot], n, hipMemcpyDeviceToHost, s_));
-  HP_HIP(hipMemcpyAsync(b.h_mask[slot], b.mask[slot], n, hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.hp(b.p1[slot]), b.p1[slot], span(b.p1[slot], b.mask[slot] + n), hipMemcpyDeviceToHost, s_));
 }
 
 void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out) {
@@ -584,10 +574,12 @@ void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1,
   }
   Bufs &b = *b_;
   mask_out.resize(j.n);
+  const float *h_p1 = b.hp(b.p1[slot]);
+  const uint8_t *h_st = b.hp(b.st[slot]), *h_mask = b.hp(b.mask[slot]);
   for (int i = 0; i < j.n; i++) {
-    k1[i].x = b.h_p1[slot][2 * i];
-    k1[i].y = b.h_p1[slot][2 * i + 1];
-    mask_out[i] = (b.h_st[slot][i] && b.h_mask[slot][i]) ? 1 : 0;
+    k1[i].x = h_p1[2 * i];
+    k1[i].y = h_p1[2 * i + 1];
+    mask_out[i] = (h_st[i] && h_mask[i]) ? 1 : 0;
   }
 }
 

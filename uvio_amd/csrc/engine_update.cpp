@@ -560,20 +560,15 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   if (max_meas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
   size_t lds = feature_lds_bytes(max_meas, max_nf);
   if (lds + 4096 > 160 * 1024) throw HpError(UVIO_HP_E_CAPACITY, "feature LDS footprint too large");
-  // pack into pinned staging, one async copy per table
-  char *pb = (char *)d_.pin;
-  auto stage = [&](void *dst, const void *src, size_t bytes) {
-    if (bytes == 0) return;
-    std::memcpy(pb, src, bytes);
-    HP_HIP(hipMemcpyAsync(dst, pb, bytes, hipMemcpyHostToDevice, d_.stream));
-    pb += (bytes + 255) / 256 * 256;
-  };
-  stage(d_.feats, b.feats.data(), sizeof(DFeat) * nf);
-  stage(d_.meas, b.meas.data(), sizeof(DMeas) * b.meas.size());
-  stage(d_.vars, b.vars.data(), sizeof(DVar) * b.vars.size());
-  stage(d_.clones, b.clones.data(), sizeof(DClone) * b.clones.size());
-  stage(d_.cams, b.cams.data(), sizeof(DCam) * b.cams.size());
-  stage(d_.hidx, b.hidx.data(), sizeof(int) * b.hidx.size());
+  // the batch tables go up packed in one copy
+  const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
+  const DMeas *t_meas = stage(b.meas.data(), b.meas.size());
+  const DVar *t_vars = stage(b.vars.data(), b.vars.size());
+  const DClone *t_clones = stage(b.clones.data(), b.clones.size());
+  const DCam *t_cams = stage(b.cams.data(), b.cams.size());
+  const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
+  stage_flush();
+  b.hidx_dev = t_hidx;
   DBatchParams bp{};
   bp.nfeat = nf;
   bp.n_canon = b.n_canon;
@@ -601,7 +596,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
   if (tsdump) HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 8 * nf));
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
-  launch_feature_linearize(d_.stream, bp, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams, d_.P, d_.chi2, d_.H, d_.fout,
+  launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
   {
     int max_rows_f = 0;
@@ -609,7 +604,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
       int rows_out = (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
       max_rows_f = std::max(max_rows_f, rows_out - (mode >= 2 ? 3 : 0));
     }
-    launch_chi2_batch(d_.stream, bp, d_.feats, d_.P, d_.hidx, d_.H, b.rows, d_.Tall, d_.Pc, d_.chi2, d_.fout,
+    launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.Pc, d_.chi2, d_.fout,
                       max_rows_f);
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
@@ -865,24 +860,34 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       HLinv[8] = (A[0] * A[4] - A[1] * A[3]) / det;
     }
     if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
-    HP_HIP(hipMemcpyAsync(d_.hidx, b.hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
-    HP_HIP(hipMemcpyAsync(d_.Phi, HLinv, sizeof(double) * 9, hipMemcpyHostToDevice, d_.stream));
-    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, d_.hidx, d_.Phi, s2, d_.ekf);
-    // landmark value update H_Linv * resinit (residual column of rows 0..2)
-    double resinit[3];
+    const double *dHLinv = stage(HLinv, 9);
+    stage_flush();
+    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, dHLinv, s2, d_.ekf);
+    // landmark value update H_Linv * resinit (residual column of rows 0..2), read back together with the
+    // update's dx; applied first, as initialize_invertible does
+    double *resinit = d_.dx_host + d_.ldp + 2;
     HP_HIP(hipMemcpy2DAsync(resinit, sizeof(double), d_.H + n, sizeof(double) * d_.ldh, sizeof(double), 3,
                             hipMemcpyDeviceToHost, d_.stream));
-    HP_HIP(hipStreamSynchronize(d_.stream));
-    double dl[3];
-    for (int a = 0; a < 3; a++) dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
-    lm->update(dl);
+    VarP lmv = lm;
+    auto land = [lmv, resinit, HLinv]() {
+      double dl[3];
+      for (int a = 0; a < 3; a++)
+        dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
+      lmv->update(dl);
+    };
     lm->id = N_;
     vars_.push_back(lm);
     N_ += 3;
     slam_.insert({f->featid, lm});
     f->to_delete = true;
     int nup = 2 * b.feats[0].nmeas - 3;
-    if (nup > 0) ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2);
+    if (nup > 0) {
+      ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
+                      b.hidx_dev, land);
+    } else {
+      HP_HIP(hipStreamSynchronize(d_.stream));
+      land();
+    }
   }
   return 0;
 }
@@ -1093,20 +1098,17 @@ int Engine::uwb_update_single(size_t anchor_id, double range) {
   H[n] = res;
   double s2 = o_.uwb_sigma_range * o_.uwb_sigma_range;
   // upload row + index, phase A (M, S), read S, gate, phase B
-  HP_HIP(hipMemcpyAsync(d_.R, H.data(), sizeof(double) * (n + 1), hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.hidx, hidx.data(), sizeof(int) * n, hipMemcpyHostToDevice, d_.stream));
-  launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, d_.R, n + 1, 1, n, d_.hidx, s2, d_.ekf);
+  const double *dH = stage(H.data(), (size_t)n + 1);
+  const int *dh = stage(hidx.data(), (size_t)n);
+  stage_flush();
+  launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, dH, n + 1, 1, n, dh, s2, d_.ekf);
   double Sval;
   HP_HIP(hipMemcpyAsync(&Sval, d_.ekf.S + 2, sizeof(double), hipMemcpyDeviceToHost, d_.stream));
   HP_HIP(hipStreamSynchronize(d_.stream));
   double chi2 = res * res / Sval;
   if (chi2 > o_.uwb_chi2_multipler * chi2_table_[1]) return 0;
-  HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
-  launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, d_.R + n, 1, d_.ekf);
-  HP_HIP(hipMemcpyAsync(d_.dx_host, d_.ekf.dx, sizeof(double) * N_, hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
-  if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, "UWB EKFUpdate: negative covariance diagonal");
+  launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, dH + n, 1, d_.ekf);
+  read_dx("UWB EKFUpdate");
   apply_dx(d_.dx_host);
   return 1;
 }

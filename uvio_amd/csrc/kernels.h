@@ -187,9 +187,10 @@ void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const in
 // cornerSubPix in place on n points (x, y); mask: (2 win + 1)^2 weights
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2);
-// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW: p1 holds the initial guess, is overwritten
+// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW: the initial guess is p1 (or p0 when init_from_p0),
+// the result goes to p1
 void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
-               int max_level, int max_iters, float eps);
+               int max_level, int max_iters, float eps, bool init_from_p0);
 // undistort both point sets, then findFundamentalMat(FM_RANSAC) mask over host-drawn subsets
 void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
                    float *p0n, float *p1n, const int *subsets, int max_iters, double thr, double conf, double *Fs,

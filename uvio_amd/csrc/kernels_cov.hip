@@ -246,7 +246,9 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 // EKF update
 // M[i][j] = sum_k P[i][hidx[k]] * H[j][k]   (N x r)   (M_a = P H^T, StateHelper.cpp:137-146)
 __global__ void __launch_bounds__(256) k_ekf_M(const double *__restrict__ P, int ldp, int N, const double *__restrict__ H,
-                                               int ldh, int r, int n, const int *__restrict__ hidx, double *__restrict__ M) {
+                                               int ldh, int r, int n, const int *__restrict__ hidx, double *__restrict__ M,
+                                               int *zero) {
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the update's negative-diagonal count
   __shared__ double Ps[16][17];
   __shared__ double Hs[16][17];
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(256) k_ekf_P(double *__restrict__ P, int ldp, 
 void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
                        const int *hidx, double sigma2, EkfScratch &sc) {
   dim3 gM((r + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, H, ldh, r, n, hidx, sc.M);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, H, ldh, r, n, hidx, sc.M, sc.neg);
   double *Sup = sc.S + 2 * (size_t)r * r;
   dim3 gS((r + 15) / 16, (r + 15) / 16);
   hipLaunchKernelGGL(k_ekf_S, gS, dim3(256), 0, s, H, ldh, r, n, hidx, sc.M, sigma2, Sup);
@@ -569,7 +571,7 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
   int l2 = b2 <= kMaxDynLds;
   hipLaunchKernelGGL(k_info_cholZ, dim3(1), dim3(512), l2 ? b2 : 0, s, E, n, sigma2, Uinv, w, gbuf, l2);
   dim3 gM((n + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Linv, n, n, n, hidx, sc.M);  // V = P[:,I] L^-T
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Linv, n, n, n, hidx, sc.M, sc.neg);  // V = P[:,I] L^-T
   hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, n, Uinv, sc.W);               // X = V U^-T
   int nb = (N + 15) / 16;
   hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg);
@@ -617,7 +619,7 @@ __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const 
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc) {
   dim3 gM(1, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M);
+  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M, (int *)nullptr);
   int nt = N * 3;
   hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
                      HLinv, s2);

@@ -434,7 +434,7 @@ __device__ __forceinline__ int bilin_der(const int16_t *d, int w, int h, int X, 
 
 __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__restrict__ p0, float *__restrict__ p1,
                                            uint8_t *__restrict__ status, int n, int win, int max_level, int max_iters,
-                                           float crit_eps) {
+                                           float crit_eps, int init_from_p0) {
   const int pi = blockIdx.x;
   if (pi >= n) return;
   const int lane = threadIdx.x;
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__
   // an iteration moves the window more than kLkMargin pixels from where it was staged
   __shared__ uint8_t Jt[kLkMaxTile * kLkMaxTile];
   const int S = win + 1 + 2 * kLkMargin;
-  float qx = p1[2 * pi], qy = p1[2 * pi + 1];
+  float qx = init_from_p0 ? p0[2 * pi] : p1[2 * pi], qy = init_from_p0 ? p0[2 * pi + 1] : p1[2 * pi + 1];
   uint8_t st = 1;
   for (int level = maxL; level >= 0; level--) {
     const uint8_t *I = prev.img[level], *J = next.img[level];
@@ -828,10 +828,11 @@ void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, 
 }
 
 void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
-               int max_level, int max_iters, float eps) {
+               int max_level, int max_iters, float eps, bool init_from_p0) {
   if (n <= 0) return;
   if (win > kLkMaxWin) throw std::runtime_error("LK window larger than the kernel supports");
-  hipLaunchKernelGGL(k_lk, dim3(n), dim3(64), 0, s, prev, next, p0, p1, status, n, win, max_level, max_iters, eps * eps);
+  hipLaunchKernelGGL(k_lk, dim3(n), dim3(64), 0, s, prev, next, p0, p1, status, n, win, max_level, max_iters, eps * eps,
+                     init_from_p0 ? 1 : 0);
 }
 
 void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
