@@ -81,4 +81,86 @@ __device__ void trtri_gj_inplace(double *A, int ld, int n) {
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Blocked LDL^T, same in/out convention as ldl_inplace, in 4-column panels:
+//   * every thread owns one panel row (rows K .. nrows-1, strided by blockDim) and eliminates its 4
+//     panel entries against the 4x4 diagonal block, whose LDL every thread recomputes in registers
+//     from 10 broadcast LDS reads (no barrier inside the panel); the unnormalized entries go back to
+//     A, the normalized multipliers to Lp (nrows x 4 scratch);
+//   * the rank-4 trailing update A22 -= L21 (D L21^T) is ONE v_mfma_f64_16x16x4_f64 per 16x16 tile of
+//     the lower triangle (A operand: -Lp rows, B operand: the panel rows' unnormalized entries).
+// Two barriers per 4 columns instead of one per column, and the update work runs on the matrix cores.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ void ldl_panel4(double *A, int ld, int n, int nrows, double *Lp) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int K = 0; K < n; K += 4) {
+    const int B = min(4, n - K);
+    // 4x4 diagonal block LDL (identical arithmetic in every thread)
+    double c[4][4];  // unnormalized final values of the diagonal block rows (lower)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int p = 0; p <= q; p++) c[q][p] = (q < B) ? A[(K + q) * ld + K + p] : 0.0;
+    double dinv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      dinv[k] = (k < B) ? 1.0 / c[k][k] : 0.0;
+#pragma unroll
+      for (int q = k + 1; q < 4; q++) {
+        const double a = c[q][k] * dinv[k];
+#pragma unroll
+        for (int p = k + 1; p <= q; p++) c[q][p] -= a * c[p][k];
+      }
+    }
+    // panel rows
+    for (int i = K + threadIdx.x; i < nrows; i += blockDim.x) {
+      double v[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) v[p] = (p < B && K + p <= i) ? A[i * ld + K + p] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (k < B && i > K + k) {
+          const double a = v[k] * dinv[k];
+#pragma unroll
+          for (int p = k + 1; p < 4; p++)
+            if (p < B && K + p <= i) v[p] -= a * c[p][k];
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        if (p < B && K + p <= i) A[i * ld + K + p] = v[p];
+        Lp[(size_t)i * 4 + p] = (p < B && K + p < i) ? v[p] * dinv[p] : 0.0;
+      }
+    }
+    __syncthreads();
+    const int T0 = K + B;
+    if (T0 < n) {
+      const int nti = (nrows - T0 + 15) / 16, ntj = (n - T0 + 15) / 16;
+      const int r16 = lane & 15, kq = lane >> 4;
+      for (int t = wid; t < nti * ntj; t += nw) {
+        const int ti = t / ntj, tj = t - ti * ntj;
+        if (tj > ti) continue;
+        const int i0 = T0 + 16 * ti, j0 = T0 + 16 * tj;
+        dbl4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int row = i0 + kq + 4 * q, col = j0 + r16;
+          acc[q] = (row < nrows && col < n && col <= row) ? A[row * ld + col] : 0.0;
+        }
+        const int arow = i0 + r16, bcol = j0 + r16;
+        const double a = (arow < nrows) ? -Lp[(size_t)arow * 4 + kq] : 0.0;
+        const double b = (bcol < n && kq < B) ? A[bcol * ld + K + kq] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int row = i0 + kq + 4 * q, col = j0 + r16;
+          if (row < nrows && col < n && col <= row) A[row * ld + col] = acc[q];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace uvhp

@@ -215,7 +215,7 @@ Engine::~Engine() {
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.fout, d_.chi2, d_.H, d_.Tall, d_.Pc, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.dxneg, d_.stg_d};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
@@ -284,6 +284,7 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
+  dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   dalloc(&d_.dxneg, cap + 2);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
@@ -581,7 +582,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   if (!info && r > kMaxEkfRows) return UVIO_HP_E_CAPACITY;
   int rw = std::max(r, n + 1);
   int nch = gram_num_chunks(r);
-  double *dP, *dH, *dM, *dW, *dS, *dy, *ddx, *dPart = nullptr, *dG = nullptr;
+  double *dP, *dH, *dM, *dW, *dS, *dy, *ddx, *dDinv, *dPart = nullptr, *dG = nullptr;
   int *dI, *dneg;
   dalloc(&dP, (size_t)N * N);
   dalloc(&dH, (size_t)r * ldh);
@@ -589,6 +590,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   dalloc(&dW, (size_t)N * rw);
   dalloc(&dS, (size_t)5 * rw * rw);
   dalloc(&dy, rw);
+  dalloc(&dDinv, (size_t)(rw / 16 + 1) * 256);
   if (info) {
     dalloc(&dPart, (size_t)nch * ldh * ldh);
     dalloc(&dG, (size_t)ldh * ldh);
@@ -605,7 +607,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   HP_HIP(hipMemcpyAsync(dH, Ha.data(), sizeof(double) * Ha.size(), hipMemcpyHostToDevice, s));
   HP_HIP(hipMemcpyAsync(dI, H_index, sizeof(int) * n, hipMemcpyHostToDevice, s));
   HP_HIP(hipMemsetAsync(dneg, 0, sizeof(int), s));
-  EkfScratch sc{dM, dW, dS, dy, ddx, dneg};
+  EkfScratch sc{dM, dW, dS, dy, ddx, dneg, dDinv};
   if (info) {
     int nc2 = 0;
     launch_gram(s, dH, r, ldh, ldh, dPart, &nc2);
@@ -618,7 +620,7 @@ int Engine::ekf_update_standalone(double *P, int N, const int *H_index, int n, c
   HP_HIP(hipMemcpyAsync(dx_out, ddx, sizeof(double) * N, hipMemcpyDeviceToHost, s));
   HP_HIP(hipMemcpyAsync(&neg, dneg, sizeof(int), hipMemcpyDeviceToHost, s));
   HP_HIP(hipStreamSynchronize(s));
-  void *ptrs[] = {dP, dH, dM, dW, dS, dy, ddx, dI, dneg, dPart, dG};
+  void *ptrs[] = {dP, dH, dM, dW, dS, dy, ddx, dDinv, dI, dneg, dPart, dG};
   for (void *p : ptrs)
     if (p) hipFree(p);
   hipStreamDestroy(s);

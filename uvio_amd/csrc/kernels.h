@@ -130,7 +130,12 @@ constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-work
 struct EkfScratch {
   double *M, *W, *S, *y, *dx;
   int *neg;
+  double *Dinv;  // 16x16 diagonal-block inverses of a triangular factor: (rmax / 16 + 1) * 256
 };
+// W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
+// columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.
+void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, int N, int r, const double *L, int ldl,
+                    double *Dinv, double *W);
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
                        const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc);
 // information-form update for a compressed batch (m > n): G = [H r]^T [H r] from k_gram partials;

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) k_gemm_HP(const double *__restrict__ H, i
 
 size_t chi2_lds_bytes(int max_rows_f, int n) {
   size_t R = max_rows_f;
-  return (2 * R * (size_t)n + (R + 1) * (R | 1)) * sizeof(double);
+  return (2 * R * (size_t)n + (R + 1) * (R | 1) + 4 * (R + 1)) * sizeof(double);
 }
 
 // One workgroup per feature.  out[f] carries the feature kernel's status / rows; chi2 rows are the
@@ -108,8 +108,9 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   int ldx = ldh;
   double *S = lds;
   const int ldS = R | 1;
+  double *Lp = lds + (size_t)(R + 1) * ldS;
   if (use_lds) {
-    double *Hl = lds + (size_t)(R + 1) * ldS;
+    double *Hl = Lp + (size_t)(R + 1) * 4;
     double *Tl = Hl + (size_t)R * n;
     for (int e = tid; e < R * n; e += blockDim.x) {
       int i = e / n, j = e - i * n;
@@ -137,7 +138,7 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   }
   for (int j = tid; j < R; j += blockDim.x) S[R * ldS + j] = Hg[(size_t)j * ldh + n];
   __syncthreads();
-  ldl_inplace(S, ldS, R, R + 1);
+  ldl_panel4(S, ldS, R, R + 1, Lp);
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {
     double z = S[R * ldS + k];
@@ -180,7 +181,7 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   hipLaunchKernelGGL(k_gemm_HP, g, dim3(256), 0, s, H_all, m, n, bp.ldh, Pc, T_all, bp.ldh);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
-  if (!use_lds) bytes = (size_t)(max_rows_f + 1) * (max_rows_f | 1) * sizeof(double);
+  if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);
   static int granted = -1;
   if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
   if (bytes > 64 * 1024 && (int)bytes > granted)

@@ -288,49 +288,115 @@ __global__ void __launch_bounds__(256) k_ekf_S(const double *__restrict__ H, int
 }
 
 // Single workgroup (512 threads): LDL^T-based Cholesky of the augmented [S ; res^T] (S from the upper
-// triangle of S_up = selfadjointView<Upper>, StateHelper.cpp:160) -> L and y = L^-1 res, then L^-1 in
-// place (dense_lds.h).  LDS when (r+1) r + 16 r doubles fit, else the global scratch `Sg`.
+// triangle of S_up = selfadjointView<Upper>, StateHelper.cpp:160) -> L (lower, ld r) and y = L^-1 res
+// (dense_lds.h).  LDS when the factor plus the panel scratch fit, else the global scratch `Sg`.
 __global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Sup, int r,
                                                    const double *__restrict__ res, int res_stride,
-                                                   double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
+                                                   double *__restrict__ L_out, double *__restrict__ y_out, double *Sg,
                                                    int use_lds) {
   extern __shared__ double lds[];
   double *A = use_lds ? lds : Sg;
   const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
+  double *Lp = A + (size_t)(r + 1) * ld;
   for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
     int a = e / r, b = e % r;
     if (b <= a) A[(size_t)a * ld + b] = Sup[(size_t)b * r + a];
   }
   for (int j = threadIdx.x; j < r; j += blockDim.x) A[(size_t)r * ld + j] = res[(size_t)j * res_stride];
   __syncthreads();
-  ldl_inplace(A, ld, r, r + 1);
+  ldl_panel4(A, ld, r, r + 1, Lp);
   ldl_to_chol(A, ld, r, r + 1);
   for (int j = threadIdx.x; j < r; j += blockDim.x) y_out[j] = A[(size_t)r * ld + j];
-  trtri_gj_inplace(A, ld, r);
   for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
     int a = e / r, b = e % r;
-    Linv_out[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    L_out[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+  }
+}
+size_t ekf_small_lds_bytes(int r) { return dense_lds_bytes(r + 1, r) + (size_t)(r + 1) * 4 * sizeof(double); }
+
+// Inverses of the 16x16 diagonal blocks of a lower-triangular L (r x r, ld): one 64-lane workgroup per
+// block, lane c < 16 forms column c by forward substitution.  Dinv: block b at Dinv + 256 b, row-major.
+// Rows past r are treated as identity.
+__global__ void __launch_bounds__(64) k_trinv16(const double *__restrict__ L, int ld, int r, double *__restrict__ Dinv) {
+  const int b = blockIdx.x, c = threadIdx.x, o = 16 * b;
+  if (c >= 16) return;
+  const int nb = min(16, r - o);
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (i < c) {
+      x[i] = 0.0;
+    } else if (i >= nb) {
+      x[i] = (i == c) ? 1.0 : 0.0;
+    } else {
+      double acc = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; k++)
+        if (k >= c) acc -= L[(size_t)(o + i) * ld + o + k] * x[k];
+      x[i] = acc / L[(size_t)(o + i) * ld + o + i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) Dinv[(size_t)256 * b + i * 16 + c] = x[i];
+}
+
+// W (N x r, ld r) = M L^-T, i.e. W L^T = M, blocked by 16 columns with the matrix cores:
+//   tile = M[:, p] - W[:, <p] L[p, <p]^T   (v_mfma_f64_16x16x4_f64 over the solved columns)
+//   W[:, p] = tile Dinv_p^T                 (4 MFMAs with the diagonal block inverse)
+// One 64-lane workgroup per 16 rows of M; the solved part of its rows stays in LDS.  With hidx, M is
+// read as P[row][hidx[k]] (ldm = ldp), i.e. the columns P[:, I] of the covariance.
+constexpr int kTrsmMaxR = 264;
+__global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, int ldm, const int *__restrict__ hidx, int N,
+                                                int r, const double *__restrict__ L, int ldl,
+                                                const double *__restrict__ Dinv, double *__restrict__ W) {
+  __shared__ double Wt[16][kTrsmMaxR + 1];
+  __shared__ double Tt[16][17];
+  const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
+  const int row0 = blockIdx.x * 16;
+  for (int j0 = 0; j0 < r; j0 += 16) {
+    dbl4 acc;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = row0 + kq + 4 * q, col = j0 + r16;
+      double v = 0.0;
+      if (row < N && col < r) v = hidx ? M[(size_t)row * ldm + hidx[col]] : M[(size_t)row * ldm + col];
+      acc[q] = v;
+    }
+    for (int k0 = 0; k0 < j0; k0 += 4) {
+      const double a = -Wt[r16][k0 + kq];
+      const int jj = j0 + r16;
+      const double b = (jj < r) ? L[(size_t)jj * ldl + k0 + kq] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    // acc (C layout) -> A-operand layout through LDS
+#pragma unroll
+    for (int q = 0; q < 4; q++) Tt[kq + 4 * q][r16] = acc[q];
+    __syncthreads();
+    dbl4 w = {0.0, 0.0, 0.0, 0.0};
+    const double *Db = Dinv + (size_t)256 * (j0 / 16);
+#pragma unroll
+    for (int m0 = 0; m0 < 16; m0 += 4) {
+      const double a = Tt[r16][m0 + kq];
+      const double b = Db[r16 * 16 + m0 + kq];  // B[m][j] = Dinv[j][m]
+      w = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, w, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int rr = kq + 4 * q, col = j0 + r16;
+      if (col < r) {
+        Wt[rr][col] = w[q];
+        if (row0 + rr < N) W[(size_t)(row0 + rr) * r + col] = w[q];
+      }
+    }
+    __syncthreads();
   }
 }
 
-// W = M Linv^T  (N x r): W[i][j] = sum_{k<=j} M[i][k] Linv[j][k]
-__global__ void __launch_bounds__(256) k_ekf_W(const double *__restrict__ M, int N, int r, const double *__restrict__ Linv,
-                                               double *__restrict__ W) {
-  __shared__ double Ms[16][17];
-  __shared__ double Ls[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
-  double acc = 0.0;
-  int kmax = min(r, j0 + 16);
-  for (int k0 = 0; k0 < kmax; k0 += 16) {
-    Ms[ty][tx] = (i0 + ty < N && k0 + tx < r) ? M[(size_t)(i0 + ty) * r + k0 + tx] : 0.0;
-    Ls[ty][tx] = (j0 + ty < r && k0 + tx < r) ? Linv[(size_t)(j0 + ty) * r + k0 + tx] : 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += Ms[ty][kk] * Ls[tx][kk];
-    __syncthreads();
-  }
-  if (i0 + ty < N && j0 + tx < r) W[(size_t)(i0 + ty) * r + j0 + tx] = acc;
+void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, int N, int r, const double *L, int ldl,
+                    double *Dinv, double *W) {
+  if (r > kTrsmMaxR) throw std::runtime_error("triangular solve wider than the kernel's LDS row");
+  hipLaunchKernelGGL(k_trinv16, dim3((r + 15) / 16), dim3(64), 0, s, L, ldl, r, Dinv);
+  hipLaunchKernelGGL(k_trsm_lt, dim3((N + 15) / 16), dim3(64), 0, s, M, ldm, hidx, N, r, L, ldl, Dinv, W);
 }
 
 // P[i][j] -= sum_k W[i][k] W[j][k] for j >= i, mirrored to (j,i); dx = W y; negative-diagonal count
@@ -380,16 +446,15 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
 
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc) {
-  size_t bytes = dense_lds_bytes(r + 1, r);
+  size_t bytes = ekf_small_lds_bytes(r);
   int use_lds = bytes <= kMaxDynLds;
-  double *Linv = sc.S;
+  double *Lf = sc.S;
   double *Sup = sc.S + 2 * (size_t)r * r;
-  double *Sg = sc.S + 3 * (size_t)r * r;  // dense_lds_bytes(r+1, r) <= 2 r^2 doubles once r >= 40 (else LDS)
+  double *Sg = sc.S + 3 * (size_t)r * r;  // (r+1)(r|1) + 4(r+1) <= 2 r^2 doubles once r >= 40 (else LDS)
   ensure_lds_attrs();
-  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
+  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Lf, sc.y, Sg,
                      use_lds);
-  dim3 gM((r + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, r, Linv, sc.W);
+  launch_trsm_lt(s, sc.M, r, nullptr, N, r, Lf, r, sc.Dinv, sc.W);  // W = M L^-T
   int nb = (N + 15) / 16;
   hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg);
 }
@@ -414,8 +479,9 @@ void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H
 
 // full symmetric G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk order)
 __global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ partials, int nch, int ncol,
-                                                     double *__restrict__ G) {
+                                                     double *__restrict__ G, int *zero) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero && e == 0) *zero = 0;  // the update's negative-diagonal count
   if (e >= ncol * ncol) return;
   int a = e / ncol, b = e % ncol;
   int u = (a <= b) ? a * ncol + b : b * ncol + a;
@@ -447,19 +513,20 @@ __global__ void __launch_bounds__(256) k_gemm(int ta, int tb, int m, int n, int 
 }
 
 // Single workgroup: P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1),
-// zero upper) and L_P^-1 (n x n).
+// zero upper) and L_P (n x n, ld n).
 __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
-                                                    int n, double *__restrict__ Laug, double *__restrict__ Linv,
+                                                    int n, double *__restrict__ Laug, double *__restrict__ Lout,
                                                     double *gbuf, int use_lds) {
   extern __shared__ double lds[];
   double *A = use_lds ? lds : gbuf;
   const int ld = n | 1;
+  double *Lp = A + (size_t)n * ld;
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
     int a = e / n, b = e % n;
     if (b <= a) A[(size_t)a * ld + b] = P[(size_t)hidx[a] * ldp + hidx[b]];
   }
   __syncthreads();
-  ldl_inplace(A, ld, n, n);
+  ldl_panel4(A, ld, n, n, Lp);
   ldl_to_chol(A, ld, n, n);
   const int na = n + 1;
   for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
@@ -468,38 +535,34 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
     if (a < n && b < n) v = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
     else if (a == n && b == n) v = 1.0;
     Laug[e] = v;
-  }
-  __syncthreads();
-  trtri_gj_inplace(A, ld, n);
-  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
-    int a = e / n, b = e % n;
-    Linv[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    if (a < n && b < n) Lout[(size_t)a * n + b] = v;
   }
 }
 
 // Single workgroup: [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T
-// -> w = U^-1 c; then U^-1 in place.  Writes U^-1 (n x n) and w (n).
+// -> w = U^-1 c.  Writes U (n x n, ld n) and w (n).
 __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
-                                                    double *__restrict__ Uinv, double *__restrict__ w, double *gbuf,
+                                                    double *__restrict__ Uout, double *__restrict__ w, double *gbuf,
                                                     int use_lds) {
   extern __shared__ double lds[];
   double *A = use_lds ? lds : gbuf;
   const int ld = n | 1;
   const int na = n + 1;
+  double *Lp = A + (size_t)na * ld;
   for (int e = threadIdx.x; e < (n + 1) * n; e += blockDim.x) {
     int a = e / n, b = e % n;
     if (b <= a) A[(size_t)a * ld + b] = E[(size_t)a * na + b] + ((a == b) ? s2 : 0.0);
   }
   __syncthreads();
-  ldl_inplace(A, ld, n, n + 1);
+  ldl_panel4(A, ld, n, n + 1, Lp);
   ldl_to_chol(A, ld, n, n + 1);
   for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[(size_t)n * ld + j];
-  trtri_gj_inplace(A, ld, n);
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
     int a = e / n, b = e % n;
-    Uinv[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    Uout[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
   }
 }
+size_t info_chol_lds_bytes(int nrows, int n) { return dense_lds_bytes(nrows, n) + (size_t)nrows * 4 * sizeof(double); }
 
 
 // P[i][j] -= sum_k V[i][k] V[j][k] - s2 sum_k X[i][k] X[j][k]  for j >= i, mirrored;  dx = X w;
@@ -552,27 +615,26 @@ __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp,
 void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
                      const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc) {
   const int na = n + 1;
-  hipLaunchKernelGGL(k_gram_reduce, dim3((na * na + 255) / 256), dim3(256), 0, s, partials, nch, na, Gbuf);
+  hipLaunchKernelGGL(k_gram_reduce, dim3((na * na + 255) / 256), dim3(256), 0, s, partials, nch, na, Gbuf, sc.neg);
   double *Laug = sc.S;                            // (n+1)^2
-  double *Linv = Laug + (size_t)na * na;          // n^2
-  double *T1 = Linv + (size_t)n * n;              // (n+1)^2
+  double *Lf = Laug + (size_t)na * na;            // n^2   L_P
+  double *T1 = Lf + (size_t)n * n;                // (n+1)^2
   double *E = T1 + (size_t)na * na;               // (n+1)^2
-  double *Uinv = E + (size_t)na * na;             // n^2   (5 (n+1)^2 in total)
+  double *Uf = E + (size_t)na * na;               // n^2   U   (5 (n+1)^2 in total)
   double *w = sc.y;
-  double *gbuf = sc.M;                            // global fallback work buffer (N rmax >= dense_lds_bytes)
+  double *gbuf = sc.M;                            // global fallback work buffer (N rmax >= the factor's bytes)
   ensure_lds_attrs();
-  size_t b1 = dense_lds_bytes(n, n);
+  size_t b1 = info_chol_lds_bytes(n, n);
   int l1 = b1 <= kMaxDynLds;
-  hipLaunchKernelGGL(k_info_cholP, dim3(1), dim3(512), l1 ? b1 : 0, s, P, ldp, hidx, n, Laug, Linv, gbuf, l1);
+  hipLaunchKernelGGL(k_info_cholP, dim3(1), dim3(512), l1 ? b1 : 0, s, P, ldp, hidx, n, Laug, Lf, gbuf, l1);
   dim3 g((na + 15) / 16, (na + 15) / 16);
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 0, 0, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 1, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
-  size_t b2 = dense_lds_bytes(n + 1, n);
+  size_t b2 = info_chol_lds_bytes(n + 1, n);
   int l2 = b2 <= kMaxDynLds;
-  hipLaunchKernelGGL(k_info_cholZ, dim3(1), dim3(512), l2 ? b2 : 0, s, E, n, sigma2, Uinv, w, gbuf, l2);
-  dim3 gM((n + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Linv, n, n, n, hidx, sc.M, sc.neg);  // V = P[:,I] L^-T
-  hipLaunchKernelGGL(k_ekf_W, gM, dim3(256), 0, s, sc.M, N, n, Uinv, sc.W);               // X = V U^-T
+  hipLaunchKernelGGL(k_info_cholZ, dim3(1), dim3(512), l2 ? b2 : 0, s, E, n, sigma2, Uf, w, gbuf, l2);
+  launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);     // V = P[:,I] L^-T
+  launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
   int nb = (N + 15) / 16;
   hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg);
 }
