@@ -85,7 +85,6 @@ struct DeviceBufs {
   double *chi2 = nullptr;
   double *H = nullptr;       // H_all (max_rows x ldh)
   double *Tall = nullptr;    // H_all P_can (max_rows x ldh), chi2 gate
-  double *Pc = nullptr;      // P_can (max_ncol^2)
   double *partials = nullptr;
   double *R = nullptr;       // compressed (ncol x ncol, + global Cholesky scratch)
   int *hidx = nullptr;

@@ -214,7 +214,7 @@ Engine::~Engine() {
   hipSetDevice(device_);
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
-                  d_.fout, d_.chi2, d_.H, d_.Tall, d_.Pc, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
+                  d_.fout, d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
                   d_.ekf.Dinv, d_.dxneg, d_.stg_d};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -274,7 +274,6 @@ void Engine::alloc_device() {
   dalloc(&d_.chi2, 1000);
   dalloc(&d_.H, (size_t)d_.max_rows * d_.ldh);
   dalloc(&d_.Tall, (size_t)d_.max_rows * d_.ldh);
-  dalloc(&d_.Pc, (size_t)d_.max_ncol * d_.max_ncol);
   int maxch = (d_.max_rows + 511) / 512 + 1;
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);

@@ -604,7 +604,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
       int rows_out = (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
       max_rows_f = std::max(max_rows_f, rows_out - (mode >= 2 ? 3 : 0));
     }
-    launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.Pc, d_.chi2, d_.fout,
+    launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout,
                       max_rows_f);
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));

@@ -108,11 +108,10 @@ void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg);
 void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const DMeas *meas,
                               const DVar *vars, const DClone *clones, const DCam *cams, const double *P,
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf);
-// batched chi2 gate (kernels_chi2.hip): P_can gather, T = H_all P_can, per-feature S / LDL^T / chi2;
-// rejected MSCKF / SLAM features get zero rows.  Pc: n^2, T_all: like H_all.
+// batched chi2 gate (kernels_chi2.hip): T = H_all P[hidx, hidx], per-feature S / LDL^T / chi2;
+// rejected MSCKF / SLAM features get zero rows.  T_all: like H_all.
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
-                       double *H_all, int m, double *T_all, double *Pc, const double *chi2_table, DFeatOut *out,
-                       int max_rows_f);
+                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f);
 size_t feature_lds_bytes(int max_meas, int max_nf);
 
 // Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->

@@ -4,7 +4,8 @@
 // Every feature's projected rows [Hhat_f | r_f] sit in H_all over the batch's canonical columns, and
 // every feature's P_marg is a principal block of the same canonical covariance P_can = P[hidx, hidx]
 // (zero columns of Hhat_f drop out).  So
-//     T = H_all P_can                    one FP64 GEMM over the whole batch (m x n x n),
+//     T = H_all P_can                    one FP64 GEMM over the whole batch (m x n x n, MFMA, P_can
+//                                        gathered from P in the operand loads),
 //     S_f = T_f Hhat_f^T + s2 I          per feature, R_f x R_f,
 // and the per-feature work is only the small S_f and its factorization.  One workgroup per feature
 // stages T_f and Hhat_f in LDS, forms the lower triangle of [S_f ; r_f^T], runs the one-barrier-per-
@@ -19,61 +20,35 @@
 
 namespace uvhp {
 
-// P_can[a][b] = P[hidx[a]][hidx[b]]   (n x n)
-__global__ void k_gather_can(const double *__restrict__ P, int ldp, const int *__restrict__ hidx, int n,
-                             double *__restrict__ Pc) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * n) return;
-  int a = e / n, b = e - a * n;
-  Pc[e] = P[(size_t)hidx[a] * ldp + hidx[b]];
-}
-
-// T (m x n, ld ldt) = H (m x n, ld ldh) * Pc (n x n).  64x64 block tiles, 256 threads with 4x4
-// register tiles, K in steps of 16 through LDS.
-constexpr int GB = 64, GK = 16;
-__global__ void __launch_bounds__(256) k_gemm_HP(const double *__restrict__ H, int m, int n, int ldh,
-                                                 const double *__restrict__ Pc, double *__restrict__ T, int ldt) {
-  __shared__ double As[GK][GB + 1];  // As[k][row]
-  __shared__ double Bs[GK][GB + 1];  // Bs[k][col]
-  const int tid = threadIdx.x, tr = tid / 16, tc = tid % 16;
-  const int i0 = blockIdx.y * GB, j0 = blockIdx.x * GB;
-  double acc[4][4];
+// T (m x n, ld ldt) = H (m x n, ld ldh) * P[hidx, hidx] with the covariance gather fused into the
+// operand loads.  One 64-lane workgroup per 16x16 tile of T, v_mfma_f64_16x16x4_f64 over K = n in
+// batches of 16 (all 8 operand loads of a batch are issued before its 4 MFMAs).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, int m, int n, int ldh,
+                                                 const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
+                                                 double *__restrict__ T, int ldt) {
+  const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
+  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  const int arow = i0 + r16, bcol = j0 + r16;
+  const double *Hr = H + (size_t)min(arow, m - 1) * ldh;
+  const int pc = (bcol < n) ? hidx[bcol] : 0;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < n; k0 += 16) {
+    double a[4], b[4];
 #pragma unroll
-  for (int a = 0; a < 4; a++)
-#pragma unroll
-    for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-  for (int k0 = 0; k0 < n; k0 += GK) {
-    for (int e = tid; e < GB * GK; e += 256) {
-      int r = e / GK, k = e % GK;  // H tile: coalesced along k
-      int gi = i0 + r, gk = k0 + k;
-      As[k][r] = (gi < m && gk < n) ? H[(size_t)gi * ldh + gk] : 0.0;
-      int kk = e / GB, c = e % GB;  // Pc tile: coalesced along columns
-      int gkk = k0 + kk, gj = j0 + c;
-      Bs[kk][c] = (gkk < n && gj < n) ? Pc[(size_t)gkk * n + gj] : 0.0;
+    for (int u = 0; u < 4; u++) {
+      const int k = k0 + 4 * u + kq;
+      a[u] = (arow < m && k < n) ? Hr[k] : 0.0;
+      b[u] = (bcol < n && k < n) ? P[(size_t)hidx[k] * ldp + pc] : 0.0;
     }
-    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < GK; k++) {
-      double a[4], b[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        a[q] = As[k][tr + 16 * q];
-        b[q] = Bs[k][tc + 16 * q];
-      }
-#pragma unroll
-      for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] += a[x] * b[y];
-    }
-    __syncthreads();
+    for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
   }
 #pragma unroll
-  for (int x = 0; x < 4; x++)
-#pragma unroll
-    for (int y = 0; y < 4; y++) {
-      int gi = i0 + tr + 16 * x, gj = j0 + tc + 16 * y;
-      if (gi < m && gj < n) T[(size_t)gi * ldt + gj] = acc[x][y];
-    }
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    if (row < m && col < n) T[(size_t)row * ldt + col] = acc[q];
+  }
 }
 
 size_t chi2_lds_bytes(int max_rows_f, int n) {
@@ -172,13 +147,11 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
 }
 
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
-                       double *H_all, int m, double *T_all, double *Pc, const double *chi2_table, DFeatOut *out,
-                       int max_rows_f) {
+                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f) {
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
-  hipLaunchKernelGGL(k_gather_can, dim3((n * n + 255) / 256), dim3(256), 0, s, P, bp.ldp, hidx, n, Pc);
-  dim3 g((n + GB - 1) / GB, (m + GB - 1) / GB);
-  hipLaunchKernelGGL(k_gemm_HP, g, dim3(256), 0, s, H_all, m, n, bp.ldh, Pc, T_all, bp.ldh);
+  hipLaunchKernelGGL(k_gemm_HPg, dim3((n + 15) / 16, (m + 15) / 16), dim3(64), 0, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx,
+                     T_all, bp.ldh);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);
