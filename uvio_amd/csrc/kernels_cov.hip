@@ -315,62 +315,54 @@ __global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Su
 }
 size_t ekf_small_lds_bytes(int r) { return dense_lds_bytes(r + 1, r) + (size_t)(r + 1) * 4 * sizeof(double); }
 
-// W (N x r, ld r) = M L^-T, i.e. W L^T = M, blocked by 16 columns with the matrix cores:
-//   tile = M[:, p] - W[:, <p] L[p, <p]^T   (v_mfma_f64_16x16x4_f64 over the solved columns)
-//   W[:, p] = tile Dinv_p^T                 (4 MFMAs with the diagonal block's inverse)
-// One 64-lane workgroup per 16 rows of M.  L is staged in LDS when it fits (else read from global),
-// the 16x16 diagonal-block inverses are formed up front by forward substitution (lane = one column of
-// one block), and the solved part of the workgroup's rows stays in LDS.  With hidx, M is read as
-// P[row][hidx[k]] (ldm = ldp), i.e. the columns P[:, I] of the covariance.
-size_t trsm_lds_bytes(int r, bool stage_l) {
-  const int nb = (r + 15) / 16;
-  size_t d = (size_t)16 * (r + 1) + (size_t)nb * 256 + 16 * 17;
-  if (stage_l) d += (size_t)r * (r + 1);
-  return d * sizeof(double);
-}
-__global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, int ldm, const int *__restrict__ hidx, int N,
-                                                int r, const double *__restrict__ L, int ldl, double *__restrict__ W,
-                                                int stage_l) {
-  extern __shared__ double lds[];
-  const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
-  const int row0 = blockIdx.x * 16, nb = (r + 15) / 16, ldw = r + 1;
-  double *Wt = lds;                   // 16 x ldw: solved W rows of this workgroup
-  double *Ds = Wt + 16 * ldw;         // nb x 16 x 16: diagonal-block inverses (row-major)
-  double *Tt = Ds + (size_t)nb * 256; // 16 x 17 transpose buffer
-  const double *Lr = L;
-  int lld = ldl;
-  if (stage_l) {
-    double *Ls = Tt + 16 * 17;
-    for (int e = l; e < r * r; e += 64) {
-      const int i = e / r, j = e - i * r;
-      if (j <= i) Ls[i * ldw + j] = L[(size_t)i * ldl + j];
-    }
-    Lr = Ls;
-    lld = ldw;
-    __syncthreads();
-  }
-  // diagonal-block inverses: lane (block b, column c) by forward substitution; rows past r = identity
-  for (int t = l; t < nb * 16; t += 64) {
-    const int b = t >> 4, c = t & 15, o = 16 * b, blk = min(16, r - o);
-    double x[16];
+// Inverses of the 16x16 diagonal blocks of a lower-triangular L (r x r, ld): one 64-lane workgroup per
+// block stages the block in LDS (one load round), then lane c < 16 forms column c by forward
+// substitution.  Dinv: block b at Dinv + 256 b, row-major.  Rows past r are treated as identity.
+__global__ void __launch_bounds__(64) k_trinv16(const double *__restrict__ L, int ld, int r, double *__restrict__ Dinv) {
+  __shared__ double Lb[16][17];
+  const int b = blockIdx.x, l = threadIdx.x, o = 16 * b;
+  const int nb = min(16, r - o);
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if (i < c) {
-        x[i] = 0.0;
-      } else if (i >= blk) {
-        x[i] = (i == c) ? 1.0 : 0.0;
-      } else {
-        double acc = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < i; k++)
-          if (k >= c) acc -= Lr[(o + i) * lld + o + k] * x[k];
-        x[i] = acc / Lr[(o + i) * lld + o + i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) Ds[b * 256 + i * 16 + c] = x[i];
+  for (int q = 0; q < 4; q++) {
+    const int e = l + 64 * q, i = e >> 4, k = e & 15;
+    Lb[i][k] = (i < nb && k <= i) ? L[(size_t)(o + i) * ld + o + k] : 0.0;
   }
   __syncthreads();
+  if (l >= 16) return;
+  const int c = l;
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    if (i < c) {
+      x[i] = 0.0;
+    } else if (i >= nb) {
+      x[i] = (i == c) ? 1.0 : 0.0;
+    } else {
+      double acc = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; k++)
+        if (k >= c) acc -= Lb[i][k] * x[k];
+      x[i] = acc / Lb[i][i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) Dinv[(size_t)256 * b + i * 16 + c] = x[i];
+}
+
+// W (N x r, ld r) = M L^-T, i.e. W L^T = M, blocked by 16 columns with the matrix cores:
+//   tile = M[:, p] - W[:, <p] L[p, <p]^T   (v_mfma_f64_16x16x4_f64 over the solved columns)
+//   W[:, p] = tile Dinv_p^T                 (4 MFMAs with the diagonal block inverse)
+// One 64-lane workgroup per 16 rows of M; the solved part of its rows stays in LDS, L (L2-resident)
+// is read in batches of 16 columns so the loads of a batch are in flight together.  With hidx, M is
+// read as P[row][hidx[k]] (ldm = ldp), i.e. the columns P[:, I] of the covariance.
+constexpr int kTrsmMaxR = 264;
+__global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, int ldm, const int *__restrict__ hidx, int N,
+                                                int r, const double *__restrict__ L, int ldl,
+                                                const double *__restrict__ Dinv, double *__restrict__ W) {
+  __shared__ double Wt[16][kTrsmMaxR + 1];
+  __shared__ double Tt[16][17];
+  const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
+  const int row0 = blockIdx.x * 16;
   for (int j0 = 0; j0 < r; j0 += 16) {
     dbl4 acc;
 #pragma unroll
@@ -381,21 +373,26 @@ __global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, in
       acc[q] = v;
     }
     const int jj = j0 + r16;
-    const double *Lj = Lr + (size_t)min(jj, r - 1) * lld;
-    for (int k0 = 0; k0 < j0; k0 += 4) {
-      const double a = -Wt[r16 * ldw + k0 + kq];
-      const double b = (jj < r) ? Lj[k0 + kq] : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    const double *Lj = L + (size_t)min(jj, r - 1) * ldl;
+    for (int k0 = 0; k0 < j0; k0 += 16) {  // j0 is a multiple of 16
+      double a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        a[u] = -Wt[r16][k0 + 4 * u + kq];
+        b[u] = (jj < r) ? Lj[k0 + 4 * u + kq] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
     }
     // acc (C layout) -> A-operand layout through LDS
 #pragma unroll
-    for (int q = 0; q < 4; q++) Tt[(kq + 4 * q) * 17 + r16] = acc[q];
+    for (int q = 0; q < 4; q++) Tt[kq + 4 * q][r16] = acc[q];
     __syncthreads();
     dbl4 w = {0.0, 0.0, 0.0, 0.0};
-    const double *Db = Ds + (size_t)256 * (j0 / 16);
+    const double *Db = Dinv + (size_t)256 * (j0 / 16);
 #pragma unroll
     for (int m0 = 0; m0 < 16; m0 += 4) {
-      const double a = Tt[r16 * 17 + m0 + kq];
+      const double a = Tt[r16][m0 + kq];
       const double b = Db[r16 * 16 + m0 + kq];  // B[m][j] = Dinv[j][m]
       w = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, w, 0, 0, 0);
     }
@@ -403,7 +400,7 @@ __global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, in
     for (int q = 0; q < 4; q++) {
       const int rr = kq + 4 * q, col = j0 + r16;
       if (col < r) {
-        Wt[rr * ldw + col] = w[q];
+        Wt[rr][col] = w[q];
         if (row0 + rr < N) W[(size_t)(row0 + rr) * r + col] = w[q];
       }
     }
@@ -413,13 +410,9 @@ __global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, in
 
 void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, int N, int r, const double *L, int ldl,
                     double *Dinv, double *W) {
-  (void)Dinv;
-  static int granted = -1;
-  if (granted < 0) granted = set_dyn_lds((const void *)k_trsm_lt, kMaxDynLds);
-  bool stage_l = trsm_lds_bytes(r, true) <= (size_t)granted;
-  size_t bytes = trsm_lds_bytes(r, stage_l);
-  if (bytes > (size_t)std::max(granted, 64 * 1024)) throw std::runtime_error("triangular solve too wide for LDS");
-  hipLaunchKernelGGL(k_trsm_lt, dim3((N + 15) / 16), dim3(64), bytes, s, M, ldm, hidx, N, r, L, ldl, W, stage_l ? 1 : 0);
+  if (r > kTrsmMaxR) throw std::runtime_error("triangular solve wider than the kernel's LDS row");
+  hipLaunchKernelGGL(k_trinv16, dim3((r + 15) / 16), dim3(64), 0, s, L, ldl, r, Dinv);
+  hipLaunchKernelGGL(k_trsm_lt, dim3((N + 15) / 16), dim3(64), 0, s, M, ldm, hidx, N, r, L, ldl, Dinv, W);
 }
 
 // P[i][j] -= sum_k W[i][k] W[j][k] for j >= i, mirrored to (j,i); dx = W y; negative-diagonal count
