@@ -109,7 +109,9 @@ typedef struct {
   int n_anchors;
   uvio_hp_anchor_t anchors[UVIO_HP_MAX_ANCHORS];
   /* runtime */
-  int record_timing;          /* keep per-frame stage timings (VioManager.cpp:631-644 schema) */
+  int record_timing;          /* per-frame stage timings (VioManager.cpp:631-644 schema); 1: host wall
+                               * times + device event timing of the feature group, 2: also wait for the
+                               * device at stage boundaries so each stage time includes its kernels */
   /* InertialInitializerOptions::init_max_features (InertialInitializerOptions.h:73): the KLT tracker
    * keeps floor(init_max_features / num_cameras) tracks per camera until an initializer succeeds
    * (VioManager.cpp:131; initialize_with_gt does not raise it to num_pts, VioManagerHelper.cpp:40) */
@@ -147,6 +149,7 @@ int uvio_hp_options_load(const char *estimator_config_path, uvio_hp_options_t *o
  * uvio::UVioManager::UVioManager (uvio/src/core/UVioManager.cpp:26). device = HIP ordinal. */
 int uvio_hp_create(const uvio_hp_options_t *opts, int device, uvio_hp_t **out);
 int uvio_hp_destroy(uvio_hp_t *h);
+/* message of the last failed call on h; with h == NULL, why the last uvio_hp_create on this thread failed */
 const char *uvio_hp_last_error(const uvio_hp_t *h);
 
 /* ---- feeds (VioManager.h:75-96, UVioManager.h:48-60) ---- */

@@ -9,15 +9,16 @@ if os.path.exists(path):
 import bench, uvio_amd as U
 opts = bench.cfg2_options(U)
 sim = bench.make_stream(opts, 80, seed=5)
+frames = bench.render_frames(sim, 80, "cuda")
 mgr = U.VioManager(opts)
-drv = bench.Driver(sim, mgr)
+drv = bench.Driver(sim, mgr, frames)
 for _ in range(60):
     drv.step()
 os.environ["UVIO_HP_FEAT_TS"] = path
 for _ in range(10):
     drv.step()
 os.environ.pop("UVIO_HP_FEAT_TS")
-a = np.fromfile(path, dtype=np.int64).reshape(-1, 12)
+a = np.fromfile(path, dtype=np.int64).reshape(-1, 16)
 names = ["setup", "geom", "jacob", "nullsp", "T/S", "chol", "output"]
 for mode in sorted(set(a[:, 0])):
     for big in (False, True):
@@ -30,3 +31,8 @@ for mode in sorted(set(a[:, 0])):
         print("mode %d %s launches-feats %d  meas %.1f nf %.1f | " % (mode, "batch" if big else "single", len(sel),
               sel[:, 2].mean(), sel[:, 3].mean()) + "  ".join("%s %.0f" % (n, v) for n, v in zip(names, np.nanmean(d, axis=0))),
               " total %.0f cyc" % np.nanmean(ts[:, 7] - ts[:, 0]))
+        c = sel[:, 12:16].astype(float)
+        c = c[c[:, 3] > 0]
+        if len(c):
+            dc = np.diff(c, axis=1)
+            print("      chi2: stage+S %.0f  ldl %.0f  chi2 %.0f  cyc (n=%d)" % tuple(list(np.mean(dc, axis=0)) + [len(c)]))

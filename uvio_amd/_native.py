@@ -127,6 +127,14 @@ def load():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError("libuvio_hp.so not built: run `python -m uvio_amd.build` (hipcc, gfx950)")
+        # In a process that also uses PyTorch-ROCm (the tests / bench harness), torch's bundled HIP
+        # runtime must be loaded first so the library's HIP symbols bind to the same runtime; two HIP
+        # runtimes in one process can leave the second without a device.  Without torch the system
+        # ROCm runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = bind(C.CDLL(LIB_PATH), "uvio_hp_")
     return _lib
 

@@ -37,6 +37,8 @@ int uvio_hp_options_load(const char *path, uvio_hp_options_t *opts) {
   return options_load(path, opts, &err);
 }
 
+static thread_local std::string g_create_err = "";  // why the last uvio_hp_create on this thread failed
+
 int uvio_hp_create(const uvio_hp_options_t *opts, int device, uvio_hp_t **out) {
   if (!opts || !out) return UVIO_HP_E_ARG;
   *out = nullptr;
@@ -45,9 +47,11 @@ int uvio_hp_create(const uvio_hp_options_t *opts, int device, uvio_hp_t **out) {
     h->e = new Engine(*opts, device);
   } catch (const HpError &ex) {
     int c = ex.code;
+    g_create_err = ex.what();
     delete h;
     return c;
   } catch (const std::exception &ex) {
+    g_create_err = ex.what();
     delete h;
     return UVIO_HP_E_DEVICE;
   }
@@ -62,7 +66,7 @@ int uvio_hp_destroy(uvio_hp_t *h) {
   return 0;
 }
 
-const char *uvio_hp_last_error(const uvio_hp_t *h) { return h ? h->err.c_str() : "null handle"; }
+const char *uvio_hp_last_error(const uvio_hp_t *h) { return h ? h->err.c_str() : g_create_err.c_str(); }
 
 int uvio_hp_initialize_with_gt(uvio_hp_t *h, const double x[17]) {
   if (!h || !x) return UVIO_HP_E_ARG;

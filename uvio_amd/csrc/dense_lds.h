@@ -16,6 +16,26 @@
 
 namespace uvhp {
 
+// Stage `count` doubles: st(e, ld(e)) for e < count, with the global loads batched kStageBatch per
+// thread (issued together, so staging costs one memory round trip per batch instead of one per element).
+constexpr int kStageBatch = 8;
+template <class LoadF, class StoreF>
+__device__ __forceinline__ void staged_copy(int count, LoadF ld, StoreF st) {
+  for (int e0 = threadIdx.x; e0 < count; e0 += kStageBatch * blockDim.x) {
+    double v[kStageBatch];
+#pragma unroll
+    for (int u = 0; u < kStageBatch; u++) {
+      const int e = e0 + u * blockDim.x;
+      v[u] = (e < count) ? ld(e) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kStageBatch; u++) {
+      const int e = e0 + u * blockDim.x;
+      if (e < count) st(e, v[u]);
+    }
+  }
+}
+
 // LDS bytes for an (nrows x n) factorization: A with an odd row stride (ld = n | 1)
 __host__ __device__ inline size_t dense_lds_bytes(int nrows, int n) { return (size_t)nrows * (n | 1) * sizeof(double); }
 

@@ -226,8 +226,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     int rc = propagate_and_clone(t);
     if (rc) return rc;
   }
-  // the device queue is in order; wait here only so the stage timings are attributable
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  // the device queue is in order: propagation runs on while the host builds the update batches
+  // (record_timing >= 2 waits here so the stage timings are attributable)
+  if (o_.record_timing >= 2) HP_HIP(hipStreamSynchronize(d_.stream));
   auto rT3 = clk::now();
   timing_.timestamp = t;
   timing_.propagation = secs(rT2, rT3);
@@ -359,7 +360,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     }
   }
   marginalize_old_clone();
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  if (o_.record_timing >= 2) HP_HIP(hipStreamSynchronize(d_.stream));
   auto rT7 = clk::now();
   timing_.msckf_update = secs(rT3, rT4);
   timing_.slam_update = secs(rT4, rT5);
@@ -594,7 +595,10 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
   if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.meas.size()));
   const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
-  if (tsdump) HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 8 * nf));
+  if (tsdump) {  // 8 k_feature phases + 4 k_chi2 phases per feature
+    HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 16 * nf));
+    HP_HIP(hipMemset(bp.dbg_ts, 0, sizeof(long long) * 16 * nf));
+  }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
   launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
@@ -626,14 +630,14 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     }
   }
   if (tsdump) {
-    std::vector<long long> h(8 * (size_t)nf);
+    std::vector<long long> h(16 * (size_t)nf);
     HP_HIP(hipMemcpy(h.data(), bp.dbg_ts, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
     HP_HIP(hipFree(bp.dbg_ts));
     FILE *fp = std::fopen(tsdump, "ab");
     for (int i = 0; i < nf; i++) {
-      long long rec[12] = {mode, nf, b.feats[i].nmeas, b.feats[i].nf};
-      for (int k = 0; k < 8; k++) rec[4 + k] = h[8 * (size_t)i + k];
-      std::fwrite(rec, sizeof(long long), 12, fp);
+      long long rec[16] = {mode, nf, b.feats[i].nmeas, b.feats[i].nf};
+      for (int k = 0; k < 12; k++) rec[4 + k] = h[16 * (size_t)i + k];
+      std::fwrite(rec, sizeof(long long), 16, fp);
     }
     std::fclose(fp);
   }

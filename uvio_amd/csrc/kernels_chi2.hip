@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, i
 
 size_t chi2_lds_bytes(int max_rows_f, int n) {
   size_t R = max_rows_f;
-  return (2 * R * (size_t)n + (R + 1) * (R | 1) + 4 * (R + 1)) * sizeof(double);
+  return (2 * R * (size_t)(n | 1) + (R + 1) * (R | 1) + 4 * (R + 1)) * sizeof(double);
 }
 
 // One workgroup per feature.  out[f] carries the feature kernel's status / rows; chi2 rows are the
@@ -66,6 +66,10 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   __shared__ double red[256];
   __shared__ int st;
   const int f = blockIdx.x;
+  long long *tsp = bp.dbg_ts ? bp.dbg_ts + (size_t)f * 16 + 8 : nullptr;  // debug phase stamps
+#define CHI2_TS(k) \
+  if (tsp && threadIdx.x == 0) tsp[k] = clock64();
+  CHI2_TS(0)
   const DFeat F = feats[f];
   const DFeatOut o = out[f];
   if (o.status != 0 || o.rows <= 0) return;
@@ -85,35 +89,59 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   const int ldS = R | 1;
   double *Lp = lds + (size_t)(R + 1) * ldS;
   if (use_lds) {
+    const int ldl = n | 1;  // odd row stride: the MFMA operand reads below hit distinct banks
     double *Hl = Lp + (size_t)(R + 1) * 4;
-    double *Tl = Hl + (size_t)R * n;
-    for (int e = tid; e < R * n; e += blockDim.x) {
-      int i = e / n, j = e - i * n;
-      Hl[e] = Hg[(size_t)i * ldh + j];
-      Tl[e] = Tg[(size_t)i * ldh + j];
-    }
+    double *Tl = Hl + (size_t)R * ldl;
+    staged_copy(
+        2 * R * n,
+        [&](int e) {
+          const int h = e >= R * n, f = e - h * R * n, i = f / n, j = f - i * n;
+          return (h ? Tg : Hg)[(size_t)i * ldh + j];
+        },
+        [&](int e, double v) {
+          const int h = e >= R * n, f = e - h * R * n, i = f / n, j = f - i * n;
+          (h ? Tl : Hl)[(size_t)i * ldl + j] = v;
+        });
     Hs = Hl;
     Ts = Tl;
-    ldx = n;
+    ldx = ldl;
     __syncthreads();
   }
-  // lower triangle of S = T Hhat^T + s2 I, and the residual row
-  for (int e = tid; e < R * R; e += blockDim.x) {
-    int i = e / R, j = e - i * R;
-    if (j > i) continue;
-    const double *ti = Ts + (size_t)i * ldx, *hj = Hs + (size_t)j * ldx;
-    double a0 = 0.0, a1 = 0.0;
-    int k = 0;
-    for (; k + 2 <= n; k += 2) {
-      a0 += ti[k] * hj[k];
-      a1 += ti[k + 1] * hj[k + 1];
+  // lower triangle of S = T Hhat^T + s2 I on the matrix cores (16x16 tiles, K = n), then the residual row
+  {
+    const int lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6, r16 = lane & 15, kq = lane >> 4;
+    const int nt = (R + 15) / 16, ntiles = nt * (nt + 1) / 2;
+    for (int t = wid; t < ntiles; t += nw) {
+      int ti = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+      while (ti * (ti + 1) / 2 > t) ti--;
+      while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+      const int tj = t - ti * (ti + 1) / 2;
+      const int arow = 16 * ti + r16, bcol = 16 * tj + r16;
+      const double *ta = Ts + (size_t)min(arow, R - 1) * ldx, *hb = Hs + (size_t)min(bcol, R - 1) * ldx;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 0; k0 < n; k0 += 16) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int k = k0 + 4 * u + kq;
+          a[u] = (arow < R && k < n) ? ta[k] : 0.0;
+          b[u] = (bcol < R && k < n) ? hb[k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int i = 16 * ti + kq + 4 * q, j = 16 * tj + r16;
+        if (i < R && j <= i) S[i * ldS + j] = acc[q] + (i == j ? bp.sigma_pix_sq : 0.0);
+      }
     }
-    if (k < n) a0 += ti[k] * hj[k];
-    S[i * ldS + j] = a0 + a1 + (i == j ? bp.sigma_pix_sq : 0.0);
   }
   for (int j = tid; j < R; j += blockDim.x) S[R * ldS + j] = Hg[(size_t)j * ldh + n];
   __syncthreads();
+  CHI2_TS(1)
   ldl_panel4(S, ldS, R, R + 1, Lp);
+  CHI2_TS(2)
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {
     double z = S[R * ldS + k];
@@ -136,6 +164,8 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
     }
     st = reject;
   }
+  CHI2_TS(3)
+#undef CHI2_TS
   __syncthreads();
   if (st && F.mode <= 1) {
     double *rows = H_all + (size_t)F.row_off * ldh;

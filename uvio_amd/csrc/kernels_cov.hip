@@ -299,11 +299,21 @@ __global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Su
   double *A = use_lds ? lds : Sg;
   const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
   double *Lp = A + (size_t)(r + 1) * ld;
-  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
-    int a = e / r, b = e % r;
-    if (b <= a) A[(size_t)a * ld + b] = Sup[(size_t)b * r + a];
-  }
-  for (int j = threadIdx.x; j < r; j += blockDim.x) A[(size_t)r * ld + j] = res[(size_t)j * res_stride];
+  staged_copy(
+      r * r + r,
+      [&](int e) {
+        if (e >= r * r) return res[(size_t)(e - r * r) * res_stride];
+        const int a = e / r, b = e - a * r;
+        return (b <= a) ? Sup[(size_t)b * r + a] : 0.0;
+      },
+      [&](int e, double v) {
+        if (e >= r * r) {
+          A[(size_t)r * ld + e - r * r] = v;
+        } else {
+          const int a = e / r, b = e - a * r;
+          if (b <= a) A[(size_t)a * ld + b] = v;
+        }
+      });
   __syncthreads();
   ldl_panel4(A, ld, r, r + 1, Lp);
   ldl_to_chol(A, ld, r, r + 1);
@@ -537,10 +547,16 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
   double *A = use_lds ? lds : gbuf;
   const int ld = n | 1;
   double *Lp = A + (size_t)n * ld;
-  for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
-    int a = e / n, b = e % n;
-    if (b <= a) A[(size_t)a * ld + b] = P[(size_t)hidx[a] * ldp + hidx[b]];
-  }
+  staged_copy(
+      n * n,
+      [&](int e) {
+        const int a = e / n, b = e - a * n;
+        return (b <= a) ? P[(size_t)hidx[a] * ldp + hidx[b]] : 0.0;
+      },
+      [&](int e, double v) {
+        const int a = e / n, b = e - a * n;
+        if (b <= a) A[(size_t)a * ld + b] = v;
+      });
   __syncthreads();
   ldl_panel4(A, ld, n, n, Lp);
   ldl_to_chol(A, ld, n, n);
@@ -565,10 +581,16 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
   const int ld = n | 1;
   const int na = n + 1;
   double *Lp = A + (size_t)na * ld;
-  for (int e = threadIdx.x; e < (n + 1) * n; e += blockDim.x) {
-    int a = e / n, b = e % n;
-    if (b <= a) A[(size_t)a * ld + b] = E[(size_t)a * na + b] + ((a == b) ? s2 : 0.0);
-  }
+  staged_copy(
+      (n + 1) * n,
+      [&](int e) {
+        const int a = e / n, b = e - a * n;
+        return (b <= a) ? E[(size_t)a * na + b] + ((a == b) ? s2 : 0.0) : 0.0;
+      },
+      [&](int e, double v) {
+        const int a = e / n, b = e - a * n;
+        if (b <= a) A[(size_t)a * ld + b] = v;
+      });
   __syncthreads();
   ldl_panel4(A, ld, n, n + 1, Lp);
   ldl_to_chol(A, ld, n, n + 1);

@@ -28,7 +28,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 // Sum over the first m lanes in lane (= measurement) order, the order the reference accumulates
 // (FeatureInitializer.cpp:76-82, 268-270, 413-416), so the LM accept/stop decisions see the same
-// bits.  Values go through LDS; every lane reads them back in the same order -> identical sums.
+// bits.  Values go through LDS (red: 64 * NV + NV doubles); lane k < NV walks series k in lane order
+// (one dependent add per measurement, the NV series in parallel) and the sums come back through LDS.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -38,14 +39,17 @@ template <int NV>
 __device__ __forceinline__ void ordered_sum(double *red, const double *v, int lane, int m, double *out) {
   wave_sync();
 #pragma unroll
-  for (int k = 0; k < NV; k++) red[k * 64 + lane] = v[k];
+  for (int k = 0; k < NV; k++) red[lane * NV + k] = v[k];
+  wave_sync();
+  if (lane < NV) {
+    double s = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < m; j++) s += red[j * NV + lane];
+    red[64 * NV + lane] = s;
+  }
   wave_sync();
 #pragma unroll
-  for (int k = 0; k < NV; k++) {
-    double s = 0.0;
-    for (int j = 0; j < m; j++) s += red[k * 64 + j];
-    out[k] = s;
-  }
+  for (int k = 0; k < NV; k++) out[k] = red[64 * NV + k];
 }
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -227,11 +231,11 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
                                                  int max_nf) {
   extern __shared__ double lds[];
   __shared__ FeatShared sh;
-  long long *tsp = bp.dbg_ts ? bp.dbg_ts + (size_t)blockIdx.x * 8 : nullptr;
+  long long *tsp = bp.dbg_ts ? bp.dbg_ts + (size_t)blockIdx.x * 16 : nullptr;
 #define FEAT_TS(k) \
   if (tsp && threadIdx.x == 0) tsp[k] = clock64();
   __shared__ int canon2loc[512];
-  __shared__ double red[9 * 64];
+  __shared__ double red[9 * 64 + 16];
   const int f = blockIdx.x;
   const DFeat F = feats[f];
   const int m = F.nmeas, rows = 2 * m, nf = F.nf, ldl = nf + 1;

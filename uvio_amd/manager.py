@@ -47,7 +47,11 @@ class VioManager:
         rc = self._call("create", C.byref(options), device, C.byref(self._h)) if self._prefix == "uvio_hp_" else \
             self._call("create", C.byref(options), C.byref(self._h))
         if rc != 0:
-            raise RuntimeError("%screate failed: %s" % (self._prefix, N.ERRNAMES.get(rc, rc)))
+            why = ""
+            if self._prefix == "uvio_hp_":
+                msg = self._call("last_error", None)
+                why = ": " + msg.decode() if msg else ""
+            raise RuntimeError("%screate failed: %s%s" % (self._prefix, N.ERRNAMES.get(rc, rc), why))
         self.options = options
 
     @classmethod
