@@ -133,6 +133,9 @@ typedef struct {
   int k_feat_launches;
   double k_feat_s;
   double k_feat_flops;
+  /* host waits on the device during this frame (tracker + estimator): count and seconds blocked */
+  int device_syncs;
+  double sync_wait;
 } uvio_hp_timing_t;
 
 typedef struct uvio_hp uvio_hp_t;

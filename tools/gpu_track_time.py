@@ -50,5 +50,5 @@ print("frames %d  track %.3f ms  total %.3f ms  wall %.3f ms  fps %.1f  pos err 
     nf, 1e3 * np.mean(tr[k:]), 1e3 * np.mean(tot[k:]), 1e3 * np.mean(wall[k:]), 1.0 / np.mean(wall[k:]),
     np.abs(x[4:7] - gt[5:8]).max(), len(g.get_tracks(0)[0]), len(g.get_tracks(1)[0])))
 for key in ["tracking", "propagation", "msckf_update", "slam_update", "slam_delayed", "marg", "total", "n_msckf",
-            "n_slam", "n_slam_delayed", "msckf_rows", "k_feat_launches"]:
+            "n_slam", "n_slam_delayed", "msckf_rows", "k_feat_launches", "device_syncs", "sync_wait"]:
     print("  %-16s %10.4f" % (key, np.mean([a[key] for a in allt[k:]]) * (1e3 if isinstance(allt[0][key], float) else 1)))

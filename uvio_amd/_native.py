@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "uvio_amd", "libuvio_hp.so")
+LIB_PATH = os.environ.get("UVIO_HP_LIB", os.path.join(ROOT, "uvio_amd", "libuvio_hp.so"))  # override: A/B runs
 
 MAX_CAMS = 4
 MAX_ANCHORS = 16
@@ -64,7 +64,8 @@ class Timing(C.Structure):
                 ("marg", C.c_double), ("total", C.c_double), ("n_msckf", C.c_int), ("n_slam", C.c_int),
                 ("n_slam_delayed", C.c_int), ("n_clones", C.c_int), ("cov_dim", C.c_int),
                 ("msckf_rows", C.c_int), ("msckf_cols", C.c_int), ("k_feat_launches", C.c_int),
-                ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double)]
+                ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double), ("device_syncs", C.c_int),
+                ("sync_wait", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -198,6 +198,8 @@ class Engine {
     return (T *)stage_bytes(src, sizeof(T) * n);
   }
   void stage_flush();
+  // wait for the device (counted in the frame's timing: device_syncs, sync_wait)
+  void dev_sync();
   // dx + negative-diagonal count back to the host (one copy + sync); throws on a negative diagonal
   void read_dx(const char *who);
   void initialize_invertible_host(const VarP &v, const std::vector<std::pair<int, int>> &H_order,
@@ -215,7 +217,8 @@ class Engine {
   int propagate_uwb(double t);
 
   // updates
-  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1);
+  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1,
+                     int track_syncs = 0, double track_wait = 0.0);
   int do_feature_propagate_update(double t, const std::vector<int> &camids);
   int msckf_update(std::vector<FeatP> &feats);
   int slam_update(std::vector<FeatP> &feats);

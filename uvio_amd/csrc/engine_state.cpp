@@ -308,19 +308,19 @@ void Engine::alloc_device() {
 void Engine::upload_P_full(const std::vector<double> &Ph, int N) {
   HP_HIP(hipMemcpy2DAsync(d_.P, sizeof(double) * d_.ldp, Ph.data(), sizeof(double) * N, sizeof(double) * N, N,
                           hipMemcpyHostToDevice, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
 }
 void Engine::download_P(std::vector<double> &Ph) {
   Ph.assign((size_t)N_ * N_, 0.0);
   if (N_ == 0) return;
   HP_HIP(hipMemcpy2DAsync(Ph.data(), sizeof(double) * N_, d_.P, sizeof(double) * d_.ldp, sizeof(double) * N_, N_,
                           hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
 }
 void Engine::get_cov(double *out, int ld) {
   HP_HIP(hipMemcpy2DAsync(out, sizeof(double) * ld, d_.P, sizeof(double) * d_.ldp, sizeof(double) * N_, N_,
                           hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
 }
 
 // A ring: tables are appended after the last flushed one and the ring restarts only when full (after
@@ -330,7 +330,7 @@ void *Engine::stage_bytes(const void *src, size_t bytes) {
   if (need > d_.stg_cap) throw HpError(UVIO_HP_E_CAPACITY, "upload staging exhausted");
   if (d_.stg_used + need > d_.stg_cap) {
     stage_flush();
-    HP_HIP(hipStreamSynchronize(d_.stream));
+    dev_sync();
     d_.stg_used = d_.stg_flushed = 0;
   }
   if (bytes) std::memcpy(d_.stg_h + d_.stg_used, src, bytes);
@@ -346,9 +346,16 @@ void Engine::stage_flush() {
   d_.stg_flushed = d_.stg_used;
 }
 
+void Engine::dev_sync() {
+  auto t0 = std::chrono::steady_clock::now();
+  HP_HIP(hipStreamSynchronize(d_.stream));
+  timing_.sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  timing_.device_syncs++;
+}
+
 void Engine::read_dx(const char *who) {
   HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (1 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
 }
 
@@ -368,7 +375,7 @@ void Engine::check_neg_diag(const char *who) {
   HP_HIP(hipMemsetAsync(d_.ekf.neg, 0, sizeof(int), d_.stream));
   launch_check_diag(d_.stream, d_.P, d_.ldp, N_, d_.ekf.neg);
   HP_HIP(hipMemcpyAsync(d_.neg_host, d_.ekf.neg, sizeof(int), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
 }
 

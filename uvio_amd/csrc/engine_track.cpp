@@ -1,6 +1,7 @@
 // KLT front-end host orchestration — see tracker.h.  Reference: ov_core TrackKLT.cpp:34-886,
 // Grider_GRID.h:74-180 (restated for the checker in oracle/src/tracker_klt.cpp).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 
@@ -133,7 +134,9 @@ Tracker::~Tracker() {
 }
 
 void Tracker::sync() {
+  auto t0 = std::chrono::steady_clock::now();
   HP_HIP(hipStreamSynchronize(s_));
+  sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   device_syncs++;
 }
 
@@ -249,8 +252,13 @@ const std::vector<int> &Tracker::subsets(int count) {
 void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
                    const uint8_t *const *masks, bool device_imgs, const DbSink &db) {
   device_syncs = 0;
+  sync_wait = 0.0;
   if (histogram_method_ == 2)
     throw HpError(UVIO_HP_E_CONFIG, "histogram_method 2 (CLAHE) is not implemented by the KLT front-end");
+  if (ncam > kMaxCams) throw HpError(UVIO_HP_E_ARG, "too many cameras in one feed");
+  PyrJob job{};
+  job.ncam = ncam;
+  job.equalize = histogram_method_ == 1;
   for (int k = 0; k < ncam; k++) {
     const int cid = cam_ids[k];
     const int w = cams_[cid].w, h = cams_[cid].h;
@@ -264,14 +272,17 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
       src = c.d_raw;
       stride = w;
     }
-    launch_equalize(s_, src, w, h, stride, histogram_method_ == 1, c.d_hist, (uint8_t *)c.pyr[nw].img[0]);
-    launch_pyramid(s_, c.pyr[nw]);
+    job.p[k] = c.pyr[nw];
+    job.src[k] = src;
+    job.stride[k] = stride;
+    job.hist[k] = c.d_hist;
     c.mask_new.clear();
     if (masks && masks[k]) {
       c.mask_new.resize((size_t)w * h);
       for (int y = 0; y < h; y++) std::memcpy(&c.mask_new[(size_t)y * w], masks[k] + (size_t)y * strides[k], w);
     }
   }
+  launch_pyramids(s_, job);
   if (ncam == 1) {
     feed_monocular(t, cam_ids[0], db);
   } else if (ncam == 2 && use_stereo_) {

@@ -191,13 +191,16 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
                  [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
                    db_update(id, tt, (size_t)cam, u, v, un, vn);
                  });
-  return after_tracking(t, camids, rT1);
+  return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait);
 }
 
-int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1) {
+int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, int track_syncs,
+                           double track_wait) {
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
   timing_.tracking = secs(rT1, rT2);
+  timing_.device_syncs = track_syncs;
+  timing_.sync_wait = track_wait;
   if (!is_initialized_) return UVIO_HP_E_STATE;
   if (!past_uwb_.empty()) {
     for (auto it = past_uwb_.begin(); it != past_uwb_.lower_bound(t); it++) {
@@ -228,7 +231,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   }
   // the device queue is in order: propagation runs on while the host builds the update batches
   // (record_timing >= 2 waits here so the stage timings are attributable)
-  if (o_.record_timing >= 2) HP_HIP(hipStreamSynchronize(d_.stream));
+  if (o_.record_timing >= 2) dev_sync();
   auto rT3 = clk::now();
   timing_.timestamp = t;
   timing_.propagation = secs(rT2, rT3);
@@ -360,7 +363,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     }
   }
   marginalize_old_clone();
-  if (o_.record_timing >= 2) HP_HIP(hipStreamSynchronize(d_.stream));
+  if (o_.record_timing >= 2) dev_sync();
   auto rT7 = clk::now();
   timing_.msckf_update = secs(rT3, rT4);
   timing_.slam_update = secs(rT4, rT5);
@@ -613,7 +616,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
   outs.assign(d_.fout_host, d_.fout_host + nf);
   if (o_.record_timing) {
     float ms = 0.f;
@@ -889,7 +892,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
                       b.hidx_dev, land);
     } else {
-      HP_HIP(hipStreamSynchronize(d_.stream));
+      dev_sync();
       land();
     }
   }
@@ -1108,7 +1111,7 @@ int Engine::uwb_update_single(size_t anchor_id, double range) {
   launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, dH, n + 1, 1, n, dh, s2, d_.ekf);
   double Sval;
   HP_HIP(hipMemcpyAsync(&Sval, d_.ekf.S + 2, sizeof(double), hipMemcpyDeviceToHost, d_.stream));
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  dev_sync();
   double chi2 = res * res / Sval;
   if (chi2 > o_.uwb_chi2_multipler * chi2_table_[1]) return 0;
   launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, dH + n, 1, d_.ekf);

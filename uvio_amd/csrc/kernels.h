@@ -184,6 +184,16 @@ void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride
                      uint8_t *dst);
 // pyrDown + Scharr for every level of p (level 0 image already written)
 void launch_pyramid(hipStream_t s, DPyr &p);
+// one frame's cameras at once: equalizeHist (or copy) of src[c] (row stride stride[c]) into level 0 of
+// p[c], then every level's pyrDown + Scharr; hist[c]: 256 u32 scratch per camera
+struct PyrJob {
+  DPyr p[kMaxCams];
+  const uint8_t *src[kMaxCams];
+  int stride[kMaxCams];
+  unsigned *hist[kMaxCams];
+  int ncam, equalize;
+};
+void launch_pyramids(hipStream_t s, const PyrJob &job);
 // FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell;
 // score_map: w x h u8 scratch
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,

@@ -110,6 +110,157 @@ __global__ void k_scharr(const uint8_t *__restrict__ s, int w, int h, int16_t *_
   d[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1p + t1m) * 3 + t1 * 10);
 }
 
+// ---------------------------------------------------------------- fused multi-camera pyramid
+// All cameras of a frame in one launch per stage (blockIdx.z = camera):
+//   k_hist_multi               histograms of the input images
+//   k_eq_scharr_multi          LUT from the histogram scan, level 0 = LUT(src), Scharr of level 0
+//   k_pyr_scharr_multi(l)      level l = pyrDown(level l-1), Scharr of level l
+// A 32x8 output tile plus a 1-pixel halo (reflect-101 coordinates, so the halo holds exactly the
+// neighbours calcSharrDeriv reads) is built in LDS and the derivatives come out of LDS: 6 launches per
+// frame for all levels of all cameras instead of 11 per camera, same bits as k_pyrdown + k_scharr.
+constexpr int kTW = 32, kTH = 8;
+
+__device__ __forceinline__ void scharr_from_tile(const uint8_t (*t)[kTW + 2], int tx, int ty, int16_t *d) {
+  const int xm = tx, x = tx + 1, xp = tx + 2, ym = ty, y = ty + 1, yp = ty + 2;
+  const int t0m = (t[ym][xm] + t[yp][xm]) * 3 + t[y][xm] * 10, t0p = (t[ym][xp] + t[yp][xp]) * 3 + t[y][xp] * 10;
+  const int t1m = t[yp][xm] - t[ym][xm], t1p = t[yp][xp] - t[ym][xp], t1 = t[yp][x] - t[ym][x];
+  d[0] = (int16_t)(t0p - t0m);
+  d[1] = (int16_t)((t1p + t1m) * 3 + t1 * 10);
+}
+
+__global__ void __launch_bounds__(256) k_hist_multi(PyrJob job) {
+  __shared__ unsigned hs[256];
+  const int c = blockIdx.z;
+  const DPyr &p = job.p[c];
+  const int w = p.w[0], h = p.h[0], stride = job.stride[c];
+  const uint8_t *img = job.src[c];
+  hs[threadIdx.x] = 0;
+  __syncthreads();
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < w * h; e += gridDim.x * blockDim.x) {
+    const int y = e / w, x = e - y * w;
+    atomicAdd(&hs[img[(size_t)y * stride + x]], 1u);
+  }
+  __syncthreads();
+  if (hs[threadIdx.x]) atomicAdd(&job.hist[c][threadIdx.x], hs[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) k_eq_scharr_multi(PyrJob job) {
+  __shared__ uint8_t lut[256];
+  __shared__ int scan[256];
+  __shared__ int first;
+  __shared__ uint8_t tile[kTH + 2][kTW + 2];
+  const int c = blockIdx.z, t = threadIdx.x;
+  const DPyr &p = job.p[c];
+  const int w = p.w[0], h = p.h[0], stride = job.stride[c];
+  const uint8_t *src = job.src[c];
+  // LUT of EqualizeHistLut_Invoker (as k_equalize)
+  if (!job.equalize) {
+    lut[t] = (uint8_t)t;
+  } else {
+    const unsigned *hist = job.hist[c];
+    const int hv = (int)hist[t];
+    scan[t] = hv;
+    if (t == 0) first = 256;
+    __syncthreads();
+    if (hv) atomicMin(&first, t);
+    for (int o = 1; o < 256; o <<= 1) {
+      int v = (t >= o) ? scan[t - o] : 0;
+      __syncthreads();
+      scan[t] += v;
+      __syncthreads();
+    }
+    const int i0 = first, total = w * h, h0 = (int)hist[i0];
+    if (h0 == total) {
+      lut[t] = (uint8_t)i0;
+    } else if (t <= i0) {
+      lut[t] = 0;
+    } else {
+      float scale = __fdiv_rn(256 - 1.f, (float)(total - h0));
+      int sum = scan[t] - scan[i0];
+      int r = (int)rintf(__fmul_rn((float)sum, scale));
+      lut[t] = (uint8_t)min(255, max(0, r));
+    }
+  }
+  __syncthreads();
+  const int ntx = (w + kTW - 1) / kTW;
+  const int x0 = (blockIdx.x % ntx) * kTW, y0 = (blockIdx.x / ntx) * kTH;
+  if (y0 >= h) return;
+  for (int e = t; e < (kTW + 2) * (kTH + 2); e += blockDim.x) {
+    const int ty = e / (kTW + 2), tx = e - ty * (kTW + 2);
+    const int gx = reflect101(x0 + tx - 1, w), gy = reflect101(y0 + ty - 1, h);
+    tile[ty][tx] = lut[src[(size_t)gy * stride + gx]];
+  }
+  __syncthreads();
+  const int tx = t % kTW, ty = t / kTW, gx = x0 + tx, gy = y0 + ty;
+  if (gx < w && gy < h) {
+    ((uint8_t *)p.img[0])[(size_t)gy * w + gx] = tile[ty + 1][tx + 1];
+    scharr_from_tile(tile, tx, ty, (int16_t *)p.der[0] + ((size_t)gy * w + gx) * 2);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pyr_scharr_multi(PyrJob job, int l) {
+  __shared__ uint8_t tile[kTH + 2][kTW + 2];
+  const int c = blockIdx.z, t = threadIdx.x;
+  const DPyr &p = job.p[c];
+  if (l >= p.levels) return;
+  const int sw = p.w[l - 1], sh = p.h[l - 1], dw = p.w[l], dh = p.h[l];
+  const uint8_t *src = p.img[l - 1];
+  const int ntx = (dw + kTW - 1) / kTW;
+  const int x0 = (blockIdx.x % ntx) * kTW, y0 = (blockIdx.x / ntx) * kTH;
+  if (y0 >= dh) return;
+  const int k5[5] = {1, 4, 6, 4, 1};
+  for (int e = t; e < (kTW + 2) * (kTH + 2); e += blockDim.x) {
+    const int ty = e / (kTW + 2), tx = e - ty * (kTW + 2);
+    const int x = reflect101(x0 + tx - 1, dw), y = reflect101(y0 + ty - 1, dh);
+    int xs[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * sw;
+      int r = 0;
+#pragma unroll
+      for (int j = 0; j < 5; j++) r += k5[j] * row[xs[j]];
+      acc += k5[i] * r;
+    }
+    tile[ty][tx] = (uint8_t)((acc + 128) >> 8);
+  }
+  __syncthreads();
+  const int tx = t % kTW, ty = t / kTW, gx = x0 + tx, gy = y0 + ty;
+  if (gx < dw && gy < dh) {
+    ((uint8_t *)p.img[l])[(size_t)gy * dw + gx] = tile[ty + 1][tx + 1];
+    scharr_from_tile(tile, tx, ty, (int16_t *)p.der[l] + ((size_t)gy * dw + gx) * 2);
+  }
+}
+
+void launch_pyramids(hipStream_t s, const PyrJob &job) {
+  if (job.ncam <= 0) return;
+  int w0 = 0, h0 = 0, maxl = 0;
+  for (int c = 0; c < job.ncam; c++) {
+    w0 = max(w0, job.p[c].w[0]);
+    h0 = max(h0, job.p[c].h[0]);
+    maxl = max(maxl, job.p[c].levels);
+  }
+  if (job.equalize) {
+    for (int c = 0; c < job.ncam; c++)
+      if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
+    hipLaunchKernelGGL(k_hist_multi, dim3(min(256, (w0 * h0 + 4095) / 4096), 1, job.ncam), dim3(256), 0, s, job);
+  }
+  const int t0 = ((w0 + kTW - 1) / kTW) * ((h0 + kTH - 1) / kTH);
+  hipLaunchKernelGGL(k_eq_scharr_multi, dim3(t0, 1, job.ncam), dim3(256), 0, s, job);
+  for (int l = 1; l < maxl; l++) {
+    int wl = 0, hl = 0;
+    for (int c = 0; c < job.ncam; c++)
+      if (l < job.p[c].levels) {
+        wl = max(wl, job.p[c].w[l]);
+        hl = max(hl, job.p[c].h[l]);
+      }
+    const int tl = ((wl + kTW - 1) / kTW) * ((hl + kTH - 1) / kTH);
+    hipLaunchKernelGGL(k_pyr_scharr_multi, dim3(tl, 1, job.ncam), dim3(256), 0, s, job, l);
+  }
+}
+
 // ---------------------------------------------------------------- FAST-9 on grid cells
 // ring offsets (dx, dy) of cv::makeOffsets(pattern 16)
 __constant__ int c_fast_off[16][2] = {{0, 3},  {1, 3},  {2, 2},  {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},

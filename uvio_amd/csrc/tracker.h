@@ -39,7 +39,8 @@ class Tracker {
   bool last_pyramid(int cam, int level, int *w, int *h, std::vector<uint8_t> *img, std::vector<int16_t> *der);
 
   size_t currid;
-  int device_syncs = 0;  // host waits in the last feed
+  int device_syncs = 0;     // host waits in the last feed
+  double sync_wait = 0.0;   // seconds blocked in them
 
  private:
   struct CamState {
