@@ -159,7 +159,14 @@ int main(int argc, char **argv) {
   }
   CK(hipMemcpy(dp, g.data(), g.size() * 4, hipMemcpyHostToDevice));
   timeit("lk 200 pts", [&] {
-    launch_lk(s, A.p, B.p, dp, dq, st, 200, 15, 5, 30, 0.01f, true);
+    LkSlots lk{};
+    lk.prev[0] = A.p;
+    lk.next[0] = B.p;
+    lk.p0[0] = dp;
+    lk.p1[0] = dq;
+    lk.st[0] = st;
+    lk.n[0] = 200;
+    launch_lk(s, lk, 1, 15, 5, 30, 0.01f, true);
   });
   std::vector<float> q(400);
   std::vector<uint8_t> sv(200);

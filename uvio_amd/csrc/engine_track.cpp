@@ -53,8 +53,8 @@ struct Tracker::Bufs {
   int cap = 0, maxcells = 0, kmax = 0;
   char *dmem = nullptr, *hmem = nullptr;
   size_t mirror = 0;  // bytes [0, mirror) of the device block are mirrored in pinned host memory
-  // device (host mirror: hp(x)); per matching slot the inputs [p0 | sub] and outputs [p1 | st | mask]
-  // are contiguous so each direction is one copy
+  // device (host mirror: hp(x)); the matching inputs [p0 | sub] x 2 slots and outputs [p1 | st | mask] x 2
+  // are contiguous so each direction is one copy per frame
   float *p0[2], *p1[2], *p0n[2], *p1n[2];
   uint8_t *st[2], *mask[2];
   int *sub[2], *nm[2], *good[2];
@@ -154,9 +154,11 @@ void Tracker::ensure_cap(int n) {
   for (int pass = 0; pass < 2; pass++) {
     Arena d;
     if (pass == 1) d.base = b.dmem;
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 2; k++) {  // matching inputs of both slots: one upload
       b.p0[k] = d.take<float>(2 * cap);
       b.sub[k] = d.take<int>(7 * kRansacIters);
+    }
+    for (int k = 0; k < 2; k++) {  // matching outputs of both slots: one readback
       b.p1[k] = d.take<float>(2 * cap);
       b.st[k] = d.take<uint8_t>(cap);
       b.mask[k] = d.take<uint8_t>(cap);
@@ -351,7 +353,14 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
   HP_HIP(hipMemcpyAsync(b.det, h_det, 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
   launch_subpix(s_, p.img[0], W, H, b.det, n, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
   if (lk_to) {
-    launch_lk(s_, p, *lk_to, b.det, b.det1, b.detst, n, win_, pyr_levels_, kLkIters, kLkEps, true);
+    LkSlots lk{};
+    lk.prev[0] = p;
+    lk.next[0] = *lk_to;
+    lk.p0[0] = b.det;
+    lk.p1[0] = b.det1;
+    lk.st[0] = b.detst;
+    lk.n[0] = n;
+    launch_lk(s_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
     HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + n), hipMemcpyDeviceToHost, s_));
   } else {
     HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
@@ -551,14 +560,16 @@ void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, cons
 
 // ---------------------------------------------------------------- temporal matching
 // TrackKLT::perform_matching (TrackKLT.cpp:829-886): LK from the last pyramid, then
-// findFundamentalMat(FM_RANSAC, 2 / max focal, 0.999) on undistorted points, all on the device
-void Tracker::match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
-                           MatchJob &j) {
+// findFundamentalMat(FM_RANSAC, 2 / max focal, 0.999) on undistorted points, all on the device.
+// match_prepare stages one slot; match_run sends both slots' inputs in one copy, runs LK and RANSAC for
+// both in one launch per stage and reads both results back in one copy.
+void Tracker::match_prepare(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
+                            MatchJob &j) {
   j.n = (int)k0.size();
   j.run = j.n >= 10;
+  j.slot = slot;
   if (!j.run) return;
   const int n = j.n;
-  ensure_cap(n);
   Bufs &b = *b_;
   float *h_p0 = b.hp(b.p0[slot]);
   for (int i = 0; i < n; i++) {
@@ -567,13 +578,53 @@ void Tracker::match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, i
   }
   const std::vector<int> &sub = subsets(n);
   std::memcpy(b.hp(b.sub[slot]), sub.data(), sub.size() * sizeof(int));
-  HP_HIP(hipMemcpyAsync(b.p0[slot], h_p0, span(b.p0[slot], b.sub[slot] + sub.size()), hipMemcpyHostToDevice, s_));
-  launch_lk(s_, p0, p1, b.p0[slot], b.p1[slot], b.st[slot], n, win_, pyr_levels_, kLkIters, kLkEps, true);
-  const CamParams &c0 = cams_[cam0], &c1 = cams_[cam1];
-  const double fmax = std::max(std::max(c0.v[0], c0.v[1]), std::max(c1.v[0], c1.v[1]));
-  launch_ransac(s_, c0, c1, b.p0[slot], b.p1[slot], n, b.p0n[slot], b.p1n[slot], b.sub[slot], kRansacIters, 2.0 / fmax,
-                kRansacConf, b.F[slot], b.nm[slot], b.good[slot], b.mask[slot]);
-  HP_HIP(hipMemcpyAsync(b.hp(b.p1[slot]), b.p1[slot], span(b.p1[slot], b.mask[slot] + n), hipMemcpyDeviceToHost, s_));
+  j.prev = p0;
+  j.next = p1;
+  j.cam0 = cam0;
+  j.cam1 = cam1;
+}
+
+void Tracker::match_run(MatchJob *jobs, int nj) {
+  Bufs &b = *b_;
+  LkSlots lk{};
+  RansacSlots rs{};
+  int ns = 0, lo = 2, hi = -1;
+  for (int k = 0; k < nj; k++) {
+    const MatchJob &j = jobs[k];
+    if (!j.run) continue;
+    const int sl = j.slot;
+    lo = std::min(lo, sl);
+    hi = std::max(hi, sl);
+    lk.prev[ns] = j.prev;
+    lk.next[ns] = j.next;
+    lk.p0[ns] = b.p0[sl];
+    lk.p1[ns] = b.p1[sl];
+    lk.st[ns] = b.st[sl];
+    lk.n[ns] = j.n;
+    const CamParams &c0 = cams_[j.cam0], &c1 = cams_[j.cam1];
+    const double fmax = std::max(std::max(c0.v[0], c0.v[1]), std::max(c1.v[0], c1.v[1]));
+    const double thr = 2.0 / fmax;
+    rs.c0[ns] = c0;
+    rs.c1[ns] = c1;
+    rs.p0[ns] = b.p0[sl];
+    rs.p1[ns] = b.p1[sl];
+    rs.p0n[ns] = b.p0n[sl];
+    rs.p1n[ns] = b.p1n[sl];
+    rs.sub[ns] = b.sub[sl];
+    rs.F[ns] = b.F[sl];
+    rs.nm[ns] = b.nm[sl];
+    rs.good[ns] = b.good[sl];
+    rs.mask[ns] = b.mask[sl];
+    rs.t[ns] = (float)(thr * thr);
+    rs.n[ns] = j.n;
+    ns++;
+  }
+  if (ns == 0) return;
+  HP_HIP(hipMemcpyAsync(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters), hipMemcpyHostToDevice, s_));
+  launch_lk(s_, lk, ns, win_, pyr_levels_, kLkIters, kLkEps, true);
+  launch_ransac(s_, rs, ns, kRansacIters, kRansacConf);
+  HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.mask[hi] + b.cap), hipMemcpyDeviceToHost, s_));
+  sync();
 }
 
 void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out) {
@@ -611,8 +662,9 @@ void Tracker::feed_monocular(double t, int cam, const DbSink &db) {
   std::vector<size_t> ids_old = c.ids_last;
   detect_monocular(cam, pl, c.mask_last, pts_old, ids_old);
   MatchJob j;
-  match_launch(0, pl, pn, cam, cam, pts_old, j);
-  if (j.run) sync();
+  ensure_cap((int)pts_old.size());
+  match_prepare(0, pl, pn, cam, cam, pts_old, j);
+  match_run(&j, 1);
   std::vector<KeyPt> pts_new = pts_old;
   std::vector<uint8_t> mask_ll;
   match_collect(0, j, pts_new, mask_ll);
@@ -659,11 +711,12 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   std::vector<KeyPt> pl_old = A.pts_last, pr_old = B.pts_last;
   std::vector<size_t> il_old = A.ids_last, ir_old = B.ids_last;
   detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
-  MatchJob jl, jr;
-  ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two launches
-  match_launch(0, ll, nl, cl, cl, pl_old, jl);
-  match_launch(1, lr, nr, cr, cr, pr_old, jr);
-  if (jl.run || jr.run) sync();
+  MatchJob jm[2];
+  ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two slots
+  match_prepare(0, ll, nl, cl, cl, pl_old, jm[0]);
+  match_prepare(1, lr, nr, cr, cr, pr_old, jm[1]);
+  match_run(jm, 2);
+  const MatchJob &jl = jm[0], &jr = jm[1];
   std::vector<KeyPt> pl_new = pl_old, pr_new = pr_old;
   std::vector<uint8_t> mask_ll, mask_rr;
   match_collect(0, jl, pl_new, mask_ll);

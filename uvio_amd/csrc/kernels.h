@@ -201,13 +201,32 @@ void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const in
 // cornerSubPix in place on n points (x, y); mask: (2 win + 1)^2 weights
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2);
-// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW: the initial guess is p1 (or p0 when init_from_p0),
-// the result goes to p1
-void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
-               int max_level, int max_iters, float eps, bool init_from_p0);
-// undistort both point sets, then findFundamentalMat(FM_RANSAC) mask over host-drawn subsets
-void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
-                   float *p0n, float *p1n, const int *subsets, int max_iters, double thr, double conf, double *Fs,
-                   int *nmodels, int *good, uint8_t *mask);
+// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW for up to 2 point sets in one launch: slot k tracks
+// n[k] points p0[k] from prev[k] into next[k]; the initial guess is p1[k] (or p0[k] when init_from_p0),
+// the result goes to p1[k], the status to st[k]
+struct LkSlots {
+  DPyr prev[2], next[2];
+  const float *p0[2];
+  float *p1[2];
+  uint8_t *st[2];
+  int n[2];
+};
+void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,
+               bool init_from_p0);
+// per slot: undistort p0 (camera c0) and p1 (c1), then findFundamentalMat(FM_RANSAC, thr) over the
+// host-drawn subsets sub (max_iters x 7): hypotheses in parallel, sequential adaptive selection, inlier
+// mask.  t = thr^2 (float), scratch p0n / p1n (2n), F (27 max_iters), nm (max_iters), good (3 max_iters)
+struct RansacSlots {
+  CamParams c0[2], c1[2];
+  const float *p0[2], *p1[2];
+  float *p0n[2], *p1n[2];
+  const int *sub[2];
+  double *F[2];
+  int *nm[2], *good[2];
+  uint8_t *mask[2];
+  float t[2];
+  int n[2];
+};
+void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf);
 
 }  // namespace uvhp

@@ -583,11 +583,9 @@ __device__ __forceinline__ int bilin_der(const int16_t *d, int w, int h, int X, 
                  14);
 }
 
-__global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__restrict__ p0, float *__restrict__ p1,
-                                           uint8_t *__restrict__ status, int n, int win, int max_level, int max_iters,
-                                           float crit_eps, int init_from_p0) {
-  const int pi = blockIdx.x;
-  if (pi >= n) return;
+__device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
+                                         float *__restrict__ p1, uint8_t *__restrict__ status, int pi, int win,
+                                         int max_level, int max_iters, float crit_eps, int init_from_p0) {
   const int lane = threadIdx.x;
   const int maxL = min(max_level, min(prev.levels, next.levels) - 1);
   const float halfw = (win - 1) * 0.5f;
@@ -719,12 +717,25 @@ __global__ void __launch_bounds__(64) k_lk(DPyr prev, DPyr next, const float *__
   }
 }
 
+// point blockIdx.x of slot blockIdx.y (both cameras' temporal tracks in one launch)
+__global__ void __launch_bounds__(64) k_lk(LkSlots job, int win, int max_level, int max_iters, float crit_eps,
+                                           int init_from_p0) {
+  const int slot = blockIdx.y;
+  if ((int)blockIdx.x >= job.n[slot]) return;
+  lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], blockIdx.x, win, max_level, max_iters,
+           crit_eps, init_from_p0);
+}
+
 // ---------------------------------------------------------------- undistort + RANSAC
-__global__ void k_undistort(CamParams cam, const float *__restrict__ pts, float *__restrict__ out, int n) {
-  int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
+// set blockIdx.y = 2 slot + (0: p0 with c0, 1: p1 with c1)
+__global__ void k_undistort(RansacSlots job) {
+  const int slot = blockIdx.y >> 1, which = blockIdx.y & 1;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= job.n[slot]) return;
+  const float *pts = which ? job.p1[slot] : job.p0[slot];
+  float *out = which ? job.p1n[slot] : job.p0n[slot];
   float x, y;
-  cam_undistort_f(cam, pts[2 * p], pts[2 * p + 1], x, y);
+  cam_undistort_f(which ? job.c1[slot] : job.c0[slot], pts[2 * p], pts[2 * p + 1], x, y);
   out[2 * p] = x;
   out[2 * p + 1] = y;
 }
@@ -867,12 +878,16 @@ __device__ __forceinline__ bool epipolar_inlier(const double *f, float x0, float
 
 // one wavefront per hypothesis: every lane solves the (tiny) 7-point system redundantly, so the
 // model is wave-uniform, then the lanes split the inlier count over the points
-__global__ void __launch_bounds__(256) k_ransac_hyp(const float *__restrict__ p0n, const float *__restrict__ p1n, int n,
-                                                    const int *__restrict__ subsets, int max_iters, float t,
-                                                    double *__restrict__ Fout, int *__restrict__ nmodels,
-                                                    int *__restrict__ good) {
+__global__ void __launch_bounds__(256) k_ransac_hyp(RansacSlots job, int max_iters) {
+  const int slot = blockIdx.y;
+  const float *__restrict__ p0n = job.p0n[slot], *__restrict__ p1n = job.p1n[slot];
+  const int n = job.n[slot];
+  const int *__restrict__ subsets = job.sub[slot];
+  const float t = job.t[slot];
+  double *__restrict__ Fout = job.F[slot];
+  int *__restrict__ nmodels = job.nm[slot], *__restrict__ good = job.good[slot];
   const int it = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-  if (it >= max_iters) return;
+  if (it >= max_iters || n < 7) return;
   double x0[7], y0[7], x1[7], y1[7];
   for (int i = 0; i < 7; i++) {
     int k = subsets[it * 7 + i];
@@ -908,10 +923,19 @@ __device__ int ransac_update_iters_d(double p, double ep, int model_points, int 
 }
 
 // sequential adaptive scan (RANSACPointSetRegistrator::run) on thread 0, then the winner's mask
-__global__ void __launch_bounds__(256) k_ransac_select(const float *__restrict__ p0n, const float *__restrict__ p1n, int n,
-                                                       int max_iters, float t, double conf,
-                                                       const double *__restrict__ Fs, const int *__restrict__ nmodels,
-                                                       const int *__restrict__ good, uint8_t *__restrict__ mask) {
+__global__ void __launch_bounds__(256) k_ransac_select(RansacSlots job, int max_iters, double conf) {
+  const int slot = blockIdx.y;
+  const float *__restrict__ p0n = job.p0n[slot], *__restrict__ p1n = job.p1n[slot];
+  const int n = job.n[slot];
+  const float t = job.t[slot];
+  const double *__restrict__ Fs = job.F[slot];
+  const int *__restrict__ nmodels = job.nm[slot], *__restrict__ good = job.good[slot];
+  uint8_t *__restrict__ mask = job.mask[slot];
+  if (n <= 0) return;
+  if (n < 7) {  // findFundamentalMat needs 7 points: no inliers
+    for (int i = threadIdx.x; i < n; i += blockDim.x) mask[i] = 0;
+    return;
+  }
   __shared__ int best_it, best_m;
   if (threadIdx.x == 0) {
     int niters = max_iters, best = 0, bi = -1, bm = -1;
@@ -978,28 +1002,23 @@ void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, 
   hipLaunchKernelGGL(k_subpix, dim3(n), dim3(64), 0, s, img, w, h, pts, n, mask, win, max_iters, eps2);
 }
 
-void launch_lk(hipStream_t s, const DPyr &prev, const DPyr &next, const float *p0, float *p1, uint8_t *status, int n, int win,
-               int max_level, int max_iters, float eps, bool init_from_p0) {
-  if (n <= 0) return;
+void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,
+               bool init_from_p0) {
+  int nmax = 0;
+  for (int k = 0; k < nslot; k++) nmax = max(nmax, job.n[k]);
+  if (nmax <= 0) return;
   if (win > kLkMaxWin) throw std::runtime_error("LK window larger than the kernel supports");
-  hipLaunchKernelGGL(k_lk, dim3(n), dim3(64), 0, s, prev, next, p0, p1, status, n, win, max_level, max_iters, eps * eps,
+  hipLaunchKernelGGL(k_lk, dim3(nmax, nslot), dim3(64), 0, s, job, win, max_level, max_iters, eps * eps,
                      init_from_p0 ? 1 : 0);
 }
 
-void launch_ransac(hipStream_t s, const CamParams &c0, const CamParams &c1, const float *p0, const float *p1, int n,
-                   float *p0n, float *p1n, const int *subsets, int max_iters, double thr, double conf, double *Fs,
-                   int *nmodels, int *good, uint8_t *mask) {
-  if (n <= 0) return;
-  if (n < 7) {  // findFundamentalMat needs 7 points: no inliers
-    if (hipMemsetAsync(mask, 0, n, s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
-    return;
-  }
-  hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c0, p0, p0n, n);
-  hipLaunchKernelGGL(k_undistort, dim3((n + 127) / 128), dim3(128), 0, s, c1, p1, p1n, n);
-  float t = (float)(thr * thr);
-  hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 3) / 4), dim3(256), 0, s, p0n, p1n, n, subsets, max_iters, t, Fs,
-                     nmodels, good);
-  hipLaunchKernelGGL(k_ransac_select, dim3(1), dim3(256), 0, s, p0n, p1n, n, max_iters, t, conf, Fs, nmodels, good, mask);
+void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf) {
+  int nmax = 0;
+  for (int k = 0; k < nslot; k++) nmax = max(nmax, job.n[k]);
+  if (nmax <= 0) return;
+  hipLaunchKernelGGL(k_undistort, dim3((nmax + 127) / 128, 2 * nslot), dim3(128), 0, s, job);
+  hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 3) / 4, nslot), dim3(256), 0, s, job, max_iters);
+  hipLaunchKernelGGL(k_ransac_select, dim3(1, nslot), dim3(256), 0, s, job, max_iters, conf);
 }
 
 }  // namespace uvhp

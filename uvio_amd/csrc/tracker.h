@@ -57,8 +57,9 @@ class Tracker {
   };
   // one perform_matching in flight (slot 0 / 1)
   struct MatchJob {
-    int n = 0;
+    int n = 0, slot = 0, cam0 = 0, cam1 = 0;
     bool run = false;   // LK + RANSAC launched
+    DPyr prev{}, next{};
   };
   struct Bufs;
 
@@ -91,8 +92,9 @@ class Tracker {
   void griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &rects,
                const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
                std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st);
-  void match_launch(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
-                    MatchJob &j);
+  void match_prepare(int slot, const DPyr &p0, const DPyr &p1, int cam0, int cam1, const std::vector<KeyPt> &k0,
+                     MatchJob &j);
+  void match_run(MatchJob *jobs, int nj);
   void match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out);
 };
 
