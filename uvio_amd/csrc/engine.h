@@ -101,6 +101,7 @@ struct DeviceBufs {
   char *stg_h = nullptr, *stg_d = nullptr;
   size_t stg_cap = 0, stg_used = 0, stg_flushed = 0;
   double *dxneg = nullptr;  // [negative-diagonal count (8 B) | dx (ldp)]: one readback per update
+  int *acc = nullptr;       // accepted features of the last update batch (gates its P update)
 };
 
 class Engine {
@@ -184,12 +185,15 @@ class Engine {
   VarP clone_imu_pose(const double *dnc, bool do_dt);
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
-  void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2);
+  void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
+                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr);
   // hidx_dev: the batch's column map already on the device (staged), or nullptr to stage `hidx`;
   // pre_apply runs after the readback, before dx is applied (initialize_invertible's landmark step)
+  // gate (device count, may be null): the P update is skipped on the device when it is 0; after the
+  // readback `apply` decides whether dx goes to the host mean (true when absent)
   void ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx, const double *resdev,
                        int res_stride, double sigma2, const int *hidx_dev = nullptr,
-                       const std::function<void()> &pre_apply = nullptr);
+                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr);
   void apply_dx(const double *dx);
   // staging (see DeviceBufs): returns the device address the table will have after stage_flush()
   void *stage_bytes(const void *src, size_t bytes);
@@ -244,12 +248,16 @@ class Engine {
     std::vector<DCam> cams;
     std::vector<int> hidx;     // canonical column -> covariance id
     const int *hidx_dev = nullptr;  // its staged device copy
+    bool finished = false;          // per-feature results read back (finish_batch)
     std::vector<FeatP> fptrs;
     int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;
     std::map<double, int> slot_of_time;
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);
-  int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool compress, std::vector<DFeatOut> &outs);
+  // wait = false: only enqueue (kernels + result readback); the caller's next device sync completes it and
+  // finish_batch then fills outs
+  int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs);
+  void finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs);
 };
 
 }  // namespace uvhp

@@ -215,7 +215,7 @@ Engine::~Engine() {
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.fout, d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
@@ -285,6 +285,7 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   dalloc(&d_.dxneg, cap + 2);
+  dalloc(&d_.acc, 4);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
@@ -422,9 +423,9 @@ void Engine::apply_dx(const double *dx) {
 // EKF update of P on the device with rows H (r x n, ld) / residual; dx applied to the host mean
 void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx,
                              const double *resdev, int res_stride, double sigma2, const int *hidx_dev,
-                             const std::function<void()> &pre_apply) {
+                             const std::function<bool()> &apply, const int *gate) {
   if (r <= 0) {
-    if (pre_apply) pre_apply();
+    if (apply) apply();
     return;
   }
   if (r > kMaxEkfRows) throw HpError(UVIO_HP_E_CAPACITY, "direct EKF update with more than 256 rows");
@@ -432,19 +433,21 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
     hidx_dev = stage(hidx.data(), (size_t)n);
     stage_flush();
   }
+  d_.ekf.gate = gate;
   launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
   read_dx("EKFUpdate");
-  if (pre_apply) pre_apply();
-  apply_dx(d_.dx_host);
+  if (!apply || apply()) apply_dx(d_.dx_host);
 }
 
 // EKF update from the Gram partials of a stacked batch (compressed path, m > n)
-void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2) {
+void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
+                             const std::function<bool()> &apply, const int *gate) {
   const int *dh = stage(hidx.data(), (size_t)n);
   stage_flush();
+  d_.ekf.gate = gate;
   launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
   read_dx("EKFUpdate");
-  apply_dx(d_.dx_host);
+  if (!apply || apply()) apply_dx(d_.dx_host);
 }
 
 // StateHelper::set_initial_covariance (StateHelper.cpp:199-223).  Start-up only (initialize_with_gt,

@@ -550,7 +550,7 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
 
 // Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
 // Returns the number of stacked rows written to H_all.
-int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool, std::vector<DFeatOut> &outs) {
+int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs) {
   int nf = (int)b.feats.size();
   if (nf == 0) return 0;
   if (nf > d_.max_feat || (int)b.meas.size() > d_.max_meas_total || (int)b.vars.size() > d_.max_vars_total ||
@@ -612,26 +612,13 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
       max_rows_f = std::max(max_rows_f, rows_out - (mode >= 2 ? 3 : 0));
     }
     launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout,
-                      max_rows_f);
+                      max_rows_f, d_.acc);
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
+  if (!wait && !tsdump && !mdump) return b.rows;  // the caller's next sync completes the batch (finish_batch)
   dev_sync();
-  outs.assign(d_.fout_host, d_.fout_host + nf);
-  if (o_.record_timing) {
-    float ms = 0.f;
-    HP_HIP(hipEventElapsedTime(&ms, d_.ev0, d_.ev1));
-    timing_.k_feat_launches += 1;
-    timing_.k_feat_s += 1e-3 * ms;
-    // algorithmic FP64 FLOPs (SURVEY.md §8(d) F_feat) of the features that reached the projection
-    for (int i = 0; i < nf; i++) {
-      if (outs[i].status == 1 || outs[i].status == 2) continue;
-      double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
-      double r = (mode == 1) ? rows : rows - 3.0;
-      double refl = (mode == 1) ? 0.0 : 12.0 * rows * (nfc + 4.0);
-      timing_.k_feat_flops += refl + 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
-    }
-  }
+  finish_batch(b, mode, outs);
   if (tsdump) {
     std::vector<long long> h(16 * (size_t)nf);
     HP_HIP(hipMemcpy(h.data(), bp.dbg_ts, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
@@ -659,8 +646,30 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     }
     std::fclose(fp);
   }
-  (void)mode;
   return b.rows;
+}
+
+// per-feature results of a batch whose readback has completed (after a device sync), plus the feature
+// group's event timing
+void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
+  const int nf = (int)b.feats.size();
+  outs.assign(d_.fout_host, d_.fout_host + nf);
+  if (b.finished) return;
+  b.finished = true;
+  if (o_.record_timing) {
+    float ms = 0.f;
+    HP_HIP(hipEventElapsedTime(&ms, d_.ev0, d_.ev1));
+    timing_.k_feat_launches += 1;
+    timing_.k_feat_s += 1e-3 * ms;
+    // algorithmic FP64 FLOPs (SURVEY.md §8(d) F_feat) of the features that reached the projection
+    for (int i = 0; i < nf; i++) {
+      if (outs[i].status == 1 || outs[i].status == 2) continue;
+      double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
+      double r = (mode == 1) ? rows : rows - 3.0;
+      double refl = (mode == 1) ? 0.0 : 12.0 * rows * (nfc + 4.0);
+      timing_.k_feat_flops += refl + 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
+    }
+  }
 }
 
 // UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295)
@@ -686,45 +695,56 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   for (auto &f : fv)
     add_feature(this, f, 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf, o_, b.cams, b.slot_of_time, b.clones,
                 b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+  // The update is enqueued right behind the feature group: rejected features already have zero rows in
+  // H_all and the device skips the P update when no feature was accepted (d_.acc), so the host reads the
+  // per-feature results with the update's dx instead of waiting for them in between.
   std::vector<DFeatOut> outs;
-  int m = run_batch(b, 0, o_.msckf_sigma_pix * o_.msckf_sigma_pix, o_.msckf_chi2_multipler, true, outs);
-  int acc = 0, acc_rows = 0;
-  for (size_t i = 0; i < outs.size(); i++) {
-    last_msckf_.push_back(FeatDebug{fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
-                                    outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
-    fv[i]->to_delete = true;
-    for (int k = 0; k < 3; k++) fv[i]->p_FinG[k] = outs[i].p_FinG[k], fv[i]->p_FinA[k] = outs[i].p_FinA[k];
-    if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
-  }
-  timing_.msckf_rows = acc_rows;
-  timing_.msckf_cols = b.n_canon;
-  if (const char *dump = std::getenv("UVIO_HP_DUMP")) {  // debug: projected rows per feature
-    int nc = b.n_canon + 1;
-    std::vector<double> Hh((size_t)std::max(m, 1) * nc);
-    if (m > 0)
-      HP_HIP(hipMemcpy2D(Hh.data(), sizeof(double) * nc, d_.H, sizeof(double) * d_.ldh, sizeof(double) * nc, m,
-                         hipMemcpyDeviceToHost));
-    FILE *fp = std::fopen(dump, "ab");
+  const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
+  const int m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
+  const int n = b.n_canon, ncol = n + 1;
+  auto results = [&]() {
+    finish_batch(b, 0, outs);
+    int acc = 0, acc_rows = 0;
     for (size_t i = 0; i < outs.size(); i++) {
-      if (outs[i].status != 0) continue;
-      std::vector<double> hdr = {(double)fv[i]->featid, (double)outs[i].rows, (double)b.n_canon};
-      for (int j = 0; j < b.n_canon; j++) hdr.push_back(b.hidx[j]);
-      std::fwrite(hdr.data(), sizeof(double), hdr.size(), fp);
-      std::fwrite(Hh.data() + (size_t)b.feats[i].row_off * nc, sizeof(double), (size_t)outs[i].rows * nc, fp);
+      last_msckf_.push_back(FeatDebug{fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
+                                      outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+      fv[i]->to_delete = true;
+      for (int k = 0; k < 3; k++) fv[i]->p_FinG[k] = outs[i].p_FinG[k], fv[i]->p_FinA[k] = outs[i].p_FinA[k];
+      if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
     }
-    std::fclose(fp);
+    timing_.msckf_rows = acc_rows;
+    timing_.msckf_cols = b.n_canon;
+    if (const char *dump = std::getenv("UVIO_HP_DUMP")) {  // debug: projected rows per feature
+      int nc = b.n_canon + 1;
+      std::vector<double> Hh((size_t)std::max(m, 1) * nc);
+      if (m > 0)
+        HP_HIP(hipMemcpy2D(Hh.data(), sizeof(double) * nc, d_.H, sizeof(double) * d_.ldh, sizeof(double) * nc, m,
+                           hipMemcpyDeviceToHost));
+      FILE *fp = std::fopen(dump, "ab");
+      for (size_t i = 0; i < outs.size(); i++) {
+        if (outs[i].status != 0) continue;
+        std::vector<double> hdr = {(double)fv[i]->featid, (double)outs[i].rows, (double)b.n_canon};
+        for (int j = 0; j < b.n_canon; j++) hdr.push_back(b.hidx[j]);
+        std::fwrite(hdr.data(), sizeof(double), hdr.size(), fp);
+        std::fwrite(Hh.data() + (size_t)b.feats[i].row_off * nc, sizeof(double), (size_t)outs[i].rows * nc, fp);
+      }
+      std::fclose(fp);
+    }
+    return acc > 0;
+  };
+  if (m < 1) {
+    dev_sync();
+    results();
+    return 0;
   }
-  if (acc == 0 || m < 1) return 0;
-  int n = b.n_canon, ncol = n + 1;
-  double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
-  if (m > n) {
+  if (m > n || m > kMaxEkfRows) {
     // measurement compression (UpdaterHelper.cpp:456-487) + EKFUpdate on the compressed system, carried
     // out in information form on G = [H r]^T [H r] (see launch_ekf_info)
     int nch = 0;
     launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
-    ekf_update_info(nch, n, b.hidx, s2);
+    ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
-    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);
   }
   return 0;
 }
@@ -762,23 +782,32 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
     add_feature(this, fv[i], 1, lm->rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows,
                 lm.get(), lm_canon[i]);
   }
+  // enqueued behind the feature group as in msckf_update (rejected rows are zero, d_.acc gates P)
   std::vector<DFeatOut> outs;
-  double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
-  int m = run_batch(b, 1, s2, o_.slam_chi2_multipler, false, outs);
-  int acc = 0;
-  for (size_t i = 0; i < outs.size(); i++) {
-    fv[i]->to_delete = true;
-    if (outs[i].status == 3) slam_.at(fv[i]->featid)->fail_count++;
-    if (outs[i].status == 0) acc++;
+  const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+  const int m = run_batch(b, 1, s2, o_.slam_chi2_multipler, false, outs);
+  const int n = b.n_canon, ncol = n + 1;
+  auto results = [&]() {
+    finish_batch(b, 1, outs);
+    int acc = 0;
+    for (size_t i = 0; i < outs.size(); i++) {
+      fv[i]->to_delete = true;
+      if (outs[i].status == 3) slam_.at(fv[i]->featid)->fail_count++;
+      if (outs[i].status == 0) acc++;
+    }
+    return acc > 0;
+  };
+  if (m < 1) {
+    dev_sync();
+    results();
+    return 0;
   }
-  if (acc == 0 || m < 1) return 0;
-  int n = b.n_canon, ncol = n + 1;
-  if (m > n) {
+  if (m > n || m > kMaxEkfRows) {
     int nch = 0;
     launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
-    ekf_update_info(nch, n, b.hidx, s2);
+    ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
-    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2);
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);
   }
   return 0;
 }
@@ -810,7 +839,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     build_clone_cam_tables(b, false);
     for (auto &f : fv)
       add_feature(this, f, 2, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
-    run_batch(b, 2, s2, o_.slam_chi2_multipler, false, tri);
+    run_batch(b, 2, s2, o_.slam_chi2_multipler, true, tri);
   }
   for (size_t i = 0; i < fv.size(); i++) {
     FeatP &f = fv[i];
@@ -842,7 +871,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // triangulates the whole batch before the per-feature initialize loop
     for (int k = 0; k < 3; k++) b.feats[0].p_in[k] = f->p_FinA[k], b.feats[0].p_in_fej[k] = f->p_FinG[k];
     std::vector<DFeatOut> o1;
-    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1);
+    run_batch(b, 3, s2, o_.slam_chi2_multipler, true, o1);
     if (o1[0].status != 0) {
       f->to_delete = true;
       continue;
@@ -881,6 +910,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       for (int a = 0; a < 3; a++)
         dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
       lmv->update(dl);
+      return true;
     };
     lm->id = N_;
     vars_.push_back(lm);

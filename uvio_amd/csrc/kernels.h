@@ -111,7 +111,8 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
 // batched chi2 gate (kernels_chi2.hip): T = H_all P[hidx, hidx], per-feature S / LDL^T / chi2;
 // rejected MSCKF / SLAM features get zero rows.  T_all: like H_all.
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
-                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f);
+                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
+                       int *acc_count);
 size_t feature_lds_bytes(int max_meas, int max_nf);
 
 // Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->
@@ -130,6 +131,7 @@ struct EkfScratch {
   double *M, *W, *S, *y, *dx;
   int *neg;
   double *Dinv;  // 16x16 diagonal-block inverses of a triangular factor: (rmax / 16 + 1) * 256
+  const int *gate = nullptr;  // optional device count: when it is 0 the P update is skipped (no rows accepted)
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.

@@ -26,8 +26,9 @@ namespace uvhp {
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, int m, int n, int ldh,
                                                  const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
-                                                 double *__restrict__ T, int ldt) {
+                                                 double *__restrict__ T, int ldt, int *zero) {
   const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
+  if (zero && l == 0 && blockIdx.x == 0 && blockIdx.y == 0) *zero = 0;  // the batch's accepted-feature count
   const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
   const int arow = i0 + r16, bcol = j0 + r16;
   const double *Hr = H + (size_t)min(arow, m - 1) * ldh;
@@ -61,7 +62,7 @@ size_t chi2_lds_bytes(int max_rows_f, int n) {
 // chi2(dof = all rows), StateHelper.cpp:463-468).
 __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
                                               const double *__restrict__ T_all, const double *__restrict__ chi2_table,
-                                              DFeatOut *__restrict__ out, int use_lds) {
+                                              DFeatOut *__restrict__ out, int use_lds, int *acc_count) {
   extern __shared__ double lds[];
   __shared__ double red[256];
   __shared__ int st;
@@ -78,7 +79,10 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   const int R = o.rows - c0;
   const int tid = threadIdx.x;
   if (R <= 0) {
-    if (tid == 0) out[f].chi2 = 0.0;
+    if (tid == 0) {
+      out[f].chi2 = 0.0;
+      if (acc_count) atomicAdd(acc_count, 1);
+    }
     return;
   }
   const double *Hg = H_all + (size_t)(F.row_off + c0) * ldh;
@@ -161,6 +165,8 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
     if (reject) {
       out[f].status = 3;
       out[f].rows = 0;
+    } else if (acc_count) {
+      atomicAdd(acc_count, 1);
     }
     st = reject;
   }
@@ -177,11 +183,12 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
 }
 
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
-                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f) {
+                       double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
+                       int *acc_count) {
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
   hipLaunchKernelGGL(k_gemm_HPg, dim3((n + 15) / 16, (m + 15) / 16), dim3(64), 0, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx,
-                     T_all, bp.ldh);
+                     T_all, bp.ldh, acc_count);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);
@@ -189,7 +196,8 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
   if (bytes > 64 * 1024 && (int)bytes > granted)
     throw std::runtime_error("k_chi2 needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
-  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds);
+  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
+                     acc_count);
 }
 
 }  // namespace uvhp

@@ -427,7 +427,9 @@ void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, in
 
 // P[i][j] -= sum_k W[i][k] W[j][k] for j >= i, mirrored to (j,i); dx = W y; negative-diagonal count
 __global__ void __launch_bounds__(256) k_ekf_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ W,
-                                               int r, const double *__restrict__ y, double *__restrict__ dx, int *neg) {
+                                               int r, const double *__restrict__ y, double *__restrict__ dx, int *neg,
+                                               const int *gate) {
+  if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
   __shared__ double Wi[16][17];
   __shared__ double Wj[16][17];
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
@@ -482,7 +484,7 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
                      use_lds);
   launch_trsm_lt(s, sc.M, r, nullptr, N, r, Lf, r, sc.Dinv, sc.W);  // W = M L^-T
   int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg);
+  hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg, sc.gate);
 }
 
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
@@ -607,7 +609,8 @@ size_t info_chol_lds_bytes(int nrows, int n) { return dense_lds_bytes(nrows, n) 
 // negative-diagonal count.   (P+ = P - V (I - s2 Z^-1) V^T, see launch_ekf_info)
 __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ V,
                                                 const double *__restrict__ X, int n, double s2,
-                                                const double *__restrict__ w, double *__restrict__ dx, int *neg) {
+                                                const double *__restrict__ w, double *__restrict__ dx, int *neg, const int *gate) {
+  if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
   __shared__ double Vi[16][17], Vj[16][17], Xi[16][17], Xj[16][17];
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   int bi = blockIdx.y, bj = blockIdx.x;
@@ -674,7 +677,8 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
   launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);     // V = P[:,I] L^-T
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
   int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg);
+  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg,
+                     sc.gate);
 }
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
