@@ -15,7 +15,7 @@ Frames/s is whole-job throughput: every rank runs its own estimator on its own s
 replicas, weak scaling), value = total frames / max-over-ranks wall time.
 
 roofline: the feature launch group (k_feature: triangulation + LM, Jacobians, left-nullspace
-reflections; then k_gather_can + k_gemm_HP + k_chi2: the batched chi2 gate), timed with HIP events on
+reflections; then k_gemm_HPg + k_chi2: the batched chi2 gate, both on the FP64 matrix cores), timed with HIP events on
 the library's stream around the group; achieved = the algorithmic FP64 FLOPs of the group
 (SURVEY.md §8(d) F_feat formula on the actual feature shapes) / event time.  cpu_baseline: the oracle/
 CPU restatement (single-threaded, as the reference estimator is) on a bounded sample of the same
@@ -85,6 +85,19 @@ class Driver:
                 else:
                     mgr.feed_measurement_camera(t, cams, self.frames[i])
                 return t
+
+
+PMC_FILE = "profiles/r01_pmc_traffic.json"
+
+
+def pmc_traffic():
+    """HBM bytes per feature-group launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, tools/pmc_summary.py) of this workload, or None if absent."""
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            return json.load(f)["feature_group_traffic"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def max_over_ranks(x, device="cuda"):
@@ -188,10 +201,11 @@ def main():
                        "mean_msckf_rows": acc["rows"] / args.steps, "H_cols": acc["cols"],
                        "state_dim": acc["cov_dim"], "parallelism": "replicas%d" % world},
             "ate_rmse_m": ate,
-            "roofline": {"kernel": "feature linearize + chi2 launch group (k_feature, k_gather_can, k_gemm_HP, k_chi2)",
+            "roofline": {"kernel": "feature linearize + chi2 launch group (k_feature, k_gemm_HPg, k_chi2)",
                          "bound": "mfma",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(),
+                         "traffic_source": PMC_FILE if pmc_traffic() is not None else None,
                          "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops_per_launch},
             "cpu_baseline": cpu,
         }
