@@ -11,6 +11,14 @@ FAST grid detection, cornerSubPix, stereo + temporal pyramidal LK, RANSAC) -> pr
 MSCKF update -> SLAM update / delayed init -> marginalize.  The tracker keeps 200 features per
 camera (init_max_features 400: initialize_with_gt keeps the initializer's count, VioManager.cpp:131).
 
+Other workloads (--workload, SURVEY.md §8 cfg 3-5; parity-test cases and stress lines, not the headline):
+  cfg3  TUM-VI room1-shaped stereo fisheye 512x512 images (configs/tum_vi), 20 clones, 400 tracks per
+        camera, <= 400 MSCKF + 50 SLAM (LDS-tiled KLT stress)
+  cfg4  UZH-FPV outdoor_45-shaped stereo fisheye rig (configs/uzhfpv_outdoor_45), 25 clones, 800 MSCKF
+        features per update, each seen in all 26 clones x 2 cameras (TrackSIM feed: the backend stress case)
+  cfg5  rpng_sim 4-camera rig + 6 UWB anchors (configs/rpng_sim_uwb), IMU intrinsics + g-sensitivity
+        calibrated, 30 clones, 1500 MSCKF features per update (each in one camera), UWB ranges at 10 Hz
+
 Frames/s is whole-job throughput: every rank runs its own estimator on its own stream (independent
 replicas, weak scaling), value = total frames / max-over-ranks wall time.
 
@@ -32,19 +40,51 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-EUROC = os.path.join(ROOT, "configs", "euroc_mav", "estimator_config.yaml")
+CONFIGS = os.path.join(ROOT, "configs")
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (vector = matrix on gfx950)
+
+# workload -> (config dir, camera input, option overrides, SimStream arguments, description)
+WORKLOADS = {
+    "cfg2": ("euroc_mav", "images",
+             dict(init_max_features=400, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
+                  dt_slam_delay=1.0),
+             dict(spawn=4),
+             "cfg2 EuRoC V1_02-shaped stereo 752x480 images, 11 clones, <=200 MSCKF + 50 SLAM"),
+    "cfg3": ("tum_vi", "images",
+             dict(max_clone_size=20, init_max_features=800, num_pts=400, max_msckf_in_update=400,
+                  max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
+             dict(spawn=4),
+             "cfg3 TUM-VI room1-shaped stereo fisheye 512x512 images, 20 clones, 400 tracks/cam, <=400 MSCKF + 50 SLAM"),
+    "cfg4": ("uzhfpv_outdoor_45", "tracks",
+             dict(max_clone_size=25, max_msckf_in_update=800, max_slam_features=50, max_slam_in_update=25,
+                  dt_slam_delay=1.0),
+             dict(spawn=800, frac_lost=0.0, frac_long=0.02),
+             "cfg4 UZH-FPV outdoor_45-shaped stereo fisheye 640x480 tracks, 25 clones, 800 MSCKF feats x 52 meas"),
+    "cfg5": ("rpng_sim_uwb", "tracks",
+             dict(max_clone_size=30, max_msckf_in_update=1500, max_slam_features=50, max_slam_in_update=25,
+                  dt_slam_delay=1.0),
+             dict(spawn=1500, frac_lost=0.0, frac_long=0.02, uwb=True),
+             "cfg5 rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
+}
+
+
+def workload_options(U, name):
+    cfg, _, ov, _, _ = WORKLOADS[name]
+    return U.load_options(os.path.join(CONFIGS, cfg, "estimator_config.yaml"), record_timing=1, **ov)
 
 
 def cfg2_options(U):
-    return U.load_options(EUROC, init_max_features=400, max_msckf_in_update=200, max_slam_features=50,
-                          max_slam_in_update=25, dt_slam_delay=1.0, record_timing=1)
+    return workload_options(U, "cfg2")
 
 
-def make_stream(opts, n_frames, seed):
+def make_stream(opts, n_frames, seed, workload="cfg2"):
     from uvio_amd.sim import SimStream
-    # the simulated tracks are not used (the images are); keep their generation small
-    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, spawn=4)
+    kw = dict(WORKLOADS[workload][3])
+    anchors = None
+    if kw.pop("uwb", False):
+        anchors = [opts.anchors[i] for i in range(opts.n_anchors)]
+    # image workloads: the simulated tracks are not used (the images are); keep their generation small
+    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, anchors=anchors, **kw)
 
 
 def render_frames(sim, n_frames, device):
@@ -63,7 +103,11 @@ class Driver:
     the list of device images (feed_measurement_camera_device) or of host arrays (feed_measurement_camera)."""
 
     def __init__(self, sim, mgr, frames, device_imgs=True):
+        """frames=None: the stream's simulated tracks (TrackSIM feed), packed per frame beforehand."""
         self.sim, self.mgr, self.frames, self.device_imgs = sim, mgr, frames, device_imgs
+        if frames is None:
+            from uvio_amd.manager import pack_sim_frame
+            self.packed = [pack_sim_frame(f) for f in sim.frames]
         self.ev = [e for e in sim.events() if e[1] >= sim.t0 - 0.4]
         self.k = 0
         mgr.initialize_with_gt(sim.gt_state(sim.t0))
@@ -80,24 +124,27 @@ class Driver:
                 mgr.feed_measurement_uwb(t, sim.uwb[i][1], sim.uwb[i][2])
             elif t > sim.t0:
                 cams = list(range(sim.K))
-                if self.device_imgs:
+                if self.frames is None:
+                    mgr.feed_measurement_simulation_packed(t, cams, *self.packed[i])
+                elif self.device_imgs:
                     mgr.feed_measurement_camera_device(t, cams, self.frames[i])
                 else:
                     mgr.feed_measurement_camera(t, cams, self.frames[i])
                 return t
 
 
-PMC_FILE = "profiles/r01_pmc_traffic.json"
+PMC_FILES = {"cfg2": "profiles/r01_pmc_traffic.json"}
 
 
-def pmc_traffic():
-    """HBM bytes per feature-group launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE, tools/pmc_summary.py) of this workload, or None if absent."""
+def pmc_traffic(workload):
+    """(HBM bytes per feature-group launch, source) from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, tools/pmc_summary.py) of this workload, or (None, None) if absent."""
+    path = PMC_FILES.get(workload, "profiles/r01_pmc_traffic_%s.json" % workload)
     try:
-        with open(os.path.join(ROOT, PMC_FILE)) as f:
-            return json.load(f)["feature_group_traffic"]
+        with open(os.path.join(ROOT, path)) as f:
+            return json.load(f)["feature_group_traffic"], path
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def max_over_ranks(x, device="cuda"):
@@ -116,8 +163,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--cpu-frames", type=int, default=120, help="timed oracle frames for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=None,
+                    help="timed oracle frames for cpu_baseline (0 = skip; default: ~10-30 s of CPU work per workload)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
     args = ap.parse_args()
+    if args.cpu_frames is None:
+        args.cpu_frames = {"cfg2": 120, "cfg3": 60, "cfg4": 10, "cfg5": 6}[args.workload]
 
     import torch
     import torch.distributed as dist
@@ -129,10 +180,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import uvio_amd as U
 
-    opts = cfg2_options(U)
+    wl = args.workload
+    images = WORKLOADS[wl][1] == "images"
+    opts = workload_options(U, wl)
     n_frames = args.warmup + args.steps
-    sim = make_stream(opts, n_frames + 2, seed=5 + rank)
-    frames = render_frames(sim, n_frames + 2, torch.device("cuda", local))
+    sim = make_stream(opts, n_frames + 2, seed=5 + rank, workload=wl)
+    frames = render_frames(sim, n_frames + 2, torch.device("cuda", local)) if images else None
     mgr = U.VioManager(opts, device=local)
     drv = Driver(sim, mgr, frames)
     for _ in range(args.warmup):
@@ -173,10 +226,11 @@ def main():
         avg_s = acc["k_feat_s"] / launches
         flops_per_launch = acc["k_feat_flops"] / launches
         achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
-        ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras))
+        ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras)) if images else None
         cpu = None
         if args.cpu_frames > 0:
-            cpu = cpu_baseline(opts, args.warmup, args.cpu_frames, frames)
+            cpu = cpu_baseline(opts, wl, args.warmup, args.cpu_frames, frames)
+        traffic, traffic_src = pmc_traffic(wl)
         out = {
             "metric": "VIO frames/sec (track+propagate+update) at clones x feats",
             "value": value,
@@ -189,10 +243,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic EuRoC-shaped stream (uvio_amd/sim.py, seed 5+rank) with ray-cast images "
-                    "(uvio_amd/render.py) resident in HBM, TrackKLT front-end",
-            "config": {"workload": "cfg2 EuRoC V1_02-shaped stereo 752x480 images, 11 clones, <=200 MSCKF + 50 SLAM",
-                       "track_features_per_cam": int(opts.init_max_features) // int(opts.num_cameras),
+            "data": ("synthetic %s-shaped stream (uvio_amd/sim.py, seed 5+rank) with ray-cast images "
+                     "(uvio_amd/render.py) resident in HBM, TrackKLT front-end" % WORKLOADS[wl][0]) if images else
+                    ("synthetic %s-shaped stream (uvio_amd/sim.py, seed 5+rank): simulated feature tracks "
+                     "(TrackSIM feed, VioManager::feed_measurement_simulation)%s" %
+                     (WORKLOADS[wl][0], " + UWB ranges" if opts.use_uwb else "")),
+            "config": {"workload": WORKLOADS[wl][4],
+                       "track_features_per_cam": int(opts.init_max_features) // int(opts.num_cameras) if images else None,
                        "tracks_last_frame": ntr, "mean_tracking_ms": 1e3 * acc["tracking_s"] / args.steps,
                        "clones": int(opts.max_clone_size), "cameras": int(opts.num_cameras),
                        "max_msckf_in_update": int(opts.max_msckf_in_update),
@@ -204,8 +261,7 @@ def main():
             "roofline": {"kernel": "feature linearize + chi2 launch group (k_feature, k_gemm_HPg, k_chi2)",
                          "bound": "mfma",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(),
-                         "traffic_source": PMC_FILE if pmc_traffic() is not None else None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops_per_launch},
             "cpu_baseline": cpu,
         }
@@ -214,12 +270,15 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(opts, warmup, frames, dev_frames):
-    """oracle/ (the CPU restatement) on the same image stream (rank 0's), one thread, bounded sample."""
+def cpu_baseline(opts, wl, warmup, frames, dev_frames):
+    """oracle/ (the CPU restatement) on the same stream (rank 0's), one thread, bounded sample."""
     from oracle import oracle as O
-    frames = max(1, min(frames, len(dev_frames) - warmup - 2))
-    sim = make_stream(opts, warmup + frames + 2, seed=5)
-    host = [[im.cpu().numpy() for im in fr] for fr in dev_frames[:warmup + frames + 2]]
+    sim = make_stream(opts, warmup + frames + 2, seed=5, workload=wl)
+    if dev_frames is not None:
+        frames = max(1, min(frames, len(dev_frames) - warmup - 2))
+        host = [[im.cpu().numpy() for im in fr] for fr in dev_frames[:warmup + frames + 2]]
+    else:
+        host = None
     mgr = O.OracleManager(opts)
     drv = Driver(sim, mgr, host, device_imgs=False)
     for _ in range(warmup):
@@ -229,8 +288,8 @@ def cpu_baseline(opts, warmup, frames, dev_frames):
         drv.step()
     dt = time.perf_counter() - t0
     return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "%d frames of the cfg2 image stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
-                      (frames, warmup)}
+            "sample": "%d frames of the %s %s stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
+                      (frames, wl, "image" if dev_frames is not None else "track", warmup)}
 
 
 if __name__ == "__main__":

@@ -35,6 +35,7 @@ extern "C" {
 #define UVIO_HP_E_CONFIG (-5)   /* config file missing / unparsable */
 #define UVIO_HP_E_ORDER (-6)    /* measurement out of order (ref: std::exit in Propagator) */
 #define UVIO_HP_E_CAPACITY (-7) /* a compile-time capacity was exceeded */
+#define UVIO_HP_E_INTERNAL (-8) /* unexpected host-side error (a bug): the message names the routine */
 
 #define UVIO_HP_MAX_CAMS 4
 #define UVIO_HP_MAX_ANCHORS 16

@@ -91,3 +91,42 @@ def test_product_fails_loudly_without_gpu(euroc_yaml):
     P = [[1.0]]
     with pytest.raises(RuntimeError, match="E_DEVICE"):
         U.ekf_update(P, [0], [[1.0]], [0.5], 1.0)
+
+
+def _cfg(name):
+    return os.path.join(ROOT, "configs", name, "estimator_config.yaml")
+
+
+def test_options_load_tum_vi_t_cam_imu():
+    """TUM-VI's kalibr chain gives T_cam_imu = [R_ItoC | p_IinC]; the parser falls back to it when T_imu_cam
+    is absent and inverts it (YamlParser::parse(Matrix4d), opencv_yaml_parse.h:487-530)."""
+    import numpy as np
+    import uvio_amd as U
+    from uvio_amd.sim import quat_2_rot
+    o = U.load_options(_cfg("tum_vi"))
+    assert o.num_cameras == 2 and o.use_stereo == 1 and o.min_px_dist == 15
+    c0 = o.cams[0]
+    assert c0.model == 1 and (c0.width, c0.height) == (512, 512)
+    T = np.array([[-0.9995250378696743, 0.029615343885863205, -0.008522328211654736, 0.04727988224914392],
+                  [0.0075019185074052044, -0.03439736061393144, -0.9993800792498829, -0.047443232143367084],
+                  [-0.02989013031643309, -0.998969345370175, 0.03415885127385616, -0.0681999605066297]])
+    assert np.allclose(quat_2_rot(np.array(c0.q_ItoC[:])), T[:, :3], atol=1e-9)
+    assert np.allclose(np.array(c0.p_IinC[:]), T[:, 3], atol=1e-9)
+    assert abs(o.gravity_mag - 9.80766) < 1e-12 and abs(o.sigma_a - 0.0028) < 1e-12
+
+
+def test_options_load_uzhfpv_and_rpng_sim_uwb():
+    import uvio_amd as U
+    o = U.load_options(_cfg("uzhfpv_outdoor_45"))
+    assert o.do_calib_camera_pose == 0 and o.do_calib_camera_intrinsics == 1
+    assert o.cams[1].model == 1 and (o.cams[1].width, o.cams[1].height) == (640, 480)
+    assert abs(o.msckf_sigma_pix - 1.5) < 1e-12 and o.fast_threshold == 50 and o.track_frequency == 31.0
+    assert abs(o.calib_camimu_dt - (-0.008637511810764048)) < 1e-15
+    o = U.load_options(_cfg("rpng_sim_uwb"))
+    assert o.num_cameras == 4 and o.use_stereo == 0
+    assert o.do_calib_imu_intrinsics == 1 and o.do_calib_imu_g_sensitivity == 1
+    assert o.use_uwb == 1 and o.n_anchors == 6 and o.n_anchors_to_fix == 2
+    assert [o.anchors[i].fix for i in range(6)] == [1, 1, 0, 0, 0, 0]
+    assert list(o.anchors[4].p_AinG) == [0.0, 7.0, 1.5]
+    assert list(o.p_IinU) == [-0.01, 0.01, 0.05]  # uwb_extrinsics p_UinI -> p_IinU = -p_UinI
+    assert abs(o.cams[2].p_IinC[0] - o.cams[0].p_IinC[0]) > 0.1  # the second pair is shifted

@@ -13,9 +13,9 @@ MAX_CAMS = 4
 MAX_ANCHORS = 16
 
 OK = 0
-E_ARG, E_STATE, E_DEVICE, E_NUMERIC, E_CONFIG, E_ORDER, E_CAPACITY = -1, -2, -3, -4, -5, -6, -7
+E_ARG, E_STATE, E_DEVICE, E_NUMERIC, E_CONFIG, E_ORDER, E_CAPACITY, E_INTERNAL = -1, -2, -3, -4, -5, -6, -7, -8
 ERRNAMES = {0: "OK", -1: "E_ARG", -2: "E_STATE", -3: "E_DEVICE", -4: "E_NUMERIC", -5: "E_CONFIG", -6: "E_ORDER",
-            -7: "E_CAPACITY"}
+            -7: "E_CAPACITY", -8: "E_INTERNAL"}
 
 
 class Camera(C.Structure):

@@ -12,6 +12,14 @@ struct uvio_hp {
   std::string err;
 };
 
+// an exception that is not an HpError is a host-side logic error (e.g. std::out_of_range from a map
+// lookup): reported as UVIO_HP_E_INTERNAL with the reference routine the engine was in
+static std::string internal_error(const uvio_hp *h, const std::exception &ex) {
+  std::string m = std::string("internal error: ") + ex.what();
+  if (h && h->e && h->e->stage()[0]) m += std::string(" (in ") + h->e->stage() + ")";
+  return m;
+}
+
 #define HP_GUARD(h, body)                                    \
   try {                                                      \
     body                                                     \
@@ -19,8 +27,8 @@ struct uvio_hp {
     if (h) (h)->err = ex.what();                             \
     return ex.code;                                          \
   } catch (const std::exception &ex) {                       \
-    if (h) (h)->err = ex.what();                             \
-    return UVIO_HP_E_DEVICE;                                 \
+    if (h) (h)->err = internal_error(h, ex);                 \
+    return UVIO_HP_E_INTERNAL;                               \
   }
 
 extern "C" {

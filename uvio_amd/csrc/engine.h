@@ -173,6 +173,11 @@ class Engine {
     double chi2;
   };
   std::vector<FeatDebug> last_msckf_;
+  // the reference routine the host was in when the last call failed (error messages)
+  const char *stage() const { return stage_; }
+
+ private:
+  const char *stage_ = "";
 
  private:
 

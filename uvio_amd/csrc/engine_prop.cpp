@@ -629,6 +629,7 @@ std::vector<int> Engine::phi_order_ids(int *n) {
 }
 
 int Engine::propagate_and_clone(double timestamp) {
+  stage_ = "Propagator::propagate_and_clone";
   if (timestamp_ >= timestamp) return UVIO_HP_E_ORDER;
   if (!have_last_prop_time_offset_) {
     last_prop_time_offset_ = calib_dt_->val[0];
@@ -656,6 +657,7 @@ int Engine::propagate_and_clone(double timestamp) {
 // UVioPropagator::propagate (UVioPropagator.cpp:27-115); quirks kept: time1 has no cam-imu offset and
 // last_prop_time_offset is not updated.
 int Engine::propagate_uwb(double timestamp) {
+  stage_ = "UVioPropagator::propagate";
   if (timestamp_ >= timestamp) return UVIO_HP_E_ORDER;
   std::vector<ImuSample> prop = select_imu_readings(timestamp_ + last_prop_time_offset_, timestamp);
   int n;

@@ -124,6 +124,7 @@ void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float 
 
 // UVioManager.cpp:61-79
 int Engine::feed_uwb(double t, int n, const uint64_t *ids, const double *ranges) {
+  stage_ = "feed_uwb";
   if (!(is_initialized_ && anchors_initialized_ && distance_ > o_.min_dist_to_use_uwb)) return 0;
   if (timestamp_ >= t) return 0;
   auto &m = past_uwb_[t];
@@ -159,6 +160,7 @@ int Engine::init_anchors(int n, const uvio_hp_anchor_t *a) {
 // VioManager.cpp:191-254 + TrackSIM.cpp:30-79 (+ the UVIO range loop of UVioManager.cpp:178-188)
 int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
                             const float *uv) {
+  stage_ = "feed_simulation";
   auto rT1 = clk::now();
   size_t k = 0;
   std::vector<int> camids;
@@ -223,6 +225,7 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
 
 // VioManager.cpp:323-651
 int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids) {
+  stage_ = "feature selection";
   auto rT2 = clk::now();
   if (timestamp_ > t) return UVIO_HP_E_ORDER;
   if (timestamp_ != t) {
@@ -382,6 +385,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
 
 // StateHelper::marginalize_slam (StateHelper.cpp:631-645)
 void Engine::marginalize_slam() {
+  stage_ = "marginalize_slam";
   for (auto it = slam_.begin(); it != slam_.end();) {
     if (it->second->should_marg && (int)it->first > 4 * o_.max_aruco_features) {
       marginalize(it->second);
@@ -394,6 +398,7 @@ void Engine::marginalize_slam() {
 
 // StateHelper::marginalize_old_clone (StateHelper.cpp:618-629)
 void Engine::marginalize_old_clone() {
+  stage_ = "marginalize_old_clone";
   if ((int)clones_.size() > o_.max_clone_size) {
     double mt = margtimestep();
     marginalize(clones_.at(mt));
@@ -472,7 +477,14 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
     anchor_time = landmark->anchor_time;
   }
   F.anchor_cam = (int)anchor_cam;
-  F.anchor_slot = slot_of_time.at(anchor_time);
+  const bool rel = (rep == 2 || rep == 3 || rep == 4 || rep == 5);
+  // a global landmark's anchor clone may have been marginalized (change_anchors only re-anchors relative
+  // representations, UpdaterSLAM.cpp:481-500) and get_feature_jacobian_full never reads it for a global
+  // representation (UpdaterHelper.cpp:226-262): slot 0 is a placeholder the kernel does not use
+  auto anc = slot_of_time.find(anchor_time);
+  if (anc == slot_of_time.end() && (rel || !landmark))
+    throw HpError(UVIO_HP_E_STATE, "feature anchor clone is not in the window");
+  F.anchor_slot = (anc == slot_of_time.end()) ? 0 : anc->second;
   int loc = 0;
   std::map<int, int> clone_loc;  // slot -> local col
   std::vector<int> ext_loc(UVIO_HP_MAX_CAMS, -1), intr_loc(UVIO_HP_MAX_CAMS, -1);
@@ -497,7 +509,6 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
       }
     }
   }
-  bool rel = (rep == 2 || rep == 3 || rep == 4 || rep == 5);
   if (rel) {
     if (!clone_loc.count(F.anchor_slot)) {
       clone_loc[F.anchor_slot] = loc;
@@ -674,6 +685,7 @@ void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
 
 // UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295)
 int Engine::msckf_update(std::vector<FeatP> &fv) {
+  stage_ = "UpdaterMSCKF::update";
   last_msckf_.clear();
   if (fv.empty()) return 0;
   std::vector<double> clonetimes;
@@ -751,6 +763,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
 
 // UpdaterSLAM::update (UpdaterSLAM.cpp:253-479)
 int Engine::slam_update(std::vector<FeatP> &fv) {
+  stage_ = "UpdaterSLAM::update";
   if (fv.empty()) return 0;
   std::vector<double> clonetimes;
   for (auto &c : clones_) clonetimes.push_back(c.first);
@@ -816,6 +829,7 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
 // Triangulation of the whole batch runs first (as in the reference); each accepted landmark then
 // initializes and updates the state before the next one is linearized.
 int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
+  stage_ = "UpdaterSLAM::delayed_init";
   if (fv.empty()) return 0;
   std::vector<double> clonetimes;
   for (auto &c : clones_) clonetimes.push_back(c.first);
@@ -931,6 +945,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
 
 // UpdaterSLAM::change_anchors / perform_anchor_change (UpdaterSLAM.cpp:481-647)
 int Engine::slam_change_anchors() {
+  stage_ = "UpdaterSLAM::change_anchors";
   if ((int)clones_.size() <= o_.max_clone_size) return 0;
   double mt = margtimestep();
   for (auto &kv : slam_) {
@@ -1087,6 +1102,7 @@ int Engine::slam_change_anchors() {
 // UpdaterUWB::update_single (UpdaterUWB.cpp:53-90) + UVioUpdaterHelper::get_uwb_jacobian_single
 // (UVioUpdaterHelper.cpp:147-241).  One row; chi2 gate on the device-computed innovation variance.
 int Engine::uwb_update_single(size_t anchor_id, double range) {
+  stage_ = "UpdaterUWB::update_single";
   auto it = anchors_.find(anchor_id);
   if (it == anchors_.end()) return 0;
   const VarP &an = it->second;
@@ -1138,6 +1154,7 @@ int Engine::uwb_update_single(size_t anchor_id, double range) {
   const double *dH = stage(H.data(), (size_t)n + 1);
   const int *dh = stage(hidx.data(), (size_t)n);
   stage_flush();
+  d_.ekf.gate = nullptr;  // a single range: no accepted-count gate (the host gates on chi2 below)
   launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, dH, n + 1, 1, n, dh, s2, d_.ekf);
   double Sval;
   HP_HIP(hipMemcpyAsync(&Sval, d_.ekf.S + 2, sizeof(double), hipMemcpyDeviceToHost, d_.stream));

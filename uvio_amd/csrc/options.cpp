@@ -460,7 +460,20 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
         c.height = (int)res[1];
       }
       std::vector<std::vector<double>> T;
-      if (cam.getmat({cn, "T_imu_cam"}, T) && T.size() >= 3) {
+      bool have_T = cam.getmat({cn, "T_imu_cam"}, T) && T.size() >= 3;
+      if (!have_T && cam.getmat({cn, "T_cam_imu"}, T) && T.size() >= 3) {
+        // YamlParser::parse(Matrix4d) (opencv_yaml_parse.h:487-530): T_imu_cam missing -> read T_cam_imu
+        // = [R_ItoC p_IinC] and return its inverse [R_ItoC^T, -R_ItoC^T p_IinC]
+        std::vector<std::vector<double>> Ti(4, std::vector<double>(4, 0.0));
+        for (int r = 0; r < 3; r++) {
+          for (int cc = 0; cc < 3; cc++) Ti[r][cc] = T[cc][r];
+          Ti[r][3] = -(T[0][r] * T[0][3] + T[1][r] * T[1][3] + T[2][r] * T[2][3]);
+        }
+        Ti[3][3] = 1.0;
+        T = Ti;
+        have_T = true;
+      }
+      if (have_T) {
         // T_imu_cam = [R_CtoI p_CinI]; q_ItoC = rot_2_quat(R_CtoI^T); p_IinC = -R_CtoI^T p_CinI
         double RT[9];
         for (int r = 0; r < 3; r++)

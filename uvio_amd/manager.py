@@ -32,6 +32,14 @@ def apply_overrides(opts, overrides):
     return opts
 
 
+def pack_sim_frame(feats):
+    """(counts, ids uint64[n], uv float32[n, 2]) of one TrackSIM frame, cameras concatenated."""
+    counts = [len(f[0]) for f in feats]
+    ids = np.ascontiguousarray(np.concatenate([np.asarray(f[0], dtype=np.uint64) for f in feats]))
+    uv = np.ascontiguousarray(np.concatenate([np.asarray(f[1], dtype=np.float32).reshape(-1, 2) for f in feats]))
+    return counts, ids, uv
+
+
 def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
@@ -92,11 +100,13 @@ class VioManager:
 
     def feed_measurement_simulation(self, t, camids, feats, allow_uninit=False):
         """feats[i] = (ids uint64[n], uv float32[n,2]) for camera camids[i] (TrackSIM input)."""
+        return self.feed_measurement_simulation_packed(t, camids, *pack_sim_frame(feats), allow_uninit=allow_uninit)
+
+    def feed_measurement_simulation_packed(self, t, camids, counts, ids, uv, allow_uninit=False):
+        """feed_measurement_simulation with the cameras' tracks already concatenated (pack_sim_frame)."""
         ncam = len(camids)
         cam = (C.c_int * ncam)(*camids)
-        cnt = (C.c_int * ncam)(*[len(f[0]) for f in feats])
-        ids = np.ascontiguousarray(np.concatenate([np.asarray(f[0], dtype=np.uint64) for f in feats]))
-        uv = np.ascontiguousarray(np.concatenate([np.asarray(f[1], dtype=np.float32).reshape(-1, 2) for f in feats]))
+        cnt = (C.c_int * ncam)(*[int(c) for c in counts])
         rc = self._call("feed_simulation", self._h, C.c_double(t), ncam, cam, cnt,
                         ids.ctypes.data_as(C.POINTER(C.c_uint64)), uv.ctypes.data_as(C.POINTER(C.c_float)))
         if rc == N.E_STATE and allow_uninit:
