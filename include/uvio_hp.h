@@ -205,6 +205,28 @@ int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap,
  * may be NULL, cap = pixels available */
 int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap);
 
+/* ---- feature-sharded MSCKF update across GPUs (BASELINE.json configs 4-5) ----
+ * One process per GPU, each with its own handle fed the same measurement stream (the filter state is
+ * replicated).  Inside UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295) the selected features are split into
+ * contiguous chunks balanced by stacked rows (uvio_hp_shard_partition); each rank triangulates, linearizes,
+ * nullspace-projects and chi2-gates its own chunk and forms its Gram block [H r]^T [H r]; the blocks are
+ * summed across ranks (ncclAllReduce on the library's stream, or a host callback), and every rank applies
+ * the same information-form update (the compressed update, UpdaterHelper.cpp:456-487 +
+ * StateHelper::EKFUpdate, depends on the stacked rows only through that sum).  Updates with fewer than
+ * min_features features run unsharded on every rank.  Every rank must make every feed call. */
+/* In-place sum of count doubles (host memory) over all ranks; returns 0 on success. */
+typedef int (*uvio_hp_allreduce_fn)(double *buf, size_t count, void *user);
+/* ncclGetUniqueId: rank 0 creates it, the caller distributes the 128 bytes to every rank */
+int uvio_hp_shard_unique_id(uint8_t id[128]);
+/* RCCL communicator over the ranks (ncclCommInitRank: collective, every rank calls it) */
+int uvio_hp_shard_init_rccl(uvio_hp_t *h, int rank, int world, const uint8_t id[128], int min_features);
+/* host all-reduce callback instead of RCCL (e.g. a gloo process group; ranks may share one GPU) */
+int uvio_hp_shard_init_host(uvio_hp_t *h, int rank, int world, uvio_hp_allreduce_fn fn, void *user,
+                            int min_features);
+/* the partition the update uses: rows[i] = stacked rows of feature i (2 m_f - 3); bounds (world + 1
+ * ints) receives the contiguous ranges [bounds[r], bounds[r+1]) balanced by their row sums. */
+int uvio_hp_shard_partition(const int *rows, int n, int world, int *bounds);
+
 /* ---- inner (kernel-level) boundary used by parity tests ---- */
 /* per-feature results of the last UpdaterMSCKF::update: feature id, triangulated p_FinG (3 per
  * feature), status (0 accepted, 1 triangulation/refinement failed, 3 chi2 rejected) and chi2 */

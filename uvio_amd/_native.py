@@ -103,7 +103,14 @@ SIGNATURES = [
     ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("msckf_compressed_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("compress", _I, [_P(_D), _I, _I, _P(_D)]),
+    ("shard_unique_id", _I, [_P(C.c_uint8)]),
+    ("shard_init_rccl", _I, [C.c_void_p, _I, _I, _P(C.c_uint8), _I]),
+    ("shard_init_host", _I, [C.c_void_p, _I, _I, C.c_void_p, C.c_void_p, _I]),
+    ("shard_partition", _I, [_P(_I), _I, _I, _P(_I)]),
 ]
+
+# uvio_hp_allreduce_fn: int (*)(double *buf, size_t count, void *user)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _P(_D), C.c_size_t, C.c_void_p)
 
 # every symbol declared in include/uvio_hp.h
 EXPORTED = ["uvio_hp_" + s[0] for s in SIGNATURES]

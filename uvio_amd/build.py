@@ -22,6 +22,7 @@ SOURCES = [
     "engine_update.cpp",
     "engine_track.cpp",
     "capi.cpp",
+    "shard.cpp",
     "kernels_cov.hip",
     "kernels_feat.hip",
     "kernels_chi2.hip",
@@ -66,7 +67,7 @@ def build_product(force=False, verbose=False):
             raise RuntimeError("hipcc failed on %s" % s)
         elif verbose and out:
             sys.stderr.write(out.decode())
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
     subprocess.check_call(cmd)
     return LIB
 

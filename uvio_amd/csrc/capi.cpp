@@ -217,6 +217,31 @@ int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *statu
   return 0;
 }
 
+int uvio_hp_shard_unique_id(uint8_t id[128]) {
+  if (!id) return UVIO_HP_E_ARG;
+  std::string err;
+  int rc = rccl_unique_id(id, &err);
+  if (rc) g_create_err = err;
+  return rc;
+}
+
+int uvio_hp_shard_init_rccl(uvio_hp_t *h, int rank, int world, const uint8_t id[128], int min_features) {
+  if (!h || !id) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->shard_init_rccl(rank, world, id, min_features); return 0;)
+}
+
+int uvio_hp_shard_init_host(uvio_hp_t *h, int rank, int world, uvio_hp_allreduce_fn fn, void *user,
+                            int min_features) {
+  if (!h || !fn) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->shard_init_host(rank, world, fn, user, min_features); return 0;)
+}
+
+int uvio_hp_shard_partition(const int *rows, int n, int world, int *bounds) {
+  if (!rows || !bounds || n < 0 || world < 1) return UVIO_HP_E_ARG;
+  shard_partition(rows, n, world, bounds);
+  return 0;
+}
+
 int uvio_hp_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
                        double sigma2, double *dx_out) {
   try {

@@ -62,6 +62,27 @@ struct Feature {
 };
 using FeatP = std::shared_ptr<Feature>;
 
+// Feature-sharded MSCKF update across replicas.  Every rank holds the same filter; the
+// features of an update are split into contiguous row-balanced chunks, each rank linearizes, gates and
+// forms the Gram of its own chunk, the (n+1)^2 information blocks are all-reduced (RCCL on the library's
+// stream, or a host callback), and every rank applies the identical information-form update.
+struct ShardComm {
+  bool enabled = false;
+  int rank = 0, world = 1;
+  int min_features = 1;              // updates with fewer features run unsharded on every rank
+  void *nccl = nullptr;              // ncclComm_t (RCCL)
+  uvio_hp_allreduce_fn host_fn = nullptr;
+  void *host_user = nullptr;
+};
+
+// contiguous chunks of `rows` balanced by their sum: bounds[r] .. bounds[r+1] is rank r's range
+void shard_partition(const int *rows, int n, int world, int *bounds);
+// RCCL through dlopen (no link-time dependency; reuses the copy PyTorch already loaded, if any)
+int rccl_unique_id(uint8_t id[128], std::string *err);
+void *rccl_comm_init(int rank, int world, const uint8_t id[128]);
+void rccl_allreduce_sum(void *comm, double *buf, size_t count, hipStream_t s);
+void rccl_comm_destroy(void *comm);
+
 struct ImuSample {
   double t, wm[3], am[3];
 };
@@ -101,6 +122,8 @@ struct DeviceBufs {
   char *stg_h = nullptr, *stg_d = nullptr;
   size_t stg_cap = 0, stg_used = 0, stg_flushed = 0;
   double *dxneg = nullptr;  // [negative-diagonal count (8 B) | dx (ldp)]: one readback per update
+  // feature sharding: the all-reduced [G upper triangle (max_ncol^2) | accepted features | accepted rows]
+  double *shard = nullptr, *shard_host = nullptr;
   int *acc = nullptr;       // accepted features of the last update batch (gates its P update)
 };
 
@@ -127,6 +150,10 @@ class Engine {
   int state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars, bool fej = false);
   uvio_hp_timing_t timing() const { return timing_; }
   std::vector<double> clone_times() const;
+
+  // feature sharding
+  void shard_init_rccl(int rank, int world, const uint8_t id[128], int min_features);
+  void shard_init_host(int rank, int world, uvio_hp_allreduce_fn fn, void *user, int min_features);
 
   // standalone kernel-level entry points (parity tests)
   static int ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
@@ -164,6 +191,9 @@ class Engine {
   std::map<double, std::unordered_map<size_t, double>> past_uwb_;
   uvio_hp_timing_t timing_{};
   std::vector<double> chi2_table_;
+  ShardComm shard_;
+  void shard_allreduce(double *dev, size_t count);
+  int msckf_update_sharded(std::vector<FeatP> &fv);
 
  public:
   struct FeatDebug {
@@ -191,7 +221,8 @@ class Engine {
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
   void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
-                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr);
+                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr,
+                       const double *partials = nullptr);
   // hidx_dev: the batch's column map already on the device (staged), or nullptr to stage `hidx`;
   // pre_apply runs after the readback, before dx is applied (initialize_invertible's landmark step)
   // gate (device count, may be null): the P update is skipped on the device when it is 0; after the
@@ -259,6 +290,7 @@ class Engine {
     std::map<double, int> slot_of_time;
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);
+  void add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep);
   // wait = false: only enqueue (kernels + result readback); the caller's next device sync completes it and
   // finish_batch then fills outs
   int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs);

@@ -212,13 +212,15 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
 
 Engine::~Engine() {
   hipSetDevice(device_);
+  if (shard_.nccl) rccl_comm_destroy(shard_.nccl);
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.fout, d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
+  if (d_.shard_host) hipHostFree(d_.shard_host);
   if (d_.stg_h) hipHostFree(d_.stg_h);
   if (d_.ev0) hipEventDestroy(d_.ev0);
   if (d_.ev1) hipEventDestroy(d_.ev1);
@@ -286,6 +288,7 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   dalloc(&d_.dxneg, cap + 2);
   dalloc(&d_.acc, 4);
+  dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
@@ -441,11 +444,11 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
 
 // EKF update from the Gram partials of a stacked batch (compressed path, m > n)
 void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
-                             const std::function<bool()> &apply, const int *gate) {
+                             const std::function<bool()> &apply, const int *gate, const double *partials) {
   const int *dh = stage(hidx.data(), (size_t)n);
   stage_flush();
   d_.ekf.gate = gate;
-  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
+  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, partials ? partials : d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
   read_dx("EKFUpdate");
   if (!apply || apply()) apply_dx(d_.dx_host);
 }

@@ -559,6 +559,10 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
   feats.push_back(F);
 }
 
+void Engine::add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep) {
+  add_feature(this, f, mode, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+}
+
 // Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
 // Returns the number of stacked rows written to H_all.
 int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs) {
@@ -702,6 +706,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   if (fv.empty()) return 0;
   if (o_.feat_rep_msckf != 0 && o_.feat_rep_msckf != 4)
     throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
+  if (shard_.enabled && (int)fv.size() >= shard_.min_features) return msckf_update_sharded(fv);
   Batch b;
   build_clone_cam_tables(b, false);
   for (auto &f : fv)

@@ -119,6 +119,12 @@ size_t feature_lds_bytes(int max_meas, int max_nf);
 // R_aug ((n+1) x (n+1) upper, ld = ldr).  Rank-deficient pivots produce zero rows.
 void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, double *partials, int *nchunks_out);
 int gram_num_chunks(int m);
+// Feature sharding: a rank's Gram partials summed into one (ncol x ncol) upper triangle,
+// followed by [accepted features, accepted rows] of its batch, the buffer every rank all-reduces; after the
+// sum the accepted-feature total becomes the P-update gate again.
+void launch_shard_pack(hipStream_t s, const double *partials, int nch, int ncol, const DFeatOut *fout, int nf,
+                       const int *acc, double *buf);
+void launch_shard_unpack(hipStream_t s, const double *buf, int ncol, int *acc);
 void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks, int ncol, double *R, int ldr);
 
 // EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j

@@ -181,6 +181,47 @@ void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, doubl
   hipLaunchKernelGGL(k_gram, dim3(pairs, nch), dim3(256), 0, s, A, m, ncol, ldh, partials);
 }
 
+// Feature sharding: one rank's contribution to the all-reduced information block.  Upper triangle of the
+// rank's Gram (chunks summed in fixed order; the lower triangle is written as zero so the reduced buffer is
+// defined everywhere), then the accepted-feature count and the accepted rows of the rank's batch.
+__global__ void __launch_bounds__(256) k_shard_pack(const double *__restrict__ partials, int nch, int ncol,
+                                                    const DFeatOut *__restrict__ fout, int nf,
+                                                    const int *__restrict__ acc, double *__restrict__ buf) {
+  const int nn = ncol * ncol;
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < nn) {
+    int a = e / ncol, b = e % ncol;
+    double v = 0.0;
+    if (a <= b)
+      for (int c = 0; c < nch; c++) v += partials[(size_t)c * nn + e];
+    buf[e] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // one wavefront: accepted rows of the batch
+    int rows = 0;
+    for (int i = threadIdx.x; i < nf; i += 64)
+      if (fout[i].status == 0) rows += fout[i].rows;
+    for (int o = 32; o > 0; o >>= 1) rows += __shfl_down(rows, o, 64);
+    if (threadIdx.x == 0) {
+      buf[nn] = (nf > 0) ? (double)*acc : 0.0;
+      buf[nn + 1] = (double)rows;
+    }
+  }
+}
+
+__global__ void k_shard_unpack(const double *__restrict__ buf, int ncol, int *__restrict__ acc) {
+  if (threadIdx.x == 0) *acc = (int)(buf[ncol * ncol] + 0.5);
+}
+
+void launch_shard_pack(hipStream_t s, const double *partials, int nch, int ncol, const DFeatOut *fout, int nf,
+                       const int *acc, double *buf) {
+  int nn = ncol * ncol;
+  hipLaunchKernelGGL(k_shard_pack, dim3((nn + 255) / 256), dim3(256), 0, s, partials, nch, ncol, fout, nf, acc, buf);
+}
+
+void launch_shard_unpack(hipStream_t s, const double *buf, int ncol, int *acc) {
+  hipLaunchKernelGGL(k_shard_unpack, dim3(1), dim3(64), 0, s, buf, ncol, acc);
+}
+
 // Sum partials (fixed chunk order) into the upper triangle of G, then upper Cholesky G = R^T R.
 // G lives in `W` (LDS when it fits, else global scratch `gbuf`). Pivots <= tol*G_jj give zero rows.
 __global__ void __launch_bounds__(1024) k_gram_reduce_chol(const double *__restrict__ partials, int nch, int ncol,

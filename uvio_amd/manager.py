@@ -32,6 +32,46 @@ def apply_overrides(opts, overrides):
     return opts
 
 
+def shard_unique_id():
+    """ncclGetUniqueId (rank 0): 128 bytes to distribute to every rank for enable_feature_sharding."""
+    lib = N.load()
+    uid = (C.c_uint8 * 128)()
+    rc = lib.uvio_hp_shard_unique_id(uid)
+    if rc != 0:
+        msg = (lib.uvio_hp_last_error(None) or b"").decode()
+        raise RuntimeError("shard_unique_id failed: %s %s" % (N.ERRNAMES.get(rc, rc), msg))
+    return bytes(uid)
+
+
+def host_allreduce_callback(group=None):
+    """uvio_hp_allreduce_fn over torch.distributed: the library hands a host buffer of doubles, the
+    callback sums it in place across the ranks of `group` (default group when None)."""
+    import torch
+    import torch.distributed as dist
+
+    def _allreduce(buf, count, user):
+        try:
+            t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(count,)))
+            dist.all_reduce(t, group=group)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    return N.ALLREDUCE_FN(_allreduce)
+
+
+def shard_partition(rows, world):
+    """The feature split the sharded update uses: bounds (world + 1) of contiguous row-balanced chunks."""
+    lib = N.load()
+    r = np.ascontiguousarray(rows, dtype=np.int32)
+    b = np.zeros(world + 1, dtype=np.int32)
+    rc = lib.uvio_hp_shard_partition(r.ctypes.data_as(C.POINTER(C.c_int)), len(r), world,
+                                     b.ctypes.data_as(C.POINTER(C.c_int)))
+    if rc != 0:
+        raise RuntimeError("shard_partition failed: %s" % N.ERRNAMES.get(rc, rc))
+    return b
+
+
 def pack_sim_frame(feats):
     """(counts, ids uint64[n], uv float32[n, 2]) of one TrackSIM frame, cameras concatenated."""
     counts = [len(f[0]) for f in feats]
@@ -86,6 +126,26 @@ class VioManager:
             self.close()
         except Exception:  # noqa: BLE001
             pass
+
+    # ---- feature sharding across ranks (include/uvio_hp.h) ----
+    def enable_feature_sharding(self, rank, world, backend="rccl", unique_id=None, group=None, min_features=1):
+        """Split every MSCKF update with >= min_features features across `world` replicas of this filter
+        (one per rank, all fed the same stream).  backend "rccl": the library all-reduces on its own
+        stream over an RCCL communicator (unique_id: the 128 bytes of shard_unique_id() made on rank 0 and
+        shared with every rank).  backend "host": the blocks go through torch.distributed.all_reduce on
+        `group` (e.g. gloo; ranks may then share one GPU)."""
+        if backend == "rccl":
+            if unique_id is None or len(unique_id) != 128:
+                raise ValueError("rccl backend needs the 128-byte unique id of shard_unique_id()")
+            uid = (C.c_uint8 * 128)(*bytearray(unique_id))
+            self._check(self._call("shard_init_rccl", self._h, rank, world, uid, min_features), "shard_init_rccl")
+        elif backend == "host":
+            self._allreduce_cb = host_allreduce_callback(group)  # kept alive with the handle
+            fn = C.cast(self._allreduce_cb, C.c_void_p)
+            self._check(self._call("shard_init_host", self._h, rank, world, fn, None, min_features),
+                        "shard_init_host")
+        else:
+            raise ValueError("backend must be 'rccl' or 'host'")
 
     # ---- feeds ----
     def initialize_with_gt(self, imustate17):
