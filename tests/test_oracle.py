@@ -161,3 +161,38 @@ def test_oracle_closed_loop_tracks_ground_truth(euroc_yaml):
     ev = np.linalg.eigvalsh(P)
     assert ev.min() > -1e-12 * ev.max()
     assert np.all(np.diag(P) > 0)
+
+
+def test_libstdcxx_small_map_iteration_is_reverse_insertion(tmp_path):
+    """The product stores a feature's per-camera tracks in a small vector ordered like the reference's
+    unordered_map<size_t, vector<...>> members (engine.h Feature::tracks): with libstdc++ and <= 4 camera
+    keys, iteration runs in reverse first-insertion order.  Pinned here for every insertion sequence."""
+    import subprocess
+    src = r'''
+#include <unordered_map>
+#include <vector>
+#include <algorithm>
+#include <cstdio>
+int main() {
+  int bad = 0, tot = 0;
+  for (int mask = 1; mask < 16; mask++) {
+    std::vector<size_t> sub;
+    for (int k = 0; k < 4; k++) if (mask >> k & 1) sub.push_back(k);
+    do {
+      std::unordered_map<size_t, std::vector<double>> m;
+      for (size_t k : sub) { m[k].push_back(1.0); m[k].push_back(2.0); }
+      std::vector<size_t> it;
+      for (auto &p : m) it.push_back(p.first);
+      tot++;
+      if (it != std::vector<size_t>(sub.rbegin(), sub.rend())) bad++;
+    } while (std::next_permutation(sub.begin(), sub.end()));
+  }
+  std::printf("%d %d\n", bad, tot);
+}
+'''
+    c = tmp_path / "m.cpp"
+    c.write_text(src)
+    exe = tmp_path / "m"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", str(c), "-o", str(exe)])
+    bad, tot = map(int, subprocess.check_output([str(exe)]).split())
+    assert tot == 64 and bad == 0

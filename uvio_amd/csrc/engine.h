@@ -17,6 +17,7 @@
 
 #include "hp_common.h"
 #include "kernels.h"
+#include "pool.h"
 #include "tracker.h"
 
 namespace uvhp {
@@ -43,20 +44,44 @@ struct Var {
 };
 using VarP = std::shared_ptr<Var>;
 
+// One camera's measurements of a feature (Feature::uvs / uvs_norm / timestamps of that camera,
+// Feature.h:39-96), stored together
+struct FeatMeas {
+  float u, v, un, vn;
+  double t;
+};
+struct CamTrack {
+  size_t cam;
+  std::vector<FeatMeas> m;
+};
+
 struct Feature {
   size_t featid = 0;
   bool to_delete = false;
-  // per camera, in libstdc++ unordered_map order (iteration order = the reference's)
-  std::unordered_map<size_t, std::vector<std::pair<float, float>>> uvs, uvs_norm;
-  std::unordered_map<size_t, std::vector<double>> timestamps;
+  // Per camera, in the iteration order of the reference's unordered_map<size_t, vector<...>> members:
+  // with libstdc++ and at most UVIO_HP_MAX_CAMS small integer keys every key sits in its own bucket and
+  // a new key is linked at the list front, so iteration runs in reverse first-insertion order
+  // (tests/test_oracle.py pins this) -- a camera's first measurement inserts its track at the front.
+  std::vector<CamTrack> tracks;
   int anchor_cam_id = -1;
   double anchor_clone_timestamp = -1;
   double p_FinA[3] = {0, 0, 0}, p_FinG[3] = {0, 0, 0};
-  void clean_old_measurements(const std::vector<double> &valid);
+  CamTrack &track(size_t cam) {
+    for (auto &c : tracks)
+      if (c.cam == cam) return c;
+    tracks.insert(tracks.begin(), CamTrack{cam, {}});
+    return tracks.front();
+  }
+  const CamTrack *find(size_t cam) const {
+    for (auto &c : tracks)
+      if (c.cam == cam) return &c;
+    return nullptr;
+  }
+  void clean_old_measurements(const std::vector<double> &valid);  // valid: ascending
   void clean_older_measurements(double t);
   int count() const {
     int c = 0;
-    for (auto &p : timestamps) c += (int)p.second.size();
+    for (auto &p : tracks) c += (int)p.m.size();
     return c;
   }
 };
@@ -192,6 +217,7 @@ class Engine {
   uvio_hp_timing_t timing_{};
   std::vector<double> chi2_table_;
   ShardComm shard_;
+  WorkPool pool_;
   void shard_allreduce(double *dev, size_t count);
   int msckf_update_sharded(std::vector<FeatP> &fv);
 

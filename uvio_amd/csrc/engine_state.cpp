@@ -67,39 +67,19 @@ void Var::set_xyz(const double *p, bool isfej) {
 
 // ---- Feature (Feature.cpp:26-111) ----
 void Feature::clean_old_measurements(const std::vector<double> &valid) {
-  for (auto &pair : timestamps) {
-    auto &ts = pair.second;
-    auto &u = uvs[pair.first];
-    auto &un = uvs_norm[pair.first];
+  for (auto &c : tracks) {
     size_t w = 0;
-    for (size_t i = 0; i < ts.size(); i++)
-      if (std::find(valid.begin(), valid.end(), ts[i]) != valid.end()) {
-        ts[w] = ts[i];
-        u[w] = u[i];
-        un[w] = un[i];
-        w++;
-      }
-    ts.resize(w);
-    u.resize(w);
-    un.resize(w);
+    for (size_t i = 0; i < c.m.size(); i++)
+      if (std::binary_search(valid.begin(), valid.end(), c.m[i].t)) c.m[w++] = c.m[i];
+    c.m.resize(w);
   }
 }
 void Feature::clean_older_measurements(double t) {
-  for (auto &pair : timestamps) {
-    auto &ts = pair.second;
-    auto &u = uvs[pair.first];
-    auto &un = uvs_norm[pair.first];
+  for (auto &c : tracks) {
     size_t w = 0;
-    for (size_t i = 0; i < ts.size(); i++)
-      if (!(ts[i] <= t)) {
-        ts[w] = ts[i];
-        u[w] = u[i];
-        un[w] = un[i];
-        w++;
-      }
-    ts.resize(w);
-    u.resize(w);
-    un.resize(w);
+    for (size_t i = 0; i < c.m.size(); i++)
+      if (!(c.m[i].t <= t)) c.m[w++] = c.m[i];
+    c.m.resize(w);
   }
 }
 

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_set>
 
 #include "engine.h"
 
@@ -117,9 +118,7 @@ void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float 
     f->featid = id;
     db_[id] = f;
   }
-  f->uvs[cam].push_back({u, v});
-  f->uvs_norm[cam].push_back({un, vn});
-  f->timestamps[cam].push_back(t);
+  f->track(cam).m.push_back(FeatMeas{u, v, un, vn, t});
 }
 
 // UVioManager.cpp:61-79
@@ -162,18 +161,20 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
                             const float *uv) {
   stage_ = "feed_simulation";
   auto rT1 = clk::now();
-  size_t k = 0;
-  std::vector<int> camids;
+  std::vector<int> camids, cam_of;
   for (int i = 0; i < ncam; i++) {
     int cid = cam_ids[i];
-    if (cid < 0 || cid >= o_.num_cameras) return UVIO_HP_E_ARG;
+    if (cid < 0 || cid >= o_.num_cameras || counts[i] < 0) return UVIO_HP_E_ARG;
     camids.push_back(cid);
-    for (int j = 0; j < counts[i]; j++, k++) {
-      float un, vn;
-      cam_undistort_f(cams_[cid], uv[2 * k], uv[2 * k + 1], un, vn);
-      db_update((size_t)ids[k] + currid_, t, cid, uv[2 * k], uv[2 * k + 1], un, vn);
-    }
+    cam_of.insert(cam_of.end(), counts[i], cid);
   }
+  // undistort every observation (independent, on the pool), then the database updates in order
+  std::vector<float> uvn(2 * cam_of.size());
+  pool_.parallel_for(cam_of.size(), 2048, [&](size_t b, size_t e) {
+    for (size_t k = b; k < e; k++) cam_undistort_f(cams_[cam_of[k]], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
+  });
+  for (size_t k = 0; k < cam_of.size(); k++)
+    db_update((size_t)ids[k] + currid_, t, cam_of[k], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
   return after_tracking(t, camids, rT1);
 }
 
@@ -245,37 +246,49 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
 
   std::vector<FeatP> feats_lost, feats_marg, feats_slam;
   // FeatureDatabase::features_not_containing_newer(t, false, true)
-  for (auto &kv : db_) {
-    if (kv.second->to_delete) continue;
-    bool newer = false;
-    for (auto &p : kv.second->timestamps) {
-      newer = (!p.second.empty() && p.second.back() >= timestamp_);
-      if (newer) break;
-    }
-    if (!newer) feats_lost.push_back(kv.second);
-  }
-  if ((int)clones_.size() > o_.max_clone_size || (int)clones_.size() > 5) {
-    double mt = margtimestep();
-    for (auto &kv : db_) {
-      if (kv.second->to_delete) continue;
-      bool has = false;
-      for (auto &p : kv.second->timestamps) {
-        has = std::find(p.second.begin(), p.second.end(), mt) != p.second.end();
-        if (has) break;
+  // (and features_containing(margtimestep)): per-feature flags on the pool, lists built in db_ order
+  std::unordered_set<const Feature *> in_marg;
+  {
+    const bool do_marg = (int)clones_.size() > o_.max_clone_size || (int)clones_.size() > 5;
+    const double mt = do_marg ? margtimestep() : 0.0, ts = timestamp_;
+    std::vector<std::pair<FeatP, uint8_t>> all;  // feature, bit 0 lost, bit 1 marg
+    all.reserve(db_.size());
+    for (auto &kv : db_) all.emplace_back(kv.second, 0);
+    pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) {
+        const Feature &f = *all[i].first;
+        if (f.to_delete) continue;
+        bool newer = false, has = false;
+        for (auto &p : f.tracks) {
+          newer = (!p.m.empty() && p.m.back().t >= ts);
+          if (newer) break;
+        }
+        if (do_marg)
+          for (auto &p : f.tracks) {
+            has = std::find_if(p.m.begin(), p.m.end(), [mt](const FeatMeas &x) { return x.t == mt; }) != p.m.end();
+            if (has) break;
+          }
+        all[i].second = (uint8_t)((newer ? 0 : 1) | (has ? 2 : 0));
       }
-      if (has) feats_marg.push_back(kv.second);
+    });
+    for (auto &a : all) {
+      if (a.second & 1) feats_lost.push_back(a.first);
+      if (a.second & 2) {
+        feats_marg.push_back(a.first);
+        in_marg.insert(a.first.get());
+      }
     }
   }
   {
     std::vector<FeatP> keep;
     for (auto &f : feats_lost) {
       bool found = false;
-      for (auto &p : f->uvs)
-        if (std::find(camids.begin(), camids.end(), (int)p.first) != camids.end()) {
+      for (auto &p : f->tracks)
+        if (std::find(camids.begin(), camids.end(), (int)p.cam) != camids.end()) {
           found = true;
           break;
         }
-      if (found && std::find(feats_marg.begin(), feats_marg.end(), f) == feats_marg.end()) keep.push_back(f);
+      if (found && !in_marg.count(f.get())) keep.push_back(f);
     }
     feats_lost = keep;
   }
@@ -284,8 +297,8 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     std::vector<FeatP> keep;
     for (auto &f : feats_marg) {
       bool reached = false;
-      for (auto &p : f->timestamps)
-        if ((int)p.second.size() > o_.max_clone_size) {
+      for (auto &p : f->tracks)
+        if ((int)p.m.size() > o_.max_clone_size) {
           reached = true;
           break;
         }
@@ -356,14 +369,21 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   rc = slam_change_anchors();
   if (rc) return rc;
   if ((int)clones_.size() > o_.max_clone_size) {
+    // FeatureDatabase::cleanup_measurements(margtimestep): per-feature trimming on the pool, then the
+    // emptied features are erased (erasing by key keeps the others' iteration order)
     double mt = margtimestep();
-    for (auto it = db_.begin(); it != db_.end();) {
-      it->second->clean_older_measurements(mt);
-      if (it->second->count() < 1)
-        it = db_.erase(it);
-      else
-        it++;
-    }
+    std::vector<Feature *> all;
+    all.reserve(db_.size());
+    for (auto &kv : db_) all.push_back(kv.second.get());
+    std::vector<uint8_t> empty(all.size(), 0);
+    pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) {
+        all[i]->clean_older_measurements(mt);
+        empty[i] = all[i]->count() < 1;
+      }
+    });
+    for (size_t i = 0; i < all.size(); i++)
+      if (empty[i]) db_.erase(all[i]->featid);
   }
   marginalize_old_clone();
   if (o_.record_timing >= 2) dev_sync();
@@ -466,12 +486,14 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
   // anchor (FeatureInitializer.cpp:35-45): camera with most measurements (first max in map order),
   // anchor time = its last measurement
   size_t anchor_cam = 0, most = 0;
-  for (auto &p : f->timestamps)
-    if (p.second.size() > most) {
-      anchor_cam = p.first;
-      most = p.second.size();
+  for (auto &p : f->tracks)
+    if (p.m.size() > most) {
+      anchor_cam = p.cam;
+      most = p.m.size();
     }
-  double anchor_time = f->timestamps.at(anchor_cam).back();
+  const CamTrack *at = f->find(anchor_cam);
+  if (!at || at->m.empty()) throw HpError(UVIO_HP_E_STATE, "feature without measurements in a batch");
+  double anchor_time = at->m.back().t;
   if (landmark) {
     anchor_cam = (size_t)landmark->anchor_cam;
     anchor_time = landmark->anchor_time;
@@ -486,10 +508,11 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
     throw HpError(UVIO_HP_E_STATE, "feature anchor clone is not in the window");
   F.anchor_slot = (anc == slot_of_time.end()) ? 0 : anc->second;
   int loc = 0;
-  std::map<int, int> clone_loc;  // slot -> local col
-  std::vector<int> ext_loc(UVIO_HP_MAX_CAMS, -1), intr_loc(UVIO_HP_MAX_CAMS, -1);
-  for (auto &p : f->timestamps) {
-    int c = (int)p.first;
+  std::vector<int> clone_loc(clones.size(), -1);  // slot -> local col
+  int ext_loc[UVIO_HP_MAX_CAMS], intr_loc[UVIO_HP_MAX_CAMS];
+  for (int k = 0; k < UVIO_HP_MAX_CAMS; k++) ext_loc[k] = intr_loc[k] = -1;
+  for (auto &p : f->tracks) {
+    int c = (int)p.cam;
     if (o.do_calib_camera_pose) {
       vars.push_back(DVar{cams[c].pid_ext, cams[c].canon_ext, 6, loc});
       ext_loc[c] = loc;
@@ -500,9 +523,9 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
       intr_loc[c] = loc;
       loc += 8;
     }
-    for (size_t m = 0; m < p.second.size(); m++) {
-      int s = slot_of_time.at(p.second[m]);
-      if (!clone_loc.count(s)) {
+    for (size_t m = 0; m < p.m.size(); m++) {
+      int s = slot_of_time.at(p.m[m].t);
+      if (clone_loc[s] < 0) {
         clone_loc[s] = loc;
         vars.push_back(DVar{clones[s].pid, clones[s].canon, 6, loc});
         loc += 6;
@@ -510,7 +533,7 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
     }
   }
   if (rel) {
-    if (!clone_loc.count(F.anchor_slot)) {
+    if (clone_loc[F.anchor_slot] < 0) {
       clone_loc[F.anchor_slot] = loc;
       vars.push_back(DVar{clones[F.anchor_slot].pid, clones[F.anchor_slot].canon, 6, loc});
       loc += 6;
@@ -520,7 +543,7 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
       vars.push_back(DVar{cams[F.anchor_cam].pid_ext, cams[F.anchor_cam].canon_ext, 6, loc});
       loc += 6;
     }
-    F.lc_anchor_clone = clone_loc.at(F.anchor_slot);
+    F.lc_anchor_clone = clone_loc[F.anchor_slot];
     F.lc_anchor_ext = ext_loc[F.anchor_cam];
   }
   if (landmark) {
@@ -535,19 +558,18 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
   }
   F.nf = loc;
   F.nvar = (int)vars.size() - F.var_off;
-  for (auto &p : f->timestamps) {
-    int c = (int)p.first;
-    const auto &u = f->uvs.at(p.first);
-    const auto &un = f->uvs_norm.at(p.first);
-    for (size_t m = 0; m < p.second.size(); m++) {
+  for (auto &p : f->tracks) {
+    int c = (int)p.cam;
+    for (size_t m = 0; m < p.m.size(); m++) {
+      const FeatMeas &fm = p.m[m];
       DMeas d{};
-      d.u = u[m].first;
-      d.v = u[m].second;
-      d.un = un[m].first;
-      d.vn = un[m].second;
+      d.u = fm.u;
+      d.v = fm.v;
+      d.un = fm.un;
+      d.vn = fm.vn;
       d.cam = c;
-      d.slot = slot_of_time.at(p.second[m]);
-      d.lc_clone = clone_loc.at(d.slot);
+      d.slot = slot_of_time.at(fm.t);
+      d.lc_clone = clone_loc[d.slot];
       d.lc_ext = ext_loc[c];
       d.lc_intr = intr_loc[c];
       meas.push_back(d);
@@ -868,10 +890,10 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     }
     // anchor (host rule, identical to the kernel's) and triangulated position
     size_t anchor_cam = 0, most = 0;
-    for (auto &p : f->timestamps)
-      if (p.second.size() > most) anchor_cam = p.first, most = p.second.size();
+    for (auto &p : f->tracks)
+      if (p.m.size() > most) anchor_cam = p.cam, most = p.m.size();
     f->anchor_cam_id = (int)anchor_cam;
-    f->anchor_clone_timestamp = f->timestamps.at(anchor_cam).back();
+    f->anchor_clone_timestamp = f->find(anchor_cam)->m.back().t;
     for (int k = 0; k < 3; k++) f->p_FinA[k] = tri[i].p_FinA[k], f->p_FinG[k] = tri[i].p_FinG[k];
     // 2) linearize at the current state (mode 3 = given triangulation, nullspace-split rows)
     VarP lm = std::make_shared<Var>(V_LANDMARK, 3, 3);
@@ -889,60 +911,53 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // mode 3: linearize at the batch triangulation (p_in = p_FinA, p_in_fej = p_FinG), as the reference
     // triangulates the whole batch before the per-feature initialize loop
     for (int k = 0; k < 3; k++) b.feats[0].p_in[k] = f->p_FinA[k], b.feats[0].p_in_fej[k] = f->p_FinG[k];
+    // The chi2 test of StateHelper::initialize (StateHelper.cpp:451-470) is decided on the device: the
+    // batch's accepted count (d_.acc) gates initialize_invertible and the EKF update enqueued right
+    // behind it, and the host learns the decision with the update's dx (one wait per feature).  The
+    // landmark is appended tentatively and withdrawn when the feature was rejected (nothing was written).
     std::vector<DFeatOut> o1;
-    run_batch(b, 3, s2, o_.slam_chi2_multipler, true, o1);
-    if (o1[0].status != 0) {
-      f->to_delete = true;
-      continue;
-    }
-    // 3) initialize_invertible with rows 0..2, EKF update with rows 3..
+    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1);
+    // 3) initialize_invertible with rows 0..2 (H_Linv = H_finit^-1 formed on the device from HfR), EKF
+    // update with rows 3..
     int n = b.n_canon;
-    double HL[9], HLinv[9];
-    std::memcpy(HL, o1[0].HfR, sizeof(HL));
-    // inverse of the 3x3 upper-triangular H_finit (colPivHouseholderQr-equivalent for invertible H)
-    {
-      double A[9];
-      std::memcpy(A, HL, sizeof(A));
-      double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) + A[2] * (A[3] * A[7] - A[4] * A[6]);
-      HLinv[0] = (A[4] * A[8] - A[5] * A[7]) / det;
-      HLinv[1] = (A[2] * A[7] - A[1] * A[8]) / det;
-      HLinv[2] = (A[1] * A[5] - A[2] * A[4]) / det;
-      HLinv[3] = (A[5] * A[6] - A[3] * A[8]) / det;
-      HLinv[4] = (A[0] * A[8] - A[2] * A[6]) / det;
-      HLinv[5] = (A[2] * A[3] - A[0] * A[5]) / det;
-      HLinv[6] = (A[3] * A[7] - A[4] * A[6]) / det;
-      HLinv[7] = (A[1] * A[6] - A[0] * A[7]) / det;
-      HLinv[8] = (A[0] * A[4] - A[1] * A[3]) / det;
-    }
     if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
-    const double *dHLinv = stage(HLinv, 9);
-    stage_flush();
-    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, dHLinv, s2, d_.ekf);
+    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, nullptr, s2, d_.ekf, d_.fout,
+                           d_.acc);
     // landmark value update H_Linv * resinit (residual column of rows 0..2), read back together with the
     // update's dx; applied first, as initialize_invertible does
     double *resinit = d_.dx_host + d_.ldp + 2;
     HP_HIP(hipMemcpy2DAsync(resinit, sizeof(double), d_.H + n, sizeof(double) * d_.ldh, sizeof(double), 3,
                             hipMemcpyDeviceToHost, d_.stream));
-    VarP lmv = lm;
-    auto land = [lmv, resinit, HLinv]() {
-      double dl[3];
+    bool accepted = false;
+    auto land = [&]() {
+      finish_batch(b, 3, o1);
+      accepted = (o1[0].status == 0);
+      if (!accepted) return false;  // the device skipped the init and the update
+      double HLinv[9], dl[3];
+      inv3_cofactor(o1[0].HfR, HLinv);  // the device's formula: identical H_Linv
       for (int a = 0; a < 3; a++)
         dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
-      lmv->update(dl);
+      lm->update(dl);
       return true;
     };
+    const int N0 = N_;
     lm->id = N_;
     vars_.push_back(lm);
     N_ += 3;
-    slam_.insert({f->featid, lm});
     f->to_delete = true;
     int nup = 2 * b.feats[0].nmeas - 3;
     if (nup > 0) {
       ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
-                      b.hidx_dev, land);
+                      b.hidx_dev, land, d_.acc);
     } else {
       dev_sync();
       land();
+    }
+    if (accepted) {
+      slam_.insert({f->featid, lm});
+    } else {
+      vars_.pop_back();
+      N_ = N0;
     }
   }
   return 0;

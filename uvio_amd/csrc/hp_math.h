@@ -42,6 +42,20 @@ HPD void skew(const double *w, double *S) {
 }
 HPD double dot3(const double *a, const double *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 HPD double norm3(const double *a) { return sqrt(dot3(a, a)); }
+// inverse of a 3x3 (row-major) by cofactors; host and device give identical results (no contraction)
+HPD void inv3_cofactor(const double *A, double *R) {
+  const double det = A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
+                     A[2] * (A[3] * A[7] - A[4] * A[6]);
+  R[0] = (A[4] * A[8] - A[5] * A[7]) / det;
+  R[1] = (A[2] * A[7] - A[1] * A[8]) / det;
+  R[2] = (A[1] * A[5] - A[2] * A[4]) / det;
+  R[3] = (A[5] * A[6] - A[3] * A[8]) / det;
+  R[4] = (A[0] * A[8] - A[2] * A[6]) / det;
+  R[5] = (A[2] * A[3] - A[0] * A[5]) / det;
+  R[6] = (A[3] * A[7] - A[4] * A[6]) / det;
+  R[7] = (A[1] * A[6] - A[0] * A[7]) / det;
+  R[8] = (A[0] * A[4] - A[1] * A[3]) / det;
+}
 
 // quat_ops.h:152
 HPD void quat_2_Rot(const double *q, double *R) {

@@ -156,8 +156,10 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc);
 // StateHelper::initialize_invertible for a 3-dof variable appended at N (StateHelper.cpp:484-577)
+// fout != nullptr: H_Linv = inverse of fout->HfR (formed on the device); gate: skipped when *gate == 0
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
-                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc);
+                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc,
+                            const DFeatOut *fout = nullptr, const int *gate = nullptr);
 double chi2_quantile95(int dof);
 
 // Raise a kernel's dynamic-LDS limit to `want` bytes, capped so static + dynamic LDS fits the CU's

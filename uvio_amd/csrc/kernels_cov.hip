@@ -724,10 +724,23 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
 // M = P[:, hidx] Hx^T is in sc.M (N x 3, from k_ekf_M); Hx (3 x n, ld), HLinv (3x3, device), s2.
+// With fout (delayed init enqueued behind its feature group): H_Linv is the inverse of the feature's
+// H_finit (DFeatOut::HfR), formed here with the host's cofactor formula, and the whole step is skipped
+// when the gate (the batch's accepted-feature count) is 0.
 __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
                                   const double *__restrict__ Hx, int ldh, int n, const int *__restrict__ hidx,
-                                  const double *__restrict__ HLinv, double s2) {
-  __shared__ double S3[9], PLL[9];
+                                  const double *__restrict__ HLinv_in, double s2, const DFeatOut *__restrict__ fout,
+                                  const int *__restrict__ gate) {
+  __shared__ double S3[9], PLL[9], Hinv[9];
+  if (gate && *gate == 0) return;
+  if (threadIdx.x == 0) {
+    if (fout)
+      inv3_cofactor(fout->HfR, Hinv);
+    else
+      for (int k = 0; k < 9; k++) Hinv[k] = HLinv_in[k];
+  }
+  __syncthreads();
+  const double *HLinv = Hinv;
   int t = threadIdx.x + blockIdx.x * blockDim.x;
   if (blockIdx.x == 0 && threadIdx.x < 9) {
     int a = threadIdx.x / 3, b = threadIdx.x % 3;
@@ -762,12 +775,13 @@ __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const 
 }
 
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
-                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc) {
+                            const int *hidx, const double *HLinv, double s2, EkfScratch &sc, const DFeatOut *fout,
+                            const int *gate) {
   dim3 gM(1, (N + 15) / 16);
   hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M, (int *)nullptr);
   int nt = N * 3;
   hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
-                     HLinv, s2);
+                     HLinv, s2, fout, gate);
 }
 
 static void ensure_lds_attrs() {
