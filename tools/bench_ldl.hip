@@ -11,14 +11,16 @@
 using namespace uvhp;
 
 __global__ void __launch_bounds__(512) k_test(const double *Ain, int n, int nrows, int which, int mode, double *out,
-                                              long long *ts) {
+                                              long long *ts, double *gA) {
   extern __shared__ double lds[];
   const int ld = n | 1;
-  double *A = lds, *wsp = lds + (size_t)nrows * ld;
+  double *A = (which == 5) ? gA : lds, *wsp = lds + (size_t)nrows * ld;
   for (int e = threadIdx.x; e < nrows * n; e += blockDim.x) A[(e / n) * ld + e % n] = Ain[e];
   __syncthreads();
   long long t0 = clock64();
   if (which == 2) {
+    ldl_panel4(A, ld, n, nrows, wsp);
+  } else if (which == 5) {
     ldl_panel4(A, ld, n, nrows, wsp);
   } else {
     ldl_inplace(A, ld, n, nrows);
@@ -59,13 +61,15 @@ int main(int argc, char **argv) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   std::vector<double> o2(nrows * n);
-  double *dO2;
+  double *dO2, *dG;
   (void)hipMalloc(&dO2, 8 * nrows * n);
-  for (int which = 0; which < 3; which += 2)
+  (void)hipMalloc(&dG, 8 * (size_t)nrows * (n | 1));
+  const char *names[] = {"lds  ", "regs ", "panel4", "panel16", "panel16-global", "panel4-global", "panel8", "panel8-global"};
+  std::vector<std::vector<double>> outs;
+  for (int which : {0, 2, 5}) {
     for (int it = 0; it < 3; it++) {
       (void)hipEventRecord(e0);
-      hipLaunchKernelGGL(k_test, dim3(1), dim3(nt), bytes, 0, dA, n, nrows, which, mode,
-                         which == 2 ? dO2 : which ? dO1 : dO0, dts);
+      hipLaunchKernelGGL(k_test, dim3(1), dim3(nt), bytes, 0, dA, n, nrows, which, mode, dO2, dts, dG);
       (void)hipEventRecord(e1);
       (void)hipEventSynchronize(e1);
       float ms;
@@ -73,18 +77,21 @@ int main(int argc, char **argv) {
       long long ts;
       (void)hipMemcpy(&ts, dts, 8, hipMemcpyDeviceToHost);
       if (it == 2)
-        printf("%s n=%d nt=%d mode=%d kernel %.1f us  %lld cyc\n", which == 2 ? "panel" : which ? "regs " : "lds  ", n, nt,
-               mode, ms * 1e3, ts);
+        printf("%-15s n=%d nt=%d mode=%d kernel %.1f us  %lld cyc\n", names[which], n, nt, mode, ms * 1e3, ts);
     }
-  std::vector<double> o0(nrows * n), o1(nrows * n);
-  (void)hipMemcpy(o0.data(), dO0, 8 * nrows * n, hipMemcpyDeviceToHost);
-  (void)hipMemcpy(o1.data(), dO1, 8 * nrows * n, hipMemcpyDeviceToHost);
-  double err = 0;
-
-  (void)hipMemcpy(o2.data(), dO2, 8 * nrows * n, hipMemcpyDeviceToHost);
-  err = 0;
-  for (int i = 0; i < nrows; i++)
-    for (int j = 0; j < n && j <= i; j++) err = fmax(err, fabs(o0[i * n + j] - o2[i * n + j]));
-  printf("max |panel - lds| = %.3e\n", err);
-  return 0;
+    (void)hipMemcpy(o2.data(), dO2, 8 * nrows * n, hipMemcpyDeviceToHost);
+    outs.push_back(o2);
+  }
+  int bad = 0;
+  for (size_t w = 1; w < outs.size(); w++) {
+    double err = 0, mx = 0;
+    for (int i = 0; i < nrows; i++)
+      for (int j = 0; j < n && j <= i; j++) {
+        err = fmax(err, fabs(outs[0][i * n + j] - outs[w][i * n + j]));
+        mx = fmax(mx, fabs(outs[0][i * n + j]));
+      }
+    printf("variant %zu: max |x - lds| / max|lds| = %.3e\n", w, err / mx);
+    if (!(err / mx < 1e-11)) bad++;
+  }
+  return bad;
 }

@@ -133,6 +133,7 @@ __device__ void ldl_panel4(double *A, int ld, int n, int nrows, double *Lp) {
         for (int p = k + 1; p <= q; p++) c[q][p] -= a * c[p][k];
       }
     }
+    __syncthreads();  // every wave has read the diagonal block before the panel rows overwrite it
     // panel rows
     for (int i = K + threadIdx.x; i < nrows; i += blockDim.x) {
       double v[4];

@@ -317,6 +317,7 @@ class Engine {
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);
   void add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep);
+  void add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_t lo, size_t hi, int mode, int rep);
   // wait = false: only enqueue (kernels + result readback); the caller's next device sync completes it and
   // finish_batch then fills outs
   int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs);

@@ -616,6 +616,46 @@ void Engine::add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep) {
   add_feature(this, f, mode, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
 }
 
+// fv[lo, hi) appended in order.  Large batches (configs 4-5: 800-1500 features x 26-31 clones) are built
+// in contiguous chunks on the pool (add_feature only reads the batch's clone / camera tables), then the
+// chunks are stitched in order with their offsets shifted: the same tables as the sequential loop.
+void Engine::add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_t lo, size_t hi, int mode, int rep) {
+  const size_t nf = hi - lo;
+  if (nf < 256 || pool_.threads() == 1) {
+    for (size_t i = lo; i < hi; i++) add_feature_to_batch(b, fv[i], mode, rep);
+    return;
+  }
+  struct Part {
+    std::vector<DFeat> feats;
+    std::vector<DMeas> meas;
+    std::vector<DVar> vars;
+    int rows = 0;
+  };
+  const size_t nparts = std::min(nf / 64, (size_t)pool_.threads() * 4);
+  std::vector<Part> parts(nparts);
+  pool_.parallel_for(nparts, 1, [&](size_t p0, size_t p1) {
+    for (size_t p = p0; p < p1; p++) {
+      Part &P = parts[p];
+      const size_t a = lo + nf * p / nparts, e = lo + nf * (p + 1) / nparts;
+      for (size_t i = a; i < e; i++)
+        add_feature(this, fv[i], mode, rep, o_, b.cams, b.slot_of_time, b.clones, P.feats, P.meas, P.vars, P.rows,
+                    nullptr, -1);
+    }
+  });
+  for (Part &P : parts) {
+    const int mo = (int)b.meas.size(), vo = (int)b.vars.size(), ro = b.rows;
+    for (DFeat F : P.feats) {
+      F.meas_off += mo;
+      F.var_off += vo;
+      F.row_off += ro;
+      b.feats.push_back(F);
+    }
+    b.meas.insert(b.meas.end(), P.meas.begin(), P.meas.end());
+    b.vars.insert(b.vars.end(), P.vars.begin(), P.vars.end());
+    b.rows += P.rows;
+  }
+}
+
 // Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
 // Returns the number of stacked rows written to H_all.
 int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs) {
@@ -747,13 +787,19 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   if (fv.empty()) return 0;
   std::vector<double> clonetimes;
   for (auto &c : clones_) clonetimes.push_back(c.first);
+  std::vector<uint8_t> few(fv.size());
+  pool_.parallel_for(fv.size(), 64, [&](size_t b0, size_t e0) {
+    for (size_t i = b0; i < e0; i++) {
+      fv[i]->clean_old_measurements(clonetimes);
+      few[i] = fv[i]->count() < 2;
+    }
+  });
   std::vector<FeatP> keep;
-  for (auto &f : fv) {
-    f->clean_old_measurements(clonetimes);
-    if (f->count() < 2)
-      f->to_delete = true;
+  for (size_t i = 0; i < fv.size(); i++) {
+    if (few[i])
+      fv[i]->to_delete = true;
     else
-      keep.push_back(f);
+      keep.push_back(fv[i]);
   }
   fv = keep;
   if (fv.empty()) return 0;
@@ -762,9 +808,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   if (shard_.enabled && (int)fv.size() >= shard_.min_features) return msckf_update_sharded(fv);
   Batch b;
   build_clone_cam_tables(b, false);
-  for (auto &f : fv)
-    add_feature(this, f, 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf, o_, b.cams, b.slot_of_time, b.clones,
-                b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+  add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
   // The update is enqueued right behind the feature group: rejected features already have zero rows in
   // H_all and the device skips the P update when no feature was accepted (d_.acc), so the host reads the
   // per-feature results with the update's dx instead of waiting for them in between.

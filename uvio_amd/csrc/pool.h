@@ -8,6 +8,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -33,7 +34,8 @@ class WorkPool {
   }
   int threads() const { return (int)th_.size() + 1; }
 
-  // fn(begin, end) over [0, n) in chunks of `chunk`; the caller works too and returns when all are done
+  // fn(begin, end) over [0, n) in chunks of `chunk`; the caller works too and returns when all are done.
+  // An exception thrown by fn (on any thread) is rethrown here, after every chunk has finished.
   void parallel_for(size_t n, size_t chunk, const std::function<void(size_t, size_t)> &fn) {
     if (n == 0) return;
     if (th_.empty() || n <= chunk) {
@@ -47,6 +49,7 @@ class WorkPool {
       chunk_ = chunk;
       next_.store(0);
       active_ = (int)th_.size();
+      err_ = nullptr;
       gen_++;
     }
     cv_.notify_all();
@@ -54,6 +57,7 @@ class WorkPool {
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [this] { return active_ == 0; });
     job_ = nullptr;
+    if (err_) std::rethrow_exception(err_);
   }
 
  private:
@@ -61,7 +65,12 @@ class WorkPool {
     for (;;) {
       size_t b = next_.fetch_add(chunk_);
       if (b >= n_) break;
-      (*job_)(b, std::min(n_, b + chunk_));
+      try {
+        (*job_)(b, std::min(n_, b + chunk_));
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err_) err_ = std::current_exception();
+      }
     }
   }
   void worker() {
@@ -87,6 +96,7 @@ class WorkPool {
   size_t n_ = 0, chunk_ = 1;
   std::atomic<size_t> next_{0};
   int active_ = 0;
+  std::exception_ptr err_;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };

@@ -161,8 +161,7 @@ int Engine::msckf_update_sharded(std::vector<FeatP> &fv) {
   const int lo = bounds[shard_.rank], hi = bounds[shard_.rank + 1];
   Batch b;
   build_clone_cam_tables(b, false);
-  for (int i = lo; i < hi; i++)
-    add_feature_to_batch(b, fv[i], 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
+  add_features_to_batch(b, fv, (size_t)lo, (size_t)hi, 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
   std::vector<DFeatOut> outs;
   const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
   const int m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
