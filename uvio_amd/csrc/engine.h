@@ -311,6 +311,7 @@ class Engine {
     std::vector<int> hidx;     // canonical column -> covariance id
     const int *hidx_dev = nullptr;  // its staged device copy
     bool finished = false;          // per-feature results read back (finish_batch)
+    bool chi2 = true;               // the batch chi2 kernels ran (run_batch)
     std::vector<FeatP> fptrs;
     int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;
     std::map<double, int> slot_of_time;
@@ -320,7 +321,9 @@ class Engine {
   void add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_t lo, size_t hi, int mode, int rep);
   // wait = false: only enqueue (kernels + result readback); the caller's next device sync completes it and
   // finish_batch then fills outs
-  int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs);
+  // chi2 = false: the feature kernel only (delayed init gates on its own update factor instead)
+  int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs,
+                bool chi2 = true);
   void finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs);
 };
 

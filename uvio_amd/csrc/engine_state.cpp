@@ -266,7 +266,7 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
-  dalloc(&d_.dxneg, cap + 2);
+  dalloc(&d_.dxneg, cap + 4);
   dalloc(&d_.acc, 4);
   dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
@@ -338,7 +338,8 @@ void Engine::dev_sync() {
 }
 
 void Engine::read_dx(const char *who) {
-  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (1 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
+  // [neg | dx (N) | chi2, accepted of a delayed-init chi2 gate (EkfScratch::chi2_gate)]
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (3 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
   dev_sync();
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
 }

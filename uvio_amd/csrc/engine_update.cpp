@@ -658,9 +658,11 @@ void Engine::add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_
 
 // Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
 // Returns the number of stacked rows written to H_all.
-int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs) {
+int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs,
+                      bool chi2) {
   int nf = (int)b.feats.size();
   if (nf == 0) return 0;
+  b.chi2 = chi2;
   if (nf > d_.max_feat || (int)b.meas.size() > d_.max_meas_total || (int)b.vars.size() > d_.max_vars_total ||
       b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol)
     throw HpError(UVIO_HP_E_CAPACITY, "update batch exceeds device capacity");
@@ -713,7 +715,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
   launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
                            max_meas, max_nf);
-  {
+  if (chi2) {
     int max_rows_f = 0;
     for (auto &F : b.feats) {
       int rows_out = (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
@@ -775,7 +777,8 @@ void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
       double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
       double r = (mode == 1) ? rows : rows - 3.0;
       double refl = (mode == 1) ? 0.0 : 12.0 * rows * (nfc + 4.0);
-      timing_.k_feat_flops += refl + 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
+      const double chi2 = b.chi2 ? 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0 : 0.0;
+      timing_.k_feat_flops += refl + chi2;
     }
   }
 }
@@ -990,24 +993,29 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // batch's accepted count (d_.acc) gates initialize_invertible and the EKF update enqueued right
     // behind it, and the host learns the decision with the update's dx (one wait per feature).  The
     // landmark is appended tentatively and withdrawn when the feature was rejected (nothing was written).
+    // The chi2 of StateHelper::initialize uses S = H_up P_up H_up^T + R_up, exactly the S the EKF update
+    // of the same rows factors, so the test runs on that factor (chi2 = |L^-1 r_up|^2, dof = all rows)
+    // instead of a separate chi2 kernel: the feature kernel alone linearizes.
     std::vector<DFeatOut> o1;
-    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1);
+    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1, false);
     // 3) initialize_invertible with rows 0..2 (H_Linv = H_finit^-1 formed on the device from HfR), EKF
     // update with rows 3..
     int n = b.n_canon;
     if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
     launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, nullptr, s2, d_.ekf, d_.fout,
-                           d_.acc);
+                           nullptr);
     // landmark value update H_Linv * resinit (residual column of rows 0..2), read back together with the
     // update's dx; applied first, as initialize_invertible does
     double *resinit = d_.dx_host + d_.ldp + 2;
     HP_HIP(hipMemcpy2DAsync(resinit, sizeof(double), d_.H + n, sizeof(double) * d_.ldh, sizeof(double), 3,
                             hipMemcpyDeviceToHost, d_.stream));
     bool accepted = false;
+    const int nup = 2 * b.feats[0].nmeas - 3;
     auto land = [&]() {
       finish_batch(b, 3, o1);
-      accepted = (o1[0].status == 0);
-      if (!accepted) return false;  // the device skipped the init and the update
+      // [chi2, accepted] of the update factor's gate land at dx[N], dx[N+1] (N with the landmark)
+      accepted = (o1[0].status == 0) && (nup <= 0 || d_.dx_host[N_ + 1] > 0.5);
+      if (!accepted) return false;  // the device skipped the update; the landmark slot is withdrawn
       double HLinv[9], dl[3];
       inv3_cofactor(o1[0].HfR, HLinv);  // the device's formula: identical H_Linv
       for (int a = 0; a < 3; a++)
@@ -1020,8 +1028,13 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     vars_.push_back(lm);
     N_ += 3;
     f->to_delete = true;
-    int nup = 2 * b.feats[0].nmeas - 3;
     if (nup > 0) {
+      struct GateScope {  // the chi2 gate applies to this update only, also when it throws
+        EkfScratch &e;
+        ~GateScope() { e.chi2_gate = nullptr; }
+      } scope{d_.ekf};
+      d_.ekf.chi2_gate = d_.acc;
+      d_.ekf.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * b.feats[0].nmeas, 999)];
       ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
                       b.hidx_dev, land, d_.acc);
     } else {

@@ -138,6 +138,11 @@ struct EkfScratch {
   int *neg;
   double *Dinv;  // 16x16 diagonal-block inverses of a triangular factor: (rmax / 16 + 1) * 256
   const int *gate = nullptr;  // optional device count: when it is 0 the P update is skipped (no rows accepted)
+  // StateHelper::initialize's chi2 test (StateHelper.cpp:458-470) on the update's own factor: when
+  // chi2_gate is set, chi2 = |L^-1 r|^2 of the factored S is compared with chi2_thr right after the
+  // factorization; *chi2_gate (the P-update gate) = accepted, and [chi2, accepted] go to dx[N], dx[N+1]
+  int *chi2_gate = nullptr;
+  double chi2_thr = 0.0;
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.

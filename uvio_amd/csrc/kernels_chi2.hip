@@ -52,6 +52,82 @@ __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, i
   }
 }
 
+// The same product for large batches (configs 4-5: m ~ 80k stacked rows, n = 172-242): 256-thread
+// workgroups own a 64 x 64 tile of T, K runs in slabs of 16 staged in LDS (the H slab as rows, the
+// gathered P_can slab as a 16 x 64 block), each wave computes a 32 x 32 quarter with four MFMA tiles;
+// the next slab's global loads are issued before the current slab's MFMAs (register double buffer).
+// Operand reuse: every staged element feeds 4 MFMAs instead of 1 (k_gemm_HPg reloads per tile).
+constexpr int HPB = 64, HPK = 16;
+__global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict__ H, int m, int n, int ldh,
+                                                        const double *__restrict__ P, int ldp,
+                                                        const int *__restrict__ hidx, double *__restrict__ T, int ldt,
+                                                        int *zero) {
+  __shared__ double As[HPB][HPK + 1];
+  __shared__ double Bs[HPK][HPB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int wr = w >> 1, wc = w & 1;
+  if (zero && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *zero = 0;
+  const int i0 = blockIdx.y * HPB, j0 = blockIdx.x * HPB;
+  // staging map: A slab element e = tid + 256 u (u < 4): row e / 16, k e % 16; B slab: k e / 64, col e % 64
+  int pcol[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int c = j0 + ((tid + 256 * u) & 63);
+    pcol[u] = (c < n) ? hidx[c] : 0;
+  }
+  double ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = tid + 256 * u;
+      const int ar = i0 + (e >> 4), ak = k0 + (e & 15);
+      ra[u] = (ar < m && ak < n) ? H[(size_t)ar * ldh + ak] : 0.0;
+      const int bk = k0 + (e >> 6), bc = j0 + (e & 63);
+      rb[u] = (bk < n && bc < n) ? P[(size_t)hidx[bk] * ldp + pcol[u]] : 0.0;
+    }
+  };
+  dbl4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  load(0);
+  for (int k0 = 0; k0 < n; k0 += HPK) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = tid + 256 * u;
+      As[e >> 4][e & 15] = ra[u];
+      Bs[e >> 6][e & 63] = rb[u];
+    }
+    __syncthreads();
+    if (k0 + HPK < n) load(k0 + HPK);
+#pragma unroll
+    for (int kk = 0; kk < HPK; kk += 4) {
+      double a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        a[t] = As[32 * wr + 16 * t + r16][kk + kq];
+        b[t] = Bs[kk + kq][32 * wc + 16 * t + r16];
+      }
+#pragma unroll
+      for (int ta = 0; ta < 2; ta++)
+#pragma unroll
+        for (int tb = 0; tb < 2; tb++) acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int ta = 0; ta < 2; ta++)
+#pragma unroll
+    for (int tb = 0; tb < 2; tb++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int row = i0 + 32 * wr + 16 * ta + kq + 4 * q, col = j0 + 32 * wc + 16 * tb + r16;
+        if (row < m && col < n) T[(size_t)row * ldt + col] = acc[ta][tb][q];
+      }
+}
+
 size_t chi2_lds_bytes(int max_rows_f, int n) {
   size_t R = max_rows_f;
   return (2 * R * (size_t)(n | 1) + (R + 1) * (R | 1) + 4 * (R + 1)) * sizeof(double);
@@ -187,8 +263,12 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
                        int *acc_count) {
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
-  hipLaunchKernelGGL(k_gemm_HPg, dim3((n + 15) / 16, (m + 15) / 16), dim3(64), 0, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx,
-                     T_all, bp.ldh, acc_count);
+  if (m >= 4096)  // enough 64 x 64 tiles to fill the 256 CUs
+    hipLaunchKernelGGL(k_gemm_HPg_tiled, dim3((n + HPB - 1) / HPB, (m + HPB - 1) / HPB), dim3(256), 0, s, H_all, m, n,
+                       bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
+  else
+    hipLaunchKernelGGL(k_gemm_HPg, dim3((n + 15) / 16, (m + 15) / 16), dim3(64), 0, s, H_all, m, n, bp.ldh, P, bp.ldp,
+                       hidx, T_all, bp.ldh, acc_count);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);

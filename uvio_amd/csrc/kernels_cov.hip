@@ -173,7 +173,87 @@ __global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int 
     }
 }
 
+// The Gram of a large stack (configs 4-5: ~80k rows x 173-243 columns) on the matrix cores: a 256-thread
+// workgroup owns a 64 x 64 upper tile pair of G for one chunk of GCHUNK_BIG rows; rows run in slabs of
+// 16 staged in LDS (the two 16 x 64 column blocks of the slab), each wave accumulates a 32 x 32 quarter
+// with four v_mfma_f64_16x16x4_f64 tiles (A operand = the slab transposed: k = row).  The next slab's
+// loads are issued before the current slab's MFMAs.  Partials: same layout as k_gram (chunk-major,
+// every entry a <= b written).
+constexpr int GB = 64, GK = 16, GCHUNK_BIG = 1024;
+__global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A, int m, int ncol, int ldh,
+                                                   double *__restrict__ partials) {
+  __shared__ double Xs[GK][GB + 1];
+  __shared__ double Ys[GK][GB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int wr = w >> 1, wc = w & 1;
+  const int nt = (ncol + GB - 1) / GB;
+  int pair = blockIdx.x, ti = 0;
+  while (pair >= nt - ti) {
+    pair -= nt - ti;
+    ti++;
+  }
+  const int tj = ti + pair;
+  const int c0i = ti * GB, c0j = tj * GB;
+  const int r0 = blockIdx.y * GCHUNK_BIG, r1 = min(m, r0 + GCHUNK_BIG);
+  double rx[4], ry[4];
+  auto load = [&](int rb) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = tid + 256 * u, row = rb + (e >> 6), c = e & 63;
+      rx[u] = (row < r1 && c0i + c < ncol) ? A[(size_t)row * ldh + c0i + c] : 0.0;
+      ry[u] = (row < r1 && c0j + c < ncol) ? A[(size_t)row * ldh + c0j + c] : 0.0;
+    }
+  };
+  dbl4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  load(r0);
+  for (int rb = r0; rb < r1; rb += GK) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = tid + 256 * u;
+      Xs[e >> 6][e & 63] = rx[u];
+      Ys[e >> 6][e & 63] = ry[u];
+    }
+    __syncthreads();
+    if (rb + GK < r1) load(rb + GK);
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      double a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        a[t] = Xs[kk + kq][32 * wr + 16 * t + r16];
+        b[t] = Ys[kk + kq][32 * wc + 16 * t + r16];
+      }
+#pragma unroll
+      for (int ta = 0; ta < 2; ta++)
+#pragma unroll
+        for (int tb = 0; tb < 2; tb++) acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
+    }
+  }
+  double *out = partials + (size_t)blockIdx.y * ncol * ncol;
+#pragma unroll
+  for (int ta = 0; ta < 2; ta++)
+#pragma unroll
+    for (int tb = 0; tb < 2; tb++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int a = c0i + 32 * wr + 16 * ta + kq + 4 * q, b = c0j + 32 * wc + 16 * tb + r16;
+        if (a < ncol && b < ncol) out[(size_t)a * ncol + b] = acc[ta][tb][q];
+      }
+}
+
 void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, double *partials, int *nchunks_out) {
+  if (m >= 8 * GCHUNK_BIG) {
+    const int ntb = (ncol + GB - 1) / GB, nchb = (m + GCHUNK_BIG - 1) / GCHUNK_BIG;
+    *nchunks_out = nchb;
+    hipLaunchKernelGGL(k_gram_mfma, dim3(ntb * (ntb + 1) / 2, nchb), dim3(256), 0, s, A, m, ncol, ldh, partials);
+    return;
+  }
   int nt = (ncol + GT - 1) / GT;
   int pairs = nt * (nt + 1) / 2;
   int nch = gram_num_chunks(m);
@@ -513,6 +593,21 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
   hipLaunchKernelGGL(k_ekf_S, gS, dim3(256), 0, s, H, ldh, r, n, hidx, sc.M, sigma2, Sup);
 }
 
+// chi2 = |y|^2 (y = L^-1 r from k_ekf_small; one wavefront, fixed order) against thr: the P-update gate,
+// and [chi2, accepted] into out[0], out[1] (read back with dx)
+__global__ void k_chi2_gate(const double *__restrict__ y, int r, double thr, int *__restrict__ gate,
+                            double *__restrict__ out) {
+  double s = 0.0;
+  for (int k = threadIdx.x; k < r; k += 64) s += y[k] * y[k];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if (threadIdx.x == 0) {
+    const int acc = !(s > thr);
+    *gate = acc;
+    out[0] = s;
+    out[1] = acc;
+  }
+}
+
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc) {
   size_t bytes = ekf_small_lds_bytes(r);
@@ -523,6 +618,10 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   ensure_lds_attrs();
   hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Lf, sc.y, Sg,
                      use_lds);
+  if (sc.chi2_gate) {  // StateHelper::initialize's chi2 test on this factor
+    hipLaunchKernelGGL(k_chi2_gate, dim3(1), dim3(64), 0, s, sc.y, r, sc.chi2_thr, sc.chi2_gate, sc.dx + N);
+    sc.gate = sc.chi2_gate;
+  }
   launch_trsm_lt(s, sc.M, r, nullptr, N, r, Lf, r, sc.Dinv, sc.W);  // W = M L^-T
   int nb = (N + 15) / 16;
   hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg, sc.gate);
