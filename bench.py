@@ -133,7 +133,7 @@ class Driver:
                 return t
 
 
-PMC_FILES = {"cfg2": "profiles/r01_pmc_traffic.json"}
+PMC_FILES = {"cfg2": "profiles/r01e_pmc_traffic.json"}
 
 
 def pmc_traffic(workload):

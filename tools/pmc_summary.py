@@ -22,7 +22,11 @@ for k in sorted(set(F) | set(W)):
     f, w = F.get(k, [0.0]), W.get(k, [0.0])
     fb, wb = 1024 * sum(f) / len(f), 1024 * sum(w) / len(w)
     out["kernels"][k] = {"launches": len(f), "fetch": 2.0 * fb, "write": wb, "traffic": 2.0 * fb + wb}
-grp = ["k_feature", "k_gemm_HPg", "k_chi2"]
-out["feature_group_traffic"] = sum(out["kernels"][k]["traffic"] for k in grp if k in out["kernels"])
+grp = ["k_feature", "k_gemm_HPg", "k_gemm_HPg_tiled", "k_chi2"]
+# per launch group (one k_feature each; the T GEMM is one of the two variants; the delayed-init groups run
+# no chi2 kernel): the group kernels' total bytes over the number of groups
+ngroups = out["kernels"]["k_feature"]["launches"]
+out["feature_group_traffic"] = sum(out["kernels"][k]["traffic"] * out["kernels"][k]["launches"]
+                                   for k in grp if k in out["kernels"]) / ngroups
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print("feature group traffic per launch: %.0f bytes" % out["feature_group_traffic"])
