@@ -10,11 +10,11 @@
 #include "dense_lds.h"
 using namespace uvhp;
 
-__global__ void __launch_bounds__(512) k_test(const double *Ain, int n, int nrows, int which, int mode, double *out,
+__global__ void __launch_bounds__(1024) k_test(const double *Ain, int n, int nrows, int which, int mode, double *out,
                                               long long *ts, double *gA) {
   extern __shared__ double lds[];
   const int ld = n | 1;
-  double *A = (which == 5) ? gA : lds, *wsp = lds + (size_t)nrows * ld;
+  double *A = (which == 5 || which == 4) ? gA : lds, *wsp = lds + (size_t)nrows * ld;
   for (int e = threadIdx.x; e < nrows * n; e += blockDim.x) A[(e / n) * ld + e % n] = Ain[e];
   __syncthreads();
   long long t0 = clock64();
@@ -22,6 +22,8 @@ __global__ void __launch_bounds__(512) k_test(const double *Ain, int n, int nrow
     ldl_panel4(A, ld, n, nrows, wsp);
   } else if (which == 5) {
     ldl_panel4(A, ld, n, nrows, wsp);
+  } else if (which == 3 || which == 4) {
+    ldl_blk16(A, ld, n, nrows, wsp);
   } else {
     ldl_inplace(A, ld, n, nrows);
   }
@@ -64,9 +66,9 @@ int main(int argc, char **argv) {
   double *dO2, *dG;
   (void)hipMalloc(&dO2, 8 * nrows * n);
   (void)hipMalloc(&dG, 8 * (size_t)nrows * (n | 1));
-  const char *names[] = {"lds  ", "regs ", "panel4", "panel16", "panel16-global", "panel4-global", "panel8", "panel8-global"};
+  const char *names[] = {"lds  ", "regs ", "panel4", "blk16", "blk16-global", "panel4-global"};
   std::vector<std::vector<double>> outs;
-  for (int which : {0, 2, 5}) {
+  for (int which : {0, 2, 5, 3, 4}) {
     for (int it = 0; it < 3; it++) {
       (void)hipEventRecord(e0);
       hipLaunchKernelGGL(k_test, dim3(1), dim3(nt), bytes, 0, dA, n, nrows, which, mode, dO2, dts, dG);

@@ -184,4 +184,119 @@ __device__ void ldl_panel4(double *A, int ld, int n, int nrows, double *Lp) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-level blocked LDL^T, same in/out convention (and the same nrows x 4 scratch Lp) as ldl_panel4.
+// Columns go in blocks of 16; inside a block the 4-column steps of ldl_panel4 update only the block's
+// own later columns (one 16-wide tile column), and the rest of the matrix gets the block's rank-16
+// update once, as four v_mfma_f64_16x16x4_f64 per tile with the normalized multipliers formed from the
+// stored unnormalized entries and the block's 1/d_k.  The per-step work that scales with the trailing
+// size runs once per 16 columns instead of once per 4.
+__device__ void ldl_blk16(double *A, int ld, int n, int nrows, double *Lp) {
+  __shared__ double Dv[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  for (int KB = 0; KB < n; KB += 16) {
+    const int nb = min(n, KB + 16);  // columns KB .. nb-1 form the block
+    for (int K = KB; K < nb; K += 4) {
+      const int B = min(4, nb - K);
+      double c[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int p = 0; p <= q; p++) c[q][p] = (q < B) ? A[(size_t)(K + q) * ld + K + p] : 0.0;
+      double dinv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        dinv[k] = (k < B) ? 1.0 / c[k][k] : 0.0;
+#pragma unroll
+        for (int q = k + 1; q < 4; q++) {
+          const double a = c[q][k] * dinv[k];
+#pragma unroll
+          for (int p = k + 1; p <= q; p++) c[q][p] -= a * c[p][k];
+        }
+      }
+      if (threadIdx.x < 4) Dv[K - KB + threadIdx.x] = dinv[threadIdx.x];
+      __syncthreads();  // every wave has read the diagonal block before the panel rows overwrite it
+      for (int i = K + threadIdx.x; i < nrows; i += blockDim.x) {
+        double v[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) v[p] = (p < B && K + p <= i) ? A[(size_t)i * ld + K + p] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (k < B && i > K + k) {
+            const double a = v[k] * dinv[k];
+#pragma unroll
+            for (int p = k + 1; p < 4; p++)
+              if (p < B && K + p <= i) v[p] -= a * c[p][k];
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+          if (p < B && K + p <= i) A[(size_t)i * ld + K + p] = v[p];
+          Lp[(size_t)i * 4 + p] = (p < B && K + p < i) ? v[p] * dinv[p] : 0.0;
+        }
+      }
+      __syncthreads();
+      // rank-4 update of the block's own later columns (one tile column)
+      const int T0 = K + B;
+      if (T0 < nb) {
+        const int nti = (nrows - T0 + 15) / 16;
+        for (int ti = wid; ti < nti; ti += nw) {
+          const int i0 = T0 + 16 * ti, j0 = T0;
+          dbl4 acc;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int row = i0 + kq + 4 * q, col = j0 + r16;
+            acc[q] = (row < nrows && col < nb && col <= row) ? A[(size_t)row * ld + col] : 0.0;
+          }
+          const int arow = i0 + r16, bcol = j0 + r16;
+          const double a = (arow < nrows) ? -Lp[(size_t)arow * 4 + kq] : 0.0;
+          const double b = (bcol < nb && kq < B) ? A[(size_t)bcol * ld + K + kq] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int row = i0 + kq + 4 * q, col = j0 + r16;
+            if (row < nrows && col < nb && col <= row) A[(size_t)row * ld + col] = acc[q];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // rank-16 update of everything right of the block (rows >= nb, columns nb .. n-1)
+    if (nb < n) {
+      const int BB = nb - KB;
+      const int nti = (nrows - nb + 15) / 16, ntj = (n - nb + 15) / 16;
+      for (int t = wid; t < nti * ntj; t += nw) {
+        const int ti = t / ntj, tj = t - ti * ntj;
+        if (tj > ti) continue;
+        const int i0 = nb + 16 * ti, j0 = nb + 16 * tj;
+        const int arow = i0 + r16, bcol = j0 + r16;
+        const double *Ar = A + (size_t)min(arow, nrows - 1) * ld + KB;
+        const double *Br = A + (size_t)min(bcol, n - 1) * ld + KB;
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int kk = 4 * u + kq;
+          a[u] = (arow < nrows && kk < BB) ? -Ar[kk] * Dv[kk] : 0.0;
+          b[u] = (bcol < n && kk < BB) ? Br[kk] : 0.0;
+        }
+        dbl4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int row = i0 + kq + 4 * q, col = j0 + r16;
+          acc[q] = (row < nrows && col < n && col <= row) ? A[(size_t)row * ld + col] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int row = i0 + kq + 4 * q, col = j0 + r16;
+          if (row < nrows && col < n && col <= row) A[(size_t)row * ld + col] = acc[q];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace uvhp

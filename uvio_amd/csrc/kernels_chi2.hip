@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
   for (int j = tid; j < R; j += blockDim.x) S[R * ldS + j] = Hg[(size_t)j * ldh + n];
   __syncthreads();
   CHI2_TS(1)
-  ldl_panel4(S, ldS, R, R + 1, Lp);
+  ldl_blk16(S, ldS, R, R + 1, Lp);
   CHI2_TS(2)
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {

@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Su
         }
       });
   __syncthreads();
-  ldl_panel4(A, ld, r, r + 1, Lp);
+  ldl_blk16(A, ld, r, r + 1, Lp);
   ldl_to_chol(A, ld, r, r + 1);
   for (int j = threadIdx.x; j < r; j += blockDim.x) y_out[j] = A[(size_t)r * ld + j];
   for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
         if (b <= a) A[(size_t)a * ld + b] = v;
       });
   __syncthreads();
-  ldl_panel4(A, ld, n, n, Lp);
+  ldl_blk16(A, ld, n, n, Lp);
   ldl_to_chol(A, ld, n, n);
   const int na = n + 1;
   for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
@@ -734,7 +734,7 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
         if (b <= a) A[(size_t)a * ld + b] = v;
       });
   __syncthreads();
-  ldl_panel4(A, ld, n, n + 1, Lp);
+  ldl_blk16(A, ld, n, n + 1, Lp);
   ldl_to_chol(A, ld, n, n + 1);
   for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[(size_t)n * ld + j];
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
