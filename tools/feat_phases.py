@@ -1,4 +1,6 @@
-"""Per-phase cycle counts of the feature kernel (UVIO_HP_FEAT_TS debug dump) on the bench stream."""
+"""Per-phase cycle counts of the feature kernel (UVIO_HP_FEAT_TS debug dump) on a bench workload.
+
+usage: python tools/feat_phases.py [cfg2|cfg3|cfg4|cfg5]"""
 import os, sys
 sys.path.insert(0, '.')
 import numpy as np
@@ -7,12 +9,15 @@ path = "gpurun_out/feat_ts.bin"
 if os.path.exists(path):
     os.remove(path)
 import bench, uvio_amd as U
-opts = bench.cfg2_options(U)
-sim = bench.make_stream(opts, 80, seed=5)
-frames = bench.render_frames(sim, 80, "cuda")
+wl = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+opts = bench.workload_options(U, wl)
+warm = int(opts.max_clone_size) + 8
+sim = bench.make_stream(opts, warm + 12, seed=5, workload=wl)
+images = bench.WORKLOADS[wl][1] == "images"
+frames = bench.render_frames(sim, warm + 12, "cuda") if images else None
 mgr = U.VioManager(opts)
 drv = bench.Driver(sim, mgr, frames)
-for _ in range(60):
+for _ in range(warm):
     drv.step()
 os.environ["UVIO_HP_FEAT_TS"] = path
 for _ in range(10):

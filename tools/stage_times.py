@@ -39,3 +39,4 @@ for k in keys:
     print("  %-14s %8.3f ms" % (k, 1e3 * np.mean(acc[k])))
 for k in ["device_syncs", "n_msckf", "msckf_rows"]:
     print("  %-14s %8.1f" % (k, np.mean(acc[k])))
+mgr.close()  # prints the UVIO_HP_HOST_PROF sections when enabled

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "hp_common.h"
+#include "hprof.h"
 #include "kernels.h"
 #include "pool.h"
 #include "tracker.h"
@@ -218,6 +219,8 @@ class Engine {
   std::vector<double> chi2_table_;
   ShardComm shard_;
   WorkPool pool_;
+  std::vector<FeatP> pending_delete_;  // features handed to an updater this frame (cleanup candidates)
+  HostProf hprof_;                     // UVIO_HP_HOST_PROF section timer (debug)
   void shard_allreduce(double *dev, size_t count);
   int msckf_update_sharded(std::vector<FeatP> &fv);
 

@@ -339,6 +339,7 @@ void Engine::dev_sync() {
 
 void Engine::read_dx(const char *who) {
   // [neg | dx (N) | chi2, accepted of a delayed-init chi2 gate (EkfScratch::chi2_gate)]
+  HPROF("read_dx");
   HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (3 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
   dev_sync();
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
@@ -418,7 +419,10 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
     stage_flush();
   }
   d_.ekf.gate = gate;
-  launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
+  {
+    HPROF("ekf_rows.launch");
+    launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
+  }
   read_dx("EKFUpdate");
   if (!apply || apply()) apply_dx(d_.dx_host);
 }

@@ -276,18 +276,21 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   if (timestamp_ != t) return 0;
 
   std::vector<FeatP> feats_lost, feats_marg, feats_slam;
+  auto t_sel = clk::now();
   // FeatureDatabase::features_not_containing_newer(t, false, true)
   // (and features_containing(margtimestep)): per-feature flags on the pool, lists built in db_ order
   std::unordered_set<const Feature *> in_marg;
   {
     const bool do_marg = (int)clones_.size() > o_.max_clone_size || (int)clones_.size() > 5;
     const double mt = do_marg ? margtimestep() : 0.0, ts = timestamp_;
-    std::vector<std::pair<FeatP, uint8_t>> all;  // feature, bit 0 lost, bit 1 marg
+    // pointers to the map's values (no shared_ptr copies: a reference-count round trip per feature
+    // costs more than the scan at cfg4's database sizes); nothing inserts into db_ during the scan
+    std::vector<std::pair<const FeatP *, uint8_t>> all;  // feature, bit 0 lost, bit 1 marg
     all.reserve(db_.size());
-    for (auto &kv : db_) all.emplace_back(kv.second, 0);
+    for (auto &kv : db_) all.emplace_back(&kv.second, 0);
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
-        const Feature &f = *all[i].first;
+        const Feature &f = **all[i].first;
         if (f.to_delete) continue;
         bool newer = false, has = false;
         for (auto &p : f.tracks) {
@@ -303,10 +306,10 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       }
     });
     for (auto &a : all) {
-      if (a.second & 1) feats_lost.push_back(a.first);
+      if (a.second & 1) feats_lost.push_back(*a.first);
       if (a.second & 2) {
-        feats_marg.push_back(a.first);
-        in_marg.insert(a.first.get());
+        feats_marg.push_back(*a.first);
+        in_marg.insert(a.first->get());
       }
     }
   }
@@ -373,7 +376,16 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   up.insert(up.end(), feats_maxtracks.begin(), feats_maxtracks.end());
   std::sort(up.begin(), up.end(), [](const FeatP &a, const FeatP &b) { return a->count() < b->count(); });
   if ((int)up.size() > o_.max_msckf_in_update) up.erase(up.begin(), up.end() - o_.max_msckf_in_update);
+  // every feature the updaters may flag to_delete (the MSCKF list, SLAM updates, delayed inits); a
+  // frame that returns early keeps its entries for the next frame's cleanup
+  pending_delete_.insert(pending_delete_.end(), up.begin(), up.end());
+  pending_delete_.insert(pending_delete_.end(), feats_slam.begin(), feats_slam.end());
   timing_.n_msckf = (int)up.size();
+  if (hprof_.on) {
+    auto &a = hprof_.acc["select"];
+    a.first += secs(t_sel, clk::now());
+    a.second++;
+  }
   int rc = msckf_update(up);
   if (rc) return rc;
   auto rT4 = clk::now();
@@ -389,14 +401,16 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   rc = slam_delayed_init(slam_delayed);
   if (rc) return rc;
   auto rT6 = clk::now();
+  HPROF("marg.total");
   for (auto &f : up) f->to_delete = true;
-  // FeatureDatabase::cleanup
-  for (auto it = db_.begin(); it != db_.end();) {
-    if (it->second->to_delete)
-      it = db_.erase(it);
-    else
-      it++;
+  // FeatureDatabase::cleanup: only features handed to an updater can carry to_delete, so they are
+  // erased by key (erasing a node keeps the others' iteration order, as the reference's scan does)
+  for (auto &f : pending_delete_) {
+    if (!f->to_delete) continue;
+    auto it = db_.find(f->featid);
+    if (it != db_.end() && it->second == f) db_.erase(it);
   }
+  pending_delete_.clear();
   rc = slam_change_anchors();
   if (rc) return rc;
   if ((int)clones_.size() > o_.max_clone_size) {
@@ -772,7 +786,7 @@ void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
     timing_.k_feat_launches += 1;
     timing_.k_feat_s += 1e-3 * ms;
     // algorithmic FP64 FLOPs (SURVEY.md §8(d) F_feat) of the features that reached the projection
-    for (int i = 0; i < nf; i++) {
+    for (int i = 0; i < nf && mode != 2; i++) {  // mode 2 triangulates only
       if (outs[i].status == 1 || outs[i].status == 2) continue;
       double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
       double r = (mode == 1) ? rows : rows - 3.0;
@@ -788,6 +802,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   stage_ = "UpdaterMSCKF::update";
   last_msckf_.clear();
   if (fv.empty()) return 0;
+  HPROF("msckf.total");
   std::vector<double> clonetimes;
   for (auto &c : clones_) clonetimes.push_back(c.first);
   std::vector<uint8_t> few(fv.size());
@@ -810,16 +825,24 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
     throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
   if (shard_.enabled && (int)fv.size() >= shard_.min_features) return msckf_update_sharded(fv);
   Batch b;
-  build_clone_cam_tables(b, false);
-  add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
+  {
+    HPROF("msckf.build");
+    build_clone_cam_tables(b, false);
+    add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
+  }
   // The update is enqueued right behind the feature group: rejected features already have zero rows in
   // H_all and the device skips the P update when no feature was accepted (d_.acc), so the host reads the
   // per-feature results with the update's dx instead of waiting for them in between.
   std::vector<DFeatOut> outs;
   const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
-  const int m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
+  int m;
+  {
+    HPROF("msckf.run_batch");
+    m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
+  }
   const int n = b.n_canon, ncol = n + 1;
   auto results = [&]() {
+    HPROF("msckf.results");
     finish_batch(b, 0, outs);
     int acc = 0, acc_rows = 0;
     for (size_t i = 0; i < outs.size(); i++) {
@@ -952,13 +975,16 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
   if (rep != 0 && rep != 2 && rep != 4) throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
   double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
   // 1) triangulate + refine all features against the pre-update state (UpdaterSLAM.cpp:119-141)
+  HPROF("di.total");
   std::vector<DFeatOut> tri;
   {
+    HPROF("di.tri");
     Batch b;
     build_clone_cam_tables(b, false);
     for (auto &f : fv)
       add_feature(this, f, 2, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
-    run_batch(b, 2, s2, o_.slam_chi2_multipler, true, tri);
+    // triangulation only: the rows and chi2 come from the per-feature mode-3 linearization below
+    run_batch(b, 2, s2, o_.slam_chi2_multipler, true, tri, false);
   }
   for (size_t i = 0; i < fv.size(); i++) {
     FeatP &f = fv[i];
@@ -984,8 +1010,11 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     lm->set_xyz(relr ? f->p_FinA : f->p_FinG, false);
     lm->set_xyz(relr ? f->p_FinA : f->p_FinG, true);
     Batch b;
-    build_clone_cam_tables(b, false);
-    add_feature(this, f, 3, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+    {
+      HPROF("di.prep");
+      build_clone_cam_tables(b, false);
+      add_feature(this, f, 3, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+    }
     // mode 3: linearize at the batch triangulation (p_in = p_FinA, p_in_fej = p_FinG), as the reference
     // triangulates the whole batch before the per-feature initialize loop
     for (int k = 0; k < 3; k++) b.feats[0].p_in[k] = f->p_FinA[k], b.feats[0].p_in_fej[k] = f->p_FinG[k];
@@ -997,7 +1026,10 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // of the same rows factors, so the test runs on that factor (chi2 = |L^-1 r_up|^2, dof = all rows)
     // instead of a separate chi2 kernel: the feature kernel alone linearizes.
     std::vector<DFeatOut> o1;
-    run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1, false);
+    {
+      HPROF("di.run_batch");
+      run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1, false);
+    }
     // 3) initialize_invertible with rows 0..2 (H_Linv = H_finit^-1 formed on the device from HfR), EKF
     // update with rows 3..
     int n = b.n_canon;
@@ -1028,6 +1060,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     vars_.push_back(lm);
     N_ += 3;
     f->to_delete = true;
+    HPROF("di.ekf");
     if (nup > 0) {
       struct GateScope {  // the chi2 gate applies to this update only, also when it throws
         EkfScratch &e;

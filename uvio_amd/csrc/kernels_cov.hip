@@ -841,12 +841,25 @@ __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const 
   __syncthreads();
   const double *HLinv = Hinv;
   int t = threadIdx.x + blockIdx.x * blockDim.x;
-  if (blockIdx.x == 0 && threadIdx.x < 9) {
-    int a = threadIdx.x / 3, b = threadIdx.x % 3;
-    double acc = 0.0;
-    for (int k = 0; k < n; k++) acc += Hx[(size_t)a * ldh + k] * M[(size_t)hidx[k] * 3 + b];
-    // M.selfadjointView<Upper>(): use the upper element for both halves
-    S3[threadIdx.x] = acc + (a == b ? s2 : 0.0);
+  if (blockIdx.x == 0) {
+    // S3 = Hx M[hidx, :] + s2 I: each of the 9 entries summed by 28 threads over strided k, the 28
+    // partials then added in fixed order (blockDim = 256 >= 9 x 28)
+    __shared__ double part[9][28];
+    const int e = threadIdx.x / 28, j = threadIdx.x % 28;
+    if (e < 9) {
+      const int a = e / 3, b = e % 3;
+      double acc = 0.0;
+      for (int k = j; k < n; k += 28) acc += Hx[(size_t)a * ldh + k] * M[(size_t)hidx[k] * 3 + b];
+      part[e][j] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 9) {
+      const int a = threadIdx.x / 3, b = threadIdx.x % 3;
+      double acc = 0.0;
+      for (int q = 0; q < 28; q++) acc += part[threadIdx.x][q];
+      // M.selfadjointView<Upper>(): use the upper element for both halves
+      S3[threadIdx.x] = acc + (a == b ? s2 : 0.0);
+    }
   }
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x < 9) {

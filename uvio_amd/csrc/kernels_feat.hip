@@ -252,9 +252,11 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   for (int j = tid; j <= bp.n_canon; j += 256) canon2loc[j] = -1;
   for (int e = tid; e < rows * ldl; e += 256) Hl[e] = 0.0;
   __syncthreads();
-  for (int v = 0; v < F.nvar; v++) {
-    DVar dv = vars[F.var_off + v];
-    for (int k = tid; k < dv.size; k += 256) {
+  // one thread per (variable, element): the variable records load in parallel (sizes are <= 8)
+  for (int e = tid; e < F.nvar * 8; e += 256) {
+    const DVar dv = vars[F.var_off + (e >> 3)];
+    const int k = e & 7;
+    if (k < dv.size) {
       loc2pid[dv.loc + k] = dv.pid + k;
       if (dv.canon >= 0) canon2loc[dv.canon + k] = dv.loc + k;
     }
@@ -422,6 +424,18 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   }
   __syncthreads();
   const int status0 = sh.status;
+  if (F.mode == 2) {  // batch triangulation for the delayed initialization: no rows are formed
+    if (tid == 0) {
+      DFeatOut o;
+      for (int k = 0; k < 3; k++) o.p_FinA[k] = sh.p_FinA[k], o.p_FinG[k] = sh.p_FinG[k];
+      o.chi2 = -1.0;
+      for (int k = 0; k < 9; k++) o.HfR[k] = 0.0;
+      o.status = status0;
+      o.rows = 0;
+      out[f] = o;
+    }
+    return;
+  }
 
   FEAT_TS(2)
   // ---- Jacobians (one thread per measurement) ----
@@ -610,49 +624,86 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
 
   FEAT_TS(3)
   // ---- left-nullspace projection: 3 Householder reflections of H_f (MSCKF) ----
+  // Wave 0 forms the reflectors v_c (beta_c) on H_f's 3 columns in sequence.  The local Jacobian
+  // [Hl | r] then takes all three in one read and one write pass per column: with w_c = v_c^T A,
+  //   u_1 = b_1 w_1,  u_2 = b_2 (w_2 - g21 u_1),  u_3 = b_3 (w_3 - g31 u_1 - g32 u_2),  g_ab = v_a^T v_b,
+  // H_3 H_2 H_1 A = A - v_1 u_1 - v_2 u_2 - v_3 u_3.
   int r0 = 0;  // first output row in Hl
   if (status0 == 0 && F.mode != 1) {
-    for (int c = 0; c < 3; c++) {
-      if (wave == 0) {
-        // v = x - alpha e_c over rows c..rows-1
+    if (wave == 0) {
+      for (int c = 0; c < 3; c++) {
+        // v = x - alpha e_c over rows c..rows-1 (zero above)
         double ss = 0.0;
         for (int i = c + lane; i < rows; i += 64) {
           double x = Hf[i * 3 + c];
           ss += x * x;
         }
         ss = wave_sum(ss);
-        double x0 = Hf[c * 3 + c];
-        double alpha = (x0 > 0) ? -sqrt(ss) : sqrt(ss);
-        for (int i = c + lane; i < rows; i += 64) {
-          V[i * 3 + c] = (i == c) ? (x0 - alpha) : Hf[i * 3 + c];
+        const double x0 = Hf[c * 3 + c];
+        const double alpha = (x0 > 0) ? -sqrt(ss) : sqrt(ss);
+        for (int i = lane; i < rows; i += 64) {
+          V[i * 3 + c] = (i < c) ? 0.0 : (i == c) ? (x0 - alpha) : Hf[i * 3 + c];
           // the reflected column c is alpha e_c (H_finit = the upper 3x3 of the reflected H_f)
-          Hf[i * 3 + c] = (i == c) ? alpha : 0.0;
+          if (i >= c) Hf[i * 3 + c] = (i == c) ? alpha : 0.0;
         }
-        double vn = ss - x0 * x0 + (x0 - alpha) * (x0 - alpha);
-        if (lane == 0) sh.beta[c] = (vn > 0) ? 2.0 / vn : 0.0;
-      }
-      __syncthreads();
-      double b = sh.beta[c];
-      // apply to Hf columns c+1..2 and all Hl columns
-      int ncols_tot = (3 - c - 1) + ldl;
-      for (int j = tid; j < ncols_tot; j += 256) {
-        bool isf = j < (3 - c - 1);
-        double *colp;
-        int stride;
-        if (isf) {
-          colp = Hf + (c + 1 + j);
-          stride = 3;
-        } else {
-          colp = Hl + (j - (3 - c - 1));
-          stride = ldl;
+        const double vn = ss - x0 * x0 + (x0 - alpha) * (x0 - alpha);
+        const double b = (vn > 0) ? 2.0 / vn : 0.0;
+        if (lane == 0) sh.beta[c] = b;
+        wave_sync();
+        for (int j = c + 1; j < 3; j++) {  // reflect H_f's later columns
+          double d = 0.0;
+          for (int i = c + lane; i < rows; i += 64) d += V[i * 3 + c] * Hf[i * 3 + j];
+          d = b * wave_sum(d);
+          for (int i = c + lane; i < rows; i += 64) Hf[i * 3 + j] -= d * V[i * 3 + c];
         }
-        double s = 0.0;
-        for (int i = c; i < rows; i++) s += V[i * 3 + c] * colp[(size_t)i * stride];
-        s *= b;
-        for (int i = c; i < rows; i++) colp[(size_t)i * stride] -= s * V[i * 3 + c];
+        wave_sync();
       }
-      __syncthreads();
+      double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+      for (int i = lane; i < rows; i += 64) {
+        const double a = V[i * 3], bq = V[i * 3 + 1], cq = V[i * 3 + 2];
+        g0 += bq * a;
+        g1 += cq * a;
+        g2 += cq * bq;
+      }
+      g0 = wave_sum(g0);
+      g1 = wave_sum(g1);
+      g2 = wave_sum(g2);
+      if (lane == 0) red[0] = g0, red[1] = g1, red[2] = g2;
     }
+    __syncthreads();
+    const double b1 = sh.beta[0], b2 = sh.beta[1], b3 = sh.beta[2];
+    const double g21 = red[0], g31 = red[1], g32 = red[2];
+    for (int j = tid; j < ldl; j += 256) {
+      double w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0}, w3[4] = {0, 0, 0, 0};
+      int i = 0;
+      for (; i + 4 <= rows; i += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const double a = Hl[(size_t)(i + q) * ldl + j];
+          w1[q] += V[(i + q) * 3] * a;
+          w2[q] += V[(i + q) * 3 + 1] * a;
+          w3[q] += V[(i + q) * 3 + 2] * a;
+        }
+      }
+      for (; i < rows; i++) {
+        const double a = Hl[(size_t)i * ldl + j];
+        w1[0] += V[i * 3] * a;
+        w2[0] += V[i * 3 + 1] * a;
+        w3[0] += V[i * 3 + 2] * a;
+      }
+      const double s1 = (w1[0] + w1[1]) + (w1[2] + w1[3]);
+      const double s2 = (w2[0] + w2[1]) + (w2[2] + w2[3]);
+      const double s3 = (w3[0] + w3[1]) + (w3[2] + w3[3]);
+      const double u1 = b1 * s1;
+      const double u2 = b2 * (s2 - g21 * u1);
+      const double u3 = b3 * (s3 - g31 * u1 - g32 * u2);
+#pragma unroll 4
+      for (int k = 0; k < rows; k++) {
+        double *p = Hl + (size_t)k * ldl + j;
+        *p -= V[k * 3] * u1 + V[k * 3 + 1] * u2 + V[k * 3 + 2] * u3;
+      }
+    }
+    __syncthreads();
     r0 = 3;
   }
   const int R = rows - r0;
@@ -664,14 +715,25 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   // ---- output rows (canonical dense columns; zeros when rejected) ----
   const int out_r0 = (F.mode == 0) ? 3 : 0;
   const int nrows_out = max(rows - out_r0, 0);
-  for (int e = tid; e < nrows_out * (bp.n_canon + 1); e += 256) {
-    int i = e / (bp.n_canon + 1), j = e % (bp.n_canon + 1);
-    double v = 0.0;
-    if (status == 0) {
-      int lc = (j == bp.n_canon) ? nf : canon2loc[j];
-      if (lc >= 0) v = Hl[(size_t)(out_r0 + i) * ldl + lc];
+  {
+    // one wave per row, lanes over the canonical columns (n_canon + 1 <= 512: 8 column slots per lane,
+    // their local column cached in registers); rejected features write zero rows
+    const int nc = bp.n_canon + 1;
+    int lcs[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int j = lane + 64 * q;
+      lcs[q] = (status != 0 || j >= nc) ? -1 : (j == bp.n_canon) ? nf : canon2loc[j];
     }
-    H_all[(size_t)(F.row_off + i) * bp.ldh + j] = v;
+    for (int i = wave; i < nrows_out; i += 4) {
+      const double *src = Hl + (size_t)(out_r0 + i) * ldl;
+      double *dst = H_all + (size_t)(F.row_off + i) * bp.ldh;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int j = lane + 64 * q;
+        if (j < nc) dst[j] = (lcs[q] >= 0) ? src[lcs[q]] : 0.0;
+      }
+    }
   }
   if (tid == 0) {
     DFeatOut o;
@@ -693,6 +755,9 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
                               const DVar *vars, const DClone *clones, const DCam *cams, const double *P,
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf) {
   if (bp.nfeat <= 0) return;
+  if (bp.n_canon >= 512 || max_meas > 64)  // canon2loc[512]; one lane per measurement
+    throw std::runtime_error("k_feature: n_canon " + std::to_string(bp.n_canon) + " / measurements per feature " +
+                             std::to_string(max_meas) + " beyond the kernel's limits (511 / 64)");
   size_t bytes = feature_lds_bytes(max_meas, max_nf);
   static int granted = -1;
   if (granted < 0) granted = set_dyn_lds((const void *)k_feature, 156 * 1024);
