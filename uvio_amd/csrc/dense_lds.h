@@ -63,12 +63,19 @@ __device__ void ldl_inplace(double *A, int ld, int n, int nrows) {
 
 // LDL^T (as left by ldl_inplace) -> Cholesky factor L D^1/2 in place; extra rows -> b L^-T.
 __device__ void ldl_to_chol(double *A, int ld, int n, int nrows) {
+  // d_k^-1/2 formed once per column (256-column chunks through LDS), then the rows scale by it
+  __shared__ double isd[256];
   const int c0 = threadIdx.x % kRowLanes, rstep = blockDim.x / kRowLanes;
-  for (int i = threadIdx.x / kRowLanes; i < nrows; i += rstep) {
-    const int jmax = min(i - 1, n - 1);
-    for (int k = c0; k <= jmax; k += kRowLanes) A[i * ld + k] *= 1.0 / sqrt(A[k * ld + k]);
+  for (int k0 = 0; k0 < n; k0 += 256) {
+    const int k1 = min(n, k0 + 256);
+    for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) isd[k - k0] = 1.0 / sqrt(A[k * ld + k]);
+    __syncthreads();
+    for (int i = threadIdx.x / kRowLanes; i < nrows; i += rstep) {
+      const int jmax = min(min(i - 1, n - 1), k1 - 1);
+      for (int k = k0 + c0; k <= jmax; k += kRowLanes) A[i * ld + k] *= isd[k - k0];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int k = threadIdx.x; k < n; k += blockDim.x) A[k * ld + k] = sqrt(A[k * ld + k]);
   __syncthreads();
 }

@@ -142,12 +142,17 @@ struct DeviceBufs {
   double *dx_host = nullptr;
   int *neg_host = nullptr;
   DFeatOut *fout_host = nullptr;
+  double *aux_host = nullptr;  // 16 host-only landing slots (delayed-init residual, shard totals)
+  int fout_pending = 0;        // feature results not yet copied: they ride along with the next readback
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // feature-kernel timing
   // upload staging ring: small host tables of one launch group are packed into pinned memory and sent
   // with ONE copy (stage / stage_flush); the kernels read the device copy directly
   char *stg_h = nullptr, *stg_d = nullptr;
   size_t stg_cap = 0, stg_used = 0, stg_flushed = 0;
-  double *dxneg = nullptr;  // [negative-diagonal count (8 B) | dx (ldp)]: one readback per update
+  // [negative-diagonal count (8 B) | dx (cap + 15) | feature results (max features)], mirrored in pinned
+  // memory at neg_host / dx_host / fout_host: an update's dx and its batch's results come back in ONE copy
+  double *dxneg = nullptr;
+  size_t dx_bytes = 0;  // bytes of [count | dx] (the offset of the feature results)
   // feature sharding: the all-reduced [G upper triangle (max_ncol^2) | accepted features | accepted rows]
   double *shard = nullptr, *shard_host = nullptr;
   int *acc = nullptr;       // accepted features of the last update batch (gates its P update)
@@ -245,8 +250,8 @@ class Engine {
   void upload_P_full(const std::vector<double> &Ph, int N);
   void download_P(std::vector<double> &Ph);
   void cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
-                     const std::vector<double> &Q);
-  VarP clone_imu_pose(const double *dnc, bool do_dt);
+                     const std::vector<double> &Q, const std::vector<int> *rows = nullptr);
+  VarP clone_imu_pose(const double *dnc, bool do_dt, const double *staged = nullptr);
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
   void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,

@@ -643,13 +643,15 @@ int Engine::propagate_and_clone(double timestamp) {
   accumulate_phi(prop, Phi, Qd, n);
   double lw[3];
   last_w(prop, lw);
+  // the clone's time-offset column (augment_clone, StateHelper.cpp:579-616) goes up with Phi / Qd
+  double dnc[6] = {lw[0], lw[1], lw[2], imu_->val[7], imu_->val[8], imu_->val[9]};
+  const bool do_dt = o_.do_calib_camera_timeoffset != 0;
+  const double *ddnc = do_dt ? stage(dnc, 6) : nullptr;
   cov_propagate(imu_->id, n, ids, Phi, Qd);
   timestamp_ = timestamp;
   last_prop_time_offset_ = t_off_new;
-  // augment_clone (StateHelper.cpp:579-616)
   if (clones_.find(timestamp_) != clones_.end()) return UVIO_HP_E_STATE;
-  double dnc[6] = {lw[0], lw[1], lw[2], imu_->val[7], imu_->val[8], imu_->val[9]};
-  VarP pose = clone_imu_pose(dnc, o_.do_calib_camera_timeoffset != 0);
+  VarP pose = clone_imu_pose(dnc, do_dt, ddnc);
   clones_[timestamp_] = pose;
   return 0;
 }

@@ -195,7 +195,7 @@ Engine::~Engine() {
   if (shard_.nccl) rccl_comm_destroy(shard_.nccl);
   tracker_.reset();
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
-                  d_.fout, d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
+                  d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
                   d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -252,7 +252,6 @@ void Engine::alloc_device() {
   dalloc(&d_.vars, d_.max_vars_total);
   dalloc(&d_.clones, C + 4);
   dalloc(&d_.cams, UVIO_HP_MAX_CAMS);
-  dalloc(&d_.fout, maxf);
   dalloc(&d_.chi2, 1000);
   dalloc(&d_.H, (size_t)d_.max_rows * d_.ldh);
   dalloc(&d_.Tall, (size_t)d_.max_rows * d_.ldh);
@@ -266,7 +265,9 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
-  dalloc(&d_.dxneg, cap + 4);
+  d_.dx_bytes = sizeof(double) * (cap + 16);
+  HP_HIP(hipMalloc((void **)&d_.dxneg, d_.dx_bytes + sizeof(DFeatOut) * maxf));
+  d_.fout = (DFeatOut *)((char *)d_.dxneg + d_.dx_bytes);
   dalloc(&d_.acc, 4);
   dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
@@ -277,12 +278,14 @@ void Engine::alloc_device() {
   // pinned staging: batch upload + small downloads
   d_.pin_bytes = sizeof(DFeat) * maxf + sizeof(DMeas) * d_.max_meas_total + sizeof(DVar) * d_.max_vars_total +
                  sizeof(DClone) * (C + 4) + sizeof(DCam) * UVIO_HP_MAX_CAMS + sizeof(int) * (d_.max_ncol + d_.max_rows) +
-                 sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 4096;
+                 sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + sizeof(double) * 16 + 4096;
   HP_HIP(hipHostMalloc(&d_.pin, d_.pin_bytes, hipHostMallocDefault));
-  char *pb = (char *)d_.pin + d_.pin_bytes - (sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + 64);
+  char *pb = (char *)d_.pin + d_.pin_bytes -
+             (d_.dx_bytes + sizeof(DFeatOut) * maxf + sizeof(double) * 16 + 64);
   d_.neg_host = (int *)pb;  // same layout as dxneg
   d_.dx_host = (double *)(pb + sizeof(double));
-  d_.fout_host = (DFeatOut *)(pb + sizeof(double) * (cap + 16));
+  d_.fout_host = (DFeatOut *)(pb + d_.dx_bytes);
+  d_.aux_host = (double *)(pb + d_.dx_bytes + sizeof(DFeatOut) * maxf);
   // upload staging (batch tables, Phi / Q, column maps)
   d_.stg_cap = d_.pin_bytes + 2 * 64 * 64 * sizeof(double) + 64 * 1024;
   HP_HIP(hipHostMalloc(&d_.stg_h, d_.stg_cap, hipHostMallocDefault));
@@ -331,6 +334,11 @@ void Engine::stage_flush() {
 }
 
 void Engine::dev_sync() {
+  if (d_.fout_pending) {  // feature results of a batch whose update did not read back (yet)
+    HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * d_.fout_pending, hipMemcpyDeviceToHost,
+                          d_.stream));
+    d_.fout_pending = 0;
+  }
   auto t0 = std::chrono::steady_clock::now();
   HP_HIP(hipStreamSynchronize(d_.stream));
   timing_.sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -340,21 +348,27 @@ void Engine::dev_sync() {
 void Engine::read_dx(const char *who) {
   // [neg | dx (N) | chi2, accepted of a delayed-init chi2 gate (EkfScratch::chi2_gate)]
   HPROF("read_dx");
-  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, sizeof(double) * (3 + (size_t)N_), hipMemcpyDeviceToHost, d_.stream));
+  // [count | dx], and the pending batch results behind them in the same copy
+  const size_t bytes = d_.fout_pending ? d_.dx_bytes + sizeof(DFeatOut) * d_.fout_pending
+                                       : sizeof(double) * (3 + (size_t)N_);
+  d_.fout_pending = 0;
+  HP_HIP(hipMemcpyAsync(d_.neg_host, d_.dxneg, bytes, hipMemcpyDeviceToHost, d_.stream));
   dev_sync();
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
 }
 
-// StateHelper::EKFPropagation on the device (StateHelper.cpp:36-114)
+// StateHelper::EKFPropagation on the device (StateHelper.cpp:36-114).  The new block is rows
+// s0 .. s0+p-1, or the rows listed in `rows` (several variables at once, block-row Phi).
 void Engine::cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
-                           const std::vector<double> &Q) {
+                           const std::vector<double> &Q, const std::vector<int> *rows) {
   int q = (int)iold.size();
   if (p > 64 || q > 256) throw HpError(UVIO_HP_E_CAPACITY, "propagation block too large");
   const double *dPhi = stage(Phi.data(), (size_t)p * q);
   const double *dQ = stage(Q.data(), (size_t)p * p);
   const int *diold = stage(iold.data(), (size_t)q);
+  const int *drows = rows ? stage(rows->data(), rows->size()) : nullptr;
   stage_flush();
-  launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, diold, q, dPhi, dQ, d_.T);
+  launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, diold, q, dPhi, dQ, d_.T, drows);
 }
 
 void Engine::check_neg_diag(const char *who) {
@@ -366,12 +380,15 @@ void Engine::check_neg_diag(const char *who) {
 }
 
 // StateHelper::clone(imu->pose()) + augment_clone (StateHelper.cpp:341-391, 579-616)
-VarP Engine::clone_imu_pose(const double *dnc, bool do_dt) {
+VarP Engine::clone_imu_pose(const double *dnc, bool do_dt, const double *staged) {
   if (N_ + 6 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
   const double *ddnc = d_.dnc;
   if (do_dt) {
-    ddnc = stage(dnc, 6);
-    stage_flush();
+    ddnc = staged;  // already on the device (staged and flushed by the caller)
+    if (!ddnc) {
+      ddnc = stage(dnc, 6);
+      stage_flush();
+    }
   }
   launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, ddnc, do_dt ? 1 : 0);
   VarP pose = mk(V_POSE, 6, 7);

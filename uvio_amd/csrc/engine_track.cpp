@@ -4,6 +4,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <unordered_map>
+#include <unordered_set>
 
 #include "tracker.h"
 
@@ -513,6 +515,7 @@ void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, cons
     std::vector<int> boxes;  // drawn into a clone of the LEFT mask (TrackKLT.cpp:713)
     std::vector<KeyPt> kp;
     std::vector<size_t> kid;
+    const std::unordered_set<size_t> left_ids(ids0.begin(), ids0.end());
     for (size_t i = 0; i < pts1.size(); i++) {
       const KeyPt &k = pts1[i];
       const int x = (int)k.x, y = (int)k.y, edge = 10;
@@ -521,7 +524,7 @@ void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, cons
       if (xc < 0 || xc >= scw || yc < 0 || yc >= sch) continue;
       const int xg = (int)std::floor(k.x / size_x), yg = (int)std::floor(k.y / size_y);
       if (xg < 0 || xg >= grid_x_ || yg < 0 || yg >= grid_y_) continue;
-      const bool is_stereo = std::find(ids0.begin(), ids0.end(), ids1[i]) != ids0.end();
+      const bool is_stereo = left_ids.count(ids1[i]) != 0;
       if (close.at(xc, yc) > 127 && !is_stereo) continue;
       if (mask_px(mask1, W, x, y) > 127) continue;
       close.at(xc, yc) = 255;
@@ -731,16 +734,15 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   const int Wl = nl.w[0], Hl = nl.h[0], Wr = nr.w[0], Hr = nr.h[0];
   std::vector<KeyPt> gl, gr;
   std::vector<size_t> gil, gir;
+  // first index of each id among the right points (the reference's linear search returns the first)
+  std::unordered_map<size_t, size_t> first_r;
+  first_r.reserve(ir_old.size() * 2);
+  for (size_t n = 0; n < ir_old.size(); n++) first_r.emplace(ir_old[n], n);
   for (size_t i = 0; i < pl_new.size(); i++) {
     if (pl_new[i].x < 0 || pl_new[i].y < 0 || (int)pl_new[i].x > Wl || (int)pl_new[i].y > Hl) continue;
-    bool found = false;
-    size_t ir = 0;
-    for (size_t n = 0; n < ir_old.size(); n++)
-      if (il_old[i] == ir_old[n]) {
-        found = true;
-        ir = n;
-        break;
-      }
+    const auto fr = first_r.find(il_old[i]);
+    const bool found = fr != first_r.end();
+    const size_t ir = found ? fr->second : 0;
     if (mask_ll[i] && found && mask_rr[ir]) {
       if (pr_new[ir].x < 0 || pr_new[ir].y < 0 || (int)pr_new[ir].x >= Wr || (int)pr_new[ir].y >= Hr) continue;
       gl.push_back(pl_new[i]);
@@ -752,12 +754,14 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
       gil.push_back(il_old[i]);
     }
   }
+  std::unordered_set<size_t> in_gir(gir.begin(), gir.end());  // membership in gir, kept in step with it
   for (size_t i = 0; i < pr_new.size(); i++) {
     if (pr_new[i].x < 0 || pr_new[i].y < 0 || (int)pr_new[i].x >= Wr || (int)pr_new[i].y >= Hr) continue;
-    const bool added = std::find(gir.begin(), gir.end(), ir_old[i]) != gir.end();
+    const bool added = in_gir.count(ir_old[i]) != 0;
     if (mask_rr[i] && !added) {
       gr.push_back(pr_new[i]);
       gir.push_back(ir_old[i]);
+      in_gir.insert(ir_old[i]);
     }
   }
   for (size_t i = 0; i < gl.size(); i++) {

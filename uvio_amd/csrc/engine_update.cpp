@@ -221,10 +221,13 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
     camids.push_back(cid);
   }
   if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream));
-  tracker_->feed(t, ncam, cam_ids, imgs, strides, masks, device_imgs,
-                 [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
-                   db_update(id, tt, (size_t)cam, u, v, un, vn);
-                 });
+  {
+    HPROF("track.feed");
+    tracker_->feed(t, ncam, cam_ids, imgs, strides, masks, device_imgs,
+                   [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
+                     db_update(id, tt, (size_t)cam, u, v, un, vn);
+                   });
+  }
   return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait);
 }
 
@@ -261,6 +264,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   auto rT2 = clk::now();
   if (timestamp_ > t) return UVIO_HP_E_ORDER;
   if (timestamp_ != t) {
+    HPROF("prop");
     int rc = propagate_and_clone(t);
     if (rc) return rc;
   }
@@ -739,7 +743,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
                       max_rows_f, d_.acc);
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
-  HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * nf, hipMemcpyDeviceToHost, d_.stream));
+  d_.fout_pending = nf;  // copied with the next readback (read_dx) or before the next wait (dev_sync)
   if (!wait && !tsdump && !mdump) return b.rows;  // the caller's next sync completes the batch (finish_batch)
   dev_sync();
   finish_batch(b, mode, outs);
@@ -1034,13 +1038,12 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // update with rows 3..
     int n = b.n_canon;
     if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
+    // the residual column of rows 0..2 lands behind the chi2 gate's [chi2, accepted] (dx[N+3], dx[N+4] once
+    // the landmark is appended) and comes back with the update's dx readback
+    const int N0 = N_;
     launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, nullptr, s2, d_.ekf, d_.fout,
-                           nullptr);
-    // landmark value update H_Linv * resinit (residual column of rows 0..2), read back together with the
-    // update's dx; applied first, as initialize_invertible does
-    double *resinit = d_.dx_host + d_.ldp + 2;
-    HP_HIP(hipMemcpy2DAsync(resinit, sizeof(double), d_.H + n, sizeof(double) * d_.ldh, sizeof(double), 3,
-                            hipMemcpyDeviceToHost, d_.stream));
+                           nullptr, d_.ekf.dx + N0 + 5);
+    const double *resinit = d_.dx_host + N0 + 5;
     bool accepted = false;
     const int nup = 2 * b.feats[0].nmeas - 3;
     auto land = [&]() {
@@ -1055,7 +1058,6 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       lm->update(dl);
       return true;
     };
-    const int N0 = N_;
     lm->id = N_;
     vars_.push_back(lm);
     N_ += 3;
@@ -1071,7 +1073,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
                       b.hidx_dev, land, d_.acc);
     } else {
-      dev_sync();
+      read_dx("initialize_invertible");  // the batch results and the residual column
       land();
     }
     if (accepted) {
@@ -1089,6 +1091,24 @@ int Engine::slam_change_anchors() {
   stage_ = "UpdaterSLAM::change_anchors";
   if ((int)clones_.size() <= o_.max_clone_size) return 0;
   double mt = margtimestep();
+  // The landmarks' propagations are batched into one EKFPropagation with a block-row Phi: each
+  // landmark's rows reference only its own inputs (old/new anchor clone, calibration, itself), so the
+  // sequential per-landmark propagations of the reference compose to exactly this single one.
+  std::vector<int> b_rows, b_iold;
+  std::vector<std::vector<std::pair<int, double>>> b_phi;  // per batched row: (cov id, value)
+  auto flush = [&]() {
+    if (b_rows.empty()) return;
+    std::unordered_map<int, int> col;
+    for (size_t k = 0; k < b_iold.size(); k++) col[b_iold[k]] = (int)k;
+    const int pr = (int)b_rows.size(), q = (int)b_iold.size();
+    std::vector<double> Phi((size_t)pr * q, 0.0), Q((size_t)pr * pr, 0.0);
+    for (int x = 0; x < pr; x++)
+      for (auto &e : b_phi[x]) Phi[(size_t)x * q + col.at(e.first)] += e.second;
+    cov_propagate(0, pr, b_iold, Phi, Q, &b_rows);
+    b_rows.clear();
+    b_iold.clear();
+    b_phi.clear();
+  };
   for (auto &kv : slam_) {
     VarP lm = kv.second;
     if (lm->rep == 0 || lm->rep == 1) continue;
@@ -1232,11 +1252,21 @@ int Engine::slam_change_anchors() {
     std::vector<int> iold_ids;
     for (auto &o : order)
       for (int k = 0; k < o.second; k++) iold_ids.push_back(o.first + k);
-    cov_propagate(lm->id, 3, iold_ids, Phi, Q);
+    if (b_rows.size() + 3 > 63 || b_iold.size() + iold_ids.size() > 256) flush();
+    for (int id : iold_ids)
+      if (std::find(b_iold.begin(), b_iold.end(), id) == b_iold.end()) b_iold.push_back(id);
+    for (int i = 0; i < 3; i++) {
+      b_rows.push_back(lm->id + i);
+      std::vector<std::pair<int, double>> rowv;
+      for (int c = 0; c < cur; c++)
+        if (Phi[(size_t)i * cur + c] != 0.0) rowv.push_back({iold_ids[c], Phi[(size_t)i * cur + c]});
+      b_phi.push_back(rowv);
+    }
     lm->anchor_time = timestamp_;
     lm->set_xyz(p_new, false);
     lm->set_xyz(p_new_fej, true);
   }
+  flush();
   return 0;
 }
 

@@ -96,7 +96,7 @@ struct DBatchParams {
 // EKFPropagation (StateHelper.cpp:36-114) for a contiguous new block [s0, s0+p) with old index list
 // iold (q entries, device), Phi (p x q) and Q (p x p) in device memory.  T is N x p scratch.
 void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
-                          const double *Phi, const double *Q, double *T);
+                          const double *Phi, const double *Q, double *T, const int *rows = nullptr);
 // StateHelper::clone of imu->pose() + augment_clone time-offset term (StateHelper.cpp:341-391,579-616)
 void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt);
 // StateHelper::marginalize (StateHelper.cpp:271-339): Pout <- P without rows/cols [m0, m0+ms)
@@ -161,10 +161,11 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc);
 // StateHelper::initialize_invertible for a 3-dof variable appended at N (StateHelper.cpp:484-577)
-// fout != nullptr: H_Linv = inverse of fout->HfR (formed on the device); gate: skipped when *gate == 0
+// fout != nullptr: H_Linv = inverse of fout->HfR (formed on the device); gate: skipped when *gate == 0;
+// resout != nullptr: receives the residual column of rows 0..2 (Hx[a][n]), for the host's value update
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc,
-                            const DFeatOut *fout = nullptr, const int *gate = nullptr);
+                            const DFeatOut *fout = nullptr, const int *gate = nullptr, double *resout = nullptr);
 double chi2_quantile95(int dof);
 
 // Raise a kernel's dynamic-LDS limit to `want` bytes, capped so static + dynamic LDS fits the CU's

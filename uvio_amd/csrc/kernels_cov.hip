@@ -33,29 +33,39 @@ __global__ void k_prop_T(const double *__restrict__ P, int ld, int N, int p, con
   T[(size_t)i * p + a] = acc;
 }
 
-// rows/cols of the new block <- T, block <- Q(upper-sym) + Phi * T[iold,:]   (StateHelper.cpp:88-101)
-__global__ void k_prop_write(double *__restrict__ P, int ld, int N, int s0, int p, const int *__restrict__ iold, int q,
-                             const double *__restrict__ Phi, const double *__restrict__ Q, const double *__restrict__ T) {
+// rows/cols of the new block <- T, block <- Q(upper-sym) + Phi * T[iold,:]   (StateHelper.cpp:88-101).
+// The new block is rows s0 .. s0+p-1, or the listed rows (rows != nullptr): several variables
+// propagated at once with a block-row Phi (each row of Phi references only its own variable's inputs).
+__global__ void k_prop_write(double *__restrict__ P, int ld, int N, int s0, const int *__restrict__ rows, int p,
+                             const int *__restrict__ iold, int q, const double *__restrict__ Phi,
+                             const double *__restrict__ Q, const double *__restrict__ T) {
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= N * p) return;
   int i = idx / p, a = idx % p;
-  if (i >= s0 && i < s0 + p) {
-    int x = i - s0;
+  int x = -1;
+  if (rows) {
+    for (int k = 0; k < p; k++)
+      if (rows[k] == i) x = k;
+  } else if (i >= s0 && i < s0 + p) {
+    x = i - s0;
+  }
+  const int col = rows ? rows[a] : s0 + a;
+  if (x >= 0) {
     double acc = (x <= a) ? Q[x * p + a] : Q[a * p + x];
     for (int c = 0; c < q; c++) acc += Phi[x * q + c] * T[(size_t)iold[c] * p + a];
-    P[(size_t)i * ld + s0 + a] = acc;
+    P[(size_t)i * ld + col] = acc;
   } else {
     double v = T[(size_t)i * p + a];
-    P[(size_t)i * ld + s0 + a] = v;
-    P[(size_t)(s0 + a) * ld + i] = v;
+    P[(size_t)i * ld + col] = v;
+    P[(size_t)col * ld + i] = v;
   }
 }
 
 void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
-                          const double *Phi, const double *Q, double *T) {
+                          const double *Phi, const double *Q, double *T, const int *rows) {
   int n = N * p, bs = 256, gs = (n + bs - 1) / bs;
   hipLaunchKernelGGL(k_prop_T, dim3(gs), dim3(bs), 0, s, P, ld, N, p, iold, q, Phi, T);
-  hipLaunchKernelGGL(k_prop_write, dim3(gs), dim3(bs), 0, s, P, ld, N, s0, p, iold, q, Phi, Q, T);
+  hipLaunchKernelGGL(k_prop_write, dim3(gs), dim3(bs), 0, s, P, ld, N, s0, rows, p, iold, q, Phi, Q, T);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -829,8 +839,9 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
 __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
                                   const double *__restrict__ Hx, int ldh, int n, const int *__restrict__ hidx,
                                   const double *__restrict__ HLinv_in, double s2, const DFeatOut *__restrict__ fout,
-                                  const int *__restrict__ gate) {
+                                  const int *__restrict__ gate, double *__restrict__ resout) {
   __shared__ double S3[9], PLL[9], Hinv[9];
+  if (resout && blockIdx.x == 0 && threadIdx.x < 3) resout[threadIdx.x] = Hx[(size_t)threadIdx.x * ldh + n];
   if (gate && *gate == 0) return;
   if (threadIdx.x == 0) {
     if (fout)
@@ -888,12 +899,12 @@ __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const 
 
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc, const DFeatOut *fout,
-                            const int *gate) {
+                            const int *gate, double *resout) {
   dim3 gM(1, (N + 15) / 16);
   hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M, (int *)nullptr);
   int nt = N * 3;
   hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
-                     HLinv, s2, fout, gate);
+                     HLinv, s2, fout, gate, resout);
 }
 
 static void ensure_lds_attrs() {

@@ -172,7 +172,7 @@ int Engine::msckf_update_sharded(std::vector<FeatP> &fv) {
   launch_shard_pack(d_.stream, d_.partials, nch, ncol, d_.fout, (int)b.feats.size(), d_.acc, d_.shard);
   shard_allreduce(d_.shard, count);
   launch_shard_unpack(d_.stream, d_.shard, ncol, d_.acc);
-  double *tot_host = d_.dx_host + d_.ldp;  // [accepted, rows] of all ranks, read back with dx
+  double *tot_host = d_.aux_host + 4;  // [accepted, rows] of all ranks, read back with dx
   HP_HIP(hipMemcpyAsync(tot_host, d_.shard + (size_t)ncol * ncol, 2 * sizeof(double), hipMemcpyDeviceToHost,
                         d_.stream));
   auto results = [&]() {
