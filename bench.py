@@ -133,18 +133,21 @@ class Driver:
                 return t
 
 
-PMC_FILES = {"cfg2": "profiles/r01e_pmc_traffic.json"}
+# newest first: the PMC passes of the current kernels (tools/gpu_final.sh), then earlier rounds'
+PMC_FILES = {"cfg2": ["profiles/r01f_pmc_traffic_cfg2.json", "profiles/r01e_pmc_traffic.json"],
+             "cfg4": ["profiles/r01f_pmc_traffic_cfg4.json", "profiles/r01_pmc_traffic_cfg4.json"]}
 
 
 def pmc_traffic(workload):
     """(HBM bytes per feature-group launch, source) from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
     WRITE_SIZE, tools/pmc_summary.py) of this workload, or (None, None) if absent."""
-    path = PMC_FILES.get(workload, "profiles/r01_pmc_traffic_%s.json" % workload)
-    try:
-        with open(os.path.join(ROOT, path)) as f:
-            return json.load(f)["feature_group_traffic"], path
-    except (OSError, KeyError, ValueError):
-        return None, None
+    for path in PMC_FILES.get(workload, ["profiles/r01_pmc_traffic_%s.json" % workload]):
+        try:
+            with open(os.path.join(ROOT, path)) as f:
+                return json.load(f)["feature_group_traffic"], path
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
 def max_over_ranks(x, device="cuda"):
