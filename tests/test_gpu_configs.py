@@ -102,6 +102,32 @@ def test_cfg5_long_run_matches_oracle_counts():
     assert _rel(out["g"][-1]["x"], out["o"][-1]["x"]) < 1e-4
 
 
+def test_upload_staging_recycling_is_invisible():
+    """Large MSCKF batches write their tables straight into the upload staging ring; with a ring that
+    recycles every few batches (UVIO_HP_STAGE_BYTES) the run must be bit-identical to the default one."""
+    import uvio_amd as U
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(_cfg("uzhfpv_outdoor_45"), max_msckf_in_update=400, max_slam_features=10,
+                          max_slam_in_update=5, dt_slam_delay=0.3)
+    n = 40
+    runs = []
+    for cap in (None, 1 << 20):
+        if cap:
+            os.environ["UVIO_HP_STAGE_BYTES"] = str(cap)
+        try:
+            s = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=400, frac_long=0.2)
+            g = U.VioManager(opts)
+        finally:
+            os.environ.pop("UVIO_HP_STAGE_BYTES", None)
+        snaps = []
+        s.run(g, n_frames=n, on_frame=lambda nf, t: snaps.append(_snap(g)))
+        g.close()
+        runs.append(snaps)
+    assert max(a["timing"]["n_msckf"] for a in runs[0]) >= 256  # the direct-staging path ran
+    for a, b in zip(*runs):
+        assert np.array_equal(a["x"], b["x"]) and np.array_equal(a["P"], b["P"])
+
+
 def test_tracks_bit_exact_cfg3_fisheye():
     """TrackKLT on rendered equidistant 512x512 stereo frames: ids and uv equal to the oracle tracker's after
     every frame, pyramids included (test_gpu_track.py does the same for the radtan EuRoC rig)."""

@@ -267,6 +267,9 @@ class Engine {
   void apply_dx(const double *dx);
   // staging (see DeviceBufs): returns the device address the table will have after stage_flush()
   void *stage_bytes(const void *src, size_t bytes);
+  // reserve staging space the caller fills in place (host address in *host); same device-address rule.
+  // Fill it before the next stage / stage_reserve call (either may flush and recycle the ring).
+  void *stage_reserve(size_t bytes, void **host);
   template <class T>
   T *stage(const T *src, size_t n) {
     return (T *)stage_bytes(src, sizeof(T) * n);
@@ -322,6 +325,13 @@ class Engine {
     bool chi2 = true;               // the batch chi2 kernels ran (run_batch)
     std::vector<FeatP> fptrs;
     int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;
+    // large batches write their measurement / variable tables straight into the upload staging
+    // (add_features_to_batch); meas / vars then stay empty and these hold the staged tables
+    const DMeas *meas_dev = nullptr;
+    const DVar *vars_dev = nullptr;
+    size_t n_meas_dev = 0, n_vars_dev = 0;
+    size_t n_meas() const { return meas_dev ? n_meas_dev : meas.size(); }
+    size_t n_vars() const { return vars_dev ? n_vars_dev : vars.size(); }
     std::map<double, int> slot_of_time;
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);

@@ -288,6 +288,8 @@ void Engine::alloc_device() {
   d_.aux_host = (double *)(pb + d_.dx_bytes + sizeof(DFeatOut) * maxf);
   // upload staging (batch tables, Phi / Q, column maps)
   d_.stg_cap = d_.pin_bytes + 2 * 64 * 64 * sizeof(double) + 64 * 1024;
+  // test hook: a smaller ring recycles every few batches (tests/test_gpu_configs.py staging test)
+  if (const char *e = std::getenv("UVIO_HP_STAGE_BYTES")) d_.stg_cap = std::min(d_.stg_cap, (size_t)std::atoll(e));
   HP_HIP(hipHostMalloc(&d_.stg_h, d_.stg_cap, hipHostMallocDefault));
   HP_HIP(hipMalloc(&d_.stg_d, d_.stg_cap));
 }
@@ -321,6 +323,20 @@ void *Engine::stage_bytes(const void *src, size_t bytes) {
     d_.stg_used = d_.stg_flushed = 0;
   }
   if (bytes) std::memcpy(d_.stg_h + d_.stg_used, src, bytes);
+  void *dev = d_.stg_d + d_.stg_used;
+  d_.stg_used += need;
+  return dev;
+}
+
+void *Engine::stage_reserve(size_t bytes, void **host) {
+  const size_t need = (bytes + 255) / 256 * 256;
+  if (need > d_.stg_cap) throw HpError(UVIO_HP_E_CAPACITY, "upload staging exhausted");
+  if (d_.stg_used + need > d_.stg_cap) {
+    stage_flush();
+    dev_sync();
+    d_.stg_used = d_.stg_flushed = 0;
+  }
+  *host = d_.stg_h + d_.stg_used;
   void *dev = d_.stg_d + d_.stg_used;
   d_.stg_used += need;
   return dev;

@@ -631,6 +631,7 @@ static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_
 }
 
 void Engine::add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep) {
+  if (b.meas_dev) throw HpError(UVIO_HP_E_INTERNAL, "add_feature_to_batch: measurements already staged");
   add_feature(this, f, mode, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
 }
 
@@ -660,17 +661,42 @@ void Engine::add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_
                     nullptr, -1);
     }
   });
-  for (Part &P : parts) {
-    const int mo = (int)b.meas.size(), vo = (int)b.vars.size(), ro = b.rows;
-    for (DFeat F : P.feats) {
-      F.meas_off += mo;
-      F.var_off += vo;
+  // the parts' measurement / variable tables go straight into the upload staging, copied in parallel
+  // (no merged host copy); the batch must not hold host tables already
+  if (!b.meas.empty() || !b.vars.empty() || b.meas_dev)
+    throw HpError(UVIO_HP_E_INTERNAL, "add_features_to_batch: batch already holds measurements");
+  std::vector<size_t> mo(nparts + 1, 0), vo(nparts + 1, 0);
+  for (size_t p = 0; p < nparts; p++) {
+    mo[p + 1] = mo[p] + parts[p].meas.size();
+    vo[p + 1] = vo[p] + parts[p].vars.size();
+  }
+  // ONE reservation for both tables, filled before anything else is staged: a second reservation could
+  // flush and recycle the ring while the first one is still unfilled
+  const size_t mbytes = (sizeof(DMeas) * mo[nparts] + 255) / 256 * 256;
+  void *hm = nullptr;
+  char *dm = (char *)stage_reserve(mbytes + sizeof(DVar) * vo[nparts], &hm);
+  void *hv = (char *)hm + mbytes;
+  b.meas_dev = (const DMeas *)dm;
+  b.vars_dev = (const DVar *)(dm + mbytes);
+  b.n_meas_dev = mo[nparts];
+  b.n_vars_dev = vo[nparts];
+  pool_.parallel_for(nparts, 1, [&](size_t p0, size_t p1) {
+    for (size_t p = p0; p < p1; p++) {
+      if (!parts[p].meas.empty())
+        std::memcpy((DMeas *)hm + mo[p], parts[p].meas.data(), sizeof(DMeas) * parts[p].meas.size());
+      if (!parts[p].vars.empty())
+        std::memcpy((DVar *)hv + vo[p], parts[p].vars.data(), sizeof(DVar) * parts[p].vars.size());
+    }
+  });
+  for (size_t p = 0; p < nparts; p++) {
+    const int ro = b.rows;
+    for (DFeat F : parts[p].feats) {
+      F.meas_off += (int)mo[p];
+      F.var_off += (int)vo[p];
       F.row_off += ro;
       b.feats.push_back(F);
     }
-    b.meas.insert(b.meas.end(), P.meas.begin(), P.meas.end());
-    b.vars.insert(b.vars.end(), P.vars.begin(), P.vars.end());
-    b.rows += P.rows;
+    b.rows += parts[p].rows;
   }
 }
 
@@ -681,7 +707,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   int nf = (int)b.feats.size();
   if (nf == 0) return 0;
   b.chi2 = chi2;
-  if (nf > d_.max_feat || (int)b.meas.size() > d_.max_meas_total || (int)b.vars.size() > d_.max_vars_total ||
+  if (nf > d_.max_feat || (int)b.n_meas() > d_.max_meas_total || (int)b.n_vars() > d_.max_vars_total ||
       b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol)
     throw HpError(UVIO_HP_E_CAPACITY, "update batch exceeds device capacity");
   int max_meas = 0, max_nf = 0;
@@ -694,8 +720,8 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   if (lds + 4096 > 160 * 1024) throw HpError(UVIO_HP_E_CAPACITY, "feature LDS footprint too large");
   // the batch tables go up packed in one copy
   const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
-  const DMeas *t_meas = stage(b.meas.data(), b.meas.size());
-  const DVar *t_vars = stage(b.vars.data(), b.vars.size());
+  const DMeas *t_meas = b.meas_dev ? b.meas_dev : stage(b.meas.data(), b.meas.size());
+  const DVar *t_vars = b.vars_dev ? b.vars_dev : stage(b.vars.data(), b.vars.size());
   const DClone *t_clones = stage(b.clones.data(), b.clones.size());
   const DCam *t_cams = stage(b.cams.data(), b.cams.size());
   const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
@@ -724,7 +750,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   bp.fi_max_baseline = o_.fi_max_baseline;
   bp.fi_max_cond = o_.fi_max_cond_number;
   const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
-  if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.meas.size()));
+  if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.n_meas()));
   const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
   if (tsdump) {  // 8 k_feature phases + 4 k_chi2 phases per feature
     HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 16 * nf));
@@ -760,7 +786,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     std::fclose(fp);
   }
   if (mdump) {
-    std::vector<double> h(8 * b.meas.size());
+    std::vector<double> h(8 * b.n_meas());
     HP_HIP(hipMemcpy(h.data(), bp.dbg, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
     HP_HIP(hipFree(bp.dbg));
     FILE *fp = std::fopen(mdump, "ab");
