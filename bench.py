@@ -134,8 +134,10 @@ class Driver:
 
 
 # newest first: the PMC passes of the current kernels (tools/gpu_final.sh), then earlier rounds'
-PMC_FILES = {"cfg2": ["profiles/r01f_pmc_traffic_cfg2.json", "profiles/r01e_pmc_traffic.json"],
-             "cfg4": ["profiles/r01f_pmc_traffic_cfg4.json", "profiles/r01_pmc_traffic_cfg4.json"]}
+PMC_FILES = {"cfg2": ["profiles/r01g_pmc_traffic_cfg2.json", "profiles/r01f_pmc_traffic_cfg2.json",
+                      "profiles/r01e_pmc_traffic.json"],
+             "cfg4": ["profiles/r01g_pmc_traffic_cfg4.json", "profiles/r01f_pmc_traffic_cfg4.json",
+                      "profiles/r01_pmc_traffic_cfg4.json"]}
 
 
 def pmc_traffic(workload):
