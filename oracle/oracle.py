@@ -50,6 +50,17 @@ def load():
         lib.orc_camera_distort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                            C.POINTER(C.c_double), C.POINTER(C.c_double)]
         lib.orc_camera_undistort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        u8, i16, f32, f64, i32 = (C.POINTER(C.c_uint8), C.POINTER(C.c_int16), C.POINTER(C.c_float),
+                                  C.POINTER(C.c_double), C.c_int)
+        lib.orc_equalize_hist.argtypes = [u8, i32, i32, u8]
+        lib.orc_pyr_down.argtypes = [u8, i32, i32, u8]
+        lib.orc_scharr.argtypes = [u8, i32, i32, i16]
+        lib.orc_pyramid_levels.argtypes = [i32, i32, i32, i32]
+        lib.orc_fast.argtypes = [u8, i32, i32, i32, i32, i32, i32, i32, f32, i32, C.POINTER(C.c_int)]
+        lib.orc_corner_subpix.argtypes = [u8, i32, i32, f32, i32, i32, i32, C.c_double]
+        lib.orc_lk.argtypes = [u8, u8, i32, i32, i32, i32, i32, C.c_float, f32, f32, u8, i32]
+        lib.orc_ransac_mask.argtypes = [f32, f32, f32, f32, i32, C.c_double, C.c_double, i32, u8]
+        lib.orc_fundamental_7pt.argtypes = [f64, f64, f64, f64, f64]
         _lib = lib
     return _lib
 
@@ -115,6 +126,99 @@ def camera_distort(cam, xy):
     dzeta = np.zeros((n, 2, 8))
     lib.orc_camera_distort(C.byref(cam), n, _dp(xy), _dp(uv), _dp(dzn), _dp(dzeta))
     return uv, dzn, dzeta
+
+
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _f32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _img(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    assert img.ndim == 2
+    return img, img.shape[1], img.shape[0]
+
+
+def equalize_hist(img):
+    """cv::equalizeHist restatement (oracle/src/tracker.cpp)."""
+    img, w, h = _img(img)
+    out = np.empty_like(img)
+    load().orc_equalize_hist(_u8(img), w, h, _u8(out))
+    return out
+
+
+def pyr_down(img):
+    """cv::pyrDown restatement: ((w+1)/2, (h+1)/2), 5x5 binomial, BORDER_REFLECT_101."""
+    img, w, h = _img(img)
+    out = np.empty(((h + 1) // 2, (w + 1) // 2), dtype=np.uint8)
+    load().orc_pyr_down(_u8(img), w, h, _u8(out))
+    return out
+
+
+def scharr(img):
+    """calcSharrDeriv restatement: (h, w, 2) int16 (dx, dy)."""
+    img, w, h = _img(img)
+    out = np.empty((h, w, 2), dtype=np.int16)
+    load().orc_scharr(_u8(img), w, h, out.ctypes.data_as(C.POINTER(C.c_int16)))
+    return out
+
+
+def pyramid_levels(w, h, win=15, max_level=5):
+    return load().orc_pyramid_levels(w, h, win, max_level)
+
+
+def fast(img, thr, roi=None):
+    """cv::FAST(img(roi), thr, nonmax=true) restatement: (k, 3) float32 of (x, y, response), ROI coords."""
+    img, w, h = _img(img)
+    x0, y0, rw, rh = roi if roi is not None else (0, 0, w, h)
+    cap = rw * rh
+    out = np.zeros((cap, 3), dtype=np.float32)
+    n = C.c_int(0)
+    rc = load().orc_fast(_u8(img), w, h, x0, y0, rw, rh, thr, _f32(out), cap, C.byref(n))
+    assert rc == 0
+    return out[:n.value]
+
+
+def corner_subpix(img, pts, win=5, max_iters=20, eps=1e-3):
+    img, w, h = _img(img)
+    p = np.array(pts, dtype=np.float32, order="C").reshape(-1, 2)
+    load().orc_corner_subpix(_u8(img), w, h, _f32(p), p.shape[0], win, max_iters, eps)
+    return p
+
+
+def lk(prev, nxt, p0, p1=None, win=15, max_level=5, max_iters=30, eps=0.01):
+    """calcOpticalFlowPyrLK(OPTFLOW_USE_INITIAL_FLOW) restatement: (p1, status)."""
+    prev, w, h = _img(prev)
+    nxt, w2, h2 = _img(nxt)
+    assert (w, h) == (w2, h2)
+    a = np.array(p0, dtype=np.float32, order="C").reshape(-1, 2)
+    b = np.array(a if p1 is None else p1, dtype=np.float32, order="C").reshape(-1, 2)
+    st = np.zeros(a.shape[0], dtype=np.uint8)
+    load().orc_lk(_u8(prev), _u8(nxt), w, h, win, max_level, max_iters, eps, _f32(a), _f32(b), _u8(st), a.shape[0])
+    return b, st
+
+
+def ransac_mask(p0, p1, thr, conf=0.999, max_iters=1000):
+    """findFundamentalMat(FM_RANSAC) restatement: inlier mask (uint8) of the n correspondences."""
+    p0 = np.asarray(p0, dtype=np.float32)
+    p1 = np.asarray(p1, dtype=np.float32)
+    cols = [np.ascontiguousarray(c) for c in (p0[:, 0], p0[:, 1], p1[:, 0], p1[:, 1])]
+    m = np.zeros(p0.shape[0], dtype=np.uint8)
+    load().orc_ransac_mask(*[_f32(c) for c in cols], p0.shape[0], thr, conf, max_iters, _u8(m))
+    return m
+
+
+def fundamental_7pt(p0, p1):
+    """7-point solver restatement: list of the (<= 3) 3x3 fundamental matrices."""
+    p0 = np.asarray(p0, dtype=np.float64)
+    p1 = np.asarray(p1, dtype=np.float64)
+    cols = [np.ascontiguousarray(c) for c in (p0[:, 0], p0[:, 1], p1[:, 0], p1[:, 1])]
+    F = np.zeros(27)
+    n = load().orc_fundamental_7pt(*[_dp(c) for c in cols], _dp(F))
+    return [F[9 * k:9 * k + 9].reshape(3, 3) for k in range(n)]
 
 
 def camera_undistort(cam, uv):

@@ -256,6 +256,88 @@ int orc_get_pyramid(orc_handle *h, int cam, int level, int *w, int *hgt, uint8_t
   return 0;
 }
 
+// ---- the tracker's OpenCV restatements one by one (tests/test_oracle_tracker.py pins them with
+// property tests: SURVEY.md Appendix A; no OpenCV exists in this image) ----
+static GrayImg gray(const uint8_t *src, int w, int h) {
+  GrayImg g;
+  g.w = w;
+  g.h = h;
+  g.d.assign(src, src + (size_t)w * h);
+  return g;
+}
+int orc_equalize_hist(const uint8_t *src, int w, int h, uint8_t *dst) {
+  GrayImg o = equalize_hist(gray(src, w, h));
+  std::memcpy(dst, o.d.data(), o.d.size());
+  return 0;
+}
+// dst: ((w+1)/2) x ((h+1)/2)
+int orc_pyr_down(const uint8_t *src, int w, int h, uint8_t *dst) {
+  GrayImg o = pyr_down(gray(src, w, h));
+  std::memcpy(dst, o.d.data(), o.d.size());
+  return 0;
+}
+// der: w x h x 2 (dx, dy)
+int orc_scharr(const uint8_t *src, int w, int h, int16_t *der) {
+  std::vector<int16_t> d = scharr_deriv(gray(src, w, h));
+  std::memcpy(der, d.data(), d.size() * sizeof(int16_t));
+  return 0;
+}
+// number of levels buildOpticalFlowPyramid keeps (level 0 included)
+int orc_pyramid_levels(int w, int h, int win, int max_level) {
+  std::vector<uint8_t> z((size_t)w * h, 0);
+  return build_pyramid(gray(z.data(), w, h), win, max_level).levels();
+}
+// FAST on the ROI (x0, y0, rw, rh): out (x, y, response) in ROI coordinates, raster order
+int orc_fast(const uint8_t *src, int w, int h, int x0, int y0, int rw, int rh, int thr, float *out, int cap, int *n) {
+  std::vector<KeyPt> kp = fast_roi(gray(src, w, h), x0, y0, rw, rh, thr);
+  *n = (int)kp.size();
+  for (int i = 0; i < (int)kp.size() && i < cap; i++) {
+    out[3 * i] = kp[i].x;
+    out[3 * i + 1] = kp[i].y;
+    out[3 * i + 2] = kp[i].response;
+  }
+  return (int)kp.size() <= cap ? 0 : UVIO_HP_E_CAPACITY;
+}
+// cornerSubPix in place on n points (x, y)
+int orc_corner_subpix(const uint8_t *src, int w, int h, float *pts, int n, int win, int max_iters, double eps) {
+  std::vector<KeyPt> kp(n);
+  for (int i = 0; i < n; i++) kp[i] = KeyPt{pts[2 * i], pts[2 * i + 1], 0.f};
+  corner_subpix(gray(src, w, h), kp, win, max_iters, eps);
+  for (int i = 0; i < n; i++) pts[2 * i] = kp[i].x, pts[2 * i + 1] = kp[i].y;
+  return 0;
+}
+// calcOpticalFlowPyrLK between two images (pyramids built here); p1 holds the initial guess on entry
+int orc_lk(const uint8_t *prev, const uint8_t *next, int w, int h, int win, int max_level, int max_iters, float eps,
+           const float *p0, float *p1, uint8_t *status, int n) {
+  Pyramid a = build_pyramid(gray(prev, w, h), win, max_level), b = build_pyramid(gray(next, w, h), win, max_level);
+  std::vector<KeyPt> k0(n), k1(n);
+  for (int i = 0; i < n; i++) {
+    k0[i] = KeyPt{p0[2 * i], p0[2 * i + 1], 0.f};
+    k1[i] = KeyPt{p1[2 * i], p1[2 * i + 1], 0.f};
+  }
+  std::vector<uint8_t> st;
+  lk_track(a, b, k0, k1, st, win, max_level, max_iters, eps);
+  for (int i = 0; i < n; i++) {
+    p1[2 * i] = k1[i].x;
+    p1[2 * i + 1] = k1[i].y;
+    status[i] = st[i];
+  }
+  return 0;
+}
+// findFundamentalMat(FM_RANSAC, thr, conf) inlier mask on n correspondences
+int orc_ransac_mask(const float *x0, const float *y0, const float *x1, const float *y1, int n, double thr, double conf,
+                    int max_iters, uint8_t *mask) {
+  std::vector<uint8_t> m;
+  ransac_fundamental_mask(std::vector<float>(x0, x0 + n), std::vector<float>(y0, y0 + n), std::vector<float>(x1, x1 + n),
+                          std::vector<float>(y1, y1 + n), thr, conf, max_iters, m);
+  std::memcpy(mask, m.data(), (size_t)n);
+  return 0;
+}
+// 7-point fundamental matrices (<= 3, row-major 3x3 each); returns their count
+int orc_fundamental_7pt(const double *x0, const double *y0, const double *x1, const double *y1, double *F) {
+  return fundamental_7pt(x0, y0, x1, y1, F);
+}
+
 // Camera model entry points for fixture / finite-difference tests
 int orc_camera_distort(const uvio_hp_camera_t *c, int n, const double *xy, double *uv, double *dz_dzn, double *dz_dzeta) {
   Camera cam;

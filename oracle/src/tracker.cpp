@@ -65,7 +65,7 @@ GrayImg pyr_down(const GrayImg &src) {
 }
 
 // calcSharrDeriv (lkpyramid.cpp): dx = [3 10 3]^T (x) [-1 0 1], dy = its transpose, reflect-101 borders
-static std::vector<int16_t> scharr_deriv(const GrayImg &s) {
+std::vector<int16_t> scharr_deriv(const GrayImg &s) {
   std::vector<int16_t> d((size_t)s.w * s.h * 2);
   for (int y = 0; y < s.h; y++) {
     int y0 = reflect101(y - 1, s.h), y2 = reflect101(y + 1, s.h);

@@ -40,6 +40,8 @@ struct KeyPt {
 GrayImg equalize_hist(const GrayImg &src);
 // cv::pyrDown (5x5 Gaussian, BORDER_REFLECT_101, dst ((w+1)/2, (h+1)/2))
 GrayImg pyr_down(const GrayImg &src);
+// calcSharrDeriv: interleaved (dx, dy) int16 per pixel, BORDER_REFLECT_101
+std::vector<int16_t> scharr_deriv(const GrayImg &s);
 // buildOpticalFlowPyramid(win, maxLevel, withDerivatives): stops when the next level side <= win
 Pyramid build_pyramid(const GrayImg &img, int win, int max_level);
 // cv::FAST(img(roi), thr, nonmax) — keypoints in ROI coordinates, raster order
