@@ -1,17 +1,27 @@
 """Headline benchmark: VIO frames/s of the full per-frame track -> propagate -> update loop.
 
-Workload (BASELINE.json configs[1], SURVEY.md §8 cfg 2): EuRoC V1_02-shaped stereo 752x480 rig from
-configs/euroc_mav (radtan, 2 cameras, 20 Hz, 200 Hz IMU), 11 clones (+1 at update time), up to 200
-MSCKF features per update and 50 SLAM landmarks.  Input: a synthetic EuRoC-shaped stream
-(uvio_amd/sim.py: seeded smooth trajectory, IMU from analytic derivatives + the config's noise
-densities) whose camera images are ray-cast from a textured room (uvio_amd/render.py) and are
-resident in HBM before the timed region.  One step = one camera frame: the IMU samples since the
-last frame, then VioManager::feed_measurement_camera (TrackKLT on the device: equalizeHist, pyramid,
-FAST grid detection, cornerSubPix, stereo + temporal pyramidal LK, RANSAC) -> propagate + clone ->
-MSCKF update -> SLAM update / delayed init -> marginalize.  The tracker keeps 200 features per
-camera (init_max_features 400: initialize_with_gt keeps the initializer's count, VioManager.cpp:131).
+Workload at N = 1 (BASELINE.json configs[1], SURVEY.md §8 cfg 2): EuRoC V1_02-shaped stereo 752x480 rig from
+configs/euroc_mav (radtan, 2 cameras, 20 Hz, 200 Hz IMU), 11 clones (+1 at update time), up to 200 MSCKF
+features per update and 50 SLAM landmarks.  Input: a synthetic EuRoC-shaped stream (uvio_amd/sim.py: seeded
+smooth trajectory, IMU from analytic derivatives + the config's noise densities) whose camera images are
+ray-cast from a textured room (uvio_amd/render.py) and are resident in HBM before the timed region.  One
+step = one camera frame: the IMU samples since the last frame, then VioManager::feed_measurement_camera
+(TrackKLT on the device: equalizeHist, pyramid, FAST grid detection, cornerSubPix, stereo + temporal
+pyramidal LK, RANSAC) -> propagate + clone -> MSCKF update -> SLAM update / delayed init -> marginalize.
 
-Other workloads (--workload, SURVEY.md §8 cfg 3-5; parity-test cases and stress lines, not the headline):
+Steady state: the warm-up runs at least --warmup frames and then until the clone window is full
+(max_clones + 1 clones at update time) and the SLAM slots are >= 90 % populated (at most --max-warmup
+frames); the line reports the effective warm-up and whether steady state was reached.
+
+Multi-GPU (--gpus N > 1; launched either by torch.distributed.run, or by this script itself, which then
+spawns N worker processes before any GPU call): the north star's feature-sharded update --
+every rank runs the same stream and each MSCKF update's per-feature linearization, chi2 gate and Gram are
+split across the ranks with one RCCL all-reduce; cfg4 (UZH-FPV, 25 clones x 800 features) at N <= 4 and
+cfg5 (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value = frames of
+the one stream / wall time).  --replicas instead runs one independent estimator per GPU (weak scaling).
+
+Other workloads (--workload, SURVEY.md §8 cfg 1-5; parity-test cases and stress lines):
+  cfg1  EuRoC MH_01-shaped MONO 752x480 images (configs/euroc_mav, max_cameras 1), 11 clones, <= 100 MSCKF
   cfg3  TUM-VI room1-shaped stereo fisheye 512x512 images (configs/tum_vi), 20 clones, 400 tracks per
         camera, <= 400 MSCKF + 50 SLAM (LDS-tiled KLT stress)
   cfg4  UZH-FPV outdoor_45-shaped stereo fisheye rig (configs/uzhfpv_outdoor_45), 25 clones, 800 MSCKF
@@ -19,19 +29,18 @@ Other workloads (--workload, SURVEY.md §8 cfg 3-5; parity-test cases and stress
   cfg5  rpng_sim 4-camera rig + 6 UWB anchors (configs/rpng_sim_uwb), IMU intrinsics + g-sensitivity
         calibrated, 30 clones, 1500 MSCKF features per update (each in one camera), UWB ranges at 10 Hz
 
-Frames/s is whole-job throughput: every rank runs its own estimator on its own stream (independent
-replicas, weak scaling), value = total frames / max-over-ranks wall time.
-
-roofline: the feature launch group (k_feature: triangulation + LM, Jacobians, left-nullspace
-reflections; then k_gemm_HPg + k_chi2: the batched chi2 gate, both on the FP64 matrix cores), timed with HIP events on
-the library's stream around the group; achieved = the algorithmic FP64 FLOPs of the group
-(SURVEY.md §8(d) F_feat formula on the actual feature shapes) / event time.  cpu_baseline: the oracle/
-CPU restatement (single-threaded, as the reference estimator is) on a bounded sample of the same
-image stream, rank 0 only.
+roofline: live HIP-event timing of the kernel classes (uvio_hp_set_kernel_timing) over the timed region;
+achieved = algorithmic FLOPs (FP64 classes) or bytes (tracker classes) of the class's launches (SURVEY.md
+§8(d), formulas in DESIGN.md §6) / their summed event time; "roofline" is the class with the largest device
+time, "rooflines" lists every class.  traffic = HBM bytes per launch from the committed rocprofv3 PMC passes
+of the same workload (profiles/, FETCH_SIZE x 2 + WRITE_SIZE).  cpu_baseline: the oracle/ CPU restatement
+(single-threaded) on a bounded sample of the same stream, rank 0 only.  ate: posyaw-aligned ATE RMSE against
+the stream's ground truth (ov_eval's definition, uvio_amd/evaluation.py).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -41,10 +50,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = os.path.join(ROOT, "configs")
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (vector = matrix on gfx950)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (vector = matrix on gfx950), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak, MI355X_MICROARCH.md "HBM"
 
 # workload -> (config dir, camera input, option overrides, SimStream arguments, description)
 WORKLOADS = {
+    "cfg1": ("euroc_mav", "images",
+             dict(num_cameras=1, use_stereo=0, init_max_features=200, max_msckf_in_update=100, max_slam_features=50,
+                  max_slam_in_update=25, dt_slam_delay=1.0),
+             dict(spawn=4),
+             "cfg1 EuRoC MH_01-shaped mono 752x480 images, 11 clones, <=100 MSCKF + 50 SLAM"),
     "cfg2": ("euroc_mav", "images",
              dict(init_max_features=400, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
                   dt_slam_delay=1.0),
@@ -67,6 +82,9 @@ WORKLOADS = {
              "cfg5 rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
 }
 
+# oracle frames in the cpu_baseline sample (~10-30 s of single-core CPU work per workload)
+CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg3": 60, "cfg4": 3, "cfg5": 2}
+
 
 def workload_options(U, name):
     cfg, _, ov, _, _ = WORKLOADS[name]
@@ -87,30 +105,50 @@ def make_stream(opts, n_frames, seed, workload="cfg2"):
     return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, anchors=anchors, **kw)
 
 
-def render_frames(sim, n_frames, device):
-    """All camera images of the first n_frames frames, resident in HBM (u8 tensors)."""
-    import torch
-    from uvio_amd.render import SceneRenderer
-    r = SceneRenderer(sim.opts, device=device)
-    frames = [[r.render(k, *sim.camera_pose(i, k), frame_seed=i) for k in range(sim.K)]
-              for i in range(min(n_frames, len(sim.cam_t)))]
-    torch.cuda.synchronize(device)
-    return frames
+class Frames:
+    """Camera images of the stream's frames as u8 CUDA tensors, rendered on first use and kept resident."""
+
+    def __init__(self, sim, device):
+        import torch
+        from uvio_amd.render import SceneRenderer
+        self.sim, self.device, self.torch = sim, device, torch
+        self.r = SceneRenderer(sim.opts, device=device)
+        self.cache = {}
+
+    def __getitem__(self, i):
+        if i not in self.cache:
+            self.cache[i] = [self.r.render(k, *self.sim.camera_pose(i, k), frame_seed=i) for k in range(self.sim.K)]
+        return self.cache[i]
+
+    def prerender(self, lo, hi):
+        for i in range(lo, min(hi, len(self.sim.cam_t))):
+            self[i]
+        self.torch.cuda.synchronize(self.device)
 
 
 class Driver:
     """Feeds one stream into one manager frame by frame (events precomputed).  frames: per camera frame
-    the list of device images (feed_measurement_camera_device) or of host arrays (feed_measurement_camera)."""
+    the list of device images (feed_measurement_camera_device) or of host arrays (feed_measurement_camera);
+    None: the stream's simulated tracks (TrackSIM feed), packed per frame beforehand."""
 
     def __init__(self, sim, mgr, frames, device_imgs=True):
-        """frames=None: the stream's simulated tracks (TrackSIM feed), packed per frame beforehand."""
         self.sim, self.mgr, self.frames, self.device_imgs = sim, mgr, frames, device_imgs
         if frames is None:
             from uvio_amd.manager import pack_sim_frame
             self.packed = [pack_sim_frame(f) for f in sim.frames]
         self.ev = [e for e in sim.events() if e[1] >= sim.t0 - 0.4]
         self.k = 0
+        self.frame = -1  # index of the last fed camera frame
         mgr.initialize_with_gt(sim.gt_state(sim.t0))
+
+    def next_frame(self):
+        """index of the camera frame the next step() feeds"""
+        k = self.k
+        while True:
+            kind, t, i = self.ev[k]
+            k += 1
+            if kind == "cam" and t > self.sim.t0:
+                return i
 
     def step(self):
         """Feed events up to and including the next camera frame; returns its timestamp."""
@@ -130,25 +168,31 @@ class Driver:
                     mgr.feed_measurement_camera_device(t, cams, self.frames[i])
                 else:
                     mgr.feed_measurement_camera(t, cams, self.frames[i])
+                self.frame = i
                 return t
 
 
-# newest first: the PMC passes of the current kernels (tools/gpu_final.sh), then earlier rounds'
-PMC_FILES = {"cfg2": ["profiles/r01g_pmc_traffic_cfg2.json", "profiles/r01f_pmc_traffic_cfg2.json",
-                      "profiles/r01e_pmc_traffic.json"],
-             "cfg4": ["profiles/r01g_pmc_traffic_cfg4.json", "profiles/r01f_pmc_traffic_cfg4.json",
-                      "profiles/r01_pmc_traffic_cfg4.json"]}
+# committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py), newest first
+def pmc_files(workload):
+    names = sorted((f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc_traffic_%s.json" % workload)),
+                   reverse=True)
+    return [os.path.join("profiles", f) for f in names]
 
 
-def pmc_traffic(workload):
-    """(HBM bytes per feature-group launch, source) from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE, tools/pmc_summary.py) of this workload, or (None, None) if absent."""
-    for path in PMC_FILES.get(workload, ["profiles/r01_pmc_traffic_%s.json" % workload]):
+def pmc_class_traffic(workload, kernels):
+    """(HBM bytes per launch of the kernel class, source file) from the newest PMC summary holding it."""
+    for path in pmc_files(workload):
         try:
             with open(os.path.join(ROOT, path)) as f:
-                return json.load(f)["feature_group_traffic"], path
+                k = json.load(f)["kernels"]
         except (OSError, KeyError, ValueError):
             continue
+        hit = [n for n in kernels if n in k]
+        if not hit:
+            continue
+        # per launch of the class: the members' bytes over the launches of the class's first member present
+        tot = sum(k[n]["traffic"] * k[n]["launches"] for n in hit)
+        return tot / max(k[hit[0]]["launches"], 1), path
     return None, None
 
 
@@ -163,20 +207,101 @@ def max_over_ranks(x, device="cuda"):
     return float(t.item())
 
 
+def all_ranks_true(flag, device="cuda"):
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return flag
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def spawn_workers(n, argv, script=None):
+    """--gpus N without a launcher: N worker processes (one per GPU) started before this process touches the
+    GPU; rank 0's JSON line is passed through, the exit code is the worst of the workers'."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [p.wait() for p in procs]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def roofline_entry(name, st, wl):
+    bound = st["bound"]
+    secs = st["seconds"]
+    n = max(st["launches"], 1)
+    avg = secs / n
+    if bound == "mfma":
+        per = st["flops"] / n
+        achieved = per / avg / 1e12 if avg > 0 else 0.0
+        peak, unit = FP64_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        per = st["bytes"] / n
+        achieved = per / avg / 1e9 if avg > 0 else 0.0
+        peak, unit = HBM_PEAK_GBS, "GB/s"
+    traffic, src = pmc_class_traffic(wl, st["kernels"])
+    return {"kernel": name, "kernels": st["kernels"], "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "traffic": traffic, "traffic_source": src, "launches": st["launches"],
+            "avg_launch_us": avg * 1e6, ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per,
+            "device_s": secs}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=40, help="minimum warm-up frames (then until steady state)")
+    ap.add_argument("--max-warmup", type=int, default=200, help="warm-up cap while waiting for steady state")
     ap.add_argument("--cpu-frames", type=int, default=None,
                     help="timed oracle frames for cpu_baseline (0 = skip; default: ~10-30 s of CPU work per workload)")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
-    ap.add_argument("--shard", action="store_true",
-                    help="one stream, MSCKF features sharded across the ranks (SURVEY §8e; strong scaling)")
+    ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto",
+                    help="auto: cfg2 at 1 GPU, feature-sharded cfg4 at 2-4 GPUs, cfg5 beyond")
+    ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
+    ap.add_argument("--shard", action="store_true", help="feature sharding also at N = 1 (RCCL world of 1)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
+    ap.add_argument("--ktime-period", type=int, default=10,
+                    help="kernel-class event timing on every k-th frame of the timed region (0 = off)")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if args.gpus > 1:
+            return spawn_workers(args.gpus, sys.argv[1:])
+        world = 1
+    if args.gpus != world:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    shard = (world > 1 and not args.replicas) or args.shard
+    wl = args.workload
+    if wl == "auto":
+        wl = "cfg2" if world == 1 else ("cfg4" if world <= 4 else "cfg5")
     if args.cpu_frames is None:
-        args.cpu_frames = {"cfg2": 120, "cfg3": 60, "cfg4": 3, "cfg5": 2}[args.workload]
+        args.cpu_frames = CPU_FRAMES[wl]
     # stdout carries exactly the one JSON line: whatever the libraries print (RCCL's version banner at
     # communicator creation, ...) goes to stderr
     sys.stdout.flush()
@@ -185,93 +310,119 @@ def main():
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import uvio_amd as U
+    from uvio_amd.evaluation import ate as ate_fn
 
-    wl = args.workload
     images = WORKLOADS[wl][1] == "images"
     opts = workload_options(U, wl)
-    n_frames = args.warmup + args.steps
-    # replicas: one stream per rank; --shard: every rank runs the same stream and splits its MSCKF updates
-    sim = make_stream(opts, n_frames + 2, seed=5 if args.shard else 5 + rank, workload=wl)
-    frames = render_frames(sim, n_frames + 2, torch.device("cuda", local)) if images else None
+    max_warm = max(args.warmup, args.max_warmup)
+    n_frames = max_warm + args.steps + 2
+    # replicas: one stream per rank; sharded: every rank runs the same stream and splits its MSCKF updates
+    sim = make_stream(opts, n_frames + 2, seed=5 if shard else 5 + rank, workload=wl)
+    dev = torch.device("cuda", local)
+    frames = Frames(sim, dev) if images else None
+    if frames is not None:
+        frames.prerender(0, args.warmup + 2)
     mgr = U.VioManager(opts, device=local)
-    if args.shard:
+    if shard:
         from uvio_amd.manager import shard_unique_id
         uid = [shard_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
         mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
     drv = Driver(sim, mgr, frames)
-    for _ in range(args.warmup):
+
+    # warm-up: at least --warmup frames, then until the clone window is full and the SLAM slots are populated
+    want_slam = int(0.9 * opts.max_slam_features)
+    warm, steady = 0, False
+    while True:
         drv.step()
+        warm += 1
+        tm = mgr.get_timing()
+        ok = tm["n_clones"] >= opts.max_clone_size + 1 and tm["n_slam"] >= want_slam
+        if warm >= args.warmup:
+            steady = all_ranks_true(ok, dev)
+            if steady or warm >= max_warm:
+                break
+    if frames is not None:
+        nxt = drv.next_frame()
+        frames.prerender(nxt, nxt + args.steps + 1)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    acc = {"k_feat_s": 0.0, "k_feat_flops": 0.0, "k_feat_launches": 0, "rows": 0, "n_msckf": 0, "n_slam": 0,
-           "cols": 0, "cov_dim": 0, "tracks": 0, "tracking_s": 0.0}
-    pos_err = []
+    acc = {"rows": 0, "n_msckf": 0, "n_slam": 0, "cols": 0, "cov_dim": 0, "tracking_s": 0.0, "syncs": 0}
+    est_p, est_q, gt_p, gt_q = [], [], [], []
+    mgr.set_kernel_timing(args.ktime_period)
+    ks0 = mgr.kernel_stats(flush=True)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         t = drv.step()
         tm = mgr.get_timing()
-        acc["k_feat_s"] += tm["k_feat_s"]
-        acc["k_feat_flops"] += tm["k_feat_flops"]
-        acc["k_feat_launches"] += tm["k_feat_launches"]
         acc["rows"] += tm["msckf_rows"]
         acc["n_msckf"] += tm["n_msckf"]
         acc["n_slam"] += tm["n_slam"]
         acc["cols"] = max(acc["cols"], tm["msckf_cols"])
         acc["cov_dim"] = max(acc["cov_dim"], tm["cov_dim"])
         acc["tracking_s"] += tm["tracking"]
+        acc["syncs"] += tm["device_syncs"]
         _, x = mgr.get_imu_state()
-        pos_err.append(x[4:7] - sim.traj.pos(t))
+        est_q.append(x[0:4].copy())
+        est_p.append(x[4:7].copy())
+        g = sim.gt_state(t)
+        gt_q.append(g[1:5])
+        gt_p.append(g[5:8])
     barrier()
     t1 = time.perf_counter()
     elapsed = max_over_ranks(t1 - t0)
-    ate = float(np.sqrt(np.mean(np.sum(np.array(pos_err) ** 2, axis=1))))
+    ks1 = mgr.kernel_stats(flush=True)
+    acc_ate = ate_fn(est_p, gt_p, est_q, gt_q, align="posyaw")
+    raw = ate_fn(est_p, gt_p, align="none")
 
     if rank == 0:
-        # replicas: world streams were processed; --shard: one stream, split
-        value = (1 if args.shard else world) * args.steps / elapsed
-        launches = max(acc["k_feat_launches"], 1)
-        avg_s = acc["k_feat_s"] / launches
-        flops_per_launch = acc["k_feat_flops"] / launches
-        achieved = flops_per_launch / avg_s / 1e12 if avg_s > 0 else 0.0
+        # replicas: world streams were processed; sharded: one stream, split
+        value = (1 if shard else world) * args.steps / elapsed
+        ks = {}
+        for k, a in ks1.items():
+            b = ks0[k]
+            ks[k] = dict(a, launches=a["launches"] - b["launches"], seconds=a["seconds"] - b["seconds"],
+                         flops=a["flops"] - b["flops"], bytes=a["bytes"] - b["bytes"])
+        rl = {k: roofline_entry(k, v, wl) for k, v in ks.items() if v["launches"] > 0}
+        # the dominant kernel (class) by device time; the EKF-update chain contains the LDL class
+        cand = {k: v for k, v in rl.items() if k != "ekf_update"}
+        dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
         ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras)) if images else None
         cpu = None
         if args.cpu_frames > 0:
             # the oracle needs only the clone window filled; fewer warm-up frames bound its run time
-            cpu_warm = args.warmup if images else min(args.warmup, int(opts.max_clone_size) + 3)
+            cpu_warm = warm if images else min(warm, int(opts.max_clone_size) + 3)
             cpu = cpu_baseline(opts, wl, cpu_warm, args.cpu_frames, frames)
-        traffic, traffic_src = pmc_traffic(wl)
         out = {
             "metric": "VIO frames/sec (track+propagate+update) at clones x feats",
             "value": value,
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": warm,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong" if args.shard else "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("synthetic %s-shaped stream (uvio_amd/sim.py, seed 5+rank) with ray-cast images "
-                     "(uvio_amd/render.py) resident in HBM, TrackKLT front-end" % WORKLOADS[wl][0]) if images else
-                    ("synthetic %s-shaped stream (uvio_amd/sim.py, seed 5+rank): simulated feature tracks "
+            "data": ("synthetic %s-shaped stream (uvio_amd/sim.py, seed %s) with ray-cast images "
+                     "(uvio_amd/render.py) resident in HBM, TrackKLT front-end" %
+                     (WORKLOADS[wl][0], "5" if shard else "5+rank")) if images else
+                    ("synthetic %s-shaped stream (uvio_amd/sim.py, seed %s): simulated feature tracks "
                      "(TrackSIM feed, VioManager::feed_measurement_simulation)%s" %
-                     (WORKLOADS[wl][0], " + UWB ranges" if opts.use_uwb else "")),
+                     (WORKLOADS[wl][0], "5" if shard else "5+rank", " + UWB ranges" if opts.use_uwb else "")),
             "config": {"workload": WORKLOADS[wl][4],
+                       "steady": steady, "warmup_requested": args.warmup,
                        "track_features_per_cam": int(opts.init_max_features) // int(opts.num_cameras) if images else None,
                        "tracks_last_frame": ntr, "mean_tracking_ms": 1e3 * acc["tracking_s"] / args.steps,
                        "clones": int(opts.max_clone_size), "cameras": int(opts.num_cameras),
@@ -279,31 +430,32 @@ def main():
                        "max_slam_features": int(opts.max_slam_features),
                        "mean_msckf_feats": acc["n_msckf"] / args.steps, "mean_slam_feats": acc["n_slam"] / args.steps,
                        "mean_msckf_rows": acc["rows"] / args.steps, "H_cols": acc["cols"],
-                       "state_dim": acc["cov_dim"],
-                       "parallelism": ("feature-shard%d" % world) if args.shard else ("replicas%d" % world)},
-            "ate_rmse_m": ate,
-            "roofline": {"kernel": "feature linearize + chi2 launch group (k_feature, k_gemm_HPg, k_chi2)",
-                         "bound": "mfma",
-                         "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "avg_launch_us": avg_s * 1e6, "flops_per_launch": flops_per_launch},
+                       "state_dim": acc["cov_dim"], "host_waits_per_frame": acc["syncs"] / args.steps,
+                       "parallelism": ("feature-shard%d" % world) if shard else ("replicas%d" % world)},
+            "ate_rmse_m": acc_ate["pos_m"],
+            "ate": {"align": "posyaw (ov_eval AlignTrajectory.cpp:84-106)", "pos_rmse_m": acc_ate["pos_m"],
+                    "ori_rmse_deg": acc_ate["ori_deg"], "unaligned_pos_rmse_m": raw["pos_m"],
+                    "frames": args.steps},
+            "roofline": rl.get(dom),
+            "rooflines": rl,
             "cpu_baseline": cpu,
         }
         result_out.write(json.dumps(out) + "\n")
         result_out.flush()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def cpu_baseline(opts, wl, warmup, frames, dev_frames):
     """oracle/ (the CPU restatement) on the same stream (rank 0's), one thread, bounded sample."""
     from oracle import oracle as O
     sim = make_stream(opts, warmup + frames + 2, seed=5, workload=wl)
+    host = None
     if dev_frames is not None:
-        frames = max(1, min(frames, len(dev_frames) - warmup - 2))
-        host = [[im.cpu().numpy() for im in fr] for fr in dev_frames[:warmup + frames + 2]]
-    else:
-        host = None
+        host = {}
+        for i in range(warmup + frames + 2):
+            host[i] = [im.cpu().numpy() for im in dev_frames[i]]
     mgr = O.OracleManager(opts)
     drv = Driver(sim, mgr, host, device_imgs=False)
     for _ in range(warmup):
@@ -312,10 +464,11 @@ def cpu_baseline(opts, wl, warmup, frames, dev_frames):
     for _ in range(frames):
         drv.step()
     dt = time.perf_counter() - t0
-    return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "%d frames of the %s %s stream after %d warm-up frames, oracle/liboracle.so (g++ -O3)" %
-                      (frames, wl, "image" if dev_frames is not None else "track", warmup)}
+    return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
+            "sample": "%d frames of the %s %s stream after %d warm-up frames, oracle/liboracle.so (g++ -O3, one "
+                      "thread: the reference estimator is single-threaded; its tracker's cv::parallel_for_ is not "
+                      "restated)" % (frames, wl, "image" if dev_frames is not None else "track", warmup)}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -97,7 +97,8 @@ typedef struct {
   /* TrackKLT front-end (estimator_config.yaml: num_pts .. histogram_method) */
   int num_pts, fast_threshold, grid_x, grid_y, min_px_dist;
   int histogram_method;       /* 0 none, 1 histogram, 2 clahe */
-  int downsample_cameras;
+  int downsample_cameras;     /* cams[].width/height/fx fy cx cy are the halved values (VioManagerOptions.h:251-260);
+                               * camera feeds then take the raw 2 width x 2 height images */
   double track_frequency;
   /* uvio (UVioManagerOptions.h:52-90, UVioStateOptions.h:45, UVioUpdaterOptions.h:46) */
   int use_uwb;
@@ -117,6 +118,13 @@ typedef struct {
    * keeps floor(init_max_features / num_cameras) tracks per camera until an initializer succeeds
    * (VioManager.cpp:131; initialize_with_gt does not raise it to num_pts, VioManagerHelper.cpp:40) */
   int init_max_features;
+  /* UpdaterZeroVelocity (VioManagerOptions.h:83-95, zupt_chi2_multipler :175) */
+  int try_zupt;
+  double zupt_chi2_multipler, zupt_max_velocity, zupt_noise_multiplier, zupt_max_disparity;
+  int zupt_only_at_beginning;
+  /* front-end selection (VioManagerOptions.h:440-452): the KLT front-end is the one implemented; use_klt = 0
+   * (ORB descriptors) and use_aruco = 1 are rejected with UVIO_HP_E_CONFIG by uvio_hp_create */
+  int use_klt, use_aruco;
 } uvio_hp_options_t;
 
 /* Per-frame stage timings in seconds, the reference CSV schema
@@ -138,6 +146,19 @@ typedef struct {
   int device_syncs;
   double sync_wait;
 } uvio_hp_timing_t;
+
+/* Live device timing of the kernel classes the benchmark prices against a roofline (HIP events on the
+ * library stream around each launch of the class): cumulative since the timing was
+ * switched on.  bound: 0 = HBM bandwidth (bytes), 1 = FP64 matrix / vector peak (flops); flops / bytes are
+ * the ALGORITHMIC counts of the launches; kernels = the kernel names of the class as
+ * rocprofv3 reports them (comma separated). */
+typedef struct {
+  char name[24];
+  char kernels[192];
+  int bound;
+  long long launches;
+  double seconds, flops, bytes;
+} uvio_hp_kstat_t;
 
 typedef struct uvio_hp uvio_hp_t;
 
@@ -195,6 +216,12 @@ int uvio_hp_get_state_vector(uvio_hp_t *h, double *out, int cap, int *len, int *
 int uvio_hp_get_fej_vector(uvio_hp_t *h, double *out, int cap, int *len);
 /* timings of the last processed frame */
 int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out);
+/* live per-class kernel timing: 0 = off (default), k > 0 = the launches of every k-th camera / simulated
+ * frame are timed (each timed launch costs two event records on the host) */
+int uvio_hp_set_kernel_timing(uvio_hp_t *h, int period);
+/* the per-class statistics (*n receives the number of classes); flush = 1 waits for the device first so
+ * every launch enqueued so far is counted */
+int uvio_hp_get_kernel_stats(uvio_hp_t *h, int flush, uvio_hp_kstat_t *out, int cap, int *n);
 /* number of clones and their timestamps (ascending) */
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
 /* TrackBase::get_last_obs / get_last_ids (TrackBase.h:137-148) for one camera: ids and raw (u, v) of

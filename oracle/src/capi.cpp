@@ -46,17 +46,24 @@ int orc_feed_camera(orc_handle *h, double t, int ncam, const int *cam_ids, const
                     const uint8_t *const *masks) {
   std::vector<int> camids(cam_ids, cam_ids + ncam);
   std::vector<GrayImg> im(ncam), mk(ncam);
+  // downsample_cameras (VioManager.cpp:270-278): the configured size is the halved one, the inputs are the
+  // raw 2w x 2h images and both image and mask are pyrDown'ed before tracking
+  const int f = h->m.o.downsample_cameras ? 2 : 1;
   for (int i = 0; i < ncam; i++) {
     const uvio_hp_camera_t &c = h->m.o.cams[cam_ids[i]];
-    im[i].w = c.width;
-    im[i].h = c.height;
-    im[i].d.resize((size_t)c.width * c.height);
-    for (int y = 0; y < c.height; y++)
-      std::memcpy(&im[i].d[(size_t)y * c.width], imgs[i] + (size_t)y * strides[i], c.width);
+    im[i].w = f * c.width;
+    im[i].h = f * c.height;
+    im[i].d.resize((size_t)im[i].w * im[i].h);
+    for (int y = 0; y < im[i].h; y++)
+      std::memcpy(&im[i].d[(size_t)y * im[i].w], imgs[i] + (size_t)y * strides[i], im[i].w);
     if (masks && masks[i]) {
       mk[i] = im[i];
-      for (int y = 0; y < c.height; y++)
-        std::memcpy(&mk[i].d[(size_t)y * c.width], masks[i] + (size_t)y * strides[i], c.width);
+      for (int y = 0; y < im[i].h; y++)
+        std::memcpy(&mk[i].d[(size_t)y * im[i].w], masks[i] + (size_t)y * strides[i], im[i].w);
+    }
+    if (f == 2) {
+      im[i] = pyr_down(im[i]);
+      if (masks && masks[i]) mk[i] = pyr_down(mk[i]);
     }
   }
   return h->m.feed_camera(t, camids, im, mk);

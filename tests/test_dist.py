@@ -51,3 +51,33 @@ def test_bench_max_over_ranks_gloo():
     assert [o[1] for o in out] == [2.5, 2.5]
     assert out[0][2] == out[1][2]
     assert out[0][3] != out[1][3]
+
+
+WORKER = r'''
+import json, os, sys
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+t = torch.tensor([float(r + 1)])
+dist.all_reduce(t)
+assert int(os.environ["LOCAL_RANK"]) == r and os.environ["MASTER_ADDR"] == "127.0.0.1"
+if r == 0:
+    print(json.dumps({"n_gpus": w, "sum": float(t.item()), "argv": sys.argv[1:]}))
+dist.destroy_process_group()
+'''
+
+
+def test_bench_launcher_spawns_world(tmp_path, capsys):
+    """bench.py --gpus N without torch.distributed.run spawns N ranks itself (env rendezvous on 127.0.0.1)
+    and passes rank 0's JSON line through; here the workers are a gloo stand-in for the GPU bench."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER)
+    rc = bench.spawn_workers(2, ["--gpus", "2", "--steps", "3"], script=str(script))
+    assert rc == 0
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["n_gpus"] == 2 and out["sum"] == 3.0
+    assert out["argv"] == ["--gpus", "2", "--steps", "3"]

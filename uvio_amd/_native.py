@@ -55,6 +55,9 @@ class Options(C.Structure):
         ("p_IinU", C.c_double * 3), ("n_anchors_to_fix", C.c_int), ("n_anchors", C.c_int),
         ("anchors", Anchor * MAX_ANCHORS),
         ("record_timing", C.c_int), ("init_max_features", C.c_int),
+        ("try_zupt", C.c_int), ("zupt_chi2_multipler", C.c_double), ("zupt_max_velocity", C.c_double),
+        ("zupt_noise_multiplier", C.c_double), ("zupt_max_disparity", C.c_double),
+        ("zupt_only_at_beginning", C.c_int), ("use_klt", C.c_int), ("use_aruco", C.c_int),
     ]
 
 
@@ -69,6 +72,16 @@ class Timing(C.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class KStat(C.Structure):
+    _fields_ = [("name", C.c_char * 24), ("kernels", C.c_char * 192), ("bound", C.c_int), ("launches", C.c_longlong),
+                ("seconds", C.c_double), ("flops", C.c_double), ("bytes", C.c_double)]
+
+    def as_dict(self):
+        return {"name": self.name.decode(), "kernels": self.kernels.decode().split(","),
+                "bound": "hbm" if self.bound == 0 else "mfma", "launches": int(self.launches),
+                "seconds": self.seconds, "flops": self.flops, "bytes": self.bytes}
 
 
 _P = C.POINTER
@@ -96,6 +109,8 @@ SIGNATURES = [
     ("get_fej_vector", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
     ("get_timing", _I, [C.c_void_p, _P(Timing)]),
     ("get_clone_times", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
+    ("set_kernel_timing", _I, [C.c_void_p, _I]),
+    ("get_kernel_stats", _I, [C.c_void_p, _I, _P(KStat), _I, _P(_I)]),
     ("feed_camera_device", _I, [C.c_void_p, _D, _I, _P(_I), _P(C.c_void_p), _P(_I), _P(_P(C.c_uint8))]),
     ("get_tracks", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(C.c_float), _I, _P(_I)]),
     ("get_pyramid", _I, [C.c_void_p, _I, _I, _P(_I), _P(_I), _P(C.c_uint8), _P(C.c_int16), C.c_size_t]),

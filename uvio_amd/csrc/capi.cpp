@@ -192,6 +192,18 @@ int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out) {
   return 0;
 }
 
+int uvio_hp_set_kernel_timing(uvio_hp_t *h, int on) {
+  if (!h) return UVIO_HP_E_ARG;
+  if (on < 0) return UVIO_HP_E_ARG;
+  h->e->set_kernel_timing(on);
+  return 0;
+}
+
+int uvio_hp_get_kernel_stats(uvio_hp_t *h, int flush, uvio_hp_kstat_t *out, int cap, int *n) {
+  if (!h || !n || (cap > 0 && !out)) return UVIO_HP_E_ARG;
+  HP_GUARD(h, h->e->kernel_stats(flush != 0, out, cap, n); return 0;)
+}
+
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n) {
   if (!h || !n) return UVIO_HP_E_ARG;
   auto t = h->e->clone_times();

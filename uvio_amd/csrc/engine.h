@@ -149,6 +149,7 @@ struct DeviceBufs {
   // with ONE copy (stage / stage_flush); the kernels read the device copy directly
   char *stg_h = nullptr, *stg_d = nullptr;
   size_t stg_cap = 0, stg_used = 0, stg_flushed = 0;
+  long long stg_epoch = 0;  // ring restarts so far (a reservation must not outlive one: run_batch checks)
   // [negative-diagonal count (8 B) | dx (cap + 15) | feature results (max features)], mirrored in pinned
   // memory at neg_host / dx_host / fout_host: an update's dx and its batch's results come back in ONE copy
   double *dxneg = nullptr;
@@ -181,6 +182,14 @@ class Engine {
   int state_vector(double *out, int cap, int *meta, int meta_cap, int *nvars, bool fej = false);
   uvio_hp_timing_t timing() const { return timing_; }
   std::vector<double> clone_times() const;
+
+  // live kernel timing of the roofline classes (kprof.h)
+  // period 0: off; k: the camera frames whose index is a multiple of k are timed (events cost host time)
+  void set_kernel_timing(int period) {
+    ktime_period_ = period;
+    kprof_.on = period > 0 && frames_ % period == 0;
+  }
+  void kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n);
 
   // feature sharding
   void shard_init_rccl(int rank, int world, const uint8_t id[128], int min_features);
@@ -226,6 +235,13 @@ class Engine {
   WorkPool pool_;
   std::vector<FeatP> pending_delete_;  // features handed to an updater this frame (cleanup candidates)
   HostProf hprof_;                     // UVIO_HP_HOST_PROF section timer (debug)
+  KProf kprof_;                        // live per-class kernel timing (uvio_hp_set_kernel_timing)
+  int ktime_period_ = 0;
+  long long frames_ = 0;               // camera / simulated frames fed
+  void frame_begin() {
+    frames_++;
+    kprof_.on = ktime_period_ > 0 && frames_ % ktime_period_ == 0;
+  }
   void shard_allreduce(double *dev, size_t count);
   int msckf_update_sharded(std::vector<FeatP> &fv);
 
@@ -298,6 +314,7 @@ class Engine {
                      int track_syncs = 0, double track_wait = 0.0);
   int do_feature_propagate_update(double t, const std::vector<int> &camids);
   int msckf_update(std::vector<FeatP> &feats);
+  void gram(int m, int ncol, int *nch);
   int slam_update(std::vector<FeatP> &feats);
   int slam_delayed_init(std::vector<FeatP> &feats);
   int slam_change_anchors();
@@ -330,6 +347,7 @@ class Engine {
     const DMeas *meas_dev = nullptr;
     const DVar *vars_dev = nullptr;
     size_t n_meas_dev = 0, n_vars_dev = 0;
+    long long stg_epoch = -1;  // staging ring epoch of the meas / vars reservation
     size_t n_meas() const { return meas_dev ? n_meas_dev : meas.size(); }
     size_t n_vars() const { return vars_dev ? n_vars_dev : vars.size(); }
     std::map<double, int> slot_of_time;

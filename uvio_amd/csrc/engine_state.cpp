@@ -1,5 +1,6 @@
 // Engine: state layout, device buffers and covariance operations.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "engine.h"
@@ -88,6 +89,14 @@ static VarP mk(VKind k, int size, int vlen) { return std::make_shared<Var>(k, si
 // State::State (State.cpp:28-166) + UVioManager ctor (UVioManager.cpp:26-58)
 Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) {
   if (o_.num_cameras < 1 || o_.num_cameras > UVIO_HP_MAX_CAMS) throw HpError(UVIO_HP_E_ARG, "num_cameras out of range");
+  // configurations the reference accepts but this build does not implement fail here, loudly
+  if (!o_.use_klt) throw HpError(UVIO_HP_E_CONFIG, "use_klt: false (TrackDescriptor / ORB) is not implemented");
+  if (o_.use_aruco) throw HpError(UVIO_HP_E_CONFIG, "use_aruco: true (TrackAruco) is not implemented");
+  if (o_.feat_rep_msckf != 0 && o_.feat_rep_msckf != 4)
+    throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
+  if (o_.feat_rep_slam != 0 && o_.feat_rep_slam != 2 && o_.feat_rep_slam != 4)
+    throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: only GLOBAL_3D / ANCHORED_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
+  if (o_.try_zupt) throw HpError(UVIO_HP_E_CONFIG, "try_zupt: UpdaterZeroVelocity is not implemented");
   currid_ = 4 * (size_t)o_.max_aruco_features + 1;  // TrackBase::currid (TrackBase.cpp:34)
   int cur = 0;
   imu_ = mk(V_IMU, 15, 16);
@@ -223,6 +232,8 @@ void Engine::alloc_device() {
   HP_HIP(hipStreamCreateWithFlags(&d_.stream, hipStreamNonBlocking));
   HP_HIP(hipEventCreate(&d_.ev0));
   HP_HIP(hipEventCreate(&d_.ev1));
+  kprof_.stream = d_.stream;
+  d_.ekf.kp = &kprof_;
   int C = o_.max_clone_size + 2;
   int K = o_.num_cameras;
   int cap = N_ + 6 * C + 3 * std::max(o_.max_slam_features, 0) + 5 * UVIO_HP_MAX_ANCHORS + 3 + 8;
@@ -321,6 +332,7 @@ void *Engine::stage_bytes(const void *src, size_t bytes) {
     stage_flush();
     dev_sync();
     d_.stg_used = d_.stg_flushed = 0;
+    d_.stg_epoch++;
   }
   if (bytes) std::memcpy(d_.stg_h + d_.stg_used, src, bytes);
   void *dev = d_.stg_d + d_.stg_used;
@@ -335,6 +347,7 @@ void *Engine::stage_reserve(size_t bytes, void **host) {
     stage_flush();
     dev_sync();
     d_.stg_used = d_.stg_flushed = 0;
+    d_.stg_epoch++;
   }
   *host = d_.stg_h + d_.stg_used;
   void *dev = d_.stg_d + d_.stg_used;
@@ -359,6 +372,43 @@ void Engine::dev_sync() {
   HP_HIP(hipStreamSynchronize(d_.stream));
   timing_.sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   timing_.device_syncs++;
+  if (kprof_.on) kprof_.harvest(true);
+}
+
+// cumulative per-class kernel statistics since the timing was switched on (flush: wait for the device
+// so every recorded launch is counted)
+void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
+  static const struct {
+    const char *name, *kernels;
+    int bound;
+  } info[KC_COUNT] = {
+      {"feature", "k_feature", 1},
+      {"chi2", "k_gemm_HPg,k_gemm_HPg_tiled,k_chi2", 1},
+      {"gram", "k_gram,k_gram_mfma", 1},
+      {"ekf_update", "k_ekf_M,k_ekf_S,k_ekf_small,k_chi2_gate,k_trinv16,k_trsm_lt,k_ekf_P,k_gram_reduce,k_info_cholP,"
+                     "k_gemm,k_info_cholZ,k_info_P",
+       1},
+      {"ldl", "k_ekf_small", 1},
+      {"lk", "k_lk", 0},
+      {"pyramid", "k_hist_multi,k_eq_scharr_multi,k_pyr_scharr_multi", 0},
+  };
+  if (flush) {
+    HP_HIP(hipStreamSynchronize(d_.stream));
+    kprof_.harvest(true);
+    if (tracker_) kprof_.bytes[KC_LK] = (double)tracker_->lk_bytes();
+  }
+  *n = KC_COUNT;
+  for (int k = 0; k < KC_COUNT && k < cap; k++) {
+    uvio_hp_kstat_t &o = out[k];
+    std::memset(&o, 0, sizeof(o));
+    std::snprintf(o.name, sizeof(o.name), "%s", info[k].name);
+    std::snprintf(o.kernels, sizeof(o.kernels), "%s", info[k].kernels);
+    o.bound = info[k].bound;
+    o.launches = kprof_.launches[k];
+    o.seconds = kprof_.secs[k];
+    o.flops = kprof_.flops[k];
+    o.bytes = kprof_.bytes[k];
+  }
 }
 
 void Engine::read_dx(const char *who) {
@@ -431,6 +481,14 @@ void Engine::marginalize(const VarP &m) {
   N_ -= ms;
 }
 
+// algorithmic FP64 FLOPs of one EKFUpdate with r rows over n columns of an N-dim state (SURVEY.md §8(d)
+// F_ekf: M = P H^T, S, its factor, K, P - K M^T, dx) and the bytes it must move at least (P read and
+// written once, H and the residual read)
+double ekf_flops(double N, double n, double r) {
+  return 2 * N * n * r + 2 * r * n * n + 2 * r * r * n + r * r * r + 2 * N * r * r + N * N * r + 2 * N * r;
+}
+double ekf_bytes(double N, double n, double r) { return 8.0 * (2 * N * N + r * (n + 1) + N); }
+
 void Engine::apply_dx(const double *dx) {
   for (auto &v : vars_) v->update(dx + v->id);
   if (o_.do_calib_camera_intrinsics)
@@ -454,8 +512,10 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
   d_.ekf.gate = gate;
   {
     HPROF("ekf_rows.launch");
+    KScope ks(&kprof_, KC_EKF);
     launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
   }
+  kprof_.credit(KC_EKF, ekf_flops(N_, n, r), ekf_bytes(N_, n, r));
   read_dx("EKFUpdate");
   if (!apply || apply()) apply_dx(d_.dx_host);
 }
@@ -466,7 +526,11 @@ void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, doubl
   const int *dh = stage(hidx.data(), (size_t)n);
   stage_flush();
   d_.ekf.gate = gate;
-  launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, partials ? partials : d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
+  {
+    KScope ks(&kprof_, KC_EKF);
+    launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, partials ? partials : d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
+  }
+  kprof_.credit(KC_EKF, ekf_flops(N_, n, n), ekf_bytes(N_, n, n));
   read_dx("EKFUpdate");
   if (!apply || apply()) apply_dx(d_.dx_host);
 }

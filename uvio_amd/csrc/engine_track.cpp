@@ -85,7 +85,9 @@ struct Arena {
 size_t span(const void *a, const void *b_end) { return (size_t)((const char *)b_end - (const char *)a); }
 }  // namespace
 
-Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s) : cams_(cams), s_(s) {
+Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s, KProf *kp)
+    : cams_(cams), s_(s), kp_(kp) {
+  downsample_ = o.downsample_cameras != 0;
   // TrackKLT construction in VioManager.cpp:98-107: num_pts per camera = init_max_features / ncam
   num_features_ = (int)std::floor((double)o.init_max_features / (double)o.num_cameras);
   threshold_ = o.fast_threshold;
@@ -118,6 +120,15 @@ Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t 
   }
   b_->kmax = (int)((double)num_features_ / (double)(gx * gy)) + 1;
   ensure_cap(std::max(1024, 8 * num_features_));
+  HP_HIP(hipMalloc(&d_lk_bytes_, sizeof(unsigned long long)));
+  HP_HIP(hipMemsetAsync(d_lk_bytes_, 0, sizeof(unsigned long long), s_));
+}
+
+unsigned long long Tracker::lk_bytes() {
+  unsigned long long v = 0;
+  HP_HIP(hipMemcpyAsync(&v, d_lk_bytes_, sizeof(v), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipStreamSynchronize(s_));
+  return v;
 }
 
 Tracker::~Tracker() {
@@ -125,9 +136,11 @@ Tracker::~Tracker() {
     for (int k = 0; k < 2; k++)
       if (kv.second.pyr_mem[k]) (void)hipFree(kv.second.pyr_mem[k]);
     if (kv.second.d_raw) (void)hipFree(kv.second.d_raw);
+    if (kv.second.d_half) (void)hipFree(kv.second.d_half);
     if (kv.second.d_hist) (void)hipFree(kv.second.d_hist);
     if (kv.second.d_score) (void)hipFree(kv.second.d_score);
   }
+  if (d_lk_bytes_) (void)hipFree(d_lk_bytes_);
   if (b_) {
     if (b_->dmem) (void)hipFree(b_->dmem);
     if (b_->hmem) (void)hipHostFree(b_->hmem);
@@ -224,7 +237,8 @@ void Tracker::alloc_pyr(CamState &c, int w, int h) {
       c.pyr[k].der[l] = (const int16_t *)((char *)c.pyr_mem[k] + der_off[l]);
     }
   }
-  HP_HIP(hipMalloc(&c.d_raw, (size_t)w * h));
+  HP_HIP(hipMalloc(&c.d_raw, (size_t)w * h * (downsample_ ? 4 : 1)));
+  if (downsample_) HP_HIP(hipMalloc(&c.d_half, (size_t)w * h));
   HP_HIP(hipMalloc(&c.d_hist, 256 * sizeof(unsigned)));
   HP_HIP(hipMalloc(&c.d_score, (size_t)w * h));
 }
@@ -263,17 +277,30 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
   PyrJob job{};
   job.ncam = ncam;
   job.equalize = histogram_method_ == 1;
+  DecimateJob dec{};
+  dec.ncam = downsample_ ? ncam : 0;
   for (int k = 0; k < ncam; k++) {
     const int cid = cam_ids[k];
-    const int w = cams_[cid].w, h = cams_[cid].h;
-    if (strides[k] < w) throw HpError(UVIO_HP_E_ARG, "image stride smaller than the configured width");
+    // with downsample_cameras the configured size is the halved one (VioManagerOptions.h:251-260) and the
+    // inputs are the raw 2w x 2h camera images
+    const int w = cams_[cid].w, h = cams_[cid].h, f = downsample_ ? 2 : 1, rw = f * w, rh = f * h;
+    if (strides[k] < rw) throw HpError(UVIO_HP_E_ARG, "image stride smaller than the configured width");
     CamState &c = cam_state(cid);
     const int nw = 1 - c.last;
     const uint8_t *src = imgs[k];
     int stride = strides[k];
     if (!device_imgs) {
-      HP_HIP(hipMemcpy2DAsync(c.d_raw, w, imgs[k], strides[k], w, h, hipMemcpyHostToDevice, s_));
+      HP_HIP(hipMemcpy2DAsync(c.d_raw, rw, imgs[k], strides[k], rw, rh, hipMemcpyHostToDevice, s_));
       src = c.d_raw;
+      stride = rw;
+    }
+    if (downsample_) {
+      dec.src[k] = src;
+      dec.stride[k] = stride;
+      dec.dst[k] = c.d_half;
+      dec.w[k] = w;
+      dec.h[k] = h;
+      src = c.d_half;
       stride = w;
     }
     job.p[k] = c.pyr[nw];
@@ -283,10 +310,34 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
     c.mask_new.clear();
     if (masks && masks[k]) {
       c.mask_new.resize((size_t)w * h);
-      for (int y = 0; y < h; y++) std::memcpy(&c.mask_new[(size_t)y * w], masks[k] + (size_t)y * strides[k], w);
+      if (downsample_) {  // cv::pyrDown of the mask too (VioManager.cpp:276)
+        for (int y = 0; y < h; y++)
+          for (int x = 0; x < w; x++) {
+            static const int k5[5] = {1, 4, 6, 4, 1};
+            auto refl = [](int p, int n) {
+              while (p < 0 || p >= n) p = (p < 0) ? -p : 2 * n - 2 - p;
+              return p;
+            };
+            int acc = 0;
+            for (int i = 0; i < 5; i++) {
+              const uint8_t *row = masks[k] + (size_t)refl(2 * y + i - 2, rh) * strides[k];
+              int r = 0;
+              for (int j = 0; j < 5; j++) r += k5[j] * row[refl(2 * x + j - 2, rw)];
+              acc += k5[i] * r;
+            }
+            c.mask_new[(size_t)y * w + x] = (uint8_t)((acc + 128) >> 8);
+          }
+      } else {
+        for (int y = 0; y < h; y++) std::memcpy(&c.mask_new[(size_t)y * w], masks[k] + (size_t)y * strides[k], w);
+      }
     }
   }
-  launch_pyramids(s_, job);
+  launch_decimate(s_, dec);
+  {
+    KScope ks(kp_, KC_PYR);
+    launch_pyramids(s_, job);
+  }
+  if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
   if (ncam == 1) {
     feed_monocular(t, cam_ids[0], db);
   } else if (ncam == 2 && use_stereo_) {
@@ -362,7 +413,11 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
     lk.p1[0] = b.det1;
     lk.st[0] = b.detst;
     lk.n[0] = n;
-    launch_lk(s_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
+    lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
+    {
+      KScope ks(kp_, KC_LK);
+      launch_lk(s_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
+    }
     HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + n), hipMemcpyDeviceToHost, s_));
   } else {
     HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
@@ -624,7 +679,11 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
   }
   if (ns == 0) return;
   HP_HIP(hipMemcpyAsync(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters), hipMemcpyHostToDevice, s_));
-  launch_lk(s_, lk, ns, win_, pyr_levels_, kLkIters, kLkEps, true);
+  lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
+  {
+    KScope ks(kp_, KC_LK);
+    launch_lk(s_, lk, ns, win_, pyr_levels_, kLkIters, kLkEps, true);
+  }
   launch_ransac(s_, rs, ns, kRansacIters, kRansacConf);
   HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.mask[hi] + b.cap), hipMemcpyDeviceToHost, s_));
   sync();

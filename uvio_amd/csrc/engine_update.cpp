@@ -161,6 +161,7 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
                             const float *uv) {
   stage_ = "feed_simulation";
   auto rT1 = clk::now();
+  frame_begin();
   std::vector<int> camids, cam_of;
   for (int i = 0; i < ncam; i++) {
     int cid = cam_ids[i];
@@ -214,13 +215,14 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
 int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
                         const uint8_t *const *masks, bool device_imgs) {
   auto rT1 = clk::now();
+  frame_begin();
   std::vector<int> camids;
   for (int i = 0; i < ncam; i++) {
     int cid = cam_ids[i];
     if (cid < 0 || cid >= o_.num_cameras || !imgs[i]) return UVIO_HP_E_ARG;
     camids.push_back(cid);
   }
-  if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream));
+  if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream, &kprof_));
   {
     HPROF("track.feed");
     tracker_->feed(t, ncam, cam_ids, imgs, strides, masks, device_imgs,
@@ -443,6 +445,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   timing_.marg = secs(rT6, rT7);
   timing_.n_slam = (int)slam_.size();
   timing_.cov_dim = N_;
+  if (kprof_.on) kprof_.harvest(false);
   if (timelastupdate_ != -1 && clones_.find(timelastupdate_) != clones_.end()) {
     const double *a = imu_->val + 4, *b = clones_.at(timelastupdate_)->val + 4;
     double d[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
@@ -678,6 +681,7 @@ void Engine::add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_
   void *hv = (char *)hm + mbytes;
   b.meas_dev = (const DMeas *)dm;
   b.vars_dev = (const DVar *)(dm + mbytes);
+  b.stg_epoch = d_.stg_epoch;
   b.n_meas_dev = mo[nparts];
   b.n_vars_dev = vo[nparts];
   pool_.parallel_for(nparts, 1, [&](size_t p0, size_t p1) {
@@ -726,6 +730,11 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   const DCam *t_cams = stage(b.cams.data(), b.cams.size());
   const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
   stage_flush();
+  // the measurement / variable reservation must still be intact: after a ring restart in between, the
+  // tables staged since then start at offset 0 and must end before the reservation (a ring smaller than
+  // one launch group, UVIO_HP_STAGE_BYTES, would let them overwrite it on the device)
+  if (b.meas_dev && b.stg_epoch != d_.stg_epoch && d_.stg_used > (size_t)((const char *)b.meas_dev - d_.stg_d))
+    throw HpError(UVIO_HP_E_CAPACITY, "upload staging ring restarted inside one launch group (UVIO_HP_STAGE_BYTES too small)");
   b.hidx_dev = t_hidx;
   DBatchParams bp{};
   bp.nfeat = nf;
@@ -757,14 +766,18 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     HP_HIP(hipMemset(bp.dbg_ts, 0, sizeof(long long) * 16 * nf));
   }
   if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
-  launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
-                           max_meas, max_nf);
+  {
+    KScope ks(&kprof_, KC_FEATURE);
+    launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
+                             max_meas, max_nf);
+  }
   if (chi2) {
     int max_rows_f = 0;
     for (auto &F : b.feats) {
       int rows_out = (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas;
       max_rows_f = std::max(max_rows_f, rows_out - (mode >= 2 ? 3 : 0));
     }
+    KScope ks(&kprof_, KC_CHI2);
     launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout,
                       max_rows_f, d_.acc);
   }
@@ -825,6 +838,33 @@ void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
       timing_.k_feat_flops += refl + chi2;
     }
   }
+  if (kprof_.on) {
+    // the same F_feat split by class: reflections -> k_feature, the chi2 terms -> the chi2 group; bytes =
+    // the rows each writes (k_feature) / reads with their T rows (chi2) plus the P block gathered
+    double fl = 0, fb = 0, cl = 0, cb = 0;
+    for (int i = 0; i < nf; i++) {
+      const double rows = 2.0 * b.feats[i].nmeas, nfc = b.feats[i].nf;
+      fb += 8.0 * (rows * (nfc + 1) + 4.0 * b.feats[i].nmeas);
+      if (mode == 2 || outs[i].status == 1 || outs[i].status == 2) continue;
+      const double r = (mode == 1) ? rows : rows - 3.0;
+      if (mode != 1) fl += 12.0 * rows * (nfc + 4.0);
+      if (b.chi2) {
+        cl += 2.0 * r * nfc * nfc + 2.0 * r * r * nfc + r * r * r / 3.0;
+        cb += 8.0 * (2.0 * r * (nfc + 1) + nfc * nfc);
+      }
+    }
+    kprof_.credit(KC_FEATURE, fl, fb);
+    if (b.chi2) kprof_.credit(KC_CHI2, cl, cb);
+  }
+}
+
+// the Gram [H r]^T [H r] of the m stacked rows in H_all (upper triangle: m ncol (ncol + 1) FLOPs, H read once)
+void Engine::gram(int m, int ncol, int *nch) {
+  {
+    KScope ks(&kprof_, KC_GRAM);
+    launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, nch);
+  }
+  kprof_.credit(KC_GRAM, (double)m * ncol * (ncol + 1), 8.0 * ((double)m * ncol + (double)*nch * ncol * ncol));
 }
 
 // UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295)
@@ -858,7 +898,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
   {
     HPROF("msckf.build");
     build_clone_cam_tables(b, false);
-    add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
+    add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf);
   }
   // The update is enqueued right behind the feature group: rejected features already have zero rows in
   // H_all and the device skips the P update when no feature was accepted (d_.acc), so the host reads the
@@ -911,7 +951,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
     // measurement compression (UpdaterHelper.cpp:456-487) + EKFUpdate on the compressed system, carried
     // out in information form on G = [H r]^T [H r] (see launch_ekf_info)
     int nch = 0;
-    launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
+    gram(m, ncol, &nch);
     ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
     ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);
@@ -975,7 +1015,7 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
   }
   if (m > n || m > kMaxEkfRows) {
     int nch = 0;
-    launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
+    gram(m, ncol, &nch);
     ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
     ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);

@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "hp_math.h"
+#include "kprof.h"
 
 namespace uvhp {
 
@@ -143,6 +144,7 @@ struct EkfScratch {
   // factorization; *chi2_gate (the P-update gate) = accepted, and [chi2, accepted] go to dx[N], dx[N+1]
   int *chi2_gate = nullptr;
   double chi2_thr = 0.0;
+  KProf *kp = nullptr;  // live kernel timing (kprof.h), null = off
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.
@@ -210,6 +212,18 @@ struct PyrJob {
   int ncam, equalize;
 };
 void launch_pyramids(hipStream_t s, const PyrJob &job);
+// algorithmic bytes of launch_pyramids: histogram read, equalized level 0 + Scharr
+// written, every further level's source read, level and Scharr written
+double pyramid_bytes(const PyrJob &job);
+// downsample_cameras (VioManager.cpp:270-278): dst[c] (w x h) = pyrDown(src[c]) of the 2w x 2h input
+// (row stride stride[c]), BORDER_REFLECT_101, (sum + 128) >> 8, all cameras in one launch
+struct DecimateJob {
+  const uint8_t *src[kMaxCams];
+  uint8_t *dst[kMaxCams];
+  int stride[kMaxCams], w[kMaxCams], h[kMaxCams];
+  int ncam;
+};
+void launch_decimate(hipStream_t s, const DecimateJob &job);
 // FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell;
 // score_map: w x h u8 scratch
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
@@ -226,6 +240,9 @@ struct LkSlots {
   float *p1[2];
   uint8_t *st[2];
   int n[2];
+  // optional: algorithmic bytes of the launch accumulated on the device (SURVEY.md §8(d) LK term:
+  // 256 (5 + iterations) per point and pyramid level visited)
+  unsigned long long *bytes = nullptr;
 };
 void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,
                bool init_from_p0);

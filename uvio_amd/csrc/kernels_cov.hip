@@ -626,8 +626,14 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   double *Sup = sc.S + 2 * (size_t)r * r;
   double *Sg = sc.S + 3 * (size_t)r * r;  // (r+1)(r|1) + 4(r+1) <= 2 r^2 doubles once r >= 40 (else LDS)
   ensure_lds_attrs();
-  hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Lf, sc.y, Sg,
-                     use_lds);
+  {
+    KScope ks(sc.kp, KC_LDL);
+    hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Lf, sc.y, Sg,
+                       use_lds);
+  }
+  // LDL^T of the r x r innovation covariance with the residual as an extra row: r^3/3 + r^2 FLOPs; the
+  // lower triangle and the residual read, the factor written
+  if (sc.kp) sc.kp->credit(KC_LDL, (double)r * r * r / 3.0 + (double)r * r, 8.0 * (1.5 * r * r + 2.0 * r));
   if (sc.chi2_gate) {  // StateHelper::initialize's chi2 test on this factor
     hipLaunchKernelGGL(k_chi2_gate, dim3(1), dim3(64), 0, s, sc.y, r, sc.chi2_thr, sc.chi2_gate, sc.dx + N);
     sc.gate = sc.chi2_gate;

@@ -261,6 +261,49 @@ void launch_pyramids(hipStream_t s, const PyrJob &job) {
   }
 }
 
+double pyramid_bytes(const PyrJob &job) {
+  double b = 0.0;
+  for (int c = 0; c < job.ncam; c++) {
+    const DPyr &p = job.p[c];
+    const double a0 = (double)p.w[0] * p.h[0];
+    b += (job.equalize ? a0 : 0.0) + a0 + a0 + 4.0 * a0;  // histogram read, source read, level 0 + Scharr
+    for (int l = 1; l < p.levels; l++) b += (double)p.w[l - 1] * p.h[l - 1] + 5.0 * p.w[l] * p.h[l];
+  }
+  return b;
+}
+
+// downsample_cameras: cv::pyrDown of the raw 2w x 2h camera image before tracking (VioManager.cpp:270-278),
+// the same 5x5 binomial and rounding as the pyramid levels; one output pixel per thread, 64 x 4 blocks
+// (coalesced rows), blockIdx.z = camera
+__global__ void __launch_bounds__(256) k_decimate_multi(DecimateJob job) {
+  const int c = blockIdx.z;
+  const int dw = job.w[c], dh = job.h[c], sw = 2 * dw, sh = 2 * dh, ld = job.stride[c];
+  const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (x >= dw || y >= dh) return;
+  const uint8_t *src = job.src[c];
+  const int k5[5] = {1, 4, 6, 4, 1};
+  int xs[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
+  int acc = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * ld;
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) r += k5[j] * row[xs[j]];
+    acc += k5[i] * r;
+  }
+  job.dst[c][(size_t)y * dw + x] = (uint8_t)((acc + 128) >> 8);
+}
+
+void launch_decimate(hipStream_t s, const DecimateJob &job) {
+  if (job.ncam <= 0) return;
+  int w = 0, h = 0;
+  for (int c = 0; c < job.ncam; c++) w = max(w, job.w[c]), h = max(h, job.h[c]);
+  hipLaunchKernelGGL(k_decimate_multi, dim3((w + 63) / 64, (h + 3) / 4, job.ncam), dim3(256), 0, s, job);
+}
+
 // ---------------------------------------------------------------- FAST-9 on grid cells
 // ring offsets (dx, dy) of cv::makeOffsets(pattern 16)
 __constant__ int c_fast_off[16][2] = {{0, 3},  {1, 3},  {2, 2},  {3, 1},  {3, 0},  {3, -1}, {2, -2}, {1, -3},
@@ -585,7 +628,8 @@ __device__ __forceinline__ int bilin_der(const int16_t *d, int w, int h, int X, 
 
 __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
                                          float *__restrict__ p1, uint8_t *__restrict__ status, int pi, int win,
-                                         int max_level, int max_iters, float crit_eps, int init_from_p0) {
+                                         int max_level, int max_iters, float crit_eps, int init_from_p0,
+                                         unsigned long long *bytes) {
   const int lane = threadIdx.x;
   const int maxL = min(max_level, min(prev.levels, next.levels) - 1);
   const float halfw = (win - 1) * 0.5f;
@@ -600,6 +644,7 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
   const int S = win + 1 + 2 * kLkMargin;
   float qx = init_from_p0 ? p0[2 * pi] : p1[2 * pi], qy = init_from_p0 ? p0[2 * pi + 1] : p1[2 * pi + 1];
   uint8_t st = 1;
+  int nlev = 0, nit = 0;  // levels with a prev window gathered, iterations (algorithmic bytes, LkSlots::bytes)
   for (int level = maxL; level >= 0; level--) {
     const uint8_t *I = prev.img[level], *J = next.img[level];
     const int16_t *dI = prev.der[level];
@@ -654,6 +699,7 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
       continue;
     }
     D = 1.f / D;
+    nlev++;
     float nx = qx - halfw, ny = qy - halfw;
     float pdx = 0.f, pdy = 0.f;
     int ox = -(1 << 28), oy = -(1 << 28);
@@ -680,6 +726,7 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
       iw10 = (int)rintf((1.f - a) * b * WSCALE);
       iw11 = (1 << 14) - iw00 - iw01 - iw10;
       long long ib1 = 0, ib2 = 0;
+      nit++;
 #pragma unroll
       for (int q = 0; q < kPer; q++) {
         const int e = lane + 64 * q;
@@ -714,6 +761,7 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     p1[2 * pi] = qx;
     p1[2 * pi + 1] = qy;
     status[pi] = st;
+    if (bytes) atomicAdd(bytes, (unsigned long long)(256 * (5 * nlev + nit)));
   }
 }
 
@@ -723,7 +771,7 @@ __global__ void __launch_bounds__(64) k_lk(LkSlots job, int win, int max_level, 
   const int slot = blockIdx.y;
   if ((int)blockIdx.x >= job.n[slot]) return;
   lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], blockIdx.x, win, max_level, max_iters,
-           crit_eps, init_from_p0);
+           crit_eps, init_from_p0, job.bytes);
 }
 
 // ---------------------------------------------------------------- undistort + RANSAC

@@ -317,6 +317,15 @@ void options_default(uvio_hp_options_t *o) {
   o->min_dist_to_use_uwb = 0.5;
   o->record_timing = 1;
   o->init_max_features = 50;
+  // UpdaterZeroVelocity (VioManagerOptions.h:83-95; UpdaterOptions chi2_multipler default 5)
+  o->try_zupt = 0;
+  o->zupt_chi2_multipler = 5;
+  o->zupt_max_velocity = 1.0;
+  o->zupt_noise_multiplier = 1.0;
+  o->zupt_max_disparity = 1.0;
+  o->zupt_only_at_beginning = 0;
+  o->use_klt = 1;
+  o->use_aruco = 0;
 }
 
 int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
@@ -343,8 +352,23 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
   est.get({"num_aruco"}, o->max_aruco_features);
   est.get({"max_cameras"}, o->num_cameras);
   std::string rep;
-  if (est.gets({"feat_rep_msckf"}, rep) && rep_from_string(rep) >= 0) o->feat_rep_msckf = rep_from_string(rep);
-  if (est.gets({"feat_rep_slam"}, rep) && rep_from_string(rep) >= 0) o->feat_rep_slam = rep_from_string(rep);
+  for (auto key : {"feat_rep_msckf", "feat_rep_slam"}) {
+    if (!est.gets({key}, rep)) continue;
+    const int r = rep_from_string(rep);
+    if (r < 0) {  // LandmarkRepresentation::from_string (LandmarkRepresentation.h:80-101) knows no other name
+      if (err) *err = std::string(key) + ": unknown landmark representation '" + rep + "'";
+      return UVIO_HP_E_CONFIG;
+    }
+    (std::string(key) == "feat_rep_msckf" ? o->feat_rep_msckf : o->feat_rep_slam) = r;
+  }
+  est.getb({"try_zupt"}, o->try_zupt);
+  est.get({"zupt_chi2_multipler"}, o->zupt_chi2_multipler);
+  est.get({"zupt_max_velocity"}, o->zupt_max_velocity);
+  est.get({"zupt_noise_multiplier"}, o->zupt_noise_multiplier);
+  est.get({"zupt_max_disparity"}, o->zupt_max_disparity);
+  est.getb({"zupt_only_at_beginning"}, o->zupt_only_at_beginning);
+  est.getb({"use_klt"}, o->use_klt);
+  est.getb({"use_aruco"}, o->use_aruco);
   est.getb({"use_stereo"}, o->use_stereo);
   est.get({"dt_slam_delay"}, o->dt_slam_delay);
   est.get({"gravity_mag"}, o->gravity_mag);
@@ -458,6 +482,18 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
       if (cam.getvec({cn, "resolution"}, res) && res.size() == 2) {
         c.width = (int)res[0];
         c.height = (int)res[1];
+      }
+      if (o->downsample_cameras) {
+        // VioManagerOptions.h:251-260: fx fy cx cy and the resolution halved (the trackers run on the
+        // pyrDown'ed images, VioManager.cpp:270-278).  An odd raw size has no exact 2:1 inverse in the
+        // feed's contract (raw = 2 w x 2 h), so it is refused.
+        if (c.width % 2 || c.height % 2) {
+          if (err) *err = cn + ": downsample_cameras needs an even resolution";
+          return UVIO_HP_E_CONFIG;
+        }
+        c.width /= 2;
+        c.height /= 2;
+        for (int k = 0; k < 4; k++) c.intrinsics[k] /= 2.0;
       }
       std::vector<std::vector<double>> T;
       bool have_T = cam.getmat({cn, "T_imu_cam"}, T) && T.size() >= 3;

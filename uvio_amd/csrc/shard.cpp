@@ -161,13 +161,13 @@ int Engine::msckf_update_sharded(std::vector<FeatP> &fv) {
   const int lo = bounds[shard_.rank], hi = bounds[shard_.rank + 1];
   Batch b;
   build_clone_cam_tables(b, false);
-  add_features_to_batch(b, fv, (size_t)lo, (size_t)hi, 0, o_.feat_rep_msckf == 5 ? 4 : o_.feat_rep_msckf);
+  add_features_to_batch(b, fv, (size_t)lo, (size_t)hi, 0, o_.feat_rep_msckf);
   std::vector<DFeatOut> outs;
   const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
   const int m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
   const int n = b.n_canon, ncol = n + 1;
   int nch = 0;
-  if (m > 0) launch_gram(d_.stream, d_.H, m, ncol, d_.ldh, d_.partials, &nch);
+  if (m > 0) gram(m, ncol, &nch);
   const size_t count = (size_t)ncol * ncol + 2;
   launch_shard_pack(d_.stream, d_.partials, nch, ncol, d_.fout, (int)b.feats.size(), d_.acc, d_.shard);
   shard_allreduce(d_.shard, count);

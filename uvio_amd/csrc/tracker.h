@@ -23,7 +23,7 @@ using DbSink = std::function<void(size_t id, double t, int cam, float u, float v
 
 class Tracker {
  public:
-  Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s);
+  Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s, KProf *kp = nullptr);
   ~Tracker();
   Tracker(const Tracker &) = delete;
   Tracker &operator=(const Tracker &) = delete;
@@ -41,6 +41,8 @@ class Tracker {
   size_t currid;
   int device_syncs = 0;     // host waits in the last feed
   double sync_wait = 0.0;   // seconds blocked in them
+  // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand
+  unsigned long long lk_bytes();
 
  private:
   struct CamState {
@@ -48,7 +50,8 @@ class Tracker {
     void *pyr_mem[2] = {nullptr, nullptr};
     int last = 0;            // slot of pyr_last
     bool have_last = false;
-    uint8_t *d_raw = nullptr;  // staging of a host image
+    uint8_t *d_raw = nullptr;  // staging of a host image (the raw 2w x 2h one with downsample_cameras)
+    uint8_t *d_half = nullptr;  // downsample_cameras: the pyrDown'ed input (w x h)
     unsigned *d_hist = nullptr;
     uint8_t *d_score = nullptr;  // FAST score map (w x h)
     std::vector<uint8_t> mask_last, mask_new;  // host masks (empty = none)
@@ -65,6 +68,9 @@ class Tracker {
 
   const CamParams *cams_;
   hipStream_t s_;
+  KProf *kp_ = nullptr;
+  unsigned long long *d_lk_bytes_ = nullptr;
+  bool downsample_ = false;  // VioManager.cpp:270-278: the inputs are 2w x 2h and pyrDown'ed first
   int num_features_, threshold_, grid_x_, grid_y_, min_px_dist_, histogram_method_;
   bool use_stereo_;
   const int pyr_levels_ = 5, win_ = 15;

@@ -284,6 +284,20 @@ class VioManager:
         self._check(self._call("get_timing", self._h, C.byref(t)), "get_timing")
         return t.as_dict()
 
+    def set_kernel_timing(self, period=1):
+        """Live per-class device timing of the roofline kernels (HIP events, include/uvio_hp.h): the launches
+        of every `period`-th frame are timed (0 = off)."""
+        self._check(self._call("set_kernel_timing", self._h, int(period)), "set_kernel_timing")
+
+    def kernel_stats(self, flush=True):
+        """{class name: {kernels, bound, launches, seconds, flops, bytes}} cumulative since switched on."""
+        cap = 16
+        arr = (N.KStat * cap)()
+        n = C.c_int()
+        self._check(self._call("get_kernel_stats", self._h, 1 if flush else 0, arr, cap, C.byref(n)),
+                    "get_kernel_stats")
+        return {d["name"]: d for d in (arr[i].as_dict() for i in range(min(n.value, cap)))}
+
     def debug_last_msckf(self):
         cap = 8192
         ids = np.zeros(cap, dtype=np.uint64)
