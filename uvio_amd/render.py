@@ -61,6 +61,15 @@ class SceneRenderer:
         self.sizes = []
         for i in range(opts.num_cameras):
             c = opts.cams[i]
+            if opts.downsample_cameras:
+                # the configured camera is the halved one (VioManagerOptions.h:251-260); the feed takes the raw
+                # 2w x 2h image, so render at the raw resolution and intrinsics (exact: a power-of-two scale)
+                from . import _native as N
+                raw = N.Camera.from_buffer_copy(c)
+                raw.width, raw.height = 2 * c.width, 2 * c.height
+                for k in range(4):
+                    raw.intrinsics[k] = 2.0 * c.intrinsics[k]
+                c = raw
             x, y = _undistort_grid(c)
             d = np.stack([x, y, np.ones_like(x)], axis=-1)
             d /= np.linalg.norm(d, axis=-1, keepdims=True)
