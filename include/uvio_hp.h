@@ -125,6 +125,10 @@ typedef struct {
   /* front-end selection (VioManagerOptions.h:440-452): the KLT front-end is the one implemented; use_klt = 0
    * (ORB descriptors) and use_aruco = 1 are rejected with UVIO_HP_E_CONFIG by uvio_hp_create */
   int use_klt, use_aruco;
+  /* VioManagerOptions.h:98-101: per-frame timing rows in the reference CSV schema (VioManager.cpp:105-122,
+   * 631-644); the file is recreated at uvio_hp_create */
+  int record_timing_information;
+  char record_timing_filepath[256];
 } uvio_hp_options_t;
 
 /* Per-frame stage timings in seconds, the reference CSV schema
@@ -145,6 +149,7 @@ typedef struct {
   /* host waits on the device during this frame (tracker + estimator): count and seconds blocked */
   int device_syncs;
   double sync_wait;
+  int zupt;  /* 1: this frame ended in a zero-velocity update (UpdaterZeroVelocity::try_update accepted) */
 } uvio_hp_timing_t;
 
 /* Live device timing of the kernel classes the benchmark prices against a roofline (HIP events on the
@@ -222,6 +227,12 @@ int uvio_hp_set_kernel_timing(uvio_hp_t *h, int period);
 /* the per-class statistics (*n receives the number of classes); flush = 1 waits for the device first so
  * every launch enqueued so far is counted */
 int uvio_hp_get_kernel_stats(uvio_hp_t *h, int flush, uvio_hp_kstat_t *out, int cap, int *n);
+/* VioManager::get_active_tracks (VioManager.h:114, filled by retriangulate_active_tracks,
+ * VioManagerHelper.cpp:190-388): the current tracks' positions p_FinG (3 per track) and, for the tracks seen
+ * by camera 0 in front of it and inside its image, (u, v, depth) (3 per track, uvd_valid 1); *t receives
+ * active_tracks_time.  *n receives the number of tracks (E_CAPACITY if > cap). */
+int uvio_hp_get_active_tracks(uvio_hp_t *h, double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid,
+                              int cap, int *n);
 /* number of clones and their timestamps (ascending) */
 int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n);
 /* TrackBase::get_last_obs / get_last_ids (TrackBase.h:137-148) for one camera: ids and raw (u, v) of

@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 _ORC_NAMES = ["create", "destroy", "initialize_with_gt", "feed_imu", "feed_simulation", "feed_uwb", "init_anchors",
               "get_imu_state", "get_cov_dim", "get_cov", "get_state_vector", "get_timing", "get_clone_times",
               "ekf_update", "compress", "debug_last_msckf", "get_fej_vector",
-              "msckf_compressed_update", "feed_camera", "get_tracks", "get_pyramid"]
+              "msckf_compressed_update", "feed_camera", "get_tracks", "get_pyramid", "get_active_tracks"]
 
 _lib = None
 

@@ -151,6 +151,27 @@ int orc_get_clone_times(orc_handle *h, double *out, int cap, int *n) {
   return 0;
 }
 
+// VioManager::get_active_tracks (retriangulate_active_tracks outputs)
+int orc_get_active_tracks(orc_handle *h, double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid, int cap,
+                          int *n) {
+  const auto &P = h->m.active_tracks_posinG;
+  const auto &U = h->m.active_tracks_uvd;
+  *t = h->m.active_tracks_time;
+  // tracks with a uvd but no position cannot exist (uvd is derived from the position)
+  *n = (int)P.size();
+  if ((int)P.size() > cap) return UVIO_HP_E_CAPACITY;
+  int k = 0;
+  for (const auto &kv : P) {
+    ids[k] = (uint64_t)kv.first;
+    for (int j = 0; j < 3; j++) posinG[3 * k + j] = kv.second[j];
+    auto u = U.find(kv.first);
+    uvd_valid[k] = u != U.end();
+    for (int j = 0; j < 3; j++) uvd[3 * k + j] = (u != U.end()) ? u->second[j] : 0.0;
+    k++;
+  }
+  return 0;
+}
+
 // StateHelper::EKFUpdate on a standalone covariance (variables = one Vec of size N)
 int orc_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res, double sigma2,
                    double *dx_out) {

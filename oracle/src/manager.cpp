@@ -21,6 +21,7 @@ Manager::Manager(const uvio_hp_options_t &opt)
   tracker.use_stereo = opt.use_stereo != 0;
   tracker.currid = 4 * (size_t)opt.max_aruco_features + 1;
   tracker.cams = &state.cams;
+  if (o.try_zupt) zupt.reset(new UpdaterZUPT(opt));
   // UVioManager ctor (UVioManager.cpp:33-58)
   if (o.use_uwb) {
     if (o.do_calib_uwb_extrinsics) {
@@ -64,6 +65,7 @@ void Manager::feed_imu(double t, const double wm[3], const double am[3]) {
     d.am[k] = am[k];
   }
   prop.feed_imu(d, oldest_time);
+  if (is_initialized && zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) zupt->feed_imu(d, oldest_time);
 }
 
 // UVioManager.cpp:61-79
@@ -135,34 +137,34 @@ int Manager::feed_simulation(double t, const std::vector<int> &camids,
       db.update_feature(id, t, cam_id, f.second.first, f.second.second, un, vn);
     }
   }
-  auto rT2 = clk::now();
-  timing = uvio_hp_timing_t{};
-  timing.tracking = secs(rT1, rT2);
-  if (!is_initialized) return UVIO_HP_E_STATE;
-  if (!past_uwb.empty()) {
-    for (auto it = past_uwb.begin(); it != past_uwb.lower_bound(t); it++) {
-      if (it->first < t && it->first > state.timestamp) {
-        int rc = do_uwb_propagate_update(it->second);
-        if (rc < 0) return rc;
-      }
-    }
-    past_uwb.erase(past_uwb.begin(), past_uwb.upper_bound(t));
-  }
-  int rc = do_feature_propagate_update(t, camids);
-  auto rT7 = clk::now();
-  timing.total = secs(rT1, rT7);
-  return rc;
+  for (size_t i = 0; i < camids.size(); i++) sim_last[camids[i]] = feats[i];
+  return after_tracking(t, camids, rT1);
 }
 
-// VioManager.cpp:255-321 (track_image_and_update, no ZUPT / ArUco / downsampling)
-int Manager::feed_camera(double t, const std::vector<int> &camids, const std::vector<GrayImg> &imgs,
-                         const std::vector<GrayImg> &masks) {
-  auto rT1 = clk::now();
-  tracker.feed(t, camids, imgs, masks, db);
+int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1) {
   auto rT2 = clk::now();
   timing = uvio_hp_timing_t{};
   timing.tracking = secs(rT1, rT2);
   if (!is_initialized) return UVIO_HP_E_STATE;
+  // UVioManager.cpp:147-162 / VioManager.cpp:291-307: zero-velocity update; on success the frame ends here
+  if (zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) {
+    if (state.timestamp != t) {
+      int z = zupt->try_update(state, db, t);
+      if (z < 0) return z;
+      did_zupt_update = z == 1;
+    }
+    if (did_zupt_update) {
+      const double c = t + state.calib_dt->val[0] - 0.10;
+      prop.clean_old_imu_measurements(c);
+      zupt->clean_old_imu_measurements(c);
+      timing.zupt = 1;
+      timing.timestamp = t;
+      timing.n_clones = (int)state.clones.size();
+      timing.cov_dim = state.Cov.r;
+      timing.total = secs(rT1, clk::now());
+      return 0;
+    }
+  }
   if (!past_uwb.empty()) {
     for (auto it = past_uwb.begin(); it != past_uwb.lower_bound(t); it++) {
       if (it->first < t && it->first > state.timestamp) {
@@ -175,6 +177,14 @@ int Manager::feed_camera(double t, const std::vector<int> &camids, const std::ve
   int rc = do_feature_propagate_update(t, camids);
   timing.total = secs(rT1, clk::now());
   return rc;
+}
+
+// VioManager.cpp:255-321 (track_image_and_update; downsampling in capi.cpp, no ArUco)
+int Manager::feed_camera(double t, const std::vector<int> &camids, const std::vector<GrayImg> &imgs,
+                         const std::vector<GrayImg> &masks) {
+  auto rT1 = clk::now();
+  tracker.feed(t, camids, imgs, masks, db);
+  return after_tracking(t, camids, rT1);
 }
 
 // VioManager.cpp:323-651
@@ -192,6 +202,7 @@ int Manager::do_feature_propagate_update(double t, const std::vector<int> &camid
   timing.cov_dim = state.Cov.r;
   if ((int)state.clones.size() < std::min(state.opt.max_clone_size, 5)) return 0;
   if (state.timestamp != t) return 0;
+  has_moved_since_zupt = true;
 
   std::vector<FeatP> feats_lost, feats_marg, feats_slam;
   feats_lost = db.features_not_containing_newer(state.timestamp, false, true);
@@ -293,6 +304,7 @@ int Manager::do_feature_propagate_update(double t, const std::vector<int> &camid
   rc = slam.delayed_init(state, feats_slam_DELAYED);
   if (rc < 0) return rc;
   auto rT6 = clk::now();
+  if (!camids.empty() && camids[0] == 0) retriangulate_active_tracks(t, camids);
   for (auto &f : featsup_MSCKF) f->to_delete = true;
   db.cleanup();
   rc = slam.change_anchors(state);
@@ -311,6 +323,104 @@ int Manager::do_feature_propagate_update(double t, const std::vector<int> &camid
   }
   timelastupdate = t;
   return 0;
+}
+
+// VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388)
+void Manager::retriangulate_active_tracks(double t, const std::vector<int> &camids) {
+  active_tracks_time = t;
+  active_tracks_posinG.clear();
+  active_tracks_uvd.clear();
+  std::map<size_t, Mat> A_new, b_new;
+  std::map<size_t, int> count_new;
+  std::unordered_map<size_t, Mat> posinG_new;
+  std::map<size_t, std::pair<float, float>> feat_uvs_in_cam0;
+  // TrackBase::get_last_obs / get_last_ids: TrackKLT's points of the last feed, or TrackSIM's
+  auto last_obs = [&](int cam, std::vector<std::pair<size_t, std::pair<float, float>>> &out) {
+    out.clear();
+    if (!sim_last.empty()) {
+      auto it = sim_last.find(cam);
+      if (it != sim_last.end())
+        for (auto &f : it->second) out.push_back({f.first + currid, f.second});
+      return;
+    }
+    auto it = tracker.pts_last.find((size_t)cam);
+    if (it == tracker.pts_last.end()) return;
+    const auto &ids = tracker.ids_last[(size_t)cam];
+    for (size_t i = 0; i < it->second.size(); i++) out.push_back({ids[i], {it->second[i].x, it->second[i].y}});
+  };
+  const VarP &clone = state.clones.at(active_tracks_time);
+  std::vector<std::pair<size_t, std::pair<float, float>>> obs;
+  for (int cam_id : camids) {
+    Mat R_GtoI = clone->Rot(), p_IinG = clone->pos();
+    const VarP &calib = state.calib_IMUtoCAM.at(cam_id);
+    Mat R_ItoC = calib->Rot(), p_IinC = calib->pos();
+    Mat R_GtoCi = R_ItoC * R_GtoI;
+    Mat p_CiinG = p_IinG - R_GtoCi.T() * p_IinC;
+    last_obs(cam_id, obs);
+    for (auto &ob : obs) {
+      size_t featid = ob.first;
+      if (cam_id == 0) feat_uvs_in_cam0[featid] = ob.second;
+      if (state.features_SLAM.find(featid) != state.features_SLAM.end()) continue;
+      float un, vn;
+      state.cams.at(cam_id).undistort_f(ob.second.first, ob.second.second, un, vn);
+      Mat b_i = V3(un, vn, 1);
+      b_i = R_GtoCi.T() * b_i;
+      b_i = (1.0 / norm(b_i)) * b_i;
+      Mat Bperp = skew_x(b_i);
+      Mat Ai = Bperp.T() * Bperp;
+      Mat bi = Ai * p_CiinG;
+      if (linsys_A.find(featid) == linsys_A.end()) {
+        // std::map::insert: a second camera's observation of a new track does not replace the first's
+        A_new.insert({featid, Ai});
+        b_new.insert({featid, bi});
+        count_new.insert({featid, 1});
+      } else {
+        A_new[featid] = Ai + linsys_A[featid];
+        b_new[featid] = bi + linsys_b[featid];
+        count_new[featid] = 1 + linsys_count[featid];
+      }
+      if (count_new.at(featid) > 3) {
+        Mat A = A_new[featid], b = b_new[featid];
+        Mat p_FinG = colpiv_qr_solve(A, b);
+        Mat p_FinCi = R_GtoCi * (p_FinG - p_CiinG);
+        double sv[3];
+        singular_values3(A, sv);
+        double condA = sv[0] / sv[2];
+        if (std::abs(condA) <= o.fi_max_cond_number && p_FinCi[2] >= o.fi_min_dist && p_FinCi[2] <= o.fi_max_dist &&
+            !std::isnan(norm(p_FinCi)))
+          posinG_new[featid] = p_FinG;
+      }
+    }
+  }
+  linsys_A = A_new;
+  linsys_b = b_new;
+  linsys_count = count_new;
+  active_tracks_posinG = posinG_new;
+  if (active_tracks_posinG.empty() && state.features_SLAM.empty()) return;
+  for (const auto &feat : state.features_SLAM) {
+    Mat p_FinG = feat.second->get_xyz(false);
+    if (is_relative(feat.second->rep)) {
+      const VarP &cal = state.calib_IMUtoCAM.at(feat.second->anchor_cam);
+      const VarP &anc = state.clones.at(feat.second->anchor_time);
+      p_FinG = anc->Rot().T() * (cal->Rot().T() * (feat.second->get_xyz(false) - cal->pos())) + anc->pos();
+    }
+    active_tracks_posinG[feat.second->featid] = p_FinG;
+  }
+  const VarP &cal0 = state.calib_IMUtoCAM.at(0);
+  Mat R_ItoC = cal0->Rot(), p_IinC = cal0->pos();
+  Mat R_GtoIi = clone->Rot(), p_IiinG = clone->pos();
+  const Camera &cam0 = state.cams.at(0);
+  for (const auto &feat : active_tracks_posinG) {
+    auto uv = feat_uvs_in_cam0.find(feat.first);
+    if (uv == feat_uvs_in_cam0.end()) continue;
+    Mat p_FinIi = R_GtoIi * (feat.second - p_IiinG);
+    Mat p_FinCi = R_ItoC * p_FinIi + p_IinC;
+    double depth = p_FinCi[2];
+    double u = (double)uv->second.first, v = (double)uv->second.second;
+    if (depth < 0.1) continue;
+    if (u < 0 || (int)u >= cam0.w || v < 0 || (int)v >= cam0.h) continue;
+    active_tracks_uvd[feat.first] = V3(u, v, depth);
+  }
 }
 
 }  // namespace orc

@@ -4,14 +4,18 @@
 // do_feature_propagate_update), VioManagerHelper.cpp:40-76
 // (initialize_with_gt), ov_core/src/track/TrackSIM.cpp:30-79 and
 // uvio/src/core/UVioManager.cpp:26-344 (UWB buffering, anchors, do_uwb_propagate_update).
-// retriangulate_active_tracks (VioManagerHelper.cpp:190) only feeds visualization and is not
-// restated (it changes neither the state nor the feature database).
+// UpdaterZeroVelocity (zupt.h) and retriangulate_active_tracks (VioManagerHelper.cpp:190-388: the active
+// tracks' running linear triangulation systems, their positions and depths; they change neither the state
+// nor the feature database) are restated too.
 #pragma once
 #include <chrono>
+#include <map>
+#include <memory>
 
 #include "propagator.h"
 #include "tracker.h"
 #include "updater.h"
+#include "zupt.h"
 
 namespace orc {
 
@@ -38,6 +42,16 @@ struct Manager {
   std::map<double, UwbMsg> past_uwb;
   uvio_hp_timing_t timing{};
   UpdateStats last_msckf{};
+  // UpdaterZeroVelocity (VioManager.cpp:160, 186-188, 294-307, 360)
+  std::unique_ptr<UpdaterZUPT> zupt;
+  bool did_zupt_update = false, has_moved_since_zupt = false;
+  // TrackSIM's get_last_obs / get_last_ids of the last simulated frame (TrackSIM.cpp:72-77)
+  std::map<int, std::vector<std::pair<size_t, std::pair<float, float>>>> sim_last;
+  // retriangulate_active_tracks (VioManagerHelper.cpp:190-388) state and outputs
+  std::map<size_t, Mat> linsys_A, linsys_b;
+  std::map<size_t, int> linsys_count;
+  double active_tracks_time = -1;
+  std::unordered_map<size_t, Mat> active_tracks_posinG, active_tracks_uvd;
 
   explicit Manager(const uvio_hp_options_t &opt);
   void initialize_with_gt(const double x[17]);
@@ -51,6 +65,9 @@ struct Manager {
   int init_anchors(const std::vector<uvio_hp_anchor_t> &anchors);
   int do_feature_propagate_update(double t, const std::vector<int> &camids);
   int do_uwb_propagate_update(const UwbMsg &m);
+  // UVioManager.cpp:147-205 after the tracker: ZUPT, UWB ranges, feature propagate / update
+  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1);
+  void retriangulate_active_tracks(double t, const std::vector<int> &camids);
 };
 
 }  // namespace orc

@@ -92,7 +92,7 @@ def test_lockstep_cfg1_mono_images():
     steps = _lockstep(opts, sim, n, renderer=SceneRenderer(opts, device="cuda"))
     rows, full = _stats(steps, opts.max_clone_size)
     assert steps[-1][0]["P"].shape[0] >= 15 + 1 + 14 + 6 * 11  # one camera's 14 calibration dims
-    assert sum(a["timing"]["n_slam"] for a, _ in steps) > 0
+    assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 0
     _check(rows, full)
 
 

@@ -58,6 +58,7 @@ class Options(C.Structure):
         ("try_zupt", C.c_int), ("zupt_chi2_multipler", C.c_double), ("zupt_max_velocity", C.c_double),
         ("zupt_noise_multiplier", C.c_double), ("zupt_max_disparity", C.c_double),
         ("zupt_only_at_beginning", C.c_int), ("use_klt", C.c_int), ("use_aruco", C.c_int),
+        ("record_timing_information", C.c_int), ("record_timing_filepath", C.c_char * 256),
     ]
 
 
@@ -68,7 +69,7 @@ class Timing(C.Structure):
                 ("n_slam_delayed", C.c_int), ("n_clones", C.c_int), ("cov_dim", C.c_int),
                 ("msckf_rows", C.c_int), ("msckf_cols", C.c_int), ("k_feat_launches", C.c_int),
                 ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double), ("device_syncs", C.c_int),
-                ("sync_wait", C.c_double)]
+                ("sync_wait", C.c_double), ("zupt", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -109,6 +110,7 @@ SIGNATURES = [
     ("get_fej_vector", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
     ("get_timing", _I, [C.c_void_p, _P(Timing)]),
     ("get_clone_times", _I, [C.c_void_p, _P(_D), _I, _P(_I)]),
+    ("get_active_tracks", _I, [C.c_void_p, _P(_D), _P(C.c_uint64), _P(_D), _P(_D), _P(_I), _I, _P(_I)]),
     ("set_kernel_timing", _I, [C.c_void_p, _I]),
     ("get_kernel_stats", _I, [C.c_void_p, _I, _P(KStat), _I, _P(_I)]),
     ("feed_camera_device", _I, [C.c_void_p, _D, _I, _P(_I), _P(C.c_void_p), _P(_I), _P(_P(C.c_uint8))]),

@@ -21,6 +21,7 @@ SOURCES = [
     "engine_prop.cpp",
     "engine_update.cpp",
     "engine_track.cpp",
+    "engine_retri.cpp",
     "capi.cpp",
     "shard.cpp",
     "kernels_cov.hip",

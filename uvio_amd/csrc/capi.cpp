@@ -192,6 +192,15 @@ int uvio_hp_get_timing(uvio_hp_t *h, uvio_hp_timing_t *out) {
   return 0;
 }
 
+int uvio_hp_get_active_tracks(uvio_hp_t *h, double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid,
+                              int cap, int *n) {
+  if (!h || !t || !n || (cap > 0 && (!ids || !posinG || !uvd || !uvd_valid))) return UVIO_HP_E_ARG;
+  HP_GUARD(h, {
+    *n = h->e->get_active_tracks(t, ids, posinG, uvd, uvd_valid, cap);
+    return *n <= cap ? 0 : UVIO_HP_E_CAPACITY;
+  })
+}
+
 int uvio_hp_set_kernel_timing(uvio_hp_t *h, int on) {
   if (!h) return UVIO_HP_E_ARG;
   if (on < 0) return UVIO_HP_E_ARG;

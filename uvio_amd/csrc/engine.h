@@ -235,6 +235,7 @@ class Engine {
   WorkPool pool_;
   std::vector<FeatP> pending_delete_;  // features handed to an updater this frame (cleanup candidates)
   HostProf hprof_;                     // UVIO_HP_HOST_PROF section timer (debug)
+  FILE *timing_csv_ = nullptr;         // record_timing_information (VioManager.cpp:105-122)
   KProf kprof_;                        // live per-class kernel timing (uvio_hp_set_kernel_timing)
   int ktime_period_ = 0;
   long long frames_ = 0;               // camera / simulated frames fed
@@ -300,8 +301,18 @@ class Engine {
                                   const std::vector<double> &R, const std::vector<double> &res);
   void set_initial_covariance(const std::vector<double> &cov, const std::vector<VarP> &order);
 
+  // UpdaterZeroVelocity (UpdaterZeroVelocity.cpp:65-329; VioManager.cpp:160, 186-188, 294-307, 360)
+  std::vector<ImuSample> zupt_imu_;
+  bool zupt_have_last_off_ = false;
+  double zupt_last_off_ = 0.0, last_zupt_state_timestamp_ = 0.0;
+  int last_zupt_count_ = 0;
+  bool did_zupt_update_ = false, has_moved_since_zupt_ = false;
+  // 1: the zero-velocity update was applied (state time moved to t); 0: not
+  int zupt_try_update(double t);
+
   // propagator (host mean + Phi/Qd, device covariance)
   std::vector<ImuSample> select_imu_readings(double t0, double t1);
+  static std::vector<ImuSample> select_imu(const std::vector<ImuSample> &imu, double t0, double t1);
   void accumulate_phi(const std::vector<ImuSample> &prop, std::vector<double> &Phi, std::vector<double> &Qd, int n);
   void predict_and_compute(const ImuSample &a, const ImuSample &b, double *F, double *Qd, int n);
   void last_w(const std::vector<ImuSample> &prop, double *w);
@@ -312,9 +323,29 @@ class Engine {
   // updates
   int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1,
                      int track_syncs = 0, double track_wait = 0.0);
-  int do_feature_propagate_update(double t, const std::vector<int> &camids);
+  int do_feature_propagate_update(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT2);
   int msckf_update(std::vector<FeatP> &feats);
   void gram(int m, int ncol, int *nch);
+  // VioManager::retriangulate_active_tracks on the device (engine_retri.cpp)
+  struct RetriState {
+    int cap = 0, obs_cap = 0, slam_cap = 0, cur = 0, nslam = 0;
+    unsigned long long *keys[2] = {nullptr, nullptr};
+    DRetriEntry *ent[2] = {nullptr, nullptr};
+    DRetriObs *d_obs = nullptr, *h_obs = nullptr;
+    DRetriSlam *d_slam = nullptr;
+    double *scratch = nullptr;
+    hipEvent_t copied = nullptr;
+    bool copy_pending = false, valid = false;
+    double time = -1;
+  } rt_;
+  std::vector<DRetriObs> frame_obs_;  // the simulated feed's observations of the current frame
+  void retri_alloc(int nobs);
+  void retriangulate_active_tracks(double t, const std::vector<int> &camids);
+
+ public:
+  int get_active_tracks(double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid, int cap);
+
+ private:
   int slam_update(std::vector<FeatP> &feats);
   int slam_delayed_init(std::vector<FeatP> &feats);
   int slam_change_anchors();

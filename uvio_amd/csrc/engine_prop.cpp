@@ -165,6 +165,11 @@ std::vector<ImuSample> Engine::select_imu_readings(double time0, double time1) {
     std::lock_guard<std::mutex> lk(imu_mtx_);
     imu = imu_data_;
   }
+  return select_imu(imu, time0, time1);
+}
+
+// Propagator::select_imu_readings (Propagator.cpp:269-393) on a given buffer
+std::vector<ImuSample> Engine::select_imu(const std::vector<ImuSample> &imu, double time0, double time1) {
   auto interp = [](const ImuSample &a, const ImuSample &b, double t) {
     double lambda = (t - a.t) / (b.t - a.t);
     ImuSample d;
@@ -669,6 +674,250 @@ int Engine::propagate_uwb(double timestamp) {
   cov_propagate(imu_->id, n, ids, Phi, Qd);
   timestamp_ = timestamp;
   return 0;
+}
+
+}  // namespace uvhp
+
+namespace uvhp {
+
+namespace {
+// UpdaterHelper::measurement_compress_inplace (UpdaterHelper.cpp:456-487): Givens QR of the stacked rows
+// [H | res] (Eigen makeGivens / applyOnTheLeft(0, 1, G.adjoint()) conventions), keeping min(m, n) rows
+void givens_compress(std::vector<double> &H, std::vector<double> &res, int &m, int n) {
+  if (m <= n) return;
+  for (int c = 0; c < n; c++)
+    for (int r = m - 1; r > c; r--) {
+      const double p = H[(size_t)(r - 1) * n + c], q = H[(size_t)r * n + c];
+      double cs = 1, sn = 0;
+      if (q == 0) {
+        cs = p < 0 ? -1.0 : 1.0;
+        sn = 0;
+      } else if (p == 0) {
+        cs = 0;
+        sn = q < 0 ? 1.0 : -1.0;
+      } else if (std::abs(p) > std::abs(q)) {
+        const double t = q / p;
+        double u = std::sqrt(1.0 + t * t);
+        if (p < 0) u = -u;
+        cs = 1.0 / u;
+        sn = -t * cs;
+      } else {
+        const double t = p / q;
+        double u = std::sqrt(1.0 + t * t);
+        if (q < 0) u = -u;
+        sn = -1.0 / u;
+        cs = -t * sn;
+      }
+      auto rot = [&](double &x, double &y) {
+        const double xi = x, yi = y;
+        x = cs * xi - sn * yi;
+        y = sn * xi + cs * yi;
+      };
+      for (int j = c; j < n; j++) rot(H[(size_t)(r - 1) * n + j], H[(size_t)r * n + j]);
+      rot(res[r - 1], res[r]);
+    }
+  m = n;
+  H.resize((size_t)m * n);
+  res.resize(m);
+}
+}  // namespace
+
+// UpdaterZeroVelocity::try_update (UpdaterZeroVelocity.cpp:65-329) with the reference's defaults
+// (integrated_accel_constraint = false, model_time_varying_bias = true, override_with_disparity_check = true,
+// explicitly_enforce_zero_motion = false).  The residual / Jacobian over the IMU readings (6 rows per
+// interval, 9 columns [theta, bg, ba]) and their Givens compression are host math on ~60 x 9; the chi2 test
+// reads the 9 x 9 marginal covariance from the device; the bias propagation and the EKF update run on the
+// device like every other covariance operation.
+int Engine::zupt_try_update(double timestamp) {
+  stage_ = "UpdaterZeroVelocity::try_update";
+  std::vector<ImuSample> imu;
+  {
+    std::lock_guard<std::mutex> lk(imu_mtx_);
+    imu = zupt_imu_;
+  }
+  if (imu.empty()) {
+    last_zupt_state_timestamp_ = 0.0;
+    return 0;
+  }
+  if (timestamp_ == timestamp) {
+    last_zupt_state_timestamp_ = 0.0;
+    return 0;
+  }
+  if (!zupt_have_last_off_) {
+    zupt_last_off_ = calib_dt_->val[0];
+    zupt_have_last_off_ = true;
+  }
+  const double t_off_new = calib_dt_->val[0];
+  // Propagator::select_imu_readings on the ZUPT's own buffer
+  std::vector<ImuSample> recent = select_imu(imu, timestamp_ + zupt_last_off_, timestamp + t_off_new);
+  zupt_last_off_ = t_off_new;
+  if (recent.size() < 2) {
+    last_zupt_state_timestamp_ = 0.0;
+    return 0;
+  }
+  const int n = 9;
+  int m = 6 * ((int)recent.size() - 1);
+  std::vector<double> H((size_t)m * n, 0.0), res(m, 0.0);
+  double Dw[9], Da[9], Tg[9], Ra[9], Rw[9], R[9], Rj[9], g[3] = {0, 0, o_.gravity_mag};
+  Dm(o_.imu_model, dw_->val, Dw);
+  Dm(o_.imu_model, da_->val, Da);
+  TgM(tg_->val, Tg);
+  quat_2_Rot(qa_->val, Ra);
+  quat_2_Rot(qg_->val, Rw);
+  quat_2_Rot(imu_->val, R);
+  quat_2_Rot(o_.do_fej ? imu_->fej : imu_->val, Rj);
+  const double *bg = imu_->val + 10, *ba = imu_->val + 13;
+  double dt_summed = 0;
+  for (size_t i = 0; i + 1 < recent.size(); i++) {
+    const double dt = recent[i + 1].t - recent[i].t;
+    double t1[3], t2[3], a_hat[3], w_hat[3], Ta[3], Rg[3], Sg[9];
+    for (int k = 0; k < 3; k++) t1[k] = recent[i].am[k] - ba[k];
+    m3_vec(Da, t1, t2);
+    m3_vec(Ra, t2, a_hat);
+    m3_vec(Tg, a_hat, Ta);
+    for (int k = 0; k < 3; k++) t1[k] = recent[i].wm[k] - bg[k] - Ta[k];
+    m3_vec(Dw, t1, t2);
+    m3_vec(Rw, t2, w_hat);
+    const double w_omega = std::sqrt(dt) / o_.sigma_w, w_accel = std::sqrt(dt) / o_.sigma_a;
+    m3_vec(R, g, Rg);
+    const size_t r0 = 6 * i;
+    for (int k = 0; k < 3; k++) {
+      res[r0 + k] = -w_omega * w_hat[k];
+      res[r0 + 3 + k] = -w_accel * (a_hat[k] - Rg[k]);
+    }
+    m3_vec(Rj, g, Rg);
+    skew(Rg, Sg);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) {
+        H[(r0 + a) * n + 3 + b] = (a == b) ? -w_omega : 0.0;
+        H[(r0 + 3 + a) * n + b] = -w_accel * Sg[3 * a + b];
+        H[(r0 + 3 + a) * n + 6 + b] = (a == b) ? -w_accel : 0.0;
+      }
+    dt_summed += dt;
+  }
+  givens_compress(H, res, m, n);
+  if (m < 1) return 0;
+  const double Rn = o_.zupt_noise_multiplier;
+  double Qb[36] = {0};
+  for (int k = 0; k < 3; k++) {
+    Qb[7 * k] = dt_summed * o_.sigma_wb * o_.sigma_wb;
+    Qb[7 * (k + 3)] = dt_summed * o_.sigma_ab * o_.sigma_ab;
+  }
+  // chi2 with P_marg of [theta, bg, ba] (+ the bias evolution the update would apply)
+  std::vector<double> Pimu(15 * 15);
+  HP_HIP(hipMemcpy2DAsync(Pimu.data(), sizeof(double) * 15, d_.P + (size_t)imu_->id * d_.ldp + imu_->id,
+                          sizeof(double) * d_.ldp, sizeof(double) * 15, 15, hipMemcpyDeviceToHost, d_.stream));
+  dev_sync();
+  const int idx[9] = {0, 1, 2, 9, 10, 11, 12, 13, 14};
+  double Pm[81];
+  for (int a = 0; a < 9; a++)
+    for (int b = 0; b < 9; b++) Pm[9 * a + b] = Pimu[15 * idx[a] + idx[b]];
+  for (int a = 0; a < 6; a++)
+    for (int b = 0; b < 6; b++) Pm[9 * (3 + a) + 3 + b] += Qb[6 * a + b];
+  std::vector<double> HP((size_t)m * n, 0.0), S((size_t)m * m, 0.0);
+  for (int i = 0; i < m; i++)
+    for (int k = 0; k < n; k++) {
+      const double h = H[(size_t)i * n + k];
+      if (h == 0.0) continue;
+      for (int j = 0; j < n; j++) HP[(size_t)i * n + j] += h * Pm[9 * k + j];
+    }
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < m; j++) {
+      double acc = 0;
+      for (int k = 0; k < n; k++) acc += HP[(size_t)i * n + k] * H[(size_t)j * n + k];
+      S[(size_t)i * m + j] = acc + (i == j ? Rn : 0.0);
+    }
+  // LLT solve S x = res
+  std::vector<double> L((size_t)m * m, 0.0), y(res);
+  for (int j = 0; j < m; j++) {
+    double d = S[(size_t)j * m + j];
+    for (int k = 0; k < j; k++) d -= L[(size_t)j * m + k] * L[(size_t)j * m + k];
+    if (!(d > 0)) return 0;
+    L[(size_t)j * m + j] = std::sqrt(d);
+    for (int i = j + 1; i < m; i++) {
+      double v = S[(size_t)i * m + j];
+      for (int k = 0; k < j; k++) v -= L[(size_t)i * m + k] * L[(size_t)j * m + k];
+      L[(size_t)i * m + j] = v / L[(size_t)j * m + j];
+    }
+  }
+  for (int i = 0; i < m; i++) {
+    for (int k = 0; k < i; k++) y[i] -= L[(size_t)i * m + k] * y[k];
+    y[i] /= L[(size_t)i * m + i];
+  }
+  for (int i = m - 1; i >= 0; i--) {
+    for (int k = i + 1; k < m; k++) y[i] -= L[(size_t)k * m + i] * y[k];
+    y[i] /= L[(size_t)i * m + i];
+  }
+  double chi2 = 0;
+  for (int i = 0; i < m; i++) chi2 += res[i] * y[i];
+  const double chi2_check = chi2_table_[std::min(m, 999)];
+  // FeatureHelper::compute_disparity(db, state time, frame time) (FeatureHelper.h:60-108): raw-pixel
+  // displacement of every feature seen at both times, in the database's iteration order
+  const double time0 = timestamp_, time1 = timestamp;
+  std::vector<double> disp;
+  for (auto &kv : db_) {
+    const Feature &f = *kv.second;
+    if (f.to_delete) continue;
+    bool has0 = false;
+    for (auto &tr : f.tracks)
+      for (auto &ms : tr.m) has0 |= (ms.t == time0);
+    if (!has0) continue;
+    for (auto &tr : f.tracks) {
+      int i0 = -1, i1 = -1;
+      for (int k = 0; k < (int)tr.m.size(); k++) {
+        if (i0 < 0 && tr.m[k].t == time0) i0 = k;
+        if (i1 < 0 && tr.m[k].t == time1) i1 = k;
+      }
+      if (i0 < 0 || i1 < 0) continue;
+      const float dx = tr.m[i1].u - tr.m[i0].u, dy = tr.m[i1].v - tr.m[i0].v;
+      disp.push_back((double)std::sqrt(dx * dx + dy * dy));
+    }
+  }
+  double disp_avg = 0;
+  for (double d : disp) disp_avg += d;
+  disp_avg /= (double)disp.size();  // NaN without features, as the reference
+  const bool disparity_passed = disp_avg < o_.zupt_max_disparity && (int)disp.size() > 20;
+  const double vnorm = norm3(imu_->val + 7);
+  if (!disparity_passed && (chi2 > o_.zupt_chi2_multipler * chi2_check || vnorm > o_.zupt_max_velocity)) {
+    last_zupt_state_timestamp_ = 0.0;
+    last_zupt_count_ = 0;
+    return 0;
+  }
+  // FeatureDatabase::cleanup_measurements_exact (FeatureDatabase.cpp:245-263)
+  if (last_zupt_count_ >= 2) {
+    const double te = last_zupt_state_timestamp_;
+    for (auto it = db_.begin(); it != db_.end();) {
+      int ct = 0;
+      for (auto &tr : it->second->tracks) {
+        tr.m.erase(std::remove_if(tr.m.begin(), tr.m.end(), [te](const FeatMeas &x) { return x.t == te; }), tr.m.end());
+        ct += (int)tr.m.size();
+      }
+      if (ct < 1)
+        it = db_.erase(it);
+      else
+        it++;
+    }
+  }
+  // bias random walk over the window (EKFPropagation with Phi = I), then the EKF update with R = mult I
+  std::vector<int> bias_ids;
+  for (int k = 9; k < 15; k++) bias_ids.push_back(imu_->id + k);
+  std::vector<double> Phi(36, 0.0), Q(Qb, Qb + 36);
+  for (int k = 0; k < 6; k++) Phi[7 * k] = 1.0;
+  cov_propagate(imu_->id + 9, 6, bias_ids, Phi, Q);
+  std::vector<double> Hr((size_t)m * (n + 1));
+  for (int i = 0; i < m; i++) {
+    for (int j = 0; j < n; j++) Hr[(size_t)i * (n + 1) + j] = H[(size_t)i * n + j];
+    Hr[(size_t)i * (n + 1) + n] = res[i];
+  }
+  std::vector<int> hidx;
+  for (int k : idx) hidx.push_back(imu_->id + k);
+  const double *dH = stage(Hr.data(), Hr.size());
+  stage_flush();
+  ekf_update_rows(dH, n + 1, m, n, hidx, dH + n, n + 1, Rn);
+  timestamp_ = timestamp;
+  last_zupt_state_timestamp_ = timestamp;
+  last_zupt_count_++;
+  return 1;
 }
 
 }  // namespace uvhp

@@ -1,4 +1,6 @@
 // Engine: state layout, device buffers and covariance operations.
+#include <sys/stat.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -96,7 +98,6 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
     throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
   if (o_.feat_rep_slam != 0 && o_.feat_rep_slam != 2 && o_.feat_rep_slam != 4)
     throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: only GLOBAL_3D / ANCHORED_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
-  if (o_.try_zupt) throw HpError(UVIO_HP_E_CONFIG, "try_zupt: UpdaterZeroVelocity is not implemented");
   currid_ = 4 * (size_t)o_.max_aruco_features + 1;  // TrackBase::currid (TrackBase.cpp:34)
   int cur = 0;
   imu_ = mk(V_IMU, 15, 16);
@@ -185,6 +186,18 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
     }
   }
   upload_P_full(Ph, N_);
+  if (o_.record_timing_information) {
+    // VioManager.cpp:105-122: the old file is replaced, its directory created
+    std::string path(o_.record_timing_filepath);
+    std::remove(path.c_str());
+    for (size_t k = 1; k < path.size(); k++)
+      if (path[k] == '/') mkdir(path.substr(0, k).c_str(), 0755);
+    timing_csv_ = std::fopen(path.c_str(), "a");
+    if (!timing_csv_) throw HpError(UVIO_HP_E_CONFIG, "record_timing_filepath: cannot open " + path);
+    std::fprintf(timing_csv_, "# timestamp (sec),tracking,propagation,msckf update,");
+    if (o_.max_slam_features > 0) std::fprintf(timing_csv_, "slam update,slam delayed,");
+    std::fprintf(timing_csv_, "re-tri & marg,total\n");
+  }
   // uvio
   p_IinU_ = mk(V_VEC, 3, 3);
   for (int k = 0; k < 3; k++) p_IinU_->val[k] = p_IinU_->fej[k] = o_.p_IinU[k];
@@ -200,9 +213,15 @@ Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) 
 }
 
 Engine::~Engine() {
+  if (timing_csv_) std::fclose(timing_csv_);
   hipSetDevice(device_);
   if (shard_.nccl) rccl_comm_destroy(shard_.nccl);
   tracker_.reset();
+  void *rptrs[] = {rt_.keys[0], rt_.keys[1], rt_.ent[0], rt_.ent[1], rt_.d_obs, rt_.d_slam, rt_.scratch};
+  for (void *p : rptrs)
+    if (p) hipFree(p);
+  if (rt_.h_obs) hipHostFree(rt_.h_obs);
+  if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
                   d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard};
@@ -233,6 +252,7 @@ void Engine::alloc_device() {
   HP_HIP(hipEventCreate(&d_.ev0));
   HP_HIP(hipEventCreate(&d_.ev1));
   kprof_.stream = d_.stream;
+  HP_HIP(hipEventCreateWithFlags(&rt_.copied, hipEventDisableTiming));
   d_.ekf.kp = &kprof_;
   int C = o_.max_clone_size + 2;
   int K = o_.num_cameras;

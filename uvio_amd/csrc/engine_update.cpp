@@ -92,6 +92,13 @@ void Engine::feed_imu(double t, const double wm[3], const double am[3]) {
   std::lock_guard<std::mutex> lk(imu_mtx_);
   imu_data_.push_back(s);
   double cut = oldest - 0.10;
+  // UpdaterZeroVelocity::feed_imu (VioManager.cpp:186-188; UpdaterZeroVelocity.h:77-107)
+  if (is_initialized_ && o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
+    zupt_imu_.push_back(s);
+    if (cut >= 0)
+      zupt_imu_.erase(std::remove_if(zupt_imu_.begin(), zupt_imu_.end(), [&](const ImuSample &a) { return a.t < cut; }),
+                      zupt_imu_.end());
+  }
   if (cut >= 0) {
     auto it = imu_data_.begin();
     while (it != imu_data_.end() && it->t < cut) it++;
@@ -198,6 +205,17 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
     }
     fp[k] = it->second.get();
   }
+  frame_obs_.resize(nobs);
+  for (size_t k = 0; k < nobs; k++) {
+    DRetriObs &o = frame_obs_[k];
+    o.featid = (unsigned long long)(ids[k] + currid_);
+    o.u = uv[2 * k];
+    o.v = uv[2 * k + 1];
+    o.un = uvn[2 * k];
+    o.vn = uvn[2 * k + 1];
+    o.cam = cam_of[k];
+    o.pad = 0;
+  }
   const int nw = pool_.threads();
   pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
     for (size_t w = b; w < e; w++)
@@ -241,6 +259,26 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
   timing_.device_syncs = track_syncs;
   timing_.sync_wait = track_wait;
   if (!is_initialized_) return UVIO_HP_E_STATE;
+  // zero-velocity update (UVioManager.cpp:147-162, VioManager.cpp:291-307): on success the frame ends here
+  if (o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
+    if (timestamp_ != t) did_zupt_update_ = zupt_try_update(t) == 1;
+    if (did_zupt_update_) {
+      // Propagator / UpdaterZeroVelocity::clean_old_imu_measurements(t + dt - 0.10)
+      const double cut = t + calib_dt_->val[0] - 0.10;
+      std::lock_guard<std::mutex> lk(imu_mtx_);
+      if (cut >= 0) {
+        auto old = [&](const ImuSample &a) { return a.t < cut; };
+        imu_data_.erase(std::remove_if(imu_data_.begin(), imu_data_.end(), old), imu_data_.end());
+        zupt_imu_.erase(std::remove_if(zupt_imu_.begin(), zupt_imu_.end(), old), zupt_imu_.end());
+      }
+      timing_.zupt = 1;
+      timing_.timestamp = t;
+      timing_.n_clones = (int)clones_.size();
+      timing_.cov_dim = N_;
+      timing_.total = secs(rT1, clk::now());
+      return 0;
+    }
+  }
   if (!past_uwb_.empty()) {
     for (auto it = past_uwb_.begin(); it != past_uwb_.lower_bound(t); it++) {
       if (it->first < t && it->first > timestamp_) {
@@ -255,15 +293,23 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
     }
     past_uwb_.erase(past_uwb_.begin(), past_uwb_.upper_bound(t));
   }
-  int rc = do_feature_propagate_update(t, camids);
+  int rc = do_feature_propagate_update(t, camids, rT2);
   timing_.total = secs(rT1, clk::now());
+  // VioManager.cpp:631-644: one row per frame that ran the whole update, times in the reference's columns
+  // (the UWB ranges processed before the propagation land in "propagation", as in UVioManager.cpp:147-188)
+  if (rc == 0 && timing_csv_ && timing_.n_clones >= std::min(o_.max_clone_size, 5)) {
+    std::fprintf(timing_csv_, "%.15f,%.5f,%.5f,%.5f,", timestamp_ + calib_dt_->val[0], timing_.tracking,
+                 timing_.propagation, timing_.msckf_update);
+    if (o_.max_slam_features > 0) std::fprintf(timing_csv_, "%.5f,%.5f,", timing_.slam_update, timing_.slam_delayed);
+    std::fprintf(timing_csv_, "%.5f,%.5f\n", timing_.marg, timing_.total);
+    std::fflush(timing_csv_);
+  }
   return rc;
 }
 
-// VioManager.cpp:323-651
-int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids) {
+// VioManager.cpp:323-651 (rT2: the end of tracking, UVioManager.cpp:147)
+int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids, clk::time_point rT2) {
   stage_ = "feature selection";
-  auto rT2 = clk::now();
   if (timestamp_ > t) return UVIO_HP_E_ORDER;
   if (timestamp_ != t) {
     HPROF("prop");
@@ -280,6 +326,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   timing_.cov_dim = N_;
   if ((int)clones_.size() < std::min(o_.max_clone_size, 5)) return 0;
   if (timestamp_ != t) return 0;
+  has_moved_since_zupt_ = true;
 
   std::vector<FeatP> feats_lost, feats_marg, feats_slam;
   auto t_sel = clk::now();
@@ -408,6 +455,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   if (rc) return rc;
   auto rT6 = clk::now();
   HPROF("marg.total");
+  retriangulate_active_tracks(t, camids);
   for (auto &f : up) f->to_delete = true;
   // FeatureDatabase::cleanup: only features handed to an updater can carry to_delete, so they are
   // erased by key (erasing a node keeps the others' iteration order, as the reference's scan does)

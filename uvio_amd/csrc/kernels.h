@@ -170,6 +170,48 @@ void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const doub
                             const DFeatOut *fout = nullptr, const int *gate = nullptr, double *resout = nullptr);
 double chi2_quantile95(int dof);
 
+// ---- VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388) on the device ----
+// Every observation of the frame (cameras in message order, each camera's tracks in get_last_obs order)
+// updates its track's running linear triangulation system; the systems live in a featid-keyed open-
+// addressing hash table (two generations: last frame's, this frame's).
+struct DRetriObs {
+  unsigned long long featid;
+  float un, vn, u, v;  // undistorted (undistort_cv) and raw pixel coordinates
+  int cam, pad;
+};
+struct DRetriEntry {
+  double A[9], b[3];
+  int cnt;
+  int last_obs, last_pass;  // index of the track's last observation / last one that triangulated
+  int has_uv0;              // seen by camera 0 this frame
+  float u0, v0;
+  double pos[3];            // p_FinG (valid when last_pass >= 0)
+  double uvd[3];
+  int uvd_valid;
+  int first_obs;  // a track new this frame keeps its FIRST observation's system (std::map::insert)
+};
+struct DRetriSlam {  // SLAM landmarks: position from the state, cam0 pixel from this frame's tracks
+  unsigned long long featid;
+  double pos[3];
+  double uvd[3];
+  int has_uv0, uvd_valid;
+  float u0, v0;
+};
+struct RetriJob {
+  int nobs, nslam, cap;  // cap: hash capacity (power of two)
+  const DRetriObs *obs;
+  double *scratch;       // per observation: A 9, b 3, cnt, pos 3, pass
+  unsigned long long *keys_old, *keys_new;
+  DRetriEntry *ent_old, *ent_new;
+  DRetriSlam *slam;
+  double R_GtoC[kMaxCams][9], p_CinG[kMaxCams][3];  // camera poses at the current clone
+  double R_ItoC0[9], p_IinC0[3], R_GtoI[9], p_IinG[3];
+  int w0, h0;
+  double max_cond, min_dist, max_dist;
+};
+constexpr unsigned long long kRetriEmpty = ~0ull;
+void launch_retriangulate(hipStream_t s, const RetriJob &job);
+
 // Raise a kernel's dynamic-LDS limit to `want` bytes, capped so static + dynamic LDS fits the CU's
 // 160 KiB.  Returns the granted bytes (0 on failure); a failed call's sticky runtime error is cleared so
 // it cannot surface in another library (torch) on this thread.

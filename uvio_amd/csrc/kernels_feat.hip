@@ -767,4 +767,173 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
                      chi2_table, H_all, out, max_meas, max_nf);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388).  The reference walks the frame's
+// observations camera by camera; per track it sets A_new = A_i + A_old (A_old: the track's system of the
+// LAST frame, so a second camera's observation overwrites the first's, a reference quirk kept here), count_new
+// = 1 + count_old, and once count_new > 3 solves A_new p = b_new (colPivHouseholderQr) and keeps p if cond(A)
+// <= max_cond and the depth in the observing camera lies in [min_dist, max_dist]; a later observation's
+// result overwrites an earlier one's.  Here every observation is one thread (k_retri_obs: hash lookup of the
+// track's old system, insertion of its new slot, its own A_new / solve; atomicMax marks the track's last
+// observation and its last successful one), then k_retri_final keeps those two per track and k_retri_uvd
+// projects the tracks and the SLAM landmarks seen by camera 0 into it.
+__device__ __forceinline__ unsigned retri_hash(unsigned long long k, int cap) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (unsigned)(k & (unsigned long long)(cap - 1));
+}
+__device__ int retri_find(const unsigned long long *keys, int cap, unsigned long long id) {
+  unsigned h = retri_hash(id, cap);
+  for (int p = 0; p < cap; p++, h = (h + 1) & (cap - 1)) {
+    const unsigned long long k = keys[h];
+    if (k == id) return (int)h;
+    if (k == kRetriEmpty) return -1;
+  }
+  return -1;
+}
+__device__ int retri_insert(unsigned long long *keys, int cap, unsigned long long id) {
+  unsigned h = retri_hash(id, cap);
+  for (int p = 0; p < cap; p++, h = (h + 1) & (cap - 1)) {
+    const unsigned long long prev = atomicCAS(&keys[h], kRetriEmpty, id);
+    if (prev == kRetriEmpty || prev == id) return (int)h;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(256) k_retri_reset(RetriJob job) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < job.cap) {
+    job.keys_new[i] = kRetriEmpty;
+    DRetriEntry &e = job.ent_new[i];
+    e.last_obs = e.last_pass = -1;
+    e.first_obs = 0x7fffffff;
+    e.has_uv0 = 0;
+    e.uvd_valid = 0;
+  }
+  if (i < job.nslam) {
+    job.slam[i].has_uv0 = 0;
+    job.slam[i].uvd_valid = 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_retri_obs(RetriJob job) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= job.nobs) return;
+  const DRetriObs o = job.obs[i];
+  // feat_uvs_in_cam0 is recorded before the SLAM skip
+  for (int s = 0; s < job.nslam; s++)
+    if (job.slam[s].featid == o.featid) {
+      if (o.cam == 0) {
+        job.slam[s].u0 = o.u;
+        job.slam[s].v0 = o.v;
+        job.slam[s].has_uv0 = 1;
+      }
+      return;
+    }
+  const int slot = retri_insert(job.keys_new, job.cap, o.featid);
+  if (slot < 0) return;
+  DRetriEntry &e = job.ent_new[slot];
+  if (o.cam == 0) {
+    e.u0 = o.u;
+    e.v0 = o.v;
+    e.has_uv0 = 1;
+  }
+  const double *R = job.R_GtoC[o.cam], *pC = job.p_CinG[o.cam];
+  double b0[3] = {(double)o.un, (double)o.vn, 1.0}, bi[3];
+  m3t_vec(R, b0, bi);
+  const double inv = 1.0 / norm3(bi);
+  for (int k = 0; k < 3; k++) bi[k] = inv * bi[k];
+  double Bp[9], Ai[9], bb[3];
+  skew(bi, Bp);
+  m3_mul_at(Bp, Bp, Ai);
+  m3_vec(Ai, pC, bb);
+  double *sc = job.scratch + (size_t)17 * i;
+  const int old = retri_find(job.keys_old, job.cap, o.featid);
+  int cnt = 1;
+  if (old >= 0) {
+    const DRetriEntry &eo = job.ent_old[old];
+    for (int k = 0; k < 9; k++) Ai[k] = Ai[k] + eo.A[k];
+    for (int k = 0; k < 3; k++) bb[k] = bb[k] + eo.b[k];
+    cnt = 1 + eo.cnt;
+  }
+  for (int k = 0; k < 9; k++) sc[k] = Ai[k];
+  for (int k = 0; k < 3; k++) sc[9 + k] = bb[k];
+  int pass = 0;
+  if (cnt > 3) {
+    double p[3], d[3], pc[3], sv[3];
+    colpiv_solve3(Ai, bb, p);
+    for (int k = 0; k < 3; k++) d[k] = p[k] - pC[k];
+    m3_vec(R, d, pc);
+    singular_values3(Ai, sv);
+    const double cond = sv[0] / sv[2];
+    if (fabs(cond) <= job.max_cond && pc[2] >= job.min_dist && pc[2] <= job.max_dist && !isnan(norm3(pc))) {
+      pass = 1;
+      for (int k = 0; k < 3; k++) sc[13 + k] = p[k];
+    }
+  }
+  sc[16] = pass;
+  sc[12] = (double)cnt + (old >= 0 ? 0.5 : 0.0);  // the fraction marks a track with an old system
+  atomicMax(&e.last_obs, i);
+  atomicMin(&e.first_obs, i);
+  if (pass) atomicMax(&e.last_pass, i);
+}
+
+__global__ void __launch_bounds__(256) k_retri_final(RetriJob job) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= job.nobs) return;
+  const DRetriObs o = job.obs[i];
+  const int slot = retri_find(job.keys_new, job.cap, o.featid);
+  if (slot < 0) return;  // a SLAM landmark (never inserted)
+  DRetriEntry &e = job.ent_new[slot];
+  const double *sc = job.scratch + (size_t)17 * i;
+  // a track with an old system keeps its last observation's (operator[] overwrites), a new one its first
+  const bool had_old = sc[12] != (double)(int)sc[12];
+  if ((had_old ? e.last_obs : e.first_obs) == i) {
+    for (int k = 0; k < 9; k++) e.A[k] = sc[k];
+    for (int k = 0; k < 3; k++) e.b[k] = sc[9 + k];
+    e.cnt = (int)sc[12];
+  }
+  if (e.last_pass == i)
+    for (int k = 0; k < 3; k++) e.pos[k] = sc[13 + k];
+}
+
+__device__ __forceinline__ int retri_uvd(const RetriJob &job, const double *pos, float u0, float v0, double *uvd) {
+  double d[3], pI[3], pC[3];
+  for (int k = 0; k < 3; k++) d[k] = pos[k] - job.p_IinG[k];
+  m3_vec(job.R_GtoI, d, pI);
+  m3_vec(job.R_ItoC0, pI, pC);
+  for (int k = 0; k < 3; k++) pC[k] = pC[k] + job.p_IinC0[k];
+  const double depth = pC[2], u = (double)u0, v = (double)v0;
+  if (depth < 0.1) return 0;
+  if (u < 0 || (int)u >= job.w0 || v < 0 || (int)v >= job.h0) return 0;
+  uvd[0] = u;
+  uvd[1] = v;
+  uvd[2] = depth;
+  return 1;
+}
+
+__global__ void __launch_bounds__(256) k_retri_uvd(RetriJob job) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < job.cap) {
+    DRetriEntry &e = job.ent_new[i];
+    if (job.keys_new[i] != kRetriEmpty && e.last_pass >= 0 && e.has_uv0)
+      e.uvd_valid = retri_uvd(job, e.pos, e.u0, e.v0, e.uvd);
+  }
+  if (i < job.nslam) {
+    DRetriSlam &sl = job.slam[i];
+    if (sl.has_uv0) sl.uvd_valid = retri_uvd(job, sl.pos, sl.u0, sl.v0, sl.uvd);
+  }
+}
+
+void launch_retriangulate(hipStream_t s, const RetriJob &job) {
+  const int nr = std::max(job.cap, job.nslam);
+  hipLaunchKernelGGL(k_retri_reset, dim3((nr + 255) / 256), dim3(256), 0, s, job);
+  if (job.nobs > 0) {
+    hipLaunchKernelGGL(k_retri_obs, dim3((job.nobs + 255) / 256), dim3(256), 0, s, job);
+    hipLaunchKernelGGL(k_retri_final, dim3((job.nobs + 255) / 256), dim3(256), 0, s, job);
+  }
+  hipLaunchKernelGGL(k_retri_uvd, dim3((nr + 255) / 256), dim3(256), 0, s, job);
+}
+
 }  // namespace uvhp

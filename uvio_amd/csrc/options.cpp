@@ -326,6 +326,8 @@ void options_default(uvio_hp_options_t *o) {
   o->zupt_only_at_beginning = 0;
   o->use_klt = 1;
   o->use_aruco = 0;
+  o->record_timing_information = 0;
+  std::snprintf(o->record_timing_filepath, sizeof(o->record_timing_filepath), "%s", "ov_msckf_timing.txt");
 }
 
 int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
@@ -400,8 +402,11 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
   est.getb({"downsample_cameras"}, o->downsample_cameras);
   std::string hm;
   if (est.gets({"histogram_method"}, hm)) o->histogram_method = hm == "NONE" ? 0 : (hm == "CLAHE" ? 2 : 1);
-  est.getb({"record_timing_information"}, o->record_timing);
-  o->record_timing = 1;  // timings are always kept (cheap); the CSV write is the caller's choice
+  est.getb({"record_timing_information"}, o->record_timing_information);
+  std::string tpath;
+  if (est.gets({"record_timing_filepath"}, tpath))
+    std::snprintf(o->record_timing_filepath, sizeof(o->record_timing_filepath), "%s", tpath.c_str());
+  o->record_timing = 1;  // the per-frame timing struct is always kept (cheap); the CSV file is the option above
 
   // IMU chain (relative_config_imu)
   std::string rel;

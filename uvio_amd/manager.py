@@ -310,6 +310,23 @@ class VioManager:
         k = n.value
         return ids[:k].copy(), pG[:k].copy(), st[:k].copy(), c2[:k].copy()
 
+    def get_active_tracks(self):
+        """VioManager::get_active_tracks: (time, {featid: p_FinG}, {featid: (u, v, depth)})."""
+        cap = 16384
+        t = C.c_double()
+        ids = np.zeros(cap, dtype=np.uint64)
+        pos = np.zeros((cap, 3))
+        uvd = np.zeros((cap, 3))
+        ok = np.zeros(cap, dtype=np.int32)
+        n = C.c_int()
+        self._check(self._call("get_active_tracks", self._h, C.byref(t), ids.ctypes.data_as(C.POINTER(C.c_uint64)),
+                               _dp(pos), _dp(uvd), ok.ctypes.data_as(C.POINTER(C.c_int)), cap, C.byref(n)),
+                    "get_active_tracks")
+        k = n.value
+        P = {int(ids[i]): pos[i].copy() for i in range(k)}
+        D = {int(ids[i]): uvd[i].copy() for i in range(k) if ok[i]}
+        return t.value, P, D
+
     def get_clone_times(self):
         out = np.zeros(256)
         n = C.c_int()

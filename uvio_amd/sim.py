@@ -55,9 +55,13 @@ def quat_2_rot(q):
 
 
 class Trajectory:
-    """Seeded smooth SE(3): sum of sinusoids in a ~10 x 10 x 3 m room, +-30 deg/s rotations."""
+    """Seeded smooth SE(3): sum of sinusoids in a ~10 x 10 x 3 m room, +-30 deg/s rotations.
 
-    def __init__(self, seed=5, speed=1.0):
+    static_until: the platform rests until this time and then starts moving smoothly over `ramp` seconds
+    (a C2 time warp tau(t) with tau' = smoothstep), e.g. to exercise the zero-velocity update."""
+
+    def __init__(self, seed=5, speed=1.0, static_until=None, ramp=1.0):
+        self.static_until, self.ramp = static_until, ramp
         rng = np.random.default_rng(seed)
         self.ap = rng.uniform(0.5, 1.5, (3, 3)) * np.array([[2.0], [2.0], [0.4]]) * speed
         self.wp = rng.uniform(0.2, 0.6, (3, 3))
@@ -66,17 +70,34 @@ class Trajectory:
         self.we = rng.uniform(0.3, 0.9, (3, 2))
         self.phe = rng.uniform(0, 2 * np.pi, (3, 2))
 
+    def warp(self, t):
+        """(tau, dtau/dt, d2tau/dt2)"""
+        if self.static_until is None:
+            return t, 1.0, 0.0
+        t0, T = self.static_until, self.ramp
+        x = (t - t0) / T
+        if x <= 0:
+            return t0, 0.0, 0.0
+        if x >= 1:
+            return t0 + 0.5 * T + (t - t0 - T), 1.0, 0.0
+        return t0 + T * (x ** 3 - 0.5 * x ** 4), 3 * x ** 2 - 2 * x ** 3, (6 * x - 6 * x ** 2) / T
+
     def pos(self, t):
-        return np.sum(self.ap * np.sin(self.wp * t + self.php), axis=1)
+        tau = self.warp(t)[0]
+        return np.sum(self.ap * np.sin(self.wp * tau + self.php), axis=1)
 
     def vel(self, t):
-        return np.sum(self.ap * self.wp * np.cos(self.wp * t + self.php), axis=1)
+        tau, d1, _ = self.warp(t)
+        return d1 * np.sum(self.ap * self.wp * np.cos(self.wp * tau + self.php), axis=1)
 
     def acc(self, t):
-        return np.sum(-self.ap * self.wp ** 2 * np.sin(self.wp * t + self.php), axis=1)
+        tau, d1, d2 = self.warp(t)
+        return (d1 * d1 * np.sum(-self.ap * self.wp ** 2 * np.sin(self.wp * tau + self.php), axis=1) +
+                d2 * np.sum(self.ap * self.wp * np.cos(self.wp * tau + self.php), axis=1))
 
     def euler(self, t):
-        return np.sum(self.ae * np.sin(self.we * t + self.phe), axis=1)
+        tau = self.warp(t)[0]
+        return np.sum(self.ae * np.sin(self.we * tau + self.phe), axis=1)
 
     def R_ItoG(self, t):
         yaw, pitch, roll = self.euler(t)
@@ -127,10 +148,11 @@ class SimStream:
 
     def __init__(self, opts, duration=6.0, cam_rate=None, imu_rate=200.0, seed=5, spawn=200, life_full=None,
                  frac_lost=0.10, frac_long=0.05, sigma_pix=1.0, depth=(5.0, 7.0), noisy_imu=True, speed=1.0,
-                 anchors=None, uwb_rate=10.0, uwb_sigma=0.5):
+                 anchors=None, uwb_rate=10.0, uwb_sigma=0.5, static_for=None):
+        """static_for: seconds after the start (t0 = 1 s) during which the platform rests (ZUPT workloads)."""
         self.opts = opts
         self.rng = np.random.default_rng(seed + 1000)
-        self.traj = Trajectory(seed, speed)
+        self.traj = Trajectory(seed, speed, static_until=(1.0 + static_for) if static_for else None)
         self.cam_rate = cam_rate if cam_rate else (opts.track_frequency if opts.track_frequency > 0 else 20.0)
         self.imu_rate = imu_rate
         self.K = opts.num_cameras
