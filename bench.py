@@ -356,7 +356,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    acc = {"rows": 0, "n_msckf": 0, "n_slam": 0, "cols": 0, "cov_dim": 0, "tracking_s": 0.0, "syncs": 0}
+    acc = {"rows": 0, "n_msckf": 0, "n_slam": 0, "cols": 0, "cov_dim": 0, "tracking_s": 0.0, "syncs": 0,
+           "sync_wait": 0.0}
+    stages = ("propagation", "msckf_update", "slam_update", "slam_delayed", "marg", "total")
+    stage_s = dict.fromkeys(stages, 0.0)
     est_p, est_q, gt_p, gt_q = [], [], [], []
     mgr.set_kernel_timing(args.ktime_period)
     ks0 = mgr.kernel_stats(flush=True)
@@ -372,6 +375,9 @@ def main():
         acc["cov_dim"] = max(acc["cov_dim"], tm["cov_dim"])
         acc["tracking_s"] += tm["tracking"]
         acc["syncs"] += tm["device_syncs"]
+        acc["sync_wait"] += tm["sync_wait"]
+        for k in stages:
+            stage_s[k] += tm[k]
         _, x = mgr.get_imu_state()
         est_q.append(x[0:4].copy())
         est_p.append(x[4:7].copy())
@@ -431,6 +437,8 @@ def main():
                        "mean_msckf_feats": acc["n_msckf"] / args.steps, "mean_slam_feats": acc["n_slam"] / args.steps,
                        "mean_msckf_rows": acc["rows"] / args.steps, "H_cols": acc["cols"],
                        "state_dim": acc["cov_dim"], "host_waits_per_frame": acc["syncs"] / args.steps,
+                       "host_wait_ms_per_frame": 1e3 * acc["sync_wait"] / args.steps,
+                       "stage_ms": {k: round(1e3 * v / args.steps, 4) for k, v in stage_s.items()},
                        "parallelism": ("feature-shard%d" % world) if shard else ("replicas%d" % world)},
             "ate_rmse_m": acc_ate["pos_m"],
             "ate": {"align": "posyaw (ov_eval AlignTrajectory.cpp:84-106)", "pos_rmse_m": acc_ate["pos_m"],

@@ -58,7 +58,20 @@ int main(int argc, char **argv) {
   (void)hipMalloc(&dts, 16);
   (void)hipMemcpy(dA, A.data(), 8 * nrows * n, hipMemcpyHostToDevice);
   size_t bytes = (size_t)nrows * (n | 1) * 8 + (size_t)(4 * nrows) * 8;
-  (void)hipFuncSetAttribute((const void *)k_test, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+  // static + dynamic LDS must fit the CU's 160 KiB (the same rule as set_dyn_lds in kernels.h): a launch
+  // asking for more aborts the queue (HSA_STATUS_ERROR_INVALID_ALLOCATION), so it is refused here
+  hipFuncAttributes fa{};
+  (void)hipFuncGetAttributes(&fa, (const void *)k_test);
+  const size_t lds_limit = 160 * 1024 - (size_t)fa.sharedSizeBytes;
+  if (bytes > lds_limit) {
+    printf("n=%d needs %zu B of dynamic LDS > %zu available: skipped\n", n, bytes, lds_limit);
+    return 0;
+  }
+  if (hipFuncSetAttribute((const void *)k_test, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_limit) !=
+      hipSuccess) {
+    printf("dynamic LDS limit not granted\n");
+    return 1;
+  }
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -72,8 +85,16 @@ int main(int argc, char **argv) {
     for (int it = 0; it < 3; it++) {
       (void)hipEventRecord(e0);
       hipLaunchKernelGGL(k_test, dim3(1), dim3(nt), bytes, 0, dA, n, nrows, which, mode, dO2, dts, dG);
+      hipError_t le = hipGetLastError();
+      if (le != hipSuccess) {
+        printf("launch failed: %s\n", hipGetErrorString(le));
+        return 1;
+      }
       (void)hipEventRecord(e1);
-      (void)hipEventSynchronize(e1);
+      if (hipEventSynchronize(e1) != hipSuccess) {
+        printf("kernel failed\n");
+        return 1;
+      }
       float ms;
       (void)hipEventElapsedTime(&ms, e0, e1);
       long long ts;

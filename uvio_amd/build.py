@@ -25,6 +25,7 @@ SOURCES = [
     "capi.cpp",
     "shard.cpp",
     "kernels_cov.hip",
+    "kernels_ekf.hip",
     "kernels_feat.hip",
     "kernels_chi2.hip",
     "kernels_track.hip",

@@ -306,4 +306,300 @@ __device__ void ldl_blk16(double *A, int ld, int n, int nrows, double *Lp) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 1 / d with one Newton step on v_rcp_f64 (the IEEE division sequence is ~2x longer on the serial chain)
+__device__ __forceinline__ double frcp1(double d) {
+  const double x = __builtin_amdgcn_rcp(d);
+  return fma(x, fma(-d, x, 1.0), x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDL^T with the serial chain confined to ONE wavefront and (optionally) the unit-lower inverse built
+// alongside, for one workgroup of nw >= 2 waves.  A: the nrows x n lower triangle (rows n .. nrows-1 are
+// right-hand-side rows) in a storage layout (SqLayout: ld-strided square, whose upper triangle then holds
+// the inverse; PkLayout: packed lower triangle, row i at i(i+1)/2, for the large factors that only fit in
+// LDS packed).  Work goes in slots of 16 columns, ONE workgroup barrier per slot:
+//   wave 0, slot J : waits (LDS counter) for the helpers' rank-16 update of block column J by block J-1, then
+//                    factors the 16 x (nrows - 16 J) panel in registers (lane l owns rows 16 J + l + 64 s): per
+//                    column one 16-entry LDS broadcast of the pivot column of the block's own rows, frcp1;
+//   waves 1.., slot J: the rank-16 update of block column J by block J-1 first (one MFMA tile per wave,
+//                    counted), then that of block columns J+1 .., the 16x16 inverse X_PP = L_PP^-1 of block
+//                    P = J-1 (unit lower, quad-parallel, no divisions) and the off-diagonal inverse blocks
+//                    of block row I = J-2: X_IK = -X_II sum_{K'=K..I-1} L_IK' X_K'K (MFMA).
+// Output: A(i, k) (i > k) = L_u[i][k] (unit-lower LDL factor), Dd[k] = d_k; RHS rows hold D^-1 L_u^-1 b;
+// with_inv (SqLayout only): A(j, i) (j < i < n) = X[i][j], X = L_u^-1 (diagonal 1).
+// Measured on MI355X (tools/bench_fact.hip, r = 100 with the residual row): 105k cycles for LDL^T + the
+// inverse against 161k for ldl_blk16 + ldl_to_chol + a blocked triangular inverse.
+// Panel rows per lane <= SMAX: nrows <= 64 SMAX.
+struct SqLayout {
+  static constexpr bool square = true;
+  int ld;
+  __device__ __forceinline__ size_t operator()(int i, int j) const { return (size_t)i * ld + j; }
+};
+struct PkLayout {
+  static constexpr bool square = false;
+  __device__ __forceinline__ size_t operator()(int i, int j) const { return (size_t)i * (i + 1) / 2 + j; }
+};
+__host__ __device__ inline size_t packed_lds_doubles(int nrows) { return (size_t)nrows * (nrows + 1) / 2; }
+
+// acc (C layout) of the 16x16 tile at (i0, j0), masked to the stored lower triangle (col <= row)
+template <class LA>
+__device__ __forceinline__ dbl4 tile_load_lower(const double *A, LA la, int i0, int j0, int nrows, int n, int kq,
+                                                int r16) {
+  dbl4 acc;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    acc[q] = (row < nrows && col < n && col <= row) ? A[la(row, col)] : 0.0;
+  }
+  return acc;
+}
+template <class LA>
+__device__ __forceinline__ void tile_store_lower(double *A, LA la, int i0, int j0, int nrows, int n, int kq, int r16,
+                                                 dbl4 acc) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    if (row < nrows && col < n && col <= row) A[la(row, col)] = acc[q];
+  }
+}
+// acc -= L(i0.., oP..) D_P L(j0.., oP..)^T: the rank-16 update by the factored block column P
+template <class LA>
+__device__ __forceinline__ dbl4 tile_rank16(const double *A, LA la, const double *Dd, int i0, int j0, int oP,
+                                            int nrows, int n, int kq, int r16, dbl4 acc) {
+  const int arow = min(i0 + r16, nrows - 1), bcol = min(j0 + r16, n - 1);
+  const bool av = i0 + r16 < nrows, bv = j0 + r16 < n;
+  double a[4], b[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int kk = 4 * u + kq;
+    a[u] = av ? -A[la(arow, oP + kk)] * Dd[oP + kk] : 0.0;
+    b[u] = bv ? A[la(bcol, oP + kk)] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+  return acc;
+}
+
+// One column step K of the wave-resident panel: the pivot column of the block's own rows through a
+// 16-entry LDS broadcast, the reciprocal by frcp1; compile-time loop bounds keep the panel in registers.
+// (Two-column steps with a 2x2 pivot block measured slower: the redundant elimination of the second
+// column costs more FP64 issue than the saved broadcast.)
+template <int SMAX, int K>
+__device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], double *bc, double *Dd, int oJ, int n, int nrows,
+                                            int lane) {
+  if constexpr (K < 16) {
+    if (oJ + K >= n) return;
+    if (lane < 16) bc[lane] = v[0][K];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double d = bc[K];
+    if (lane == 0) Dd[oJ + K] = d;
+    const double dinv = frcp1(d);
+    double w[16];
+#pragma unroll
+    for (int p = K + 1; p < 16; p++) w[p] = bc[p];
+    if (lane > K) {
+      const double l = v[0][K] * dinv;
+      v[0][K] = l;
+#pragma unroll
+      for (int p = K + 1; p < 16; p++) v[0][p] = fma(-l, w[p], v[0][p]);
+    }
+#pragma unroll
+    for (int s = 1; s < SMAX; s++) {
+      if (oJ + 64 * s < nrows) {
+        const double l = v[s][K] * dinv;
+        v[s][K] = l;
+#pragma unroll
+        for (int p = K + 1; p < 16; p++) v[s][p] = fma(-l, w[p], v[s][p]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // every lane has read bc before the next step overwrites it
+    panel_steps<SMAX, K + 1>(v, bc, Dd, oJ, n, nrows, lane);
+  }
+}
+
+// X[k][c] from lane 4c + (k & 3) of the quad (DPP quad_perm broadcast of both halves)
+template <int KK>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  constexpr int ctrl = KK * 85;  // quad_perm [KK, KK, KK, KK]
+  const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, ctrl, 0xf, 0xf, false);
+  const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), ctrl, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// steps k = K .. 14 of the quad-parallel unit-lower 16x16 inverse; Lb: the block's corner (square storage)
+template <int K>
+__device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *Lb, int ld, int bn, int q) {
+  if constexpr (K < 15) {
+    const double xk = quad_bcast<(K & 3)>(x[K >> 2]);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int i = q + 4 * m;
+      if (i > K && i < bn) x[m] = fma(-Lb[(size_t)i * ld + K], xk, x[m]);
+    }
+    quad_inv_steps<K + 1>(x, Lb, ld, bn, q);
+  }
+}
+
+template <int SMAX, class LA>
+__device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows, double *Dd, bool with_inv,
+                                             long long *prof = nullptr) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int nb = (n + 15) / 16, nbr = (nrows + 15) / 16;
+  if (!LA::square) with_inv = false;
+  const int nslot = with_inv ? nb + 2 : nb;
+  __shared__ int colcnt;  // column-update tiles finished so far (helpers -> wave 0)
+  if (threadIdx.x == 0) colcnt = 0;
+  __syncthreads();
+  int coltarget = 0;
+  for (int J = 0; J < nslot; J++) {
+    const int P = J - 1;
+    if (P >= 0 && J < nb) coltarget += nbr - J;
+    const long long tslot = prof ? (long long)clock64() : 0;
+    if (wid == 0) {
+      if (J < nb) {
+        const int oJ = 16 * J;
+        if (P >= 0) {
+          while (__hip_atomic_load(&colcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < coltarget)
+            __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        double v[SMAX][16];
+#pragma unroll
+        for (int s = 0; s < SMAX; s++) {
+          const int ro = lane + 64 * s, i = oJ + ro;
+#pragma unroll
+          for (int p = 0; p < 16; p++) v[s][p] = (i < nrows && oJ + p < n && p <= ro) ? A[la(i, oJ + p)] : 0.0;
+        }
+        __shared__ double bc[16];
+        panel_steps<SMAX, 0>(v, bc, Dd, oJ, n, nrows, lane);
+#pragma unroll
+        for (int s = 0; s < SMAX; s++) {
+          const int ro = lane + 64 * s, i = oJ + ro;
+#pragma unroll
+          for (int p = 0; p < 16; p++)
+            if (i < nrows && oJ + p < n && p < ro) A[la(i, oJ + p)] = v[s][p];
+        }
+      }
+    } else {
+      const int nh = nw - 1;
+      // the rank-16 update of block column J by block P (wave 0 waits for it), one tile per helper
+      if (P >= 0 && J < nb) {
+        for (int I = J + wid - 1; I < nbr; I += nh) {
+          dbl4 acc = tile_load_lower(A, la, 16 * I, 16 * J, nrows, n, kq, r16);
+          acc = tile_rank16(A, la, Dd, 16 * I, 16 * J, 16 * P, nrows, n, kq, r16, acc);
+          tile_store_lower(A, la, 16 * I, 16 * J, nrows, n, kq, r16, acc);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_fetch_add(&colcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      // then: [X_PP] [X_IK, K < I = J-2] [rank-16 tiles (I, C), C >= J+1]
+      const bool do_xd = with_inv && P >= 0 && P < nb;
+      const int I2 = J - 2;
+      const int nxo = (with_inv && I2 >= 1 && I2 < nb) ? I2 : 0;
+      int ntr = 0;
+      if (P >= 0 && P < nb)
+        for (int C = J + 1; C < nb; C++) ntr += nbr - C;
+      const int ntask = (do_xd ? 1 : 0) + nxo + ntr;
+      for (int t = wid - 1; t < ntask; t += nh) {
+        int u = t;
+        if constexpr (LA::square) {
+          const int ld = la.ld;
+          if (do_xd && u == 0) {
+            // X_PP = L_PP^-1 (unit lower), right-looking, no divisions: lane 4c + q keeps column c's entries
+            // of rows q + 4m; step k broadcasts X[k][c] inside the quad (DPP) and the rows below update
+            const int oP = 16 * P, bn = min(16, n - oP);
+            const int c = lane >> 2, q = lane & 3;
+            double x[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) x[m] = (q + 4 * m == c) ? 1.0 : 0.0;
+            quad_inv_steps<0>(x, A + (size_t)oP * ld + oP, ld, bn, q);
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+              const int i = q + 4 * m;
+              if (i > c && i < bn && c < bn) A[(size_t)(oP + c) * ld + oP + i] = x[m];
+            }
+            continue;
+          }
+          u -= do_xd ? 1 : 0;
+          if (u < nxo) {
+            // X_IK = -X_II sum_{K' = K .. I-1} L_IK' X_K'K
+            const int I = I2, K = u, oI = 16 * I, oK = 16 * K, ri = oI + r16;
+            dbl4 y = {0.0, 0.0, 0.0, 0.0};
+            for (int Kp = K; Kp < I; Kp++) {
+              const int oKp = 16 * Kp;
+              double a[4], b[4];
+#pragma unroll
+              for (int s = 0; s < 4; s++) {
+                const int kp = oKp + 4 * s + kq;  // row of X_K'K = column of L_IK'
+                const int j = oK + r16;           // column of X_K'K
+                a[s] = (ri < n && kp < n) ? A[(size_t)ri * ld + kp] : 0.0;
+                double xb = 0.0;
+                if (kp < n && j < n) {
+                  if (kp > j)
+                    xb = A[(size_t)j * ld + kp];
+                  else if (kp == j)
+                    xb = 1.0;
+                }
+                b[s] = xb;
+              }
+#pragma unroll
+              for (int s = 0; s < 4; s++) y = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], y, 0, 0, 0);
+            }
+            // X_IK = -X_II Y: Y's C layout (register q = Y[kq + 4q][r16]) is the B operand of k-slab q
+            dbl4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              const int m = oI + 4 * q + kq;  // column of X_II (row ri)
+              double xa = 0.0;
+              if (ri < n && m < n) {
+                if (m < ri)
+                  xa = -A[(size_t)m * ld + ri];
+                else if (m == ri)
+                  xa = -1.0;
+              }
+              x = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, y[q], x, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              const int i = oI + kq + 4 * q, j = oK + r16;
+              if (i < n && j < n) A[(size_t)j * ld + i] = x[q];
+            }
+            continue;
+          }
+          u -= nxo;
+        }
+        int C = J + 1;
+        while (u >= nbr - C) {
+          u -= nbr - C;
+          C++;
+        }
+        const int I = C + u;
+        dbl4 acc = tile_load_lower(A, la, 16 * I, 16 * C, nrows, n, kq, r16);
+        acc = tile_rank16(A, la, Dd, 16 * I, 16 * C, 16 * P, nrows, n, kq, r16, acc);
+        tile_store_lower(A, la, 16 * I, 16 * C, nrows, n, kq, r16, acc);
+      }
+    }
+    if (prof && lane == 0 && wid < 2 && J < 32) prof[32 * wid + J] = (long long)clock64() - tslot;  // debug timing
+    __syncthreads();
+  }
+}
+
+// SMAX dispatch: the panel rows one lane owns
+template <class LA>
+__device__ __forceinline__ void ldl_wave(double *A, LA la, int n, int nrows, double *Dd, bool with_inv) {
+  if (nrows <= 64)
+    ldl_wave_inv<1>(A, la, n, nrows, Dd, with_inv);
+  else if (nrows <= 128)
+    ldl_wave_inv<2>(A, la, n, nrows, Dd, with_inv);
+  else if (nrows <= 192)
+    ldl_wave_inv<3>(A, la, n, nrows, Dd, with_inv);
+  else
+    ldl_wave_inv<4>(A, la, n, nrows, Dd, with_inv);
+}
+constexpr int kWaveMaxRows = 256;  // ldl_wave's panel capacity (4 rows per lane)
+
 }  // namespace uvhp

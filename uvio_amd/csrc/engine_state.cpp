@@ -405,10 +405,10 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"feature", "k_feature", 1},
       {"chi2", "k_gemm_HPg,k_gemm_HPg_tiled,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
-      {"ekf_update", "k_ekf_M,k_ekf_S,k_ekf_small,k_chi2_gate,k_trinv16,k_trsm_lt,k_ekf_P,k_gram_reduce,k_info_cholP,"
-                     "k_gemm,k_info_cholZ,k_info_P",
+      {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm,k_info_cholZ,k_trinv16,"
+                     "k_trsm_lt,k_info_P",
        1},
-      {"ldl", "k_ekf_small", 1},
+      {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
       {"pyramid", "k_hist_multi,k_eq_scharr_multi,k_pyr_scharr_multi", 0},
   };
@@ -524,7 +524,7 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
     if (apply) apply();
     return;
   }
-  if (r > kMaxEkfRows) throw HpError(UVIO_HP_E_CAPACITY, "direct EKF update with more than 256 rows");
+  if (r > kMaxEkfRows) throw HpError(UVIO_HP_E_CAPACITY, "direct EKF update with more than 255 rows");
   if (!hidx_dev) {
     hidx_dev = stage(hidx.data(), (size_t)n);
     stage_flush();

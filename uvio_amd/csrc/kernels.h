@@ -130,8 +130,8 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 
 // EKF update (StateHelper::EKFUpdate, StateHelper.cpp:116-197) for H (r x n, ld = ldh) whose column j
 // maps to covariance index hidx[j] (device), residual res (r, device, stride res_stride), noise sigma2.
-// Scratch: M (N x r), W (N x r), S (3 r x r: Linv, global work, S_up), y (r), dx (N), neg (int).
-constexpr int kMaxEkfRows = 256;        // rows of one direct (uncompressed) EKF update
+// Scratch: M (N x r), W (N x r), S (5 r x r: L^-1, -, S_up, global factor work), y (r), dx (N), neg (int).
+constexpr int kMaxEkfRows = 255;        // rows of one direct (uncompressed) EKF update (+ residual <= 256)
 constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-workgroup solvers
 // S holds 5 r^2 doubles for r rows
 struct EkfScratch {
@@ -162,6 +162,9 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
                        const int *hidx, double sigma2, EkfScratch &sc);
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
                        EkfScratch &sc);
+// M = P[:, hidx] H^T (N x r, ld r) alone (k_ekf_MS without its S blocks); zero (optional): set to 0
+void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                  const int *hidx, double *M, int *zero);
 // StateHelper::initialize_invertible for a 3-dof variable appended at N (StateHelper.cpp:484-577)
 // fout != nullptr: H_Linv = inverse of fout->HfR (formed on the device); gate: skipped when *gate == 0;
 // resout != nullptr: receives the residual column of rows 0..2 (Hx[a][n]), for the host's value update

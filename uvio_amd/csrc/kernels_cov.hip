@@ -374,88 +374,6 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
                      gbuf, use_lds);
 }
 
-// ----------------------------------------------------------------------------------------------
-// EKF update
-// M[i][j] = sum_k P[i][hidx[k]] * H[j][k]   (N x r)   (M_a = P H^T, StateHelper.cpp:137-146)
-__global__ void __launch_bounds__(256) k_ekf_M(const double *__restrict__ P, int ldp, int N, const double *__restrict__ H,
-                                               int ldh, int r, int n, const int *__restrict__ hidx, double *__restrict__ M,
-                                               int *zero) {
-  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero = 0;  // the update's negative-diagonal count
-  __shared__ double Ps[16][17];
-  __shared__ double Hs[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
-  double acc = 0.0;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    int k = k0 + tx;
-    Ps[ty][tx] = (i0 + ty < N && k < n) ? P[(size_t)(i0 + ty) * ldp + hidx[k]] : 0.0;
-    Hs[ty][tx] = (j0 + ty < r && k < n) ? H[(size_t)(j0 + ty) * ldh + k] : 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += Ps[ty][kk] * Hs[tx][kk];
-    __syncthreads();
-  }
-  if (i0 + ty < N && j0 + tx < r) M[(size_t)(i0 + ty) * r + j0 + tx] = acc;
-}
-
-// S_up[a][b] = sum_k H[a][k] * M[hidx[k]][b] (+ s2 on the diagonal)   (r x r, multi-WG)
-__global__ void __launch_bounds__(256) k_ekf_S(const double *__restrict__ H, int ldh, int r, int n,
-                                               const int *__restrict__ hidx, const double *__restrict__ M, double s2,
-                                               double *__restrict__ Sout) {
-  __shared__ double Hs[16][17];
-  __shared__ double Ms[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int a0 = blockIdx.y * 16, b0 = blockIdx.x * 16;
-  double acc = 0.0;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    Hs[ty][tx] = (a0 + ty < r && k0 + tx < n) ? H[(size_t)(a0 + ty) * ldh + k0 + tx] : 0.0;
-    Ms[ty][tx] = (k0 + ty < n && b0 + tx < r) ? M[(size_t)hidx[k0 + ty] * r + b0 + tx] : 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += Hs[ty][kk] * Ms[kk][tx];
-    __syncthreads();
-  }
-  int a = a0 + ty, b = b0 + tx;
-  if (a < r && b < r) Sout[(size_t)a * r + b] = acc + (a == b ? s2 : 0.0);
-}
-
-// Single workgroup (512 threads): LDL^T-based Cholesky of the augmented [S ; res^T] (S from the upper
-// triangle of S_up = selfadjointView<Upper>, StateHelper.cpp:160) -> L (lower, ld r) and y = L^-1 res
-// (dense_lds.h).  LDS when the factor plus the panel scratch fit, else the global scratch `Sg`.
-__global__ void __launch_bounds__(512) k_ekf_small(const double *__restrict__ Sup, int r,
-                                                   const double *__restrict__ res, int res_stride,
-                                                   double *__restrict__ L_out, double *__restrict__ y_out, double *Sg,
-                                                   int use_lds) {
-  extern __shared__ double lds[];
-  double *A = use_lds ? lds : Sg;
-  const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
-  double *Lp = A + (size_t)(r + 1) * ld;
-  staged_copy(
-      r * r + r,
-      [&](int e) {
-        if (e >= r * r) return res[(size_t)(e - r * r) * res_stride];
-        const int a = e / r, b = e - a * r;
-        return (b <= a) ? Sup[(size_t)b * r + a] : 0.0;
-      },
-      [&](int e, double v) {
-        if (e >= r * r) {
-          A[(size_t)r * ld + e - r * r] = v;
-        } else {
-          const int a = e / r, b = e - a * r;
-          if (b <= a) A[(size_t)a * ld + b] = v;
-        }
-      });
-  __syncthreads();
-  ldl_blk16(A, ld, r, r + 1, Lp);
-  ldl_to_chol(A, ld, r, r + 1);
-  for (int j = threadIdx.x; j < r; j += blockDim.x) y_out[j] = A[(size_t)r * ld + j];
-  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
-    int a = e / r, b = e % r;
-    L_out[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
-  }
-}
-size_t ekf_small_lds_bytes(int r) { return dense_lds_bytes(r + 1, r) + (size_t)(r + 1) * 4 * sizeof(double); }
-
 // Inverses of the 16x16 diagonal blocks of a lower-triangular L (r x r, ld): one 64-lane workgroup per
 // block stages the block in LDS (one load round), then lane c < 16 forms column c by forward
 // substitution.  Dinv: block b at Dinv + 256 b, row-major.  Rows past r are treated as identity.
@@ -556,99 +474,6 @@ void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, in
   hipLaunchKernelGGL(k_trsm_lt, dim3((N + 15) / 16), dim3(64), 0, s, M, ldm, hidx, N, r, L, ldl, Dinv, W);
 }
 
-// P[i][j] -= sum_k W[i][k] W[j][k] for j >= i, mirrored to (j,i); dx = W y; negative-diagonal count
-__global__ void __launch_bounds__(256) k_ekf_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ W,
-                                               int r, const double *__restrict__ y, double *__restrict__ dx, int *neg,
-                                               const int *gate) {
-  if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
-  __shared__ double Wi[16][17];
-  __shared__ double Wj[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int bi = blockIdx.y, bj = blockIdx.x;
-  if (bj < bi) return;  // upper tiles only (uniform per block)
-  int i0 = bi * 16, j0 = bj * 16;
-  double acc = 0.0;
-  for (int k0 = 0; k0 < r; k0 += 16) {
-    Wi[ty][tx] = (i0 + ty < N && k0 + tx < r) ? W[(size_t)(i0 + ty) * r + k0 + tx] : 0.0;
-    Wj[ty][tx] = (j0 + ty < N && k0 + tx < r) ? W[(size_t)(j0 + ty) * r + k0 + tx] : 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += Wi[ty][kk] * Wj[tx][kk];
-    __syncthreads();
-  }
-  int i = i0 + ty, j = j0 + tx;
-  if (i < N && j < N && j >= i) {
-    double v = P[(size_t)i * ldp + j] - acc;
-    P[(size_t)i * ldp + j] = v;
-    P[(size_t)j * ldp + i] = v;
-    if (i == j && v < 0.0) atomicAdd(neg, 1);
-  }
-  // dx by the diagonal blocks' first row of threads
-  if (bi == bj && ty == 0) {
-    int row = i0 + tx;
-    if (row < N) {
-      double a = 0.0;
-      for (int k = 0; k < r; k++) a += W[(size_t)row * r + k] * y[k];
-      dx[row] = a;
-    }
-  }
-}
-
-void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
-                       const int *hidx, double sigma2, EkfScratch &sc) {
-  dim3 gM((r + 15) / 16, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, H, ldh, r, n, hidx, sc.M, sc.neg);
-  double *Sup = sc.S + 2 * (size_t)r * r;
-  dim3 gS((r + 15) / 16, (r + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_S, gS, dim3(256), 0, s, H, ldh, r, n, hidx, sc.M, sigma2, Sup);
-}
-
-// chi2 = |y|^2 (y = L^-1 r from k_ekf_small; one wavefront, fixed order) against thr: the P-update gate,
-// and [chi2, accepted] into out[0], out[1] (read back with dx)
-__global__ void k_chi2_gate(const double *__restrict__ y, int r, double thr, int *__restrict__ gate,
-                            double *__restrict__ out) {
-  double s = 0.0;
-  for (int k = threadIdx.x; k < r; k += 64) s += y[k] * y[k];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-  if (threadIdx.x == 0) {
-    const int acc = !(s > thr);
-    *gate = acc;
-    out[0] = s;
-    out[1] = acc;
-  }
-}
-
-void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
-                       EkfScratch &sc) {
-  size_t bytes = ekf_small_lds_bytes(r);
-  int use_lds = bytes <= kMaxDynLds;
-  double *Lf = sc.S;
-  double *Sup = sc.S + 2 * (size_t)r * r;
-  double *Sg = sc.S + 3 * (size_t)r * r;  // (r+1)(r|1) + 4(r+1) <= 2 r^2 doubles once r >= 40 (else LDS)
-  ensure_lds_attrs();
-  {
-    KScope ks(sc.kp, KC_LDL);
-    hipLaunchKernelGGL(k_ekf_small, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Lf, sc.y, Sg,
-                       use_lds);
-  }
-  // LDL^T of the r x r innovation covariance with the residual as an extra row: r^3/3 + r^2 FLOPs; the
-  // lower triangle and the residual read, the factor written
-  if (sc.kp) sc.kp->credit(KC_LDL, (double)r * r * r / 3.0 + (double)r * r, 8.0 * (1.5 * r * r + 2.0 * r));
-  if (sc.chi2_gate) {  // StateHelper::initialize's chi2 test on this factor
-    hipLaunchKernelGGL(k_chi2_gate, dim3(1), dim3(64), 0, s, sc.y, r, sc.chi2_thr, sc.chi2_gate, sc.dx + N);
-    sc.gate = sc.chi2_gate;
-  }
-  launch_trsm_lt(s, sc.M, r, nullptr, N, r, Lf, r, sc.Dinv, sc.W);  // W = M L^-T
-  int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_ekf_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.W, r, sc.y, sc.dx, sc.neg, sc.gate);
-}
-
-void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
-                       const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc) {
-  launch_ekf_phaseA(s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc);
-  launch_ekf_phaseB(s, P, ldp, N, r, res, res_stride, sc);
-}
-
 // ----------------------------------------------------------------------------------------------
 // Information-form EKF update for compressed (m > n) batches.
 //
@@ -696,15 +521,28 @@ __global__ void __launch_bounds__(256) k_gemm(int ta, int tb, int m, int n, int 
   if (i0 + ty < m && j0 + tx < n) C[(size_t)(i0 + ty) * ldc + j0 + tx] = acc;
 }
 
-// Single workgroup: P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1),
-// zero upper) and L_P (n x n, ld n).
+// Single-workgroup Cholesky factors of the information-form update (dense_lds.h ldl_wave: one wave
+// factors each 16-column panel, the other waves do the rank-16 updates).  Storage mode: 0 = square in
+// LDS, 1 = packed lower triangle in LDS (n up to ~195), 2 = square in the global scratch gbuf.
+// L_c = L_u D^1/2; an extra right-hand-side row b leaves as L_c^-1 b = D^1/2 (D^-1 L_u^-1 b).
+template <int SMAX, class LA>
+__device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int n, int nrows) {
+  ldl_wave_inv<SMAX>(A, la, n, nrows, Dd, false);
+  for (int k = threadIdx.x; k < n; k += blockDim.x) Dd[k] = sqrt(Dd[k]);  // sqrt(d)
+  __syncthreads();
+}
+
+// P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1), zero upper) and L_P (n x n).
+template <int SMAX, int PACKED>
 __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
                                                     int n, double *__restrict__ Laug, double *__restrict__ Lout,
-                                                    double *gbuf, int use_lds) {
+                                                    double *gbuf, int mode) {
   extern __shared__ double lds[];
-  double *A = use_lds ? lds : gbuf;
+  double *A = (mode == 2) ? gbuf : lds;
   const int ld = n | 1;
-  double *Lp = A + (size_t)n * ld;
+  const size_t asz = PACKED ? packed_lds_doubles(n) : (size_t)n * ld;
+  double *Dd = A + asz;
+  auto idx = [&](int a, int b) { return PACKED ? (size_t)a * (a + 1) / 2 + b : (size_t)a * ld + b; };
   staged_copy(
       n * n,
       [&](int e) {
@@ -713,32 +551,37 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
       },
       [&](int e, double v) {
         const int a = e / n, b = e - a * n;
-        if (b <= a) A[(size_t)a * ld + b] = v;
+        if (b <= a) A[idx(a, b)] = v;
       });
   __syncthreads();
-  ldl_blk16(A, ld, n, n, Lp);
-  ldl_to_chol(A, ld, n, n);
+  if constexpr (PACKED)
+    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n);
+  else
+    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n);
   const int na = n + 1;
   for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
-    int a = e / na, b = e % na;
+    const int a = e / na, b = e - a * na;
     double v = 0.0;
-    if (a < n && b < n) v = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    if (a < n && b < n) v = (b < a) ? A[idx(a, b)] * Dd[b] : (b == a ? Dd[a] : 0.0);
     else if (a == n && b == n) v = 1.0;
     Laug[e] = v;
     if (a < n && b < n) Lout[(size_t)a * n + b] = v;
   }
 }
 
-// Single workgroup: [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T
-// -> w = U^-1 c.  Writes U (n x n, ld n) and w (n).
+// [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T -> w = U^-1 c.
+// Writes U (n x n, ld n) and w (n).
+template <int SMAX, int PACKED>
 __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
                                                     double *__restrict__ Uout, double *__restrict__ w, double *gbuf,
-                                                    int use_lds) {
+                                                    int mode) {
   extern __shared__ double lds[];
-  double *A = use_lds ? lds : gbuf;
+  double *A = (mode == 2) ? gbuf : lds;
   const int ld = n | 1;
   const int na = n + 1;
-  double *Lp = A + (size_t)na * ld;
+  const size_t asz = PACKED ? packed_lds_doubles(na) : (size_t)na * ld;
+  double *Dd = A + asz;
+  auto idx = [&](int a, int b) { return PACKED ? (size_t)a * (a + 1) / 2 + b : (size_t)a * ld + b; };
   staged_copy(
       (n + 1) * n,
       [&](int e) {
@@ -747,18 +590,51 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
       },
       [&](int e, double v) {
         const int a = e / n, b = e - a * n;
-        if (b <= a) A[(size_t)a * ld + b] = v;
+        if (b <= a) A[idx(a, b)] = v;
       });
   __syncthreads();
-  ldl_blk16(A, ld, n, n + 1, Lp);
-  ldl_to_chol(A, ld, n, n + 1);
-  for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[(size_t)n * ld + j];
+  if constexpr (PACKED)
+    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n + 1);
+  else
+    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n + 1);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[idx(n, j)] * Dd[j];
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
-    int a = e / n, b = e % n;
-    Uout[e] = (b <= a) ? A[(size_t)a * ld + b] : 0.0;
+    const int a = e / n, b = e - a * n;
+    Uout[e] = (b < a) ? A[idx(a, b)] * Dd[b] : (b == a ? Dd[a] : 0.0);
   }
 }
-size_t info_chol_lds_bytes(int nrows, int n) { return dense_lds_bytes(nrows, n) + (size_t)nrows * 4 * sizeof(double); }
+// the instantiation for a factor of `rows` rows (panel rows per lane) and storage mode
+template <class KP>
+static KP pick_info_kernel(const KP (&tab)[4][2], int rows, int mode) {
+  const int si = rows <= 64 ? 0 : rows <= 128 ? 1 : rows <= 192 ? 2 : 3;
+  return tab[si][mode == 1 ? 1 : 0];
+}
+typedef void (*CholPFn)(const double *, int, const int *, int, double *, double *, double *, int);
+typedef void (*CholZFn)(const double *, int, double, double *, double *, double *, int);
+static const CholPFn kCholP[4][2] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>},
+                                     {k_info_cholP<2, 0>, k_info_cholP<2, 1>},
+                                     {k_info_cholP<3, 0>, k_info_cholP<3, 1>},
+                                     {k_info_cholP<4, 0>, k_info_cholP<4, 1>}};
+static const CholZFn kCholZ[4][2] = {{k_info_cholZ<1, 0>, k_info_cholZ<1, 1>},
+                                     {k_info_cholZ<2, 0>, k_info_cholZ<2, 1>},
+                                     {k_info_cholZ<3, 0>, k_info_cholZ<3, 1>},
+                                     {k_info_cholZ<4, 0>, k_info_cholZ<4, 1>}};
+
+// storage mode and dynamic LDS bytes of an info-form factor of nrows x n (+ the n doubles of D)
+static int info_chol_mode(int nrows, int n, size_t *bytes) {
+  const size_t sq = ((size_t)nrows * (n | 1) + n) * sizeof(double);
+  const size_t pk = (packed_lds_doubles(nrows) + n) * sizeof(double);
+  if (sq <= (size_t)kMaxDynLds) {
+    *bytes = sq;
+    return 0;
+  }
+  if (pk <= (size_t)kMaxDynLds) {
+    *bytes = pk;
+    return 1;
+  }
+  *bytes = 0;
+  return 2;
+}
 
 
 // P[i][j] -= sum_k V[i][k] V[j][k] - s2 sum_k X[i][k] X[j][k]  for j >= i, mirrored;  dx = X w;
@@ -821,15 +697,16 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
   double *w = sc.y;
   double *gbuf = sc.M;                            // global fallback work buffer (N rmax >= the factor's bytes)
   ensure_lds_attrs();
-  size_t b1 = info_chol_lds_bytes(n, n);
-  int l1 = b1 <= kMaxDynLds;
-  hipLaunchKernelGGL(k_info_cholP, dim3(1), dim3(512), l1 ? b1 : 0, s, P, ldp, hidx, n, Laug, Lf, gbuf, l1);
+  if (n + 1 > kWaveMaxRows) throw std::runtime_error("information-form update wider than the factorization panel");
+  size_t b1 = 0;
+  const int m1 = info_chol_mode(n, n, &b1);
+  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(512), b1, s, P, ldp, hidx, n, Laug, Lf, gbuf, m1);
   dim3 g((na + 15) / 16, (na + 15) / 16);
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 0, 0, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 1, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
-  size_t b2 = info_chol_lds_bytes(n + 1, n);
-  int l2 = b2 <= kMaxDynLds;
-  hipLaunchKernelGGL(k_info_cholZ, dim3(1), dim3(512), l2 ? b2 : 0, s, E, n, sigma2, Uf, w, gbuf, l2);
+  size_t b2 = 0;
+  const int m2 = info_chol_mode(n + 1, n, &b2);
+  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, gbuf, m2);
   launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);     // V = P[:,I] L^-T
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
   int nb = (N + 15) / 16;
@@ -838,7 +715,7 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
 }
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
-// M = P[:, hidx] Hx^T is in sc.M (N x 3, from k_ekf_M); Hx (3 x n, ld), HLinv (3x3, device), s2.
+// M = P[:, hidx] Hx^T is in sc.M (N x 3, from launch_ekf_M); Hx (3 x n, ld), HLinv (3x3, device), s2.
 // With fout (delayed init enqueued behind its feature group): H_Linv is the inverse of the feature's
 // H_finit (DFeatOut::HfR), formed here with the host's cofactor formula, and the whole step is skipped
 // when the gate (the batch's accepted-feature count) is 0.
@@ -906,8 +783,7 @@ __global__ void k_init_invertible(double *__restrict__ P, int ldp, int N, const 
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc, const DFeatOut *fout,
                             const int *gate, double *resout) {
-  dim3 gM(1, (N + 15) / 16);
-  hipLaunchKernelGGL(k_ekf_M, gM, dim3(256), 0, s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M, (int *)nullptr);
+  launch_ekf_M(s, P, ldp, N, Hx, ldh, 3, n, hidx, sc.M, nullptr);
   int nt = N * 3;
   hipLaunchKernelGGL(k_init_invertible, dim3((nt + 255) / 256), dim3(256), 0, s, P, ldp, N, sc.M, Hx, ldh, n, hidx,
                      HLinv, s2, fout, gate, resout);
@@ -916,12 +792,13 @@ void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const doub
 static void ensure_lds_attrs() {
   static bool done = false;
   if (done) return;
-  const void *fns[4] = {(const void *)k_gram_reduce_chol, (const void *)k_ekf_small, (const void *)k_info_cholP,
-                        (const void *)k_info_cholZ};
-  const int want[4] = {150 * 1024, kMaxDynLds, kMaxDynLds, kMaxDynLds};
-  for (int k = 0; k < 4; k++)
-    if (set_dyn_lds(fns[k], want[k]) < want[k])
-      throw std::runtime_error("dynamic LDS limit not granted for a covariance kernel (" + std::to_string(k) + ")");
+  if (set_dyn_lds((const void *)k_gram_reduce_chol, 150 * 1024) < 150 * 1024)
+    throw std::runtime_error("dynamic LDS limit not granted for k_gram_reduce_chol");
+  for (int a = 0; a < 4; a++)
+    for (int b = 0; b < 2; b++)
+      if (set_dyn_lds((const void *)kCholP[a][b], kMaxDynLds) < kMaxDynLds ||
+          set_dyn_lds((const void *)kCholZ[a][b], kMaxDynLds) < kMaxDynLds)
+        throw std::runtime_error("dynamic LDS limit not granted for an information-form factor kernel");
   done = true;
 }
 

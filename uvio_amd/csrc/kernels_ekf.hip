@@ -1,0 +1,335 @@
+// StateHelper::EKFUpdate (StateHelper.cpp:116-197) for a direct (uncompressed) batch of r rows, as three
+// launches whose products all run on the FP64 matrix cores (v_mfma_f64_16x16x4f64):
+//
+//   k_ekf_MS   grid:  M = P[:, I] H^T (N x r; one 16-row block per workgroup, the P rows gathered once
+//                     into LDS) and, in the same launch, S_up = H P_II H^T + s2 I (one 16-column block of S
+//                     per workgroup: T = P_II H_b^T into LDS, then the upper tiles H_a T)
+//   k_ekf_fact one workgroup: LDL^T of [S ; r^T] in LDS with the unit-lower inverse alongside (dense_lds.h
+//                     ldl_wave) -> L^-1, y = L^-1 r, and StateHelper::initialize's chi2 gate on y
+//   k_ekf_WP   grid over the upper 16x16 tile pairs (bi <= bj) of P: W_b = M_b L^-T for both row blocks
+//                     (a GEMM with the explicit inverse, recomputed per tile pair instead of a separate
+//                     launch), P_ij -= W_bi W_bj^T (written to both triangles), dx = W y on diagonal tiles
+//
+// The reference computes K = P H^T S^-1 through an LLT solve and P -= K M^T; here P -= (M L^-T)(M L^-T)^T
+// and dx = (M L^-T)(L^-1 r): the same update (S = L L^T), every product on MFMA tiles.  The earlier chain
+// (k_ekf_M, k_ekf_S, k_ekf_small, k_trinv16, k_trsm_lt, k_ekf_P: six launches, VALU tiles for the four
+// products) cost 96 us per update at cfg2 in rocprof (profiles/r01g_cfg2_per_frame.txt).
+//
+// MFMA operand layout (f64 16x16x4): A (16x4) lane l holds A[l & 15][l >> 4]; B (4x16) lane l holds
+// B[l >> 4][l & 15]; C/D register q of lane l is D[(l >> 4) + 4 q][l & 15].
+#include <stdexcept>
+
+#include "dense_lds.h"
+#include "kernels.h"
+
+namespace uvhp {
+
+__device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Accumulate one 16x16 tile over k in [0, kend): acc += sum_k A(r16, k) B(k, r16) with the operands fetched
+// through the callables (k = 4 s + kq); eight k-slabs of loads are issued before their MFMAs so a chunk
+// costs one memory round trip.
+template <class LA, class LB>
+__device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    double a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = k0 + 4 * u + kq;
+      const bool in = k < kend;
+      a[u] = in ? la(k) : 0.0;
+      b[u] = in ? lb(k) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (k0 + 4 * u < kend) acc = mfma4(a[u], b[u], acc);
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K1: M (blocks 0 .. nbM-1) and S_up (blocks nbM .. nbM + ceil(r/16) - 1; none when Sup is null)
+__global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, int ldp, int N,
+                                                const double *__restrict__ H, int ldh, int r, int n,
+                                                const int *__restrict__ hidx, double s2, double *__restrict__ M,
+                                                double *__restrict__ Sup, int nbM, int *zero) {
+  extern __shared__ double sh[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // the update's negative-diagonal count
+  if ((int)blockIdx.x < nbM) {
+    // M rows i0 .. i0+15: Ps[i][k] = P[i0 + i][hidx[k]] staged once, each wave takes column tiles of M
+    const int i0 = blockIdx.x * 16, lds = n | 1;
+    double *Ps = sh;
+    staged_copy(
+        16 * n,
+        [&](int e) {
+          const int i = e / n, k = e - i * n;
+          return (i0 + i < N) ? P[(size_t)(i0 + i) * ldp + hidx[k]] : 0.0;
+        },
+        [&](int e, double v) {
+          const int i = e / n, k = e - i * n;
+          Ps[i * lds + k] = v;
+        });
+    __syncthreads();
+    const int nct = (r + 15) / 16;
+    for (int t = wid; t < nct; t += 4) {
+      const int j0 = 16 * t, jr = j0 + r16;
+      const double *Hr = H + (size_t)min(jr, r - 1) * ldh;
+      const bool jv = jr < r;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = tile_chain(
+          0, n, kq, [&](int k) { return Ps[r16 * lds + k]; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int row = i0 + kq + 4 * q, col = j0 + r16;
+        if (row < N && col < r) M[(size_t)row * r + col] = acc[q];
+      }
+    }
+    return;
+  }
+  // S column block b: T = P_II H_b^T (n x 16) into LDS, then S_up[a-tile][b] = H_a T for a <= b
+  const int jb = blockIdx.x - nbM, j0 = 16 * jb;
+  const int npad = (n + 15) / 16 * 16;
+  double *Ts = sh;                                  // npad x 17
+  int *hs = (int *)(sh + (size_t)npad * 17);        // hidx
+  for (int k = threadIdx.x; k < n; k += blockDim.x) hs[k] = hidx[k];
+  __syncthreads();
+  {
+    const int jr = j0 + r16;
+    const double *Hb = H + (size_t)min(jr, r - 1) * ldh;
+    const bool jv = jr < r;
+    for (int kt = wid; kt < npad / 16; kt += 4) {
+      const int row = 16 * kt + r16;
+      const double *Prow = P + (size_t)hs[min(row, n - 1)] * ldp;
+      const bool rv = row < n;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = tile_chain(
+          0, n, kq, [&](int l) { return rv ? Prow[hs[l]] : 0.0; }, [&](int l) { return jv ? Hb[l] : 0.0; }, acc);
+#pragma unroll
+      for (int q = 0; q < 4; q++) Ts[(16 * kt + kq + 4 * q) * 17 + r16] = acc[q];
+    }
+  }
+  __syncthreads();
+  for (int at = wid; at <= jb; at += 4) {
+    const int ar = 16 * at + r16;
+    const double *Ha = H + (size_t)min(ar, r - 1) * ldh;
+    const bool av = ar < r;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain(
+        0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return Ts[k * 17 + r16]; }, acc);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = 16 * at + kq + 4 * q, col = j0 + r16;
+      if (row < r && col < r) Sup[(size_t)row * r + col] = acc[q] + (row == col ? s2 : 0.0);
+    }
+  }
+}
+
+static size_t ekf_ms_lds_bytes(int n, bool with_S) {
+  size_t bm = (size_t)16 * (n | 1) * sizeof(double);
+  size_t bs = with_S ? (size_t)(n + 15) / 16 * 16 * 17 * sizeof(double) + (size_t)n * sizeof(int) : 0;
+  return bm > bs ? bm : bs;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K2: one workgroup.  [S ; r^T] (S from the upper triangle of S_up = selfadjointView<Upper>,
+// StateHelper.cpp:160) -> LDL^T with the unit-lower inverse alongside (dense_lds.h ldl_wave), then
+// L^-1 = D^-1/2 L_u^-1 (lower, zeros above, ld r) into Linv_out and y = L^-1 r = D^1/2 (D^-1 L_u^-1 r).
+// chi2_gate: StateHelper::initialize's test (StateHelper.cpp:458-470) on this factor: chi2 = |y|^2 in a
+// fixed order against thr -> *chi2_gate (the P-update gate) and [chi2, accepted] into gate_out[0..1].
+template <int SMAX>
+__global__ void __launch_bounds__(512) k_ekf_fact(const double *__restrict__ Sup, int r,
+                                                  const double *__restrict__ res, int res_stride,
+                                                  double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
+                                                  int use_lds, int *chi2_gate, double chi2_thr,
+                                                  double *__restrict__ gate_out) {
+  extern __shared__ double lds[];
+  double *A = use_lds ? lds : Sg;
+  const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
+  double *Dd = A + (size_t)(r + 1) * ld, *sd = Dd + r;
+  staged_copy(
+      r * r + r,
+      [&](int e) {
+        if (e >= r * r) return res[(size_t)(e - r * r) * res_stride];
+        const int a = e / r, b = e - a * r;
+        return (b <= a) ? Sup[(size_t)b * r + a] : 0.0;
+      },
+      [&](int e, double v) {
+        if (e >= r * r) {
+          A[(size_t)r * ld + e - r * r] = v;
+        } else {
+          const int a = e / r, b = e - a * r;
+          if (b <= a) A[(size_t)a * ld + b] = v;
+        }
+      });
+  __syncthreads();
+  ldl_wave_inv<SMAX>(A, SqLayout{ld}, r, r + 1, Dd, true);
+  for (int k = threadIdx.x; k < r; k += blockDim.x) {
+    const double q = sqrt(Dd[k]);
+    sd[k] = q;
+    y_out[k] = A[(size_t)r * ld + k] * q;
+  }
+  __syncthreads();
+  if (chi2_gate && threadIdx.x < 64) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < r; k += 64) {
+      const double v = A[(size_t)r * ld + k] * sd[k];
+      s += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (threadIdx.x == 0) {
+      const int acc = !(s > chi2_thr);
+      *chi2_gate = acc;
+      gate_out[0] = s;
+      gate_out[1] = acc;
+    }
+  }
+  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
+    const int a = e / r, b = e - a * r;
+    double v = 0.0;
+    if (b < a)
+      v = A[(size_t)b * ld + a] / sd[a];
+    else if (b == a)
+      v = 1.0 / sd[a];
+    Linv_out[e] = v;
+  }
+}
+size_t ekf_small_lds_bytes(int r) { return (dense_lds_bytes(r + 1, r) + (size_t)2 * r * sizeof(double)); }
+
+// ---------------------------------------------------------------------------------------------------
+// K3: tile pair (bi, bj), bi <= bj, of the nb x nb tile grid of P (blocks enumerated row by row)
+__global__ void __launch_bounds__(256) k_ekf_WP(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
+                                                int r, const double *__restrict__ Linv, const double *__restrict__ y,
+                                                double *__restrict__ dx, int *neg, const int *gate, int nb) {
+  if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
+  extern __shared__ double sh[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  int b = blockIdx.x, bi = 0;
+  while (b >= nb - bi) {
+    b -= nb - bi;
+    bi++;
+  }
+  const int bj = bi + b;
+  const int ldw = r | 1;
+  double *Wi = sh, *Wj = sh + 16 * ldw, *red = sh + 32 * ldw;
+  // this thread's P element, fetched before the products so its latency is hidden
+  const int ei = threadIdx.x >> 4, ej = threadIdx.x & 15;
+  const int gi = 16 * bi + ei, gj = 16 * bj + ej;
+  const bool pw = gi < N && gj < N && (bi < bj || ej >= ei);
+  const double pv = pw ? P[(size_t)gi * ldp + gj] : 0.0;
+  // W_b[i][c] = sum_{k <= c} M[16 b + i][k] Linv[c][k]
+  const int nct = (r + 15) / 16, ntask = (bi == bj ? 1 : 2) * nct;
+  for (int t = wid; t < ntask; t += 4) {
+    const int which = t / nct, ct = t - which * nct;
+    double *Wd = which ? Wj : Wi;
+    const int row = 16 * (which ? bj : bi) + r16, c = 16 * ct + r16;
+    const double *Mr = M + (size_t)min(row, N - 1) * r;
+    const double *Lr = Linv + (size_t)min(c, r - 1) * r;
+    const bool rv = row < N, cv = c < r;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain(
+        0, min(16 * ct + 16, r), kq, [&](int k) { return rv ? Mr[k] : 0.0; }, [&](int k) { return cv ? Lr[k] : 0.0; },
+        acc);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (cv) Wd[(kq + 4 * q) * ldw + c] = acc[q];
+  }
+  __syncthreads();
+  const double *Wb = (bi == bj) ? Wi : Wj;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 4 * wid; k0 < r; k0 += 16) {  // wave w: k-slabs w, w + 4, ...
+    const int k = k0 + kq;
+    const double a = (k < r) ? Wi[r16 * ldw + k] : 0.0;
+    const double bb = (k < r) ? Wb[r16 * ldw + k] : 0.0;
+    acc = mfma4(a, bb, acc);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) red[wid * 256 + (kq + 4 * q) * 16 + r16] = acc[q];
+  __syncthreads();
+  if (pw) {
+    const int e = threadIdx.x;
+    const double s = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
+    const double v = pv - s;
+    P[(size_t)gi * ldp + gj] = v;
+    P[(size_t)gj * ldp + gi] = v;
+    if (gi == gj && v < 0.0) atomicAdd(neg, 1);
+  }
+  if (bi == bj && wid == 1) {
+    const int i = lane >> 2, part = lane & 3;
+    double a = 0.0;
+    for (int k = part; k < r; k += 4) a += Wi[i * ldw + k] * y[k];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (part == 0 && 16 * bi + i < N) dx[16 * bi + i] = a;
+  }
+}
+
+static void ensure_ekf_lds_attrs() {
+  static bool done = false;
+  if (done) return;
+  const void *fns[6] = {(const void *)k_ekf_MS,      (const void *)k_ekf_WP,      (const void *)k_ekf_fact<1>,
+                        (const void *)k_ekf_fact<2>, (const void *)k_ekf_fact<3>, (const void *)k_ekf_fact<4>};
+  for (int k = 0; k < 6; k++)
+    if (set_dyn_lds(fns[k], kMaxDynLds) < kMaxDynLds)
+      throw std::runtime_error("dynamic LDS limit not granted for an EKF kernel (" + std::to_string(k) + ")");
+  done = true;
+}
+
+void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                  const int *hidx, double *M, int *zero) {
+  ensure_ekf_lds_attrs();
+  const size_t lds = ekf_ms_lds_bytes(n, false);
+  if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
+  const int nbM = (N + 15) / 16;
+  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, 0.0, M,
+                     (double *)nullptr, nbM, zero);
+}
+
+void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, double sigma2, EkfScratch &sc) {
+  ensure_ekf_lds_attrs();
+  const size_t lds = ekf_ms_lds_bytes(n, true);
+  if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
+  const int nbM = (N + 15) / 16, nbS = (r + 15) / 16;
+  double *Sup = sc.S + 2 * (size_t)r * r;
+  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM + nbS), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+                     nbM, sc.neg);
+}
+
+void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
+                       EkfScratch &sc) {
+  ensure_ekf_lds_attrs();
+  if (r + 1 > kWaveMaxRows) throw std::runtime_error("direct EKF update with more rows than the factorization panel");
+  const size_t bytes = ekf_small_lds_bytes(r);
+  const int use_lds = bytes <= (size_t)kMaxDynLds;
+  double *Linv = sc.S;
+  double *Sup = sc.S + 2 * (size_t)r * r;
+  double *Sg = sc.S + 3 * (size_t)r * r;  // (r+1)(r|1) + 2r <= 2 r^2 doubles once r >= 40 (else LDS)
+  {
+    KScope ks(sc.kp, KC_LDL);
+    const int rows = r + 1;
+    auto *kf = rows <= 64 ? k_ekf_fact<1> : rows <= 128 ? k_ekf_fact<2> : rows <= 192 ? k_ekf_fact<3> : k_ekf_fact<4>;
+    hipLaunchKernelGGL(kf, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg, use_lds,
+                       sc.chi2_gate, sc.chi2_thr, sc.dx + N);
+  }
+  // LDL^T of the r x r innovation covariance with the residual as an extra row: r^3/3 + r^2 FLOPs; the
+  // lower triangle and the residual read, the factor written
+  if (sc.kp) sc.kp->credit(KC_LDL, (double)r * r * r / 3.0 + (double)r * r, 8.0 * (1.5 * r * r + 2.0 * r));
+  if (sc.chi2_gate) sc.gate = sc.chi2_gate;
+  const int nb = (N + 15) / 16;
+  const size_t lw = (size_t)(32 * (r | 1) + 1024) * sizeof(double);
+  hipLaunchKernelGGL(k_ekf_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, r, Linv, sc.y, sc.dx,
+                     sc.neg, sc.gate, nb);
+}
+
+void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
+                       const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc) {
+  launch_ekf_phaseA(s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc);
+  launch_ekf_phaseB(s, P, ldp, N, r, res, res_stride, sc);
+}
+
+}  // namespace uvhp

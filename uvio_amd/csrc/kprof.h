@@ -15,7 +15,7 @@ enum KClass {
   KC_CHI2,         // k_gemm_HPg(_tiled) + k_chi2: batched chi2 gate
   KC_GRAM,         // k_gram / k_gram_mfma: the compression Gram [H r]^T [H r]
   KC_EKF,          // one EKFUpdate (direct or information form): every kernel of the update chain
-  KC_LDL,          // k_ekf_small: LDL^T / Cholesky of the innovation covariance (inside KC_EKF)
+  KC_LDL,          // k_ekf_fact: LDL^T / Cholesky (+ inverse) of the innovation covariance (inside KC_EKF)
   KC_LK,           // k_lk: pyramidal LK
   KC_PYR,          // k_hist_multi + k_eq_scharr_multi + k_pyr_scharr_multi: equalizeHist + pyramid + Scharr
   KC_COUNT
