@@ -243,6 +243,57 @@ int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap,
  * may be NULL, cap = pixels available */
 int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint8_t *img, int16_t *der, size_t cap);
 
+/* ---- Updater-level boundary: one updater call on the handle's current state ----
+ * These mirror the reference's Updater C++ surfaces for a caller that keeps its own feature database
+ * (the feeds above run the whole VioManager frame instead).  Features come as flat arrays: feature i has
+ * id featids[i] and the measurements meas[meas_off[i] .. meas_off[i+1]) in the order they were observed
+ * (the order FeatureDatabase::update_feature appended them, FeatureDatabase.cpp:59-98); a camera's track
+ * is created at its first measurement, which reproduces ov_core::Feature's per-camera map order.  The
+ * results (one record per input feature) say what the reference leaves on the Feature and in
+ * feature_vec.  The covariance never leaves the device; each call reads back only dx. */
+typedef struct {
+  int cam;          /* camera id */
+  double t;         /* Feature::timestamps[cam] entry */
+  float u, v;       /* Feature::uvs[cam] entry (raw pixel) */
+  float un, vn;     /* Feature::uvs_norm[cam] entry (undistorted, normalized) */
+} uvio_hp_feat_meas_t;
+
+typedef struct {
+  uint64_t featid;
+  int status;       /* 0 used by the update (kept in feature_vec); 1 too few measurements or triangulation failed;
+                     * 2 Gauss-Newton refinement failed; 3 chi2 rejected (all but 0 are erased from feature_vec) */
+  int to_delete;    /* Feature::to_delete after the call */
+  double p_FinG[3]; /* the triangulated position (MSCKF / delayed init; zero when not triangulated) */
+  double chi2;      /* the chi2 the gate compared (0 when not gated) */
+} uvio_hp_feat_result_t;
+
+/* Overwrite the mean, the first estimates and the covariance (a state snapshot in the layout of
+ * uvio_hp_get_state_vector / uvio_hp_get_fej_vector / uvio_hp_get_cov: same variables, len doubles,
+ * N x N covariance with leading dimension ld).  Camera intrinsics follow the state (StateHelper.cpp:190-195). */
+int uvio_hp_set_state(uvio_hp_t *h, const double *val, const double *fej, int len, const double *P, int N, int ld);
+/* Propagator::propagate_and_clone (Propagator.h:110) to t with the IMU readings fed so far */
+int uvio_hp_propagate_and_clone(uvio_hp_t *h, double t);
+/* UpdaterMSCKF::update (UpdaterMSCKF.h:68, UpdaterMSCKF.cpp:58-295) */
+int uvio_hp_msckf_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                         const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out);
+/* UpdaterSLAM::update (UpdaterSLAM.h:70, UpdaterSLAM.cpp:253-479); every feature must be a SLAM landmark of
+ * the state (UVIO_HP_E_ARG otherwise); a chi2 rejection raises the landmark's fail count as in the reference */
+int uvio_hp_slam_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                        const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out);
+/* UpdaterSLAM::delayed_init (UpdaterSLAM.h:77, UpdaterSLAM.cpp:61-251): accepted features (status 0) become
+ * SLAM landmarks of the state in the configured feat_rep_slam */
+int uvio_hp_slam_delayed_init(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                              const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out);
+/* UpdaterSLAM::change_anchors (UpdaterSLAM.h:87, UpdaterSLAM.cpp:481-647) */
+int uvio_hp_slam_change_anchors(uvio_hp_t *h);
+/* StateHelper::marginalize_slam / marginalize_old_clone (StateHelper.h:230, :224) */
+int uvio_hp_marginalize_slam(uvio_hp_t *h);
+int uvio_hp_marginalize_old_clone(uvio_hp_t *h);
+/* UpdaterUWB::update_single (UpdaterUWB.h:55, UpdaterUWB.cpp:53-90): one range to one initialized anchor on
+ * the current state (t is the measurement time; the reference's Jacobian does not use it); *applied = 1
+ * when the chi2 test passed and the update ran, 0 when it was gated or the anchor is unknown */
+int uvio_hp_uwb_update_single(uvio_hp_t *h, double t, uint64_t anchor_id, double range, int *applied);
+
 /* ---- feature-sharded MSCKF update across GPUs (BASELINE.json configs 4-5) ----
  * One process per GPU, each with its own handle fed the same measurement stream (the filter state is
  * replicated).  Inside UpdaterMSCKF::update (UpdaterMSCKF.cpp:58-295) the selected features are split into

@@ -45,6 +45,13 @@ def load():
         lib.orc_create.argtypes = [C.POINTER(N.Options), C.POINTER(C.c_void_p)]
         lib.orc_set_state.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int,
                                       C.POINTER(C.c_double), C.c_int]
+        fm, i32p = C.POINTER(N.FeatMeas), C.POINTER(C.c_int)
+        lib.orc_updater.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint64), i32p, fm, i32p, i32p]
+        lib.orc_propagate_and_clone.argtypes = [C.c_void_p, C.c_double]
+        lib.orc_slam_change_anchors.argtypes = [C.c_void_p]
+        lib.orc_marginalize_slam.argtypes = [C.c_void_p]
+        lib.orc_marginalize_old_clone.argtypes = [C.c_void_p]
+        lib.orc_uwb_update_single.argtypes = [C.c_void_p, C.c_double, C.c_uint64, C.c_double, i32p]
         lib.orc_chi2_quantile95.restype = C.c_double
         lib.orc_chi2_quantile95.argtypes = [C.c_int]
         lib.orc_camera_distort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -73,6 +80,25 @@ class OracleManager(VioManager):
     @classmethod
     def _load(cls):
         return load()
+
+    def _updater(self, name, features):
+        """The reference updaters on the oracle's state; per feature: still in feature_vec (used) and to_delete"""
+        which = {"msckf_update": 0, "slam_update": 1, "slam_delayed_init": 2}[name]
+        ids, off, arr = self.pack_features(features)
+        n = max(len(features), 1)
+        kept, dele = (C.c_int * n)(), (C.c_int * n)()
+        rc = self._lib.orc_updater(self._h, which, len(features), ids, off, arr, kept, dele)
+        if rc != 0:
+            raise RuntimeError("orc_%s failed (%d)" % (name, rc))
+        return [{"featid": int(f[0]), "used": bool(kept[i]), "to_delete": bool(dele[i])} for i, f in enumerate(features)]
+
+    def uwb_update_single(self, t, anchor_id, rng):
+        a = C.c_int(0)
+        rc = self._lib.orc_uwb_update_single(self._h, C.c_double(t), C.c_uint64(int(anchor_id)), C.c_double(rng),
+                                             C.byref(a))
+        if rc != 0:
+            raise RuntimeError("orc_uwb_update_single failed (%d)" % rc)
+        return bool(a.value)
 
     def set_state(self, val, fej, P):
         """Lock-step parity: adopt another implementation's mean / FEJ / covariance."""

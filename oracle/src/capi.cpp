@@ -172,6 +172,68 @@ int orc_get_active_tracks(orc_handle *h, double *t, uint64_t *ids, double *posin
   return 0;
 }
 
+// ---- updater-level entries (include/uvio_hp.h "Updater-level boundary"), the reference's own calls ----
+// Features from the flat arrays, measurements appended in order (FeatureDatabase::update_feature,
+// FeatureDatabase.cpp:59-98); kept[i] = 1 when feature i is still in feature_vec after the updater
+// (used by the update), to_delete[i] = Feature::to_delete.
+static std::vector<FeatP> orc_features(int nfeat, const uint64_t *ids, const int *off, const uvio_hp_feat_meas_t *m) {
+  std::vector<FeatP> fv;
+  for (int i = 0; i < nfeat; i++) {
+    auto f = std::make_shared<Feature>();
+    f->featid = (size_t)ids[i];
+    for (int k = off[i]; k < off[i + 1]; k++) {
+      const size_t c = (size_t)m[k].cam;
+      f->uvs[c].push_back({m[k].u, m[k].v});
+      f->uvs_norm[c].push_back({m[k].un, m[k].vn});
+      f->timestamps[c].push_back(m[k].t);
+    }
+    fv.push_back(f);
+  }
+  return fv;
+}
+static void orc_outcome(const std::vector<FeatP> &in, const std::vector<FeatP> &after, int *kept, int *to_delete) {
+  for (size_t i = 0; i < in.size(); i++) {
+    kept[i] = 0;
+    for (auto &f : after)
+      if (f == in[i]) kept[i] = 1;
+    to_delete[i] = in[i]->to_delete ? 1 : 0;
+  }
+}
+int orc_updater(orc_handle *h, int which, int nfeat, const uint64_t *ids, const int *off, const uvio_hp_feat_meas_t *m,
+                int *kept, int *to_delete) {
+  std::vector<FeatP> fv = orc_features(nfeat, ids, off, m);
+  const std::vector<FeatP> in = fv;
+  int rc = 0;
+  if (which == 0)
+    rc = h->m.msckf.update(h->m.state, fv, &h->m.last_msckf);
+  else if (which == 1)
+    rc = h->m.slam.update(h->m.state, fv);
+  else
+    rc = h->m.slam.delayed_init(h->m.state, fv);
+  orc_outcome(in, fv, kept, to_delete);
+  return rc;
+}
+int orc_propagate_and_clone(orc_handle *h, double t) {
+  int st = 0;
+  if (!h->m.prop.propagate_and_clone(h->m.state, t, &st)) return st ? st : UVIO_HP_E_NUMERIC;
+  return 0;
+}
+int orc_slam_change_anchors(orc_handle *h) { return h->m.slam.change_anchors(h->m.state); }
+int orc_marginalize_slam(orc_handle *h) {
+  StateHelper::marginalize_slam(h->m.state);
+  return 0;
+}
+int orc_marginalize_old_clone(orc_handle *h) {
+  StateHelper::marginalize_old_clone(h->m.state);
+  return 0;
+}
+int orc_uwb_update_single(orc_handle *h, double t, uint64_t anchor_id, double range, int *applied) {
+  const int r = h->m.uwb.update_single(h->m.state, t, (size_t)anchor_id, range);
+  if (r < 0) return r;
+  *applied = r;
+  return 0;
+}
+
 // StateHelper::EKFUpdate on a standalone covariance (variables = one Vec of size N)
 int orc_ekf_update(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res, double sigma2,
                    double *dx_out) {

@@ -85,6 +85,18 @@ class KStat(C.Structure):
                 "seconds": self.seconds, "flops": self.flops, "bytes": self.bytes}
 
 
+class FeatMeas(C.Structure):
+    """uvio_hp_feat_meas_t: one Feature::uvs / uvs_norm / timestamps entry"""
+    _fields_ = [("cam", C.c_int), ("t", C.c_double), ("u", C.c_float), ("v", C.c_float), ("un", C.c_float),
+                ("vn", C.c_float)]
+
+
+class FeatResult(C.Structure):
+    """uvio_hp_feat_result_t: what an updater call left on a feature"""
+    _fields_ = [("featid", C.c_uint64), ("status", C.c_int), ("to_delete", C.c_int), ("p_FinG", C.c_double * 3),
+                ("chi2", C.c_double)]
+
+
 _P = C.POINTER
 _D = C.c_double
 _I = C.c_int
@@ -120,6 +132,15 @@ SIGNATURES = [
     ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("msckf_compressed_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("compress", _I, [_P(_D), _I, _I, _P(_D)]),
+    ("set_state", _I, [C.c_void_p, _P(_D), _P(_D), _I, _P(_D), _I, _I]),
+    ("propagate_and_clone", _I, [C.c_void_p, _D]),
+    ("msckf_update", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(_I), _P(FeatMeas), _P(FeatResult)]),
+    ("slam_update", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(_I), _P(FeatMeas), _P(FeatResult)]),
+    ("slam_delayed_init", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(_I), _P(FeatMeas), _P(FeatResult)]),
+    ("slam_change_anchors", _I, [C.c_void_p]),
+    ("marginalize_slam", _I, [C.c_void_p]),
+    ("marginalize_old_clone", _I, [C.c_void_p]),
+    ("uwb_update_single", _I, [C.c_void_p, _D, C.c_uint64, _D, _P(_I)]),
     ("shard_unique_id", _I, [_P(C.c_uint8)]),
     ("shard_init_rccl", _I, [C.c_void_p, _I, _I, _P(C.c_uint8), _I]),
     ("shard_init_host", _I, [C.c_void_p, _I, _I, C.c_void_p, C.c_void_p, _I]),

@@ -22,6 +22,7 @@ SOURCES = [
     "engine_update.cpp",
     "engine_track.cpp",
     "engine_retri.cpp",
+    "engine_api.cpp",
     "capi.cpp",
     "shard.cpp",
     "kernels_cov.hip",

@@ -221,6 +221,48 @@ int uvio_hp_get_clone_times(uvio_hp_t *h, double *out, int cap, int *n) {
   return 0;
 }
 
+// ---- Updater-level boundary (include/uvio_hp.h) ----
+int uvio_hp_set_state(uvio_hp_t *h, const double *val, const double *fej, int len, const double *P, int N, int ld) {
+  if (!h || !val || !fej || !P || len <= 0 || N <= 0) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_set_state(val, fej, len, P, N, ld); })
+}
+int uvio_hp_propagate_and_clone(uvio_hp_t *h, double t) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_propagate_and_clone(t); })
+}
+int uvio_hp_msckf_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                         const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_update(Engine::API_MSCKF, nfeat, featids, meas_off, meas, out); })
+}
+int uvio_hp_slam_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                        const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_update(Engine::API_SLAM, nfeat, featids, meas_off, meas, out); })
+}
+int uvio_hp_slam_delayed_init(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
+                              const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_update(Engine::API_DELAYED, nfeat, featids, meas_off, meas, out); })
+}
+int uvio_hp_slam_change_anchors(uvio_hp_t *h) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_change_anchors(); })
+}
+int uvio_hp_marginalize_slam(uvio_hp_t *h) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_marginalize_slam(); })
+}
+int uvio_hp_marginalize_old_clone(uvio_hp_t *h) {
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_marginalize_old_clone(); })
+}
+int uvio_hp_uwb_update_single(uvio_hp_t *h, double t, uint64_t anchor_id, double range, int *applied) {
+  (void)t;  // the reference's Jacobian does not read the measurement time (UVioUpdaterHelper.cpp:147-241)
+  if (!h) return UVIO_HP_E_ARG;
+  HP_GUARD(h, { return h->e->api_uwb_update_single(anchor_id, range, applied); })
+}
+
 int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n) {
   if (!h || !n) return UVIO_HP_E_ARG;
   const auto &v = h->e->last_msckf_;

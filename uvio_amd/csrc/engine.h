@@ -254,6 +254,18 @@ class Engine {
     double chi2;
   };
   std::vector<FeatDebug> last_msckf_;
+  std::vector<FeatDebug> last_upd_;  // the last SLAM update / delayed initialization, per feature
+
+  // updater-level entry points (engine_api.cpp; include/uvio_hp.h "Updater-level boundary")
+  enum ApiUpdater { API_MSCKF = 0, API_SLAM = 1, API_DELAYED = 2 };
+  int api_set_state(const double *val, const double *fej, int len, const double *P, int N, int ld);
+  int api_propagate_and_clone(double t);
+  int api_update(int which, int nfeat, const uint64_t *featids, const int *meas_off, const uvio_hp_feat_meas_t *meas,
+                 uvio_hp_feat_result_t *out);
+  int api_change_anchors();
+  int api_marginalize_slam();
+  int api_marginalize_old_clone();
+  int api_uwb_update_single(uint64_t anchor_id, double range, int *applied);
   // the reference routine the host was in when the last call failed (error messages)
   const char *stage() const { return stage_; }
 

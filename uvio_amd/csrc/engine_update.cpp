@@ -1046,10 +1046,12 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
   const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
   const int m = run_batch(b, 1, s2, o_.slam_chi2_multipler, false, outs);
   const int n = b.n_canon, ncol = n + 1;
+  last_upd_.clear();
   auto results = [&]() {
     finish_batch(b, 1, outs);
     int acc = 0;
     for (size_t i = 0; i < outs.size(); i++) {
+      last_upd_.push_back(FeatDebug{fv[i]->featid, {0.0, 0.0, 0.0}, outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
       fv[i]->to_delete = true;
       if (outs[i].status == 3) slam_.at(fv[i]->featid)->fail_count++;
       if (outs[i].status == 0) acc++;
@@ -1092,6 +1094,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
   int rep = o_.feat_rep_slam;
   if (rep != 0 && rep != 2 && rep != 4) throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
   double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+  last_upd_.clear();
   // 1) triangulate + refine all features against the pre-update state (UpdaterSLAM.cpp:119-141)
   HPROF("di.total");
   std::vector<DFeatOut> tri;
@@ -1108,6 +1111,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     FeatP &f = fv[i];
     if (tri[i].status == 1 || tri[i].status == 2) {
       f->to_delete = true;
+      last_upd_.push_back(FeatDebug{f->featid, {0.0, 0.0, 0.0}, tri[i].status, 0.0});
       continue;
     }
     // anchor (host rule, identical to the kernel's) and triangulated position
@@ -1190,6 +1194,8 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
       read_dx("initialize_invertible");  // the batch results and the residual column
       land();
     }
+    last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,
+                                  nup > 0 ? d_.dx_host[N0 + 3] : 0.0});
     if (accepted) {
       slam_.insert({f->featid, lm});
     } else {

@@ -246,6 +246,66 @@ class VioManager:
         arr = (N.Anchor * max(n, 1))(*anchors)
         self._check(self._call("init_anchors", self._h, n, arr), "try_to_initialize_uwb_anchors")
 
+    # ---- updater-level boundary (include/uvio_hp.h; UpdaterMSCKF.h:68, UpdaterSLAM.h:70-87, UpdaterUWB.h:55) ----
+    @staticmethod
+    def pack_features(features):
+        """features: [(featid, [(cam, t, u, v, un, vn), ...]), ...] in observation order -> flat C arrays"""
+        ids = (C.c_uint64 * max(len(features), 1))(*[int(f[0]) for f in features])
+        offs, meas = [0], []
+        for _, ms in features:
+            for (cam, t, u, v, un, vn) in ms:
+                meas.append(N.FeatMeas(int(cam), float(t), float(u), float(v), float(un), float(vn)))
+            offs.append(len(meas))
+        off = (C.c_int * len(offs))(*offs)
+        arr = (N.FeatMeas * max(len(meas), 1))(*meas)
+        return ids, off, arr
+
+    def set_state(self, val, fej, P):
+        """Adopt a state snapshot (mean, first estimates, covariance) in this state's layout."""
+        val = np.ascontiguousarray(val, dtype=np.float64)
+        fej = np.ascontiguousarray(fej, dtype=np.float64)
+        P = np.ascontiguousarray(P, dtype=np.float64)
+        self._check(self._call("set_state", self._h, _dp(val), _dp(fej), val.size, _dp(P), P.shape[0], P.shape[0]),
+                    "set_state")
+
+    def propagate_and_clone(self, t):
+        self._check(self._call("propagate_and_clone", self._h, C.c_double(t)), "propagate_and_clone")
+
+    def _updater(self, name, features):
+        ids, off, arr = self.pack_features(features)
+        out = (N.FeatResult * max(len(features), 1))()
+        self._check(self._call(name, self._h, len(features), ids, off, arr, out), name)
+        return [{"featid": int(o.featid), "status": o.status, "used": o.status == 0, "to_delete": bool(o.to_delete),
+                 "p_FinG": np.array(o.p_FinG[:]), "chi2": o.chi2} for o in out[:len(features)]]
+
+    def msckf_update(self, features):
+        """UpdaterMSCKF::update on the current state; one result dict per feature"""
+        return self._updater("msckf_update", features)
+
+    def slam_update(self, features):
+        """UpdaterSLAM::update (the features must be SLAM landmarks of the state)"""
+        return self._updater("slam_update", features)
+
+    def slam_delayed_init(self, features):
+        """UpdaterSLAM::delayed_init: accepted features become SLAM landmarks"""
+        return self._updater("slam_delayed_init", features)
+
+    def slam_change_anchors(self):
+        self._check(self._call("slam_change_anchors", self._h), "slam_change_anchors")
+
+    def marginalize_slam(self):
+        self._check(self._call("marginalize_slam", self._h), "marginalize_slam")
+
+    def marginalize_old_clone(self):
+        self._check(self._call("marginalize_old_clone", self._h), "marginalize_old_clone")
+
+    def uwb_update_single(self, t, anchor_id, rng):
+        """UpdaterUWB::update_single; True when the range passed the chi2 test and updated the state"""
+        a = C.c_int(0)
+        self._check(self._call("uwb_update_single", self._h, C.c_double(t), C.c_uint64(int(anchor_id)),
+                               C.c_double(rng), C.byref(a)), "uwb_update_single")
+        return bool(a.value)
+
     # ---- getters ----
     def get_imu_state(self):
         t = C.c_double()
