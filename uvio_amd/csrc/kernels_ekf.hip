@@ -29,21 +29,23 @@ __device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
 }
 
 // Accumulate one 16x16 tile over k in [0, kend): acc += sum_k A(r16, k) B(k, r16) with the operands fetched
-// through the callables (k = 4 s + kq); eight k-slabs of loads are issued before their MFMAs so a chunk
-// costs one memory round trip.
+// through the callables (k = 4 s + kq); the loads of eight k-slabs are issued before their MFMAs, so a
+// chunk costs one memory round trip.  (32-slab chunks measured slower in k_ekf_MS / k_ekf_WP: 24.4 / 10.3
+// against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
 template <class LA, class LB>
 __device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    double a[8], b[8];
+  constexpr int U = 8;
+  for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
+    double a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
+    for (int u = 0; u < U; u++) {
       const int k = k0 + 4 * u + kq;
       const bool in = k < kend;
       a[u] = in ? la(k) : 0.0;
       b[u] = in ? lb(k) : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 8; u++)
+    for (int u = 0; u < U; u++)
       if (k0 + 4 * u < kend) acc = mfma4(a[u], b[u], acc);
   }
   return acc;
@@ -125,6 +127,36 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
       const int row = 16 * at + kq + 4 * q, col = j0 + r16;
       if (row < r && col < r) Sup[(size_t)row * r + col] = acc[q] + (row == col ? s2 : 0.0);
     }
+  }
+}
+
+// M = P[:, I] H^T for r <= 4 rows (initialize_invertible's 3 x n block): a GEMV per covariance row, one
+// wavefront per row with the lanes over the columns and a butterfly reduction (the 16-row MFMA blocks of
+// k_ekf_MS would waste 13 of 16 output columns and serialize their loads per tile)
+constexpr int kSmallMRows = 4;
+__global__ void __launch_bounds__(256) k_ekf_M_small(const double *__restrict__ P, int ldp, int N,
+                                                     const double *__restrict__ H, int ldh, int r, int n,
+                                                     const int *__restrict__ hidx, double *__restrict__ M, int *zero) {
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const double *Pr = P + (size_t)row * ldp;
+  double acc[kSmallMRows] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = lane; k < n; k += 64) {
+    const double p = Pr[hidx[k]];
+#pragma unroll
+    for (int b = 0; b < kSmallMRows; b++)
+      if (b < r) acc[b] = fma(p, H[(size_t)b * ldh + k], acc[b]);
+  }
+#pragma unroll
+  for (int b = 0; b < kSmallMRows; b++)
+    for (int o = 32; o > 0; o >>= 1) acc[b] += __shfl_xor(acc[b], o, 64);
+  if (lane < r) {
+    double v = acc[0];
+#pragma unroll
+    for (int b = 1; b < kSmallMRows; b++)
+      if (lane == b) v = acc[b];
+    M[(size_t)row * r + lane] = v;
   }
 }
 
@@ -281,6 +313,10 @@ static void ensure_ekf_lds_attrs() {
 
 void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
                   const int *hidx, double *M, int *zero) {
+  if (r <= kSmallMRows) {
+    hipLaunchKernelGGL(k_ekf_M_small, dim3((N + 3) / 4), dim3(256), 0, s, P, ldp, N, H, ldh, r, n, hidx, M, zero);
+    return;
+  }
   ensure_ekf_lds_attrs();
   const size_t lds = ekf_ms_lds_bytes(n, false);
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
