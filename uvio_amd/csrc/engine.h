@@ -51,9 +51,42 @@ struct FeatMeas {
   float u, v, un, vn;
   double t;
 };
+// One camera's measurements in time order.  Trimming the oldest ones (FeatureDatabase::cleanup_measurements,
+// every frame, over every feature of the database) only advances a start offset -- the storage is compacted
+// once the dead prefix outgrows the live part -- so the per-frame cleanup touches no measurement data.
+struct MeasList {
+  std::vector<FeatMeas> v;
+  size_t b = 0;  // first live entry
+  using iterator = std::vector<FeatMeas>::iterator;
+  using const_iterator = std::vector<FeatMeas>::const_iterator;
+  size_t size() const { return v.size() - b; }
+  bool empty() const { return v.size() == b; }
+  FeatMeas &operator[](size_t i) { return v[b + i]; }
+  const FeatMeas &operator[](size_t i) const { return v[b + i]; }
+  FeatMeas &back() { return v.back(); }
+  const FeatMeas &back() const { return v.back(); }
+  const FeatMeas &front() const { return v[b]; }
+  iterator begin() { return v.begin() + (std::ptrdiff_t)b; }
+  iterator end() { return v.end(); }
+  const_iterator begin() const { return v.begin() + (std::ptrdiff_t)b; }
+  const_iterator end() const { return v.end(); }
+  void push_back(const FeatMeas &x) { v.push_back(x); }
+  iterator erase(iterator first, iterator last) { return v.erase(first, last); }
+  void drop_front(size_t k) {  // remove the k oldest live entries
+    b += k;
+    if (b == v.size()) {
+      v.clear();
+      b = 0;
+    } else if (b > 32 && 2 * b > v.size()) {
+      v.erase(v.begin(), v.begin() + (std::ptrdiff_t)b);
+      b = 0;
+    }
+  }
+  void keep_if_valid(const std::vector<double> &valid);  // keep the entries whose time is in `valid` (sorted)
+};
 struct CamTrack {
   size_t cam;
-  std::vector<FeatMeas> m;
+  MeasList m;
 };
 
 struct Feature {

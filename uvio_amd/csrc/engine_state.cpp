@@ -69,20 +69,26 @@ void Var::set_xyz(const double *p, bool isfej) {
 }
 
 // ---- Feature (Feature.cpp:26-111) ----
-void Feature::clean_old_measurements(const std::vector<double> &valid) {
-  for (auto &c : tracks) {
-    size_t w = 0;
-    for (size_t i = 0; i < c.m.size(); i++)
-      if (std::binary_search(valid.begin(), valid.end(), c.m[i].t)) c.m[w++] = c.m[i];
-    c.m.resize(w);
+void MeasList::keep_if_valid(const std::vector<double> &valid) {
+  size_t w = b;
+  for (size_t i = b; i < v.size(); i++)
+    if (std::binary_search(valid.begin(), valid.end(), v[i].t)) v[w++] = v[i];
+  v.resize(w);
+  if (v.size() == b) {
+    v.clear();
+    b = 0;
   }
 }
+// Feature::clean_old_measurements (Feature.cpp:37-60): keep the measurements at the given (sorted) times
+void Feature::clean_old_measurements(const std::vector<double> &valid) {
+  for (auto &c : tracks) c.m.keep_if_valid(valid);
+}
+// Feature::clean_older_measurements (Feature.cpp:85-104): drop every measurement at or before t.  A camera's
+// measurements are appended in time order, so they form a prefix, found by binary search.
 void Feature::clean_older_measurements(double t) {
   for (auto &c : tracks) {
-    size_t w = 0;
-    for (size_t i = 0; i < c.m.size(); i++)
-      if (!(c.m[i].t <= t)) c.m[w++] = c.m[i];
-    c.m.resize(w);
+    auto it = std::upper_bound(c.m.begin(), c.m.end(), t, [](double tt, const FeatMeas &x) { return tt < x.t; });
+    c.m.drop_front((size_t)(it - c.m.begin()));
   }
 }
 

@@ -340,7 +340,11 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     // costs more than the scan at cfg4's database sizes); nothing inserts into db_ during the scan
     std::vector<std::pair<const FeatP *, uint8_t>> all;  // feature, bit 0 lost, bit 1 marg
     all.reserve(db_.size());
-    for (auto &kv : db_) all.emplace_back(&kv.second, 0);
+    {
+      HPROF("select.walk");
+      for (auto &kv : db_) all.emplace_back(&kv.second, 0);
+    }
+    HPROF("select.flags");
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
         const Feature &f = **all[i].first;
@@ -352,7 +356,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
         }
         if (do_marg)
           for (auto &p : f.tracks) {
-            has = std::find_if(p.m.begin(), p.m.end(), [mt](const FeatMeas &x) { return x.t == mt; }) != p.m.end();
+            // time-ordered: binary search for the marginalized clone's time
+            auto it = std::lower_bound(p.m.begin(), p.m.end(), mt, [](const FeatMeas &x, double tt) { return x.t < tt; });
+            has = it != p.m.end() && it->t == mt;
             if (has) break;
           }
         all[i].second = (uint8_t)((newer ? 0 : 1) | (has ? 2 : 0));
@@ -455,7 +461,10 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   if (rc) return rc;
   auto rT6 = clk::now();
   HPROF("marg.total");
-  retriangulate_active_tracks(t, camids);
+  {
+    HPROF("marg.retri");
+    retriangulate_active_tracks(t, camids);
+  }
   for (auto &f : up) f->to_delete = true;
   // FeatureDatabase::cleanup: only features handed to an updater can carry to_delete, so they are
   // erased by key (erasing a node keeps the others' iteration order, as the reference's scan does)
@@ -465,9 +474,13 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     if (it != db_.end() && it->second == f) db_.erase(it);
   }
   pending_delete_.clear();
-  rc = slam_change_anchors();
+  {
+    HPROF("marg.anchors");
+    rc = slam_change_anchors();
+  }
   if (rc) return rc;
   if ((int)clones_.size() > o_.max_clone_size) {
+    HPROF("marg.cleanmeas");
     // FeatureDatabase::cleanup_measurements(margtimestep): per-feature trimming on the pool, then the
     // emptied features are erased (erasing by key keeps the others' iteration order)
     double mt = margtimestep();
