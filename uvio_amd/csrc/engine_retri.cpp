@@ -108,8 +108,11 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
   }
   const int nobs = (int)frame_obs_.size();
   retri_alloc(nobs);
-  if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // last frame's upload read h_obs
-  if (nobs) std::memcpy(rt_.h_obs, frame_obs_.data(), sizeof(DRetriObs) * nobs);
+  {
+    HPROF("retri.wait_copy");
+    if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // last frame's upload read h_obs
+    if (nobs) std::memcpy(rt_.h_obs, frame_obs_.data(), sizeof(DRetriObs) * nobs);
+  }
   RetriJob job{};
   job.nobs = nobs;
   job.cap = rt_.cap;

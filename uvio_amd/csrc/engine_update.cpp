@@ -178,9 +178,12 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
   }
   // undistort every observation (independent, on the pool), then the database updates in order
   std::vector<float> uvn(2 * cam_of.size());
-  pool_.parallel_for(cam_of.size(), 2048, [&](size_t b, size_t e) {
-    for (size_t k = b; k < e; k++) cam_undistort_f(cams_[cam_of[k]], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
-  });
+  {
+    HPROF("feed.undistort");
+    pool_.parallel_for(cam_of.size(), 2048, [&](size_t b, size_t e) {
+      for (size_t k = b; k < e; k++) cam_undistort_f(cams_[cam_of[k]], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
+    });
+  }
   // FeatureDatabase::update_feature for every observation, in order, in three passes with the same
   // result: (a) look up the known features (read-only, on the pool), (b) insert the new ids into db_
   // sequentially in observation order (db_'s iteration order depends on it), (c) append each
@@ -188,43 +191,52 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
   // the observations in order, so each feature's appends keep the sequential order.
   const size_t nobs = cam_of.size();
   std::vector<Feature *> fp(nobs, nullptr);
-  pool_.parallel_for(nobs, 2048, [&](size_t b, size_t e) {
-    for (size_t k = b; k < e; k++) {
-      auto it = db_.find((size_t)ids[k] + currid_);
-      if (it != db_.end()) fp[k] = it->second.get();
-    }
-  });
-  for (size_t k = 0; k < nobs; k++) {
-    if (fp[k]) continue;
-    const size_t id = (size_t)ids[k] + currid_;
-    auto it = db_.find(id);  // a new id seen by an earlier camera of this frame
-    if (it == db_.end()) {
-      auto f = std::make_shared<Feature>();
-      f->featid = id;
-      it = db_.emplace(id, f).first;
-    }
-    fp[k] = it->second.get();
-  }
-  frame_obs_.resize(nobs);
-  for (size_t k = 0; k < nobs; k++) {
-    DRetriObs &o = frame_obs_[k];
-    o.featid = (unsigned long long)(ids[k] + currid_);
-    o.u = uv[2 * k];
-    o.v = uv[2 * k + 1];
-    o.un = uvn[2 * k];
-    o.vn = uvn[2 * k + 1];
-    o.cam = cam_of[k];
-    o.pad = 0;
-  }
-  const int nw = pool_.threads();
-  pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
-    for (size_t w = b; w < e; w++)
-      for (size_t k = 0; k < nobs; k++) {
-        if (((uintptr_t)fp[k] >> 6) % (uintptr_t)nw != w) continue;
-        fp[k]->track((size_t)cam_of[k]).m.push_back(
-            FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
+  {
+    HPROF("feed.lookup");
+    pool_.parallel_for(nobs, 2048, [&](size_t b, size_t e) {
+      for (size_t k = b; k < e; k++) {
+        auto it = db_.find((size_t)ids[k] + currid_);
+        if (it != db_.end()) fp[k] = it->second.get();
       }
-  });
+    });
+  }
+  {
+    HPROF("feed.insert");
+    for (size_t k = 0; k < nobs; k++) {
+      if (fp[k]) continue;
+      const size_t id = (size_t)ids[k] + currid_;
+      auto it = db_.find(id);  // a new id seen by an earlier camera of this frame
+      if (it == db_.end()) {
+        auto f = std::make_shared<Feature>();
+        f->featid = id;
+        it = db_.emplace(id, f).first;
+      }
+      fp[k] = it->second.get();
+    }
+  }
+  {
+    HPROF("feed.obs_append");
+    frame_obs_.resize(nobs);
+    for (size_t k = 0; k < nobs; k++) {
+      DRetriObs &o = frame_obs_[k];
+      o.featid = (unsigned long long)(ids[k] + currid_);
+      o.u = uv[2 * k];
+      o.v = uv[2 * k + 1];
+      o.un = uvn[2 * k];
+      o.vn = uvn[2 * k + 1];
+      o.cam = cam_of[k];
+      o.pad = 0;
+    }
+    const int nw = pool_.threads();
+    pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
+      for (size_t w = b; w < e; w++)
+        for (size_t k = 0; k < nobs; k++) {
+          if (((uintptr_t)fp[k] >> 6) % (uintptr_t)nw != w) continue;
+          fp[k]->track((size_t)cam_of[k]).m.push_back(
+              FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
+        }
+    });
+  }
   return after_tracking(t, camids, rT1);
 }
 
