@@ -22,7 +22,7 @@ print("kernels %d  span %.1f ms  busy %.1f ms (%.0f%%)  per frame: span %.3f ms 
     len(seg) / nframes))
 d = collections.defaultdict(list)
 for s, e, n, g in seg:
-    d[n.split('(')[0].replace('uvhp::', '')].append((e - s) / 1e3)
+    d[n.split('(')[0].replace('uvhp::', '').replace('void ', '')].append((e - s) / 1e3)
 tot = sum(sum(v) for v in d.values())
 for k in sorted(d, key=lambda k: -sum(d[k]))[:28]:
     v = d[k]
