@@ -14,7 +14,9 @@ opts = bench.workload_options(U, wl)
 warm = int(opts.max_clone_size) + 8
 sim = bench.make_stream(opts, warm + 12, seed=5, workload=wl)
 images = bench.WORKLOADS[wl][1] == "images"
-frames = bench.render_frames(sim, warm + 12, "cuda") if images else None
+frames = bench.Frames(sim, "cuda") if images else None
+if frames is not None:
+    frames.prerender(0, warm + 12)
 mgr = U.VioManager(opts)
 drv = bench.Driver(sim, mgr, frames)
 for _ in range(warm):
