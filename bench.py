@@ -137,6 +137,19 @@ class Driver:
             from uvio_amd.manager import pack_sim_frame
             self.packed = [pack_sim_frame(f) for f in sim.frames]
         self.ev = [e for e in sim.events() if e[1] >= sim.t0 - 0.4]
+        # runs of consecutive IMU events go in as one feed_measurement_imu_batch call (index of the run's
+        # first event -> (t, wm, am) arrays, events in the run)
+        self.imu_runs = {}
+        k = 0
+        while k < len(self.ev):
+            j = k
+            while j < len(self.ev) and self.ev[j][0] == "imu":
+                j += 1
+            if j > k:
+                idx = [self.ev[q][2] for q in range(k, j)]
+                self.imu_runs[k] = (np.array([self.ev[q][1] for q in range(k, j)]), np.ascontiguousarray(sim.wm[idx]),
+                                    np.ascontiguousarray(sim.am[idx]), j - k)
+            k = max(j, k + 1)
         self.k = 0
         self.frame = -1  # index of the last fed camera frame
         mgr.initialize_with_gt(sim.gt_state(sim.t0))
@@ -154,6 +167,11 @@ class Driver:
         """Feed events up to and including the next camera frame; returns its timestamp."""
         sim, mgr = self.sim, self.mgr
         while True:
+            run = self.imu_runs.get(self.k)
+            if run is not None:
+                mgr.feed_measurement_imu_batch(run[0], run[1], run[2])
+                self.k += run[3]
+                continue
             kind, t, i = self.ev[self.k]
             self.k += 1
             if kind == "imu":

@@ -187,6 +187,9 @@ const char *uvio_hp_last_error(const uvio_hp_t *h);
 int uvio_hp_initialize_with_gt(uvio_hp_t *h, const double x[17]);
 /* VioManager::feed_measurement_imu (VioManager.cpp:166) */
 int uvio_hp_feed_imu(uvio_hp_t *h, double t, const double wm[3], const double am[3]);
+/* n consecutive feed_measurement_imu calls in one: t[n], wm[3n], am[3n] (a driver that receives IMU
+ * samples in bursts between camera frames saves the per-call overhead) */
+int uvio_hp_feed_imu_batch(uvio_hp_t *h, int n, const double *t, const double *wm, const double *am);
 /* VioManager::feed_measurement_simulation (VioManager.cpp:191) — TrackSIM path.  For camera i
  * (i < ncam) there are counts[i] features; ids/uv are concatenated over cameras, uv as (u,v) pairs. */
 int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const int *counts,

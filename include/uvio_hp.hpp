@@ -64,6 +64,13 @@ class Manager {
   void feed_measurement_imu(double t, const std::array<double, 3> &wm, const std::array<double, 3> &am) {
     check(uvio_hp_feed_imu(h_, t, wm.data(), am.data()));
   }
+  // a burst of samples (t[i], wm[i], am[i]) in one call
+  void feed_measurement_imu(const std::vector<double> &t, const std::vector<std::array<double, 3>> &wm,
+                            const std::vector<std::array<double, 3>> &am) {
+    if (wm.size() != t.size() || am.size() != t.size()) throw Error(UVIO_HP_E_ARG, "feed_measurement_imu: size mismatch");
+    check(uvio_hp_feed_imu_batch(h_, (int)t.size(), t.data(), wm.empty() ? nullptr : wm[0].data(),
+                                 am.empty() ? nullptr : am[0].data()));
+  }
   // TrackSIM input: per camera (feature id, raw uv); false before initialization (the reference returns silently)
   bool feed_measurement_simulation(double t, const std::vector<int> &camids,
                                    const std::vector<std::vector<std::pair<uint64_t, std::array<float, 2>>>> &feats) {

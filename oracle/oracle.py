@@ -92,6 +92,10 @@ class OracleManager(VioManager):
             raise RuntimeError("orc_%s failed (%d)" % (name, rc))
         return [{"featid": int(f[0]), "used": bool(kept[i]), "to_delete": bool(dele[i])} for i, f in enumerate(features)]
 
+    def feed_measurement_imu_batch(self, t, wm, am):
+        for i in range(len(t)):
+            self.feed_measurement_imu(float(t[i]), wm[i], am[i])
+
     def uwb_update_single(self, t, anchor_id, rng):
         a = C.c_int(0)
         rc = self._lib.orc_uwb_update_single(self._h, C.c_double(t), C.c_uint64(int(anchor_id)), C.c_double(rng),

@@ -110,6 +110,7 @@ SIGNATURES = [
     ("last_error", C.c_char_p, [C.c_void_p]),
     ("initialize_with_gt", _I, [C.c_void_p, _P(_D)]),
     ("feed_imu", _I, [C.c_void_p, _D, _P(_D), _P(_D)]),
+    ("feed_imu_batch", _I, [C.c_void_p, C.c_int, _P(_D), _P(_D), _P(_D)]),
     ("feed_simulation", _I, [C.c_void_p, _D, _I, _P(_I), _P(_I), _P(C.c_uint64), _P(C.c_float)]),
     ("feed_camera", _I, [C.c_void_p, _D, _I, _P(_I), _P(_P(C.c_uint8)), _P(_I), _P(_P(C.c_uint8))]),
     ("feed_uwb", _I, [C.c_void_p, _D, _I, _P(C.c_uint64), _P(_D)]),
@@ -154,9 +155,15 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _P(_D), C.c_size_t, C.c_void_p)
 EXPORTED = ["uvio_hp_" + s[0] for s in SIGNATURES]
 
 
+MISSING = set()  # entry points an overriding UVIO_HP_LIB (an older build in an A/B run) does not export
+
+
 def bind(lib, prefix, names=None):
     for name, res, args in SIGNATURES:
         if names is not None and name not in names:
+            continue
+        if "UVIO_HP_LIB" in os.environ and prefix == "uvio_hp_" and not hasattr(lib, prefix + name):
+            MISSING.add(name)
             continue
         f = getattr(lib, prefix + name)
         f.restype = res

@@ -86,6 +86,11 @@ int uvio_hp_feed_imu(uvio_hp_t *h, double t, const double wm[3], const double am
   HP_GUARD(h, h->e->feed_imu(t, wm, am); return 0;)
 }
 
+int uvio_hp_feed_imu_batch(uvio_hp_t *h, int n, const double *t, const double *wm, const double *am) {
+  if (!h || n < 0 || (n > 0 && (!t || !wm || !am))) return UVIO_HP_E_ARG;
+  HP_GUARD(h, for (int i = 0; i < n; i++) h->e->feed_imu(t[i], wm + 3 * i, am + 3 * i); return 0;)
+}
+
 int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
                             const float *uv) {
   if (!h || ncam <= 0 || !cam_ids || !counts) return UVIO_HP_E_ARG;

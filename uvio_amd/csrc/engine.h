@@ -339,6 +339,7 @@ class Engine {
   void stage_flush();
   // wait for the device (counted in the frame's timing: device_syncs, sync_wait)
   void dev_sync();
+  bool propagation_can_precede_tracking(double t) const;
   // dx + negative-diagonal count back to the host (one copy + sync); throws on a negative diagonal
   void read_dx(const char *who);
   void initialize_invertible_host(const VarP &v, const std::vector<std::pair<int, int>> &H_order,

@@ -141,6 +141,7 @@ Tracker::~Tracker() {
     if (kv.second.d_score) (void)hipFree(kv.second.d_score);
   }
   if (d_lk_bytes_) (void)hipFree(d_lk_bytes_);
+  if (ev_match_) (void)hipEventDestroy(ev_match_);
   if (b_) {
     if (b_->dmem) (void)hipFree(b_->dmem);
     if (b_->hmem) (void)hipHostFree(b_->hmem);
@@ -268,7 +269,9 @@ const std::vector<int> &Tracker::subsets(int count) {
 }
 
 void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
-                   const uint8_t *const *masks, bool device_imgs, const DbSink &db) {
+                   const uint8_t *const *masks, bool device_imgs, const DbSink &db,
+                   std::function<void()> in_flight) {
+  in_flight_ = std::move(in_flight);
   device_syncs = 0;
   sync_wait = 0.0;
   if (histogram_method_ == 2)
@@ -345,6 +348,7 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
   } else {
     for (int k = 0; k < ncam; k++) feed_monocular(t, cam_ids[k], db);
   }
+  in_flight_ = nullptr;  // not reached (no matching this frame): the caller does that work afterwards
   // pyr_last / mask_last <- this frame's (every TrackKLT path ends this way)
   for (int k = 0; k < ncam; k++) {
     CamState &c = cs_[cam_ids[k]];
@@ -686,6 +690,19 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
   }
   launch_ransac(s_, rs, ns, kRansacIters, kRansacConf);
   HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.mask[hi] + b.cap), hipMemcpyDeviceToHost, s_));
+  if (in_flight_) {
+    // wait for the matching results only, not for the work the callback enqueues behind them
+    if (!ev_match_) HP_HIP(hipEventCreateWithFlags(&ev_match_, hipEventDisableTiming));
+    HP_HIP(hipEventRecord(ev_match_, s_));
+    std::function<void()> f = std::move(in_flight_);
+    in_flight_ = nullptr;
+    f();
+    auto t0 = std::chrono::steady_clock::now();
+    HP_HIP(hipEventSynchronize(ev_match_));
+    sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    device_syncs++;
+    return;
+  }
   sync();
 }
 

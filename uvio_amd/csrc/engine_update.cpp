@@ -253,14 +253,39 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
     camids.push_back(cid);
   }
   if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream, &kprof_));
+  // Propagator::propagate_and_clone reads nothing the tracker produces.  When nothing can run between the
+  // tracking and the propagation (no zero-velocity check, no UWB range before t), the host computes it
+  // while the frame's LK + RANSAC are on the device and enqueues its launches behind them: the same
+  // launches in the same stream order, the host's share hidden under the tracker's wait.
+  bool early = false;
+  int early_rc = 0;
+  std::function<void()> in_flight;
+  if (propagation_can_precede_tracking(t))
+    in_flight = [&, t]() {
+      HPROF("prop");
+      early = true;
+      early_rc = propagate_and_clone(t);
+    };
   {
     HPROF("track.feed");
-    tracker_->feed(t, ncam, cam_ids, imgs, strides, masks, device_imgs,
-                   [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
-                     db_update(id, tt, (size_t)cam, u, v, un, vn);
-                   });
+    tracker_->feed(
+        t, ncam, cam_ids, imgs, strides, masks, device_imgs,
+        [this](size_t id, double tt, int cam, float u, float v, float un, float vn) {
+          db_update(id, tt, (size_t)cam, u, v, un, vn);
+        },
+        std::move(in_flight));
   }
+  if (early && early_rc) return early_rc;
   return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait);
+}
+
+// the conditions under which after_tracking's first state change is propagate_and_clone(t)
+bool Engine::propagation_can_precede_tracking(double t) const {
+  if (!is_initialized_ || timestamp_ >= t) return false;
+  if (o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) return false;
+  for (auto it = past_uwb_.begin(); it != past_uwb_.end() && it->first < t; it++)
+    if (it->first > timestamp_) return false;
+  return true;
 }
 
 int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, int track_syncs,

@@ -30,8 +30,12 @@ class Tracker {
 
   // TrackKLT::feed_new_camera.  imgs: host (device_imgs false) or device u8 images of the
   // configured size with row stride strides[k]; masks: host u8, same stride, may be null.
+  // in_flight (optional) runs once on the host while the frame's LK + RANSAC are on the device, before
+  // the tracker waits for them: work behind it on the same stream overlaps nothing of the tracker's
+  // results, only the host's wait
   void feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
-            const uint8_t *const *masks, bool device_imgs, const DbSink &db);
+            const uint8_t *const *masks, bool device_imgs, const DbSink &db,
+            std::function<void()> in_flight = nullptr);
 
   // TrackBase::get_last_obs / get_last_ids for one camera
   void last_tracks(int cam, std::vector<KeyPt> &pts, std::vector<size_t> &ids) const;
@@ -78,6 +82,8 @@ class Tracker {
   std::vector<float> spmask_host_;
   Bufs *b_ = nullptr;
   std::unordered_map<int, std::vector<int>> subset_cache_;
+  std::function<void()> in_flight_;
+  hipEvent_t ev_match_ = nullptr;
 
   CamState &cam_state(int cid);
   void alloc_pyr(CamState &c, int w, int h);

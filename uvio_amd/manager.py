@@ -158,6 +158,19 @@ class VioManager:
         a = (C.c_double * 3)(*am)
         self._check(self._call("feed_imu", self._h, C.c_double(t), w, a), "feed_measurement_imu")
 
+    def feed_measurement_imu_batch(self, t, wm, am):
+        """n consecutive feed_measurement_imu calls: t (n,), wm (n,3), am (n,3)."""
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        wm = np.ascontiguousarray(wm, dtype=np.float64)
+        am = np.ascontiguousarray(am, dtype=np.float64)
+        n = t.shape[0]
+        assert wm.shape == (n, 3) and am.shape == (n, 3)
+        if "feed_imu_batch" in N.MISSING:  # an older library under A/B
+            for i in range(n):
+                self.feed_measurement_imu(float(t[i]), wm[i], am[i])
+            return
+        self._check(self._call("feed_imu_batch", self._h, n, _dp(t), _dp(wm), _dp(am)), "feed_measurement_imu_batch")
+
     def feed_measurement_simulation(self, t, camids, feats, allow_uninit=False):
         """feats[i] = (ids uint64[n], uv float32[n,2]) for camera camids[i] (TrackSIM input)."""
         return self.feed_measurement_simulation_packed(t, camids, *pack_sim_frame(feats), allow_uninit=allow_uninit)
