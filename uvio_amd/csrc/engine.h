@@ -190,6 +190,13 @@ struct DeviceBufs {
   // feature sharding: the all-reduced [G upper triangle (max_ncol^2) | accepted features | accepted rows]
   double *shard = nullptr, *shard_host = nullptr;
   int *acc = nullptr;       // accepted features of the last update batch (gates its P update)
+  // information-form prefactor on a side stream (Engine::info_prefactor): P_II's factor and V while the
+  // feature group runs; its column map in a dedicated device buffer (pinned mirror), the run it belongs to
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_aux_in = nullptr, ev_aux_out = nullptr;
+  int *hidx_pre = nullptr, *hidx_pre_h = nullptr;
+  std::vector<int> pre_hidx;  // columns of the pending prefactor (empty: none)
+  int pre_N = -1;
 };
 
 class Engine {
@@ -316,6 +323,19 @@ class Engine {
   VarP clone_imu_pose(const double *dnc, bool do_dt, const double *staged = nullptr);
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
+  void info_prefactor(const std::vector<int> &hidx);
+  // joins an information-form prefactor its update did not consume (an early return or an exception in
+  // between): the main stream waits for it, so no later P write can overlap its reads of P
+  struct PrefactorJoin {
+    Engine *e;
+    explicit PrefactorJoin(Engine *x) : e(x) {}
+    ~PrefactorJoin() {
+      if (e->d_.pre_N < 0) return;
+      (void)hipStreamWaitEvent(e->d_.stream, e->d_.ev_aux_out, 0);
+      e->d_.pre_hidx.clear();
+      e->d_.pre_N = -1;
+    }
+  };
   void ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
                        const std::function<bool()> &apply = nullptr, const int *gate = nullptr,
                        const double *partials = nullptr);

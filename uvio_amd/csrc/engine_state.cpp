@@ -230,12 +230,16 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
   if (d_.shard_host) hipHostFree(d_.shard_host);
   if (d_.stg_h) hipHostFree(d_.stg_h);
+  if (d_.hidx_pre_h) hipHostFree(d_.hidx_pre_h);
+  if (d_.ev_aux_in) hipEventDestroy(d_.ev_aux_in);
+  if (d_.ev_aux_out) hipEventDestroy(d_.ev_aux_out);
+  if (d_.aux) hipStreamDestroy(d_.aux);
   if (d_.ev0) hipEventDestroy(d_.ev0);
   if (d_.ev1) hipEventDestroy(d_.ev1);
   if (d_.stream) hipStreamDestroy(d_.stream);
@@ -257,6 +261,9 @@ void Engine::alloc_device() {
   HP_HIP(hipStreamCreateWithFlags(&d_.stream, hipStreamNonBlocking));
   HP_HIP(hipEventCreate(&d_.ev0));
   HP_HIP(hipEventCreate(&d_.ev1));
+  HP_HIP(hipStreamCreateWithFlags(&d_.aux, hipStreamNonBlocking));
+  HP_HIP(hipEventCreateWithFlags(&d_.ev_aux_in, hipEventDisableTiming));
+  HP_HIP(hipEventCreateWithFlags(&d_.ev_aux_out, hipEventDisableTiming));
   kprof_.stream = d_.stream;
   HP_HIP(hipEventCreateWithFlags(&rt_.copied, hipEventDisableTiming));
   d_.ekf.kp = &kprof_;
@@ -296,6 +303,8 @@ void Engine::alloc_device() {
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
   dalloc(&d_.hidx, d_.max_ncol + d_.max_rows);
+  dalloc(&d_.hidx_pre, d_.max_ncol);
+  HP_HIP(hipHostMalloc((void **)&d_.hidx_pre_h, sizeof(int) * std::max(d_.max_ncol, 1), hipHostMallocDefault));
   int rmax = std::max(d_.max_ncol, kMaxEkfRows);
   dalloc(&d_.ekf.M, (size_t)cap * rmax);
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
@@ -549,16 +558,44 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
 // EKF update from the Gram partials of a stacked batch (compressed path, m > n)
 void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
                              const std::function<bool()> &apply, const int *gate, const double *partials) {
-  const int *dh = stage(hidx.data(), (size_t)n);
-  stage_flush();
+  const bool pre = d_.pre_N == N_ && d_.pre_hidx == hidx;  // the prefactor of these columns is in flight
+  d_.pre_hidx.clear();
+  d_.pre_N = -1;
   d_.ekf.gate = gate;
-  {
+  const double *G = partials ? partials : d_.partials;
+  if (pre) {
+    HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
     KScope ks(&kprof_, KC_EKF);
-    launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, partials ? partials : d_.partials, nch, n, dh, sigma2, d_.R, d_.ekf);
+    launch_ekf_info_post(d_.stream, d_.P, d_.ldp, N_, G, nch, n, sigma2, d_.R, d_.ekf);
+  } else {
+    const int *dh = stage(hidx.data(), (size_t)n);
+    stage_flush();
+    KScope ks(&kprof_, KC_EKF);
+    launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, G, nch, n, dh, sigma2, d_.R, d_.ekf);
   }
-  kprof_.credit(KC_EKF, ekf_flops(N_, n, n), ekf_bytes(N_, n, n));
+  // the timed launches: without the side-stream prefactor (Cholesky of P_II, n^3 / 3, and V, N n^2) when it ran
+  const double fl = ekf_flops(N_, n, n) - (pre ? (double)n * n * n / 3.0 + (double)N_ * n * n : 0.0);
+  kprof_.credit(KC_EKF, fl, ekf_bytes(N_, n, n));
   read_dx("EKFUpdate");
   if (!apply || apply()) apply_dx(d_.dx_host);
+}
+
+// The information-form update's prefactor (launch_ekf_info_pre: P_II = L L^T, V = P[:,I] L^-T) for the
+// columns hidx of the state as it is now, on the side stream, behind everything enqueued so far; the
+// next ekf_update_info on the same columns and state size waits for it instead of factoring again.  Between
+// the two calls only kernels that read P may be enqueued (the feature group, chi2 gate and Gram do).
+void Engine::info_prefactor(const std::vector<int> &hidx) {
+  const int n = (int)hidx.size();
+  if (n < 1 || n > d_.max_ncol) return;
+  HP_HIP(hipEventSynchronize(d_.ev_aux_out));  // the pinned column map is free (normally long since)
+  std::memcpy(d_.hidx_pre_h, hidx.data(), sizeof(int) * n);
+  HP_HIP(hipEventRecord(d_.ev_aux_in, d_.stream));
+  HP_HIP(hipStreamWaitEvent(d_.aux, d_.ev_aux_in, 0));
+  HP_HIP(hipMemcpyAsync(d_.hidx_pre, d_.hidx_pre_h, sizeof(int) * n, hipMemcpyHostToDevice, d_.aux));
+  launch_ekf_info_pre(d_.aux, d_.P, d_.ldp, N_, n, d_.hidx_pre, d_.ekf);
+  HP_HIP(hipEventRecord(d_.ev_aux_out, d_.aux));
+  d_.pre_hidx = hidx;
+  d_.pre_N = N_;
 }
 
 // StateHelper::set_initial_covariance (StateHelper.cpp:199-223).  Start-up only (initialize_with_gt,

@@ -998,6 +998,9 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
     build_clone_cam_tables(b, false);
     add_features_to_batch(b, fv, 0, fv.size(), 0, o_.feat_rep_msckf);
   }
+  // compressed (information-form) update ahead: its P_II factor and V start now, beside the feature group
+  PrefactorJoin pj(this);
+  if (b.rows > b.n_canon || b.rows > kMaxEkfRows) info_prefactor(b.hidx);
   // The update is enqueued right behind the feature group: rejected features already have zero rows in
   // H_all and the device skips the P update when no feature was accepted (d_.acc), so the host reads the
   // per-feature results with the update's dx instead of waiting for them in between.
@@ -1092,6 +1095,8 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
                 lm.get(), lm_canon[i]);
   }
   // enqueued behind the feature group as in msckf_update (rejected rows are zero, d_.acc gates P)
+  PrefactorJoin pj(this);
+  if (b.rows > b.n_canon || b.rows > kMaxEkfRows) info_prefactor(b.hidx);
   std::vector<DFeatOut> outs;
   const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
   const int m = run_batch(b, 1, s2, o_.slam_chi2_multipler, false, outs);

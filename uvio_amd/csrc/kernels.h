@@ -156,6 +156,11 @@ void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H
 // Gbuf holds (n+1)^2 doubles.  Same P / dx outputs as launch_ekf_update on the Givens R factor.
 void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
                      const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc);
+// its two halves: _pre (P_II = L L^T, V = P[:,I] L^-T; reads P and hidx only) and _post (Gram reduce, Z, X,
+// P update, dx), for running the prefactor on a side stream while the Gram's rows are formed
+void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, const int *hidx, EkfScratch &sc);
+void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
+                          double sigma2, double *Gbuf, EkfScratch &sc);
 // the same update split at the innovation covariance: phase A leaves S_up = H P H^T + s2 I (r x r) at
 // sc.S + 2 r^2 (used by gated single-row updates such as UWB); phase B finishes the update.
 void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,

@@ -685,8 +685,27 @@ __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp,
 //   P+ = P - V V^T + s2 X X^T  (= P - P[:,I] (G P_II + s2 I)^-1 G P[I,:]),   dx = X U^-1 c.
 // Z has eigenvalues >= s2, so both Cholesky factors are of SPD matrices and G itself is never
 // factored (it is exactly singular in the gauge directions of an MSCKF stack).
-void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
-                     const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc) {
+//
+// The chain splits at the Gram: the prefactor (P_II = L L^T and V = P[:,I] L^-T) reads only P and the
+// column map, both fixed once the batch's columns are known, so the engine runs it on a side stream while
+// the feature group forms the rows (launch_ekf_info_pre); launch_ekf_info_post is the rest.
+// Scratch: sc.S holds Laug | L_P | T1 | E | U (5 (n+1)^2), sc.M holds V (and is cholP's global work buffer
+// before that), sc.W is cholZ's global work buffer and then X, sc.Dinv the diagonal-block inverses.
+void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, const int *hidx, EkfScratch &sc) {
+  const int na = n + 1;
+  double *Laug = sc.S;
+  double *Lf = Laug + (size_t)na * na;
+  ensure_lds_attrs();
+  if (n + 1 > kWaveMaxRows) throw std::runtime_error("information-form update wider than the factorization panel");
+  size_t b1 = 0;
+  const int m1 = info_chol_mode(n, n, &b1);
+  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(512), b1, s, P, ldp, hidx, n, Laug, Lf, sc.M,
+                     m1);
+  launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);  // V = P[:,I] L^-T
+}
+
+void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
+                          double sigma2, double *Gbuf, EkfScratch &sc) {
   const int na = n + 1;
   hipLaunchKernelGGL(k_gram_reduce, dim3((na * na + 255) / 256), dim3(256), 0, s, partials, nch, na, Gbuf, sc.neg);
   double *Laug = sc.S;                            // (n+1)^2
@@ -695,23 +714,22 @@ void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *par
   double *E = T1 + (size_t)na * na;               // (n+1)^2
   double *Uf = E + (size_t)na * na;               // n^2   U   (5 (n+1)^2 in total)
   double *w = sc.y;
-  double *gbuf = sc.M;                            // global fallback work buffer (N rmax >= the factor's bytes)
-  ensure_lds_attrs();
-  if (n + 1 > kWaveMaxRows) throw std::runtime_error("information-form update wider than the factorization panel");
-  size_t b1 = 0;
-  const int m1 = info_chol_mode(n, n, &b1);
-  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(512), b1, s, P, ldp, hidx, n, Laug, Lf, gbuf, m1);
   dim3 g((na + 15) / 16, (na + 15) / 16);
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 0, 0, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug
   hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 1, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
-  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, gbuf, m2);
-  launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);     // V = P[:,I] L^-T
+  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2);
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
   int nb = (N + 15) / 16;
   hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg,
                      sc.gate);
+}
+
+void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
+                     const int *hidx, double sigma2, double *Gbuf, EkfScratch &sc) {
+  launch_ekf_info_pre(s, P, ldp, N, n, hidx, sc);
+  launch_ekf_info_post(s, P, ldp, N, partials, nch, n, sigma2, Gbuf, sc);
 }
 
 // StateHelper::initialize_invertible (StateHelper.cpp:484-577) for a 3-dof landmark appended at N:
