@@ -119,6 +119,16 @@ __device__ void trtri_gj_inplace(double *A, int ld, int n) {
 // Two barriers per 4 columns instead of one per column, and the update work runs on the matrix cores.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
+// XCD-aware work index (bijective on [0, nwg)): the dispatcher deals workgroups out to the 8 XCDs round
+// robin (blockIdx % 8 labels the blocks that share one XCD and its L2), so consecutive work indices --
+// the tiles of one row block, or the tile pairs of one row chunk -- land on the same XCD and share the
+// operand rows it has cached instead of each XCD fetching them again.  Only placement changes: every work
+// index is computed exactly as before.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = orig % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+}
+
 __device__ void ldl_panel4(double *A, int ld, int n, int nrows, double *Lp) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int K = 0; K < n; K += 4) {

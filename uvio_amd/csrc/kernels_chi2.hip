@@ -21,29 +21,49 @@
 namespace uvhp {
 
 // T (m x n, ld ldt) = H (m x n, ld ldh) * P[hidx, hidx] with the covariance gather fused into the
-// operand loads.  One 64-lane workgroup per 16x16 tile of T, v_mfma_f64_16x16x4_f64 over K = n in
-// batches of 16 (all 8 operand loads of a batch are issued before its 4 MFMAs).
+// operand loads.  One 64-lane workgroup per 16x16 tile of T, v_mfma_f64_16x16x4_f64 over K = n.  The
+// batches are small (cfg2: 486 x 100), so the kernel is load-latency bound: the column map is staged in
+// LDS once (the P gather then needs no dependent hidx load), and K runs in 32-wide steps whose 16 operand
+// loads are issued one step ahead of the step's 8 MFMAs (register double buffer).  The tiles are XCD-
+// swizzled row block by row block, so an XCD's L2 fetches each H row slab once.  The accumulation order
+// over k is the plain ascending one of 4-wide MFMA steps, whatever the step width.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int HPS = 32;  // K per load step
 __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, int m, int n, int ldh,
                                                  const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
                                                  double *__restrict__ T, int ldt, int *zero) {
+  extern __shared__ int sh_hidx[];
   const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
-  if (zero && l == 0 && blockIdx.x == 0 && blockIdx.y == 0) *zero = 0;  // the batch's accepted-feature count
-  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  if (zero && l == 0 && blockIdx.x == 0) *zero = 0;  // the batch's accepted-feature count
+  const int tc = (n + 15) / 16;
+  const int wid = xcd_swizzle(blockIdx.x, gridDim.x), ti = wid / tc, tj = wid - ti * tc;
+  for (int e = l; e < n; e += 64) sh_hidx[e] = hidx[e];
+  __syncthreads();
+  const int i0 = ti * 16, j0 = tj * 16;
   const int arow = i0 + r16, bcol = j0 + r16;
   const double *Hr = H + (size_t)min(arow, m - 1) * ldh;
-  const int pc = (bcol < n) ? hidx[bcol] : 0;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    double a[4], b[4];
+  const double *Pc = P + ((bcol < n) ? sh_hidx[bcol] : 0);
+  const bool ain = arow < m, bin = bcol < n;
+  double a0[HPS / 4], b0[HPS / 4], a1[HPS / 4], b1[HPS / 4];
+  auto load = [&](int k0, double *a, double *b) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < HPS / 4; u++) {
       const int k = k0 + 4 * u + kq;
-      a[u] = (arow < m && k < n) ? Hr[k] : 0.0;
-      b[u] = (bcol < n && k < n) ? P[(size_t)hidx[k] * ldp + pc] : 0.0;
+      const bool kin = k < n;
+      a[u] = (ain && kin) ? Hr[k] : 0.0;
+      b[u] = (bin && kin) ? Pc[(size_t)sh_hidx[k] * ldp] : 0.0;
     }
+  };
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  load(0, a0, b0);
+  for (int k0 = 0; k0 < n; k0 += 2 * HPS) {
+    if (k0 + HPS < n) load(k0 + HPS, a1, b1);
 #pragma unroll
-    for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+    for (int u = 0; u < HPS / 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b0[u], acc, 0, 0, 0);
+    if (k0 + HPS >= n) break;
+    if (k0 + 2 * HPS < n) load(k0 + 2 * HPS, a0, b0);
+#pragma unroll
+    for (int u = 0; u < HPS / 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b1[u], acc, 0, 0, 0);
   }
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -67,8 +87,12 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
-  if (zero && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) *zero = 0;
-  const int i0 = blockIdx.y * HPB, j0 = blockIdx.x * HPB;
+  if (zero && tid == 0 && blockIdx.x == 0) *zero = 0;
+  // work index = row tile * column tiles + column tile, XCD-swizzled: a row slab of H is fetched once per
+  // XCD (its column tiles run side by side there) instead of once per column tile
+  const int tc = (n + HPB - 1) / HPB;
+  const int wid = xcd_swizzle(blockIdx.x, gridDim.x), ti = wid / tc;
+  const int i0 = ti * HPB, j0 = (wid - ti * tc) * HPB;
   // staging map: A slab element e = tid + 256 u (u < 4): row e / 16, k e % 16; B slab: k e / 64, col e % 64
   int pcol[4];
 #pragma unroll
@@ -264,11 +288,11 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
   if (m >= 4096)  // enough 64 x 64 tiles to fill the 256 CUs
-    hipLaunchKernelGGL(k_gemm_HPg_tiled, dim3((n + HPB - 1) / HPB, (m + HPB - 1) / HPB), dim3(256), 0, s, H_all, m, n,
-                       bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
+    hipLaunchKernelGGL(k_gemm_HPg_tiled, dim3(((n + HPB - 1) / HPB) * ((m + HPB - 1) / HPB)), dim3(256), 0, s, H_all,
+                       m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
   else
-    hipLaunchKernelGGL(k_gemm_HPg, dim3((n + 15) / 16, (m + 15) / 16), dim3(64), 0, s, H_all, m, n, bp.ldh, P, bp.ldp,
-                       hidx, T_all, bp.ldh, acc_count);
+    hipLaunchKernelGGL(k_gemm_HPg, dim3(((n + 15) / 16) * ((m + 15) / 16)), dim3(64), sizeof(int) * (size_t)n, s, H_all,
+                       m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);

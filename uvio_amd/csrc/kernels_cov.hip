@@ -197,15 +197,17 @@ __global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
-  const int nt = (ncol + GB - 1) / GB;
-  int pair = blockIdx.x, ti = 0;
+  const int nt = (ncol + GB - 1) / GB, npairs = nt * (nt + 1) / 2;
+  // work index = chunk * npairs + pair, XCD-swizzled: a chunk's tile pairs share one XCD's L2
+  const int wid = xcd_swizzle(blockIdx.x, gridDim.x), chunk = wid / npairs;
+  int pair = wid - chunk * npairs, ti = 0;
   while (pair >= nt - ti) {
     pair -= nt - ti;
     ti++;
   }
   const int tj = ti + pair;
   const int c0i = ti * GB, c0j = tj * GB;
-  const int r0 = blockIdx.y * GCHUNK_BIG, r1 = min(m, r0 + GCHUNK_BIG);
+  const int r0 = chunk * GCHUNK_BIG, r1 = min(m, r0 + GCHUNK_BIG);
   double rx[4], ry[4];
   auto load = [&](int rb) {
 #pragma unroll
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A,
         for (int tb = 0; tb < 2; tb++) acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
     }
   }
-  double *out = partials + (size_t)blockIdx.y * ncol * ncol;
+  double *out = partials + (size_t)chunk * ncol * ncol;
 #pragma unroll
   for (int ta = 0; ta < 2; ta++)
 #pragma unroll
@@ -261,7 +263,7 @@ void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, doubl
   if (m >= 8 * GCHUNK_BIG) {
     const int ntb = (ncol + GB - 1) / GB, nchb = (m + GCHUNK_BIG - 1) / GCHUNK_BIG;
     *nchunks_out = nchb;
-    hipLaunchKernelGGL(k_gram_mfma, dim3(ntb * (ntb + 1) / 2, nchb), dim3(256), 0, s, A, m, ncol, ldh, partials);
+    hipLaunchKernelGGL(k_gram_mfma, dim3(ntb * (ntb + 1) / 2 * nchb), dim3(256), 0, s, A, m, ncol, ldh, partials);
     return;
   }
   int nt = (ncol + GT - 1) / GT;
