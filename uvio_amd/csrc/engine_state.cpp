@@ -299,7 +299,7 @@ void Engine::alloc_device() {
   dalloc(&d_.chi2, 1000);
   dalloc(&d_.H, (size_t)d_.max_rows * d_.ldh);
   dalloc(&d_.Tall, (size_t)d_.max_rows * d_.ldh);
-  int maxch = (d_.max_rows + 511) / 512 + 1;
+  int maxch = std::max((d_.max_rows + 511) / 512 + 1, gram_num_chunks(2048) + 1);  // 512- or 64-row chunks
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
   dalloc(&d_.hidx, d_.max_ncol + d_.max_rows);

@@ -136,10 +136,15 @@ void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg) 
 // each thread 2x2 outputs.  A is m x ncol, row-major, ld = ldh.
 constexpr int GT = 32;         // tile edge
 constexpr int GCHUNK = 512;    // rows per chunk
+constexpr int GCHUNK_SMALL = 64, GSMALL_ROWS = 2048;  // stacks up to 2048 rows: 64-row chunks
 
-int gram_num_chunks(int m) { return (m + GCHUNK - 1) / GCHUNK; }
+// Rows per chunk of the VALU Gram.  A small stack (cfg2's ~500 rows) in 512-row chunks is one chunk: ~10
+// workgroups each walking 16 dependent row slabs; 64-row chunks give ~8x the workgroups of two slabs each,
+// and the fixed-order reduction adds the chunk partials.
+static int gram_chunk_rows(int m) { return m <= GSMALL_ROWS ? GCHUNK_SMALL : GCHUNK; }
+int gram_num_chunks(int m) { return (m + gram_chunk_rows(m) - 1) / gram_chunk_rows(m); }
 
-__global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int m, int ncol, int ldh,
+__global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int m, int ncol, int ldh, int crows,
                                               double *__restrict__ partials) {
   __shared__ double As[GT][GT + 1];
   __shared__ double Bs[GT][GT + 1];
@@ -152,7 +157,7 @@ __global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int 
   }
   int tj = ti + pair;
   int chunk = blockIdx.y;
-  int r0 = chunk * GCHUNK, r1 = min(m, r0 + GCHUNK);
+  int r0 = chunk * crows, r1 = min(m, r0 + crows);
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   double acc[2][2] = {{0, 0}, {0, 0}};
   for (int rb = r0; rb < r1; rb += GT) {
@@ -270,7 +275,7 @@ void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, doubl
   int pairs = nt * (nt + 1) / 2;
   int nch = gram_num_chunks(m);
   *nchunks_out = nch;
-  hipLaunchKernelGGL(k_gram, dim3(pairs, nch), dim3(256), 0, s, A, m, ncol, ldh, partials);
+  hipLaunchKernelGGL(k_gram, dim3(pairs, nch), dim3(256), 0, s, A, m, ncol, ldh, gram_chunk_rows(m), partials);
 }
 
 // Feature sharding: one rank's contribution to the all-reduced information block.  Upper triangle of the
