@@ -345,7 +345,8 @@ class Engine {
   // readback `apply` decides whether dx goes to the host mean (true when absent)
   void ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx, const double *resdev,
                        int res_stride, double sigma2, const int *hidx_dev = nullptr,
-                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr);
+                       const std::function<bool()> &apply = nullptr, const int *gate = nullptr,
+                       const double *Tdev = nullptr);  // T = H P_II of these rows (ld ldh), if the chi2 gate left it
   void apply_dx(const double *dx);
   // staging (see DeviceBufs): returns the device address the table will have after stage_flush()
   void *stage_bytes(const void *src, size_t bytes);

@@ -534,7 +534,7 @@ void Engine::apply_dx(const double *dx) {
 // EKF update of P on the device with rows H (r x n, ld) / residual; dx applied to the host mean
 void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const std::vector<int> &hidx,
                              const double *resdev, int res_stride, double sigma2, const int *hidx_dev,
-                             const std::function<bool()> &apply, const int *gate) {
+                             const std::function<bool()> &apply, const int *gate, const double *Tdev) {
   if (r <= 0) {
     if (apply) apply();
     return;
@@ -548,7 +548,10 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
   {
     HPROF("ekf_rows.launch");
     KScope ks(&kprof_, KC_EKF);
+    d_.ekf.Tall = Tdev;
+    d_.ekf.ldt = ldh;
     launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
+    d_.ekf.Tall = nullptr;
   }
   kprof_.credit(KC_EKF, ekf_flops(N_, n, r), ekf_bytes(N_, n, r));
   read_dx("EKFUpdate");

@@ -1055,7 +1055,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
     gram(m, ncol, &nch);
     ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
-    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc, d_.Tall);
   }
   return 0;
 }
@@ -1123,7 +1123,7 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
     gram(m, ncol, &nch);
     ekf_update_info(nch, n, b.hidx, s2, results, d_.acc);
   } else {
-    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc);
+    ekf_update_rows(d_.H, d_.ldh, m, n, b.hidx, d_.H + n, d_.ldh, s2, b.hidx_dev, results, d_.acc, d_.Tall);
   }
   return 0;
 }

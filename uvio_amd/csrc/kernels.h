@@ -145,6 +145,10 @@ struct EkfScratch {
   int *chi2_gate = nullptr;
   double chi2_thr = 0.0;
   KProf *kp = nullptr;  // live kernel timing (kprof.h), null = off
+  // optional T = H P_II (r x n rows, ld ldt) of the same H and columns, left by the batch's chi2 gate with
+  // rejected rows zeroed: k_ekf_MS then forms S_up = H T^T without recomputing T
+  const double *Tall = nullptr;
+  int ldt = 0;
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.

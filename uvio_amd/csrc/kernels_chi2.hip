@@ -161,7 +161,7 @@ size_t chi2_lds_bytes(int max_rows_f, int n) {
 // feature's H_all rows from c0 = (mode >= 2 ? 3 : 0) on (delayed init tests the update rows against
 // chi2(dof = all rows), StateHelper.cpp:463-468).
 __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
-                                              const double *__restrict__ T_all, const double *__restrict__ chi2_table,
+                                              double *__restrict__ T_all, const double *__restrict__ chi2_table,
                                               DFeatOut *__restrict__ out, int use_lds, int *acc_count) {
   extern __shared__ double lds[];
   __shared__ double red[256];
@@ -274,10 +274,13 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
 #undef CHI2_TS
   __syncthreads();
   if (st && F.mode <= 1) {
+    // the rejected feature's rows of H_all and of T = H_all P_can (the direct update's S reuses T)
     double *rows = H_all + (size_t)F.row_off * ldh;
+    double *trows = T_all + (size_t)F.row_off * ldh;
     for (int e = tid; e < o.rows * (n + 1); e += blockDim.x) {
       int i = e / (n + 1), j = e - i * (n + 1);
       rows[(size_t)i * ldh + j] = 0.0;
+      if (j < n) trows[(size_t)i * ldh + j] = 0.0;
     }
   }
 }

@@ -56,7 +56,8 @@ __device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB
 __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, int ldp, int N,
                                                 const double *__restrict__ H, int ldh, int r, int n,
                                                 const int *__restrict__ hidx, double s2, double *__restrict__ M,
-                                                double *__restrict__ Sup, int nbM, int *zero) {
+                                                double *__restrict__ Sup, int nbM, int *zero,
+                                                const double *__restrict__ Tall, int ldt) {
   extern __shared__ double sh[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
@@ -89,6 +90,31 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
         const int row = i0 + kq + 4 * q, col = j0 + r16;
         if (row < N && col < r) M[(size_t)row * r + col] = acc[q];
       }
+    }
+    return;
+  }
+  if (Tall) {
+    // T = H P_II is already in HBM from the batch's chi2 gate (k_gemm_HPg, rejected features' rows zeroed
+    // there with their H rows), so S_up[a][b] = H_a T_b^T directly: one upper tile pair (a <= b) per wave,
+    // one chain of loads instead of forming T_b first (same products, same ascending k order).
+    const int nt = (r + 15) / 16;
+    int pair = (blockIdx.x - nbM) * 4 + wid, at = 0;
+    if (pair >= nt * (nt + 1) / 2) return;
+    while (pair >= nt - at) {
+      pair -= nt - at;
+      at++;
+    }
+    const int bt = at + pair;
+    const int ar = 16 * at + r16, br = 16 * bt + r16;
+    const double *Ha = H + (size_t)min(ar, r - 1) * ldh, *Tb = Tall + (size_t)min(br, r - 1) * ldt;
+    const bool av = ar < r, bv = br < r;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain(
+        0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return bv ? Tb[k] : 0.0; }, acc);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = 16 * at + kq + 4 * q, col = 16 * bt + r16;
+      if (row < r && col < r) Sup[(size_t)row * r + col] = acc[q] + (row == col ? s2 : 0.0);
     }
     return;
   }
@@ -322,7 +348,7 @@ void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
   const int nbM = (N + 15) / 16;
   hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, 0.0, M,
-                     (double *)nullptr, nbM, zero);
+                     (double *)nullptr, nbM, zero, (const double *)nullptr, 0);
 }
 
 void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const double *H, int ldh, int r, int n,
@@ -330,10 +356,11 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
   ensure_ekf_lds_attrs();
   const size_t lds = ekf_ms_lds_bytes(n, true);
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
-  const int nbM = (N + 15) / 16, nbS = (r + 15) / 16;
+  const int nbM = (N + 15) / 16, nt = (r + 15) / 16;
+  const int nbS = sc.Tall ? (nt * (nt + 1) / 2 + 3) / 4 : nt;  // tile pairs, 4 per workgroup / column blocks
   double *Sup = sc.S + 2 * (size_t)r * r;
   hipLaunchKernelGGL(k_ekf_MS, dim3(nbM + nbS), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
-                     nbM, sc.neg);
+                     nbM, sc.neg, sc.Tall, sc.ldt);
 }
 
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
