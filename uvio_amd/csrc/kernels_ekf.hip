@@ -53,7 +53,8 @@ __device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB
 
 // ---------------------------------------------------------------------------------------------------
 // K1: M (blocks 0 .. nbM-1) and S_up (blocks nbM .. nbM + ceil(r/16) - 1; none when Sup is null)
-__global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, int ldp, int N,
+constexpr int kMSThreads = 512;  // 8 waves: one M column tile / one S tile pair per wave at cfg2's r ~ 100
+__global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict__ P, int ldp, int N,
                                                 const double *__restrict__ H, int ldh, int r, int n,
                                                 const int *__restrict__ hidx, double s2, double *__restrict__ M,
                                                 double *__restrict__ Sup, int nbM, int *zero,
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
         });
     __syncthreads();
     const int nct = (r + 15) / 16;
-    for (int t = wid; t < nct; t += 4) {
+    for (int t = wid; t < nct; t += kMSThreads / 64) {
       const int j0 = 16 * t, jr = j0 + r16;
       const double *Hr = H + (size_t)min(jr, r - 1) * ldh;
       const bool jv = jr < r;
@@ -98,7 +99,7 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
     // there with their H rows), so S_up[a][b] = H_a T_b^T directly: one upper tile pair (a <= b) per wave,
     // one chain of loads instead of forming T_b first (same products, same ascending k order).
     const int nt = (r + 15) / 16;
-    int pair = (blockIdx.x - nbM) * 4 + wid, at = 0;
+    int pair = (blockIdx.x - nbM) * (kMSThreads / 64) + wid, at = 0;
     if (pair >= nt * (nt + 1) / 2) return;
     while (pair >= nt - at) {
       pair -= nt - at;
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
     const int jr = j0 + r16;
     const double *Hb = H + (size_t)min(jr, r - 1) * ldh;
     const bool jv = jr < r;
-    for (int kt = wid; kt < npad / 16; kt += 4) {
+    for (int kt = wid; kt < npad / 16; kt += kMSThreads / 64) {
       const int row = 16 * kt + r16;
       const double *Prow = P + (size_t)hs[min(row, n - 1)] * ldp;
       const bool rv = row < n;
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(256) k_ekf_MS(const double *__restrict__ P, in
     }
   }
   __syncthreads();
-  for (int at = wid; at <= jb; at += 4) {
+  for (int at = wid; at <= jb; at += kMSThreads / 64) {
     const int ar = 16 * at + r16;
     const double *Ha = H + (size_t)min(ar, r - 1) * ldh;
     const bool av = ar < r;
@@ -347,7 +348,7 @@ void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *
   const size_t lds = ekf_ms_lds_bytes(n, false);
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
   const int nbM = (N + 15) / 16;
-  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, 0.0, M,
+  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, 0.0, M,
                      (double *)nullptr, nbM, zero, (const double *)nullptr, 0);
 }
 
@@ -357,9 +358,10 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
   const size_t lds = ekf_ms_lds_bytes(n, true);
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
   const int nbM = (N + 15) / 16, nt = (r + 15) / 16;
-  const int nbS = sc.Tall ? (nt * (nt + 1) / 2 + 3) / 4 : nt;  // tile pairs, 4 per workgroup / column blocks
+  const int wpb = kMSThreads / 64;
+  const int nbS = sc.Tall ? (nt * (nt + 1) / 2 + wpb - 1) / wpb : nt;  // tile pairs, a wave each / column blocks
   double *Sup = sc.S + 2 * (size_t)r * r;
-  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM + nbS), dim3(256), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+  hipLaunchKernelGGL(k_ekf_MS, dim3(nbM + nbS), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
                      nbM, sc.neg, sc.Tall, sc.ldt);
 }
 

@@ -818,12 +818,17 @@ __global__ void __launch_bounds__(256) k_retri_reset(RetriJob job) {
 }
 
 __global__ void __launch_bounds__(256) k_retri_obs(RetriJob job) {
+  // the SLAM landmarks' ids in LDS: every observation scans them (the scan over global memory was ~50
+  // dependent loads per thread)
+  extern __shared__ unsigned long long sh_slam_id[];
+  for (int s = threadIdx.x; s < job.nslam; s += blockDim.x) sh_slam_id[s] = job.slam[s].featid;
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= job.nobs) return;
   const DRetriObs o = job.obs[i];
   // feat_uvs_in_cam0 is recorded before the SLAM skip
   for (int s = 0; s < job.nslam; s++)
-    if (job.slam[s].featid == o.featid) {
+    if (sh_slam_id[s] == o.featid) {
       if (o.cam == 0) {
         job.slam[s].u0 = o.u;
         job.slam[s].v0 = o.v;
@@ -930,7 +935,9 @@ void launch_retriangulate(hipStream_t s, const RetriJob &job) {
   const int nr = std::max(job.cap, job.nslam);
   hipLaunchKernelGGL(k_retri_reset, dim3((nr + 255) / 256), dim3(256), 0, s, job);
   if (job.nobs > 0) {
-    hipLaunchKernelGGL(k_retri_obs, dim3((job.nobs + 255) / 256), dim3(256), 0, s, job);
+    if (job.nslam > 8192) throw std::runtime_error("retriangulation: more SLAM landmarks than the LDS id table");
+    hipLaunchKernelGGL(k_retri_obs, dim3((job.nobs + 255) / 256), dim3(256),
+                       sizeof(unsigned long long) * (size_t)std::max(job.nslam, 1), s, job);
     hipLaunchKernelGGL(k_retri_final, dim3((job.nobs + 255) / 256), dim3(256), 0, s, job);
   }
   hipLaunchKernelGGL(k_retri_uvd, dim3((nr + 255) / 256), dim3(256), 0, s, job);
