@@ -149,14 +149,16 @@ __global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int 
   __shared__ double As[GT][GT + 1];
   __shared__ double Bs[GT][GT + 1];
   int nt = (ncol + GT - 1) / GT;
-  // decode upper tile pair (ti <= tj) from blockIdx.x
-  int pair = blockIdx.x, ti = 0;
+  // work index = chunk * pairs + pair, XCD-swizzled (a chunk's tile pairs share one L2); decode the upper
+  // tile pair (ti <= tj)
+  const int npairs = nt * (nt + 1) / 2, wid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int chunk = wid / npairs;
+  int pair = wid - chunk * npairs, ti = 0;
   while (pair >= nt - ti) {
     pair -= nt - ti;
     ti++;
   }
   int tj = ti + pair;
-  int chunk = blockIdx.y;
   int r0 = chunk * crows, r1 = min(m, r0 + crows);
   int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   double acc[2][2] = {{0, 0}, {0, 0}};
@@ -275,7 +277,7 @@ void launch_gram(hipStream_t s, const double *A, int m, int ncol, int ldh, doubl
   int pairs = nt * (nt + 1) / 2;
   int nch = gram_num_chunks(m);
   *nchunks_out = nch;
-  hipLaunchKernelGGL(k_gram, dim3(pairs, nch), dim3(256), 0, s, A, m, ncol, ldh, gram_chunk_rows(m), partials);
+  hipLaunchKernelGGL(k_gram, dim3(pairs * nch), dim3(256), 0, s, A, m, ncol, ldh, gram_chunk_rows(m), partials);
 }
 
 // Feature sharding: one rank's contribution to the all-reduced information block.  Upper triangle of the
