@@ -162,6 +162,10 @@ int Engine::msckf_update_sharded(std::vector<FeatP> &fv) {
   Batch b;
   build_clone_cam_tables(b, false);
   add_features_to_batch(b, fv, (size_t)lo, (size_t)hi, 0, o_.feat_rep_msckf);
+  // the information-form update always follows: its P_II factor and V run beside this rank's feature
+  // group and the all-reduce (Engine::info_prefactor)
+  PrefactorJoin pj(this);
+  info_prefactor(b.hidx);
   std::vector<DFeatOut> outs;
   const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
   const int m = run_batch(b, 0, s2, o_.msckf_chi2_multipler, false, outs);
