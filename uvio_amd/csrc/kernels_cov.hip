@@ -192,11 +192,11 @@ __global__ void __launch_bounds__(256) k_gram(const double *__restrict__ A, int 
 
 // The Gram of a large stack (configs 4-5: ~80k rows x 173-243 columns) on the matrix cores: a 256-thread
 // workgroup owns a 64 x 64 upper tile pair of G for one chunk of GCHUNK_BIG rows; rows run in slabs of
-// 16 staged in LDS (the two 16 x 64 column blocks of the slab), each wave accumulates a 32 x 32 quarter
+// 32 staged in LDS (the two 16 x 64 column blocks of the slab), each wave accumulates a 32 x 32 quarter
 // with four v_mfma_f64_16x16x4_f64 tiles (A operand = the slab transposed: k = row).  The next slab's
 // loads are issued before the current slab's MFMAs.  Partials: same layout as k_gram (chunk-major,
 // every entry a <= b written).
-constexpr int GB = 64, GK = 16, GCHUNK_BIG = 1024;
+constexpr int GB = 64, GK = 32, GCHUNK_BIG = 1024;
 __global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A, int m, int ncol, int ldh,
                                                    double *__restrict__ partials) {
   __shared__ double Xs[GK][GB + 1];
@@ -215,10 +215,11 @@ __global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A,
   const int tj = ti + pair;
   const int c0i = ti * GB, c0j = tj * GB;
   const int r0 = chunk * GCHUNK_BIG, r1 = min(m, r0 + GCHUNK_BIG);
-  double rx[4], ry[4];
+  constexpr int NU = GK / 4;  // slab elements per thread
+  double rx[NU], ry[NU];
   auto load = [&](int rb) {
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < NU; u++) {
       const int e = tid + 256 * u, row = rb + (e >> 6), c = e & 63;
       rx[u] = (row < r1 && c0i + c < ncol) ? A[(size_t)row * ldh + c0i + c] : 0.0;
       ry[u] = (row < r1 && c0j + c < ncol) ? A[(size_t)row * ldh + c0j + c] : 0.0;
@@ -233,7 +234,7 @@ __global__ void __launch_bounds__(256) k_gram_mfma(const double *__restrict__ A,
   for (int rb = r0; rb < r1; rb += GK) {
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < NU; u++) {
       const int e = tid + 256 * u;
       Xs[e >> 6][e & 63] = rx[u];
       Ys[e >> 6][e & 63] = ry[u];
