@@ -141,7 +141,8 @@ typedef struct {
   int msckf_rows;   /* stacked rows m before compression */
   int msckf_cols;   /* H columns n */
   /* device-side measurement of the per-feature linearize kernel over this frame (HIP events on the
-   * library's stream): launches, summed kernel seconds, and algorithmic FP64 FLOPs of those launches
+   * library's stream, recorded only while uvio_hp_set_kernel_timing has timing on; zero otherwise):
+   * launches, summed kernel seconds, and algorithmic FP64 FLOPs of those launches
    * (3 Householder reflections 12*(2m_f)*(n_f+4) + chi2 2 r n^2 + 2 r^2 n + r^3/3 per feature) */
   int k_feat_launches;
   double k_feat_s;

@@ -437,6 +437,7 @@ class Engine {
     std::vector<int> hidx;     // canonical column -> covariance id
     const int *hidx_dev = nullptr;  // its staged device copy
     bool finished = false;          // per-feature results read back (finish_batch)
+    bool evtimed = false;           // the feature group is bracketed by the ev0 / ev1 timing events
     bool chi2 = true;               // the batch chi2 kernels ran (run_batch)
     std::vector<FeatP> fptrs;
     int n_canon = 0, rows = 0, max_meas = 0, max_nf = 0;

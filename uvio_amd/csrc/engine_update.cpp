@@ -863,7 +863,10 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 16 * nf));
     HP_HIP(hipMemset(bp.dbg_ts, 0, sizeof(long long) * 16 * nf));
   }
-  if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
+  // the feature group's event pair only while kernel timing is on: a timing event between the upload and
+  // k_feature costs a dispatch gap on every batch
+  b.evtimed = o_.record_timing && kprof_.on;
+  if (b.evtimed) HP_HIP(hipEventRecord(d_.ev0, d_.stream));
   {
     KScope ks(&kprof_, KC_FEATURE);
     launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H, d_.fout,
@@ -879,7 +882,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout,
                       max_rows_f, d_.acc);
   }
-  if (o_.record_timing) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
+  if (b.evtimed) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   d_.fout_pending = nf;  // copied with the next readback (read_dx) or before the next wait (dev_sync)
   if (!wait && !tsdump && !mdump) return b.rows;  // the caller's next sync completes the batch (finish_batch)
   dev_sync();
@@ -921,7 +924,7 @@ void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
   outs.assign(d_.fout_host, d_.fout_host + nf);
   if (b.finished) return;
   b.finished = true;
-  if (o_.record_timing) {
+  if (b.evtimed) {
     float ms = 0.f;
     HP_HIP(hipEventElapsedTime(&ms, d_.ev0, d_.ev1));
     timing_.k_feat_launches += 1;
