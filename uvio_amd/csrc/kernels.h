@@ -113,7 +113,7 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
 // rejected MSCKF / SLAM features get zero rows.  T_all: like H_all.
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
                        double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
-                       int *acc_count);
+                       int *acc_count, double *pcan = nullptr);  // pcan: n^2 scratch for the gathered P_can
 size_t feature_lds_bytes(int max_meas, int max_nf);
 
 // Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->

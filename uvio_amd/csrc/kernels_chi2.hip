@@ -94,11 +94,13 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
   const int wid = xcd_swizzle(blockIdx.x, gridDim.x), ti = wid / tc;
   const int i0 = ti * HPB, j0 = (wid - ti * tc) * HPB;
   // staging map: A slab element e = tid + 256 u (u < 4): row e / 16, k e % 16; B slab: k e / 64, col e % 64
+  // P_can operand: with hidx the gather P[hidx[k], hidx[c]]; without it P is P_can itself (dense n x n,
+  // gathered once by k_gather_pcan), so the B loads are plain coalesced rows with no dependent index load
   int pcol[4];
 #pragma unroll
   for (int u = 0; u < 4; u++) {
     const int c = j0 + ((tid + 256 * u) & 63);
-    pcol[u] = (c < n) ? hidx[c] : 0;
+    pcol[u] = (c < n) ? (hidx ? hidx[c] : c) : 0;
   }
   double ra[4], rb[4];
   auto load = [&](int k0) {
@@ -108,7 +110,7 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
       const int ar = i0 + (e >> 4), ak = k0 + (e & 15);
       ra[u] = (ar < m && ak < n) ? H[(size_t)ar * ldh + ak] : 0.0;
       const int bk = k0 + (e >> 6), bc = j0 + (e & 63);
-      rb[u] = (bk < n && bc < n) ? P[(size_t)hidx[bk] * ldp + pcol[u]] : 0.0;
+      rb[u] = (bk < n && bc < n) ? P[(size_t)(hidx ? hidx[bk] : bk) * ldp + pcol[u]] : 0.0;
     }
   };
   dbl4 acc[2][2];
@@ -150,6 +152,15 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
         const int row = i0 + 32 * wr + 16 * ta + kq + 4 * q, col = j0 + 32 * wc + 16 * tb + r16;
         if (row < m && col < n) T[(size_t)row * ldt + col] = acc[ta][tb][q];
       }
+}
+
+// P_can = P[hidx, hidx] (n x n, dense) for the large-batch T GEMM
+__global__ void __launch_bounds__(256) k_gather_pcan(const double *__restrict__ P, int ldp,
+                                                     const int *__restrict__ hidx, int n, double *__restrict__ Pc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * n) return;
+  const int i = e / n, j = e - i * n;
+  Pc[e] = P[(size_t)hidx[i] * ldp + hidx[j]];
 }
 
 size_t chi2_lds_bytes(int max_rows_f, int n) {
@@ -287,13 +298,16 @@ __global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__re
 
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
                        double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
-                       int *acc_count) {
+                       int *acc_count, double *pcan) {
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
-  if (m >= 4096)  // enough 64 x 64 tiles to fill the 256 CUs
+  if (m >= 4096) {  // enough 64 x 64 tiles to fill the 256 CUs
+    if (pcan)
+      hipLaunchKernelGGL(k_gather_pcan, dim3((n * n + 255) / 256), dim3(256), 0, s, P, bp.ldp, hidx, n, pcan);
     hipLaunchKernelGGL(k_gemm_HPg_tiled, dim3(((n + HPB - 1) / HPB) * ((m + HPB - 1) / HPB)), dim3(256), 0, s, H_all,
-                       m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
-  else
+                       m, n, bp.ldh, pcan ? pcan : P, pcan ? n : bp.ldp, pcan ? nullptr : hidx, T_all, bp.ldh,
+                       acc_count);
+  } else
     hipLaunchKernelGGL(k_gemm_HPg, dim3(((n + 15) / 16) * ((m + 15) / 16)), dim3(64), sizeof(int) * (size_t)n, s, H_all,
                        m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
