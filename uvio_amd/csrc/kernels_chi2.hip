@@ -24,9 +24,10 @@ namespace uvhp {
 // operand loads.  One 64-lane workgroup per 16x16 tile of T, v_mfma_f64_16x16x4_f64 over K = n.  The
 // batches are small (cfg2: 486 x 100), so the kernel is load-latency bound: the column map is staged in
 // LDS once (the P gather then needs no dependent hidx load), and K runs in 32-wide steps whose 16 operand
-// loads are issued one step ahead of the step's 8 MFMAs (register double buffer).  The tiles are XCD-
-// swizzled row block by row block, so an XCD's L2 fetches each H row slab once.  The accumulation order
-// over k is the plain ascending one of 4-wide MFMA steps, whatever the step width.
+// loads are issued one step ahead of the step's 8 MFMAs (register double buffer).  The tiles run on two
+// XCDs in contiguous row-block ranges (below), so P_can is fetched into two L2s instead of eight and each H
+// row slab once (cfg2: 2.13 -> 0.75 MB per launch, profiles/r02u_pmc_traffic_cfg2.json).  The accumulation
+// order over k is the plain ascending one of 4-wide MFMA steps, whatever the step width.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int HPS = 32;  // K per load step
 __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, int m, int n, int ldh,
@@ -35,8 +36,17 @@ __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, i
   extern __shared__ int sh_hidx[];
   const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
   if (zero && l == 0 && blockIdx.x == 0) *zero = 0;  // the batch's accepted-feature count
-  const int tc = (n + 15) / 16;
-  const int wid = xcd_swizzle(blockIdx.x, gridDim.x), ti = wid / tc, tj = wid - ti * tc;
+  // Placement on XCD_GROUPS of the 8 XCDs only (blocks labelled blockIdx % 8 >= XCD_GROUPS exit at once):
+  // every XCD that runs tiles fetches all of P_can into its L2, so the small batches (cfg2: 217 single-wave
+  // tiles, a few per CU on two XCDs) read P_can twice instead of eight times; each group takes a contiguous
+  // range of tiles, i.e. whole row blocks of H.
+  constexpr int XCD_GROUPS = 2;
+  const int x = blockIdx.x % 8;
+  if (x >= XCD_GROUPS) return;
+  const int tc = (n + 15) / 16, nwg = tc * ((m + 15) / 16), per = (nwg + XCD_GROUPS - 1) / XCD_GROUPS;
+  const int wid = x * per + blockIdx.x / 8;
+  if (wid >= nwg || wid >= (x + 1) * per) return;
+  const int ti = wid / tc, tj = wid - ti * tc;
   for (int e = l; e < n; e += 64) sh_hidx[e] = hidx[e];
   __syncthreads();
   const int i0 = ti * 16, j0 = tj * 16;
@@ -308,8 +318,8 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
                        m, n, bp.ldh, pcan ? pcan : P, pcan ? n : bp.ldp, pcan ? nullptr : hidx, T_all, bp.ldh,
                        acc_count);
   } else
-    hipLaunchKernelGGL(k_gemm_HPg, dim3(((n + 15) / 16) * ((m + 15) / 16)), dim3(64), sizeof(int) * (size_t)n, s, H_all,
-                       m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
+    hipLaunchKernelGGL(k_gemm_HPg, dim3(8 * ((((n + 15) / 16) * ((m + 15) / 16) + 1) / 2)), dim3(64),
+                       sizeof(int) * (size_t)n, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);
