@@ -92,6 +92,7 @@ struct CamTrack {
 struct Feature {
   size_t featid = 0;
   bool to_delete = false;
+  size_t dense_idx = 0;  // slot in Engine::dense_
   // Per camera, in the iteration order of the reference's unordered_map<size_t, vector<...>> members:
   // with libstdc++ and at most UVIO_HP_MAX_CAMS small integer keys every key sits in its own bucket and
   // a new key is linked at the list front, so iteration runs in reverse first-insertion order
@@ -263,6 +264,23 @@ class Engine {
   std::unique_ptr<Tracker> tracker_;
   // ---- feature database (TrackSIM's / TrackKLT's) ----
   std::unordered_map<size_t, FeatP> db_;
+  // every feature of db_ in one contiguous array (order unrelated to db_'s; Feature::dense_idx is the slot)
+  // for the walks whose outcome does not depend on the order (the per-frame measurement cleanup), which then
+  // need not chase the hash map's nodes; db_insert / db_erase keep the two in step
+  std::vector<Feature *> dense_;
+  using DbIt = std::unordered_map<size_t, FeatP>::iterator;
+  DbIt db_insert(size_t id, const FeatP &f) {
+    f->dense_idx = dense_.size();
+    dense_.push_back(f.get());
+    return db_.emplace(id, f).first;
+  }
+  DbIt db_erase(DbIt it) {
+    const size_t i = it->second->dense_idx;
+    dense_[i] = dense_.back();
+    dense_[i]->dense_idx = i;
+    dense_.pop_back();
+    return db_.erase(it);
+  }
   size_t currid_;
   // ---- manager ----
   bool is_initialized_ = false;

@@ -893,7 +893,7 @@ int Engine::zupt_try_update(double timestamp) {
         ct += (int)tr.m.size();
       }
       if (ct < 1)
-        it = db_.erase(it);
+        it = db_erase(it);
       else
         it++;
     }

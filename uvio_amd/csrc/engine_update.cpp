@@ -75,7 +75,7 @@ void Engine::initialize_with_gt(const double x[17]) {
   for (auto it = db_.begin(); it != db_.end();) {
     it->second->clean_older_measurements(timestamp_);
     if (it->second->count() < 1)
-      it = db_.erase(it);
+      it = db_erase(it);
     else
       it++;
   }
@@ -123,7 +123,7 @@ void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float 
   } else {
     f = std::make_shared<Feature>();
     f->featid = id;
-    db_[id] = f;
+    db_insert(id, f);
   }
   f->track(cam).m.push_back(FeatMeas{u, v, un, vn, t});
 }
@@ -209,7 +209,7 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
       if (it == db_.end()) {
         auto f = std::make_shared<Feature>();
         f->featid = id;
-        it = db_.emplace(id, f).first;
+        it = db_insert(id, f);
       }
       fp[k] = it->second.get();
     }
@@ -508,7 +508,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   for (auto &f : pending_delete_) {
     if (!f->to_delete) continue;
     auto it = db_.find(f->featid);
-    if (it != db_.end() && it->second == f) db_.erase(it);
+    if (it != db_.end() && it->second == f) db_erase(it);
   }
   pending_delete_.clear();
   {
@@ -521,9 +521,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     // FeatureDatabase::cleanup_measurements(margtimestep): per-feature trimming on the pool, then the
     // emptied features are erased (erasing by key keeps the others' iteration order)
     double mt = margtimestep();
-    std::vector<Feature *> all;
-    all.reserve(db_.size());
-    for (auto &kv : db_) all.push_back(kv.second.get());
+    const std::vector<Feature *> all(dense_);  // (a copy: the erasures below reorder dense_)
     std::vector<uint8_t> empty(all.size(), 0);
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
@@ -532,7 +530,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       }
     });
     for (size_t i = 0; i < all.size(); i++)
-      if (empty[i]) db_.erase(all[i]->featid);
+      if (empty[i]) db_erase(db_.find(all[i]->featid));
   }
   marginalize_old_clone();
   if (o_.record_timing >= 2) dev_sync();
