@@ -181,11 +181,12 @@ size_t chi2_lds_bytes(int max_rows_f, int n) {
 // One workgroup per feature.  out[f] carries the feature kernel's status / rows; chi2 rows are the
 // feature's H_all rows from c0 = (mode >= 2 ? 3 : 0) on (delayed init tests the update rows against
 // chi2(dof = all rows), StateHelper.cpp:463-468).
-__global__ void __launch_bounds__(256) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
+constexpr int kChi2Threads = 512;
+__global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
                                               double *__restrict__ T_all, const double *__restrict__ chi2_table,
                                               DFeatOut *__restrict__ out, int use_lds, int *acc_count) {
   extern __shared__ double lds[];
-  __shared__ double red[256];
+  __shared__ double red[kChi2Threads];
   __shared__ int st;
   const int f = blockIdx.x;
   long long *tsp = bp.dbg_ts ? bp.dbg_ts + (size_t)f * 16 + 8 : nullptr;  // debug phase stamps
@@ -327,7 +328,7 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
   if (bytes > 64 * 1024 && (int)bytes > granted)
     throw std::runtime_error("k_chi2 needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
-  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(256), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
+  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(kChi2Threads), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
                      acc_count);
 }
 
