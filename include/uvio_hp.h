@@ -172,7 +172,9 @@ typedef struct uvio_hp uvio_hp_t;
 /* Defaults of the reference option structs (StateOptions.h, UpdaterOptions.h, ...). */
 int uvio_hp_options_default(uvio_hp_options_t *opts);
 /* Parse estimator_config.yaml (+ relative_config_imu / relative_config_imucam / config_uwb files)
- * with the reference's keys (YamlParser, opencv_yaml_parse.h:65-163; VioManagerOptions::print_and_load). */
+ * with the reference's keys (YamlParser, opencv_yaml_parse.h:65-163; VioManagerOptions::print_and_load).
+ * Only the keys present in the files are written: call uvio_hp_options_default on the struct first (as
+ * the reference's option structs start from their defaults). */
 int uvio_hp_options_load(const char *estimator_config_path, uvio_hp_options_t *opts);
 
 /* ---- lifetime ---- */

@@ -49,6 +49,7 @@ class Manager {
  public:
   explicit Manager(const std::string &estimator_config_yaml, int device = 0) {
     uvio_hp_options_t o;
+    check_static(uvio_hp_options_default(&o), "options_default");  // the load overlays the YAML's keys on these
     check_static(uvio_hp_options_load(estimator_config_yaml.c_str(), &o), "options_load " + estimator_config_yaml);
     create(o, device);
   }

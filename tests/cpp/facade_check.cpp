@@ -9,7 +9,7 @@
 int main(int argc, char **argv) {
   if (argc < 2) return 2;
   uvio_hp_options_t o;
-  if (uvio_hp_options_load(argv[1], &o) != 0) return 3;
+  if (uvio_hp_options_default(&o) != 0 || uvio_hp_options_load(argv[1], &o) != 0) return 3;
   auto f1 = &uvio_amd::Manager::msckf_update;
   auto f2 = &uvio_amd::Manager::slam_update;
   auto f3 = &uvio_amd::Manager::slam_delayed_init;
