@@ -326,6 +326,14 @@ int uvio_hp_shard_partition(const int *rows, int n, int world, int *bounds);
 /* per-feature results of the last UpdaterMSCKF::update: feature id, triangulated p_FinG (3 per
  * feature), status (0 accepted, 1 triangulation/refinement failed, 3 chi2 rejected) and chi2 */
 int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n);
+/* per-feature results of every updater call of the last camera frame, in call order: kind (0
+ * UpdaterMSCKF::update, 1 UpdaterSLAM::update, 2 UpdaterSLAM::delayed_init), feature id, p_FinG (MSCKF:
+ * triangulated; delayed init: triangulated before the landmark's initialization; SLAM update: 0),
+ * status (0 accepted, 1 triangulation/refinement failed or too few measurements, 3 chi2 rejected) and
+ * chi2 (delayed init: StateHelper::initialize's test, StateHelper.cpp:451-470).  The lock-step tests
+ * hand these to the oracle's rounding-tie witness (oracle/src/flip.h). */
+int uvio_hp_debug_frame_feats(uvio_hp_t *h, int *kind, uint64_t *ids, double *pG, int *status, double *chi2, int cap,
+                              int *n);
 /* StateHelper::EKFUpdate (StateHelper.cpp:116) on a standalone covariance: P (N x N, row-major,
  * in/out, host memory), H (r x n, row-major) whose column j maps to covariance index H_index[j]
  * (the H_order blocks flattened), residual (r), isotropic noise sigma2.  dx_out (N) receives K*res.

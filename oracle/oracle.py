@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 
 _ORC_NAMES = ["create", "destroy", "initialize_with_gt", "feed_imu", "feed_simulation", "feed_uwb", "init_anchors",
               "get_imu_state", "get_cov_dim", "get_cov", "get_state_vector", "get_timing", "get_clone_times",
-              "ekf_update", "compress", "debug_last_msckf", "get_fej_vector",
+              "ekf_update", "compress", "debug_last_msckf", "debug_frame_feats", "get_fej_vector",
               "msckf_compressed_update", "feed_camera", "get_tracks", "get_pyramid", "get_active_tracks"]
 
 _lib = None
@@ -52,6 +52,10 @@ def load():
         lib.orc_marginalize_slam.argtypes = [C.c_void_p]
         lib.orc_marginalize_old_clone.argtypes = [C.c_void_p]
         lib.orc_uwb_update_single.argtypes = [C.c_void_p, C.c_double, C.c_uint64, C.c_double, i32p]
+        u64p, dp = C.POINTER(C.c_uint64), C.POINTER(C.c_double)
+        lib.orc_set_steer.argtypes = [C.c_void_p, C.c_int, C.c_int, i32p, u64p, dp, i32p, dp]
+        lib.orc_get_steer_log.argtypes = [C.c_void_p, i32p, u64p, i32p, C.POINTER(C.c_int64), dp, dp, dp, i32p, i32p,
+                                          C.c_int, i32p]
         lib.orc_chi2_quantile95.restype = C.c_double
         lib.orc_chi2_quantile95.argtypes = [C.c_int]
         lib.orc_camera_distort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -103,6 +107,40 @@ class OracleManager(VioManager):
         if rc != 0:
             raise RuntimeError("orc_uwb_update_single failed (%d)" % rc)
         return bool(a.value)
+
+    def set_steer(self, frame_feats):
+        """Lock-step steering (oracle/src/flip.h, updater.h FrameDebug): the device's per-feature results of the
+        frame this oracle processes next (VioManager.debug_frame_feats()); None turns steering off."""
+        if frame_feats is None:
+            self._lib.orc_set_steer(self._h, 0, 0, None, None, None, None, None)
+            return
+        kind, ids, pG, st, c2 = [np.ascontiguousarray(a) for a in frame_feats]
+        kind, st = kind.astype(np.int32), st.astype(np.int32)
+        pG = np.ascontiguousarray(pG, dtype=np.float64)
+        ids = ids.astype(np.uint64)
+        c2 = c2.astype(np.float64)
+        self._lib.orc_set_steer(self._h, 1, len(ids), kind.ctypes.data_as(C.POINTER(C.c_int)),
+                                ids.ctypes.data_as(C.POINTER(C.c_uint64)), _dp(pG), st.ctypes.data_as(C.POINTER(C.c_int)),
+                                _dp(c2))
+        self._steer_keep = (kind, ids, pG, st, c2)
+
+    def steer_log(self):
+        """Steering events since creation: list of dicts (kind, featid, stage, index, margin, before, after,
+        found, candidates)."""
+        cap = 4096
+        i32 = lambda: np.zeros(cap, dtype=np.int32)
+        kind, stage, found, cands = i32(), i32(), i32(), i32()
+        ids = np.zeros(cap, dtype=np.uint64)
+        index = np.zeros(cap, dtype=np.int64)
+        margin, before, after = np.zeros(cap), np.zeros(cap), np.zeros(cap)
+        n = C.c_int()
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        self._lib.orc_get_steer_log(self._h, ip(kind), ids.ctypes.data_as(C.POINTER(C.c_uint64)), ip(stage),
+                                    index.ctypes.data_as(C.POINTER(C.c_int64)), _dp(margin), _dp(before), _dp(after),
+                                    ip(found), ip(cands), cap, C.byref(n))
+        keys = ("kind", "featid", "stage", "index", "margin", "before", "after", "found", "candidates")
+        cols = (kind, ids, stage, index, margin, before, after, found, cands)
+        return [{k: c[i].item() for k, c in zip(keys, cols)} for i in range(min(n.value, cap))]
 
     def set_state(self, val, fej, P):
         """Lock-step parity: adopt another implementation's mean / FEJ / covariance."""

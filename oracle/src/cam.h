@@ -6,6 +6,7 @@
 //                            fisheye::undistortPoints (OpenCV 4.2, not in /root/reference;
 //                            restated from SURVEY Appendix A)
 #pragma once
+#include "flip.h"
 #include "la.h"
 
 namespace orc {
@@ -17,7 +18,7 @@ struct Camera {
 
   // CamBase::distort_d (CamBase.h:130): double -> float -> distort_f -> float -> double
   void distort_d(double xn, double yn, double &u, double &vv) const {
-    float xf = (float)xn, yf = (float)yn;
+    float xf = fcast(xn), yf = fcast(yn);
     float uf, vf;
     distort_f(xf, yf, uf, vf);
     u = (double)uf;
@@ -31,8 +32,8 @@ struct Camera {
       double r_2 = r * r, r_4 = r_2 * r_2;
       double x1 = x * (1 + v[4] * r_2 + v[5] * r_4) + 2 * v[6] * x * y + v[7] * (r_2 + 2 * x * x);
       double y1 = y * (1 + v[4] * r_2 + v[5] * r_4) + v[6] * (r_2 + 2 * y * y) + 2 * v[7] * x * y;
-      uf = (float)(v[0] * x1 + v[2]);
-      vf = (float)(v[1] * y1 + v[3]);
+      uf = fcast(v[0] * x1 + v[2]);
+      vf = fcast(v[1] * y1 + v[3]);
     } else {
       double r = std::sqrt(x * x + y * y);
       double theta = std::atan(r);
@@ -41,8 +42,8 @@ struct Camera {
       double inv_r = (r > 1e-8) ? 1.0 / r : 1.0;
       double cdist = (r > 1e-8) ? theta_d * inv_r : 1.0;
       double x1 = x * cdist, y1 = y * cdist;
-      uf = (float)(v[0] * x1 + v[2]);
-      vf = (float)(v[1] * y1 + v[3]);
+      uf = fcast(v[0] * x1 + v[2]);
+      vf = fcast(v[1] * y1 + v[3]);
     }
   }
 

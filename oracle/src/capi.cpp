@@ -295,6 +295,59 @@ int orc_compress(const double *A, int m, int n, double *R_out) {
 
 double orc_chi2_quantile95(int dof) { return chi2_quantile95(dof); }
 
+// per-feature results of every updater call of the last frame (include/uvio_hp.h uvio_hp_debug_frame_feats)
+int orc_debug_frame_feats(orc_handle *h, int *kind, uint64_t *ids, double *pG, int *status, double *chi2, int cap,
+                          int *n) {
+  int k = 0;
+  for (const auto &kd : h->m.fdbg.feats) {
+    if (k < cap) {
+      kind[k] = kd.first;
+      ids[k] = kd.second.id;
+      for (int j = 0; j < 3; j++) pG[3 * k + j] = kd.second.p_FinG[j];
+      status[k] = kd.second.status;
+      chi2[k] = kd.second.chi2;
+    }
+    k++;
+  }
+  *n = k;
+  return 0;
+}
+
+// lock-step steering (updater.h FrameDebug): the device's per-feature results of the frame the oracle
+// processes next; on = 0 turns steering off
+int orc_set_steer(orc_handle *h, int on, int n, const int *kind, const uint64_t *ids, const double *pG,
+                  const int *status, const double *chi2) {
+  auto &d = h->m.fdbg;
+  d.steer = on != 0;
+  d.targets.clear();
+  for (int i = 0; i < n; i++)
+    d.targets[{kind[i], (size_t)ids[i]}] = SteerTarget{status[i], {pG[3 * i], pG[3 * i + 1], pG[3 * i + 2]}, chi2[i]};
+  return 0;
+}
+
+// the steering log since creation: per event kind, feature id, stage, cast index, margin, disagreement
+// before / after, found, candidates tried
+int orc_get_steer_log(orc_handle *h, int *kind, uint64_t *ids, int *stage, int64_t *index, double *margin,
+                      double *before, double *after, int *found, int *cands, int cap, int *n) {
+  int k = 0;
+  for (const auto &e : h->m.fdbg.log) {
+    if (k < cap) {
+      kind[k] = e.kind;
+      ids[k] = e.featid;
+      stage[k] = e.stage;
+      index[k] = e.index;
+      margin[k] = e.margin;
+      before[k] = e.before;
+      after[k] = e.after;
+      found[k] = e.found;
+      cands[k] = e.candidates;
+    }
+    k++;
+  }
+  *n = k;
+  return 0;
+}
+
 // per-feature results of the last MSCKF update (debug / parity tests)
 int orc_debug_last_msckf(orc_handle *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n) {
   const auto &v = h->m.last_msckf.feats;

@@ -3,7 +3,11 @@
 
 #include <algorithm>
 
+#include "flip.h"
+
 namespace orc {
+
+thread_local FlipCtl *g_flip = nullptr;
 
 // Feature.cpp:26-49
 void Feature::clean_old_measurements(const std::vector<double> &valid_times) {
@@ -237,7 +241,7 @@ double FeatureInitializer::compute_error(ClonesCam &clonesCAM, Feature &feat, do
       double hi1 = R_AtoCi(0, 0) * alpha + R_AtoCi(0, 1) * beta + R_AtoCi(0, 2) + rho * p_AinCi[0];
       double hi2 = R_AtoCi(1, 0) * alpha + R_AtoCi(1, 1) * beta + R_AtoCi(1, 2) + rho * p_AinCi[1];
       double hi3 = R_AtoCi(2, 0) * alpha + R_AtoCi(2, 1) * beta + R_AtoCi(2, 2) + rho * p_AinCi[2];
-      float z1 = (float)(hi1 / hi3), z2 = (float)(hi2 / hi3);
+      float z1 = fcast(hi1 / hi3), z2 = fcast(hi2 / hi3);
       auto un = feat.uvs_norm.at(pair.first)[m];
       float r1 = un.first - z1, r2 = un.second - z2;
       float nrm = std::sqrt(r1 * r1 + r2 * r2);
@@ -281,7 +285,7 @@ bool FeatureInitializer::single_gaussnewton(Feature &feat, ClonesCam &clonesCAM)
           H(1, 0) = (R_AtoCi(1, 0) * hi3 - hi2 * R_AtoCi(2, 0)) / h3s;
           H(1, 1) = (R_AtoCi(1, 1) * hi3 - hi2 * R_AtoCi(2, 1)) / h3s;
           H(1, 2) = (p_AinCi[1] * hi3 - hi2 * p_AinCi[2]) / h3s;
-          float z1 = (float)(hi1 / hi3), z2 = (float)(hi2 / hi3);
+          float z1 = fcast(hi1 / hi3), z2 = fcast(hi2 / hi3);
           auto un = feat.uvs_norm.at(pair.first)[m];
           float r1 = un.first - z1, r2 = un.second - z2;
           Mat res(2, 1);

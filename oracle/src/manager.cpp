@@ -12,6 +12,8 @@ static double secs(clk::time_point a, clk::time_point b) { return std::chrono::d
 
 Manager::Manager(const uvio_hp_options_t &opt)
     : o(opt), state(opt), prop(opt), msckf(opt), slam(opt), uwb(opt), currid(4 * (size_t)opt.max_aruco_features + 1) {
+  msckf.dbg = &fdbg;
+  slam.dbg = &fdbg;
   tracker.num_features = (int)std::floor((double)opt.init_max_features / (double)opt.num_cameras);
   tracker.threshold = opt.fast_threshold;
   tracker.grid_x = opt.grid_x;
@@ -145,6 +147,7 @@ int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_
   auto rT2 = clk::now();
   timing = uvio_hp_timing_t{};
   timing.tracking = secs(rT1, rT2);
+  fdbg.feats.clear();
   if (!is_initialized) return UVIO_HP_E_STATE;
   // UVioManager.cpp:147-162 / VioManager.cpp:291-307: zero-velocity update; on success the frame ends here
   if (zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) {

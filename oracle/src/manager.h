@@ -42,6 +42,7 @@ struct Manager {
   std::map<double, UwbMsg> past_uwb;
   uvio_hp_timing_t timing{};
   UpdateStats last_msckf{};
+  FrameDebug fdbg;  // this frame's per-feature results + lock-step steering (updater.h)
   // UpdaterZeroVelocity (VioManager.cpp:160, 186-188, 294-307, 360)
   std::unique_ptr<UpdaterZUPT> zupt;
   bool did_zupt_update = false, has_moved_since_zupt = false;

@@ -367,12 +367,11 @@ VarP clone(State &s, const Ref &var) {
   return pose;
 }
 
-// StateHelper.cpp:393-482. R = sigma2 * I (isotropic, asserted in the reference)
-bool initialize(State &s, VarP new_var, const std::vector<Ref> &H_order, Mat &H_R, Mat &H_L, double sigma2, Mat &res,
-                double chi2_mult, int *status) {
-  *status = 0;
-  int new_var_size = new_var->size;
-  assert(new_var_size == H_L.c);
+// StateHelper.cpp:407-470: Givens rotations separating the landmark's rows (H_L, H_R and res are
+// rotated in place), then the chi2 of the update rows (returned; Hup / resup receive those rows)
+double initialize_split(const State &s, const std::vector<Ref> &H_order, Mat &H_R, Mat &H_L, double sigma2, Mat &res,
+                        Mat &Hup, Mat &resup) {
+  int new_var_size = H_L.c;
   Givens G;
   for (int n = 0; n < H_L.c; ++n) {
     for (int m = H_L.r - 1; m > n; m--) {
@@ -382,19 +381,30 @@ bool initialize(State &s, VarP new_var, const std::vector<Ref> &H_order, Mat &H_
       for (int j = 0; j < H_R.c; j++) G.apply(H_R(m - 1, j), H_R(m, j));
     }
   }
-  Mat Hxinit = H_R.block(0, 0, new_var_size, H_R.c);
-  Mat H_finit = H_L.block(0, 0, new_var_size, new_var_size);
-  Mat resinit = res.block(0, 0, new_var_size, 1);
-  Mat Rinit = sigma2 * Mat::Identity(new_var_size);
   int nup = H_R.r - new_var_size;
-  Mat Hup = H_R.block(new_var_size, 0, nup, H_R.c);
-  Mat resup = res.block(new_var_size, 0, nup, 1);
+  Hup = H_R.block(new_var_size, 0, nup, H_R.c);
+  resup = res.block(new_var_size, 0, nup, 1);
   Mat P_up = get_marginal_covariance(s, H_order);
   Mat S = Hup * P_up * Hup.T();
   for (int i = 0; i < nup; i++) S(i, i) += sigma2;
   Mat sol = resup;
   llt_solve(S, sol);
-  double chi2 = dot(resup, sol);
+  return dot(resup, sol);
+}
+
+// StateHelper.cpp:393-482. R = sigma2 * I (isotropic, asserted in the reference)
+bool initialize(State &s, VarP new_var, const std::vector<Ref> &H_order, Mat &H_R, Mat &H_L, double sigma2, Mat &res,
+                double chi2_mult, int *status) {
+  *status = 0;
+  int new_var_size = new_var->size;
+  assert(new_var_size == H_L.c);
+  Mat Hup, resup;
+  double chi2 = initialize_split(s, H_order, H_R, H_L, sigma2, res, Hup, resup);
+  Mat Hxinit = H_R.block(0, 0, new_var_size, H_R.c);
+  Mat H_finit = H_L.block(0, 0, new_var_size, new_var_size);
+  Mat resinit = res.block(0, 0, new_var_size, 1);
+  Mat Rinit = sigma2 * Mat::Identity(new_var_size);
+  int nup = Hup.r;
   double chi2_check = chi2_quantile95(res.r);
   if (chi2 > chi2_mult * chi2_check) return false;
   initialize_invertible(s, new_var, H_order, Hxinit, H_finit, Rinit, resinit);

@@ -150,6 +150,8 @@ Mat get_marginal_covariance(const State &s, const std::vector<Ref> &vars);
 void set_initial_covariance(State &s, const Mat &cov, const std::vector<Ref> &order);
 void marginalize(State &s, VarP marg);
 VarP clone(State &s, const Ref &var);
+double initialize_split(const State &s, const std::vector<Ref> &H_order, Mat &H_R, Mat &H_L, double sigma2, Mat &res,
+                        Mat &Hup, Mat &resup);
 bool initialize(State &s, VarP new_var, const std::vector<Ref> &H_order, Mat &H_R, Mat &H_L, double sigma2, Mat &res,
                 double chi2_mult, int *status);
 void initialize_invertible(State &s, VarP new_var, const std::vector<Ref> &H_order, const Mat &H_R, const Mat &H_L,

@@ -3,6 +3,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <algorithm>
+#include <cmath>
 #include <map>
 
 namespace orc {
@@ -259,6 +261,73 @@ void measurement_compress_inplace(Mat &H_x, Mat &res) {
 
 }  // namespace UpdaterHelper
 
+// Lock-step steering (updater.h FrameDebug, flip.h): run() once recording the near-tie casts; when
+// miss() exceeds tol, re-run with one candidate cast rounded the other way (smallest margin first) until
+// miss() <= tol.  Without a target, run() runs once, unobserved.
+static const double kSteerThresh = 1e-9;  // casts recorded as candidates: relative margin below this
+static const int kSteerMaxTries = 64;
+
+template <class Run, class Miss>
+static void steer_stage(FrameDebug *dbg, const SteerTarget *t, int kind, size_t featid, int stage, double tol, Run run,
+                        Miss miss) {
+  if (!t) {
+    run();
+    return;
+  }
+  FlipCtl ctl;
+  ctl.thresh = kSteerThresh;
+  {
+    FlipScope fs(&ctl);
+    run();
+  }
+  const double m0 = miss();
+  if (!(m0 > tol)) return;
+  auto cands = ctl.near;
+  std::sort(cands.begin(), cands.end(), [](const std::pair<long, double> &a, const std::pair<long, double> &b) {
+    return a.second < b.second || (a.second == b.second && a.first < b.first);
+  });
+  if ((int)cands.size() > kSteerMaxTries) cands.resize(kSteerMaxTries);
+  for (const auto &c : cands) {
+    FlipCtl f;
+    f.thresh = 0;
+    f.force = c.first;
+    {
+      FlipScope fs(&f);
+      run();
+    }
+    const double m = miss();
+    if (m <= tol) {
+      dbg->log.push_back(SteerEvent{kind, featid, stage, c.first, c.second, m0, m, 1, (int)cands.size()});
+      return;
+    }
+  }
+  {
+    FlipCtl f;
+    f.thresh = 0;
+    FlipScope fs(&f);
+    run();
+  }
+  dbg->log.push_back(SteerEvent{kind, featid, stage, -1, 0.0, m0, miss(), 0, (int)cands.size()});
+}
+
+// stage 0 disagreement: the accept decision, then the triangulated position (m)
+static double tri_miss(const SteerTarget *t, bool ok, const Feature &f) {
+  const bool dev_ok = t->status != 1;
+  if (ok != dev_ok) return INFINITY;
+  if (!ok) return 0.0;
+  double d = 0;
+  for (int k = 0; k < 3; k++) d = std::max(d, std::fabs(f.p_FinG[k] - t->p_FinG[k]));
+  return d;
+}
+
+// stage 1 disagreement: chi2 relative to max(|chi2|, 1) (tests/test_gpu_parity.py _compare_feats)
+static double chi2_miss(const SteerTarget *t, double chi2) {
+  if (t->status == 1) return 0.0;
+  return std::fabs(chi2 - t->chi2) / std::max(std::fabs(t->chi2), 1.0);
+}
+
+static const double kTolP = 1e-9, kTolChi2 = 1e-11;  // the strict lock-step bounds
+
 static ClonesCam make_clones_cam(State &s) {
   ClonesCam clones_cam;
   for (const auto &cc : s.calib_IMUtoCAM) {
@@ -302,12 +371,22 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
   ClonesCam clones_cam = make_clones_cam(s);
   auto it1 = feature_vec.begin();
   while (it1 != feature_vec.end()) {
-    bool ok_tri = init.o.fi_triangulate_1d ? init.single_triangulation_1d(**it1, clones_cam)
-                                           : init.single_triangulation(**it1, clones_cam);
-    bool ok_ref = true;
-    if (init.o.fi_refine_features) ok_ref = init.single_gaussnewton(**it1, clones_cam);
-    if (!ok_tri || !ok_ref) {
+    bool ok = false;
+    Feature &F = **it1;
+    const SteerTarget *tg = dbg ? dbg->target(0, F.featid) : nullptr;
+    steer_stage(
+        dbg, tg, 0, F.featid, 0, kTolP,
+        [&]() {
+          bool ok_tri = init.o.fi_triangulate_1d ? init.single_triangulation_1d(F, clones_cam)
+                                                 : init.single_triangulation(F, clones_cam);
+          bool ok_ref = true;
+          if (init.o.fi_refine_features) ok_ref = init.single_gaussnewton(F, clones_cam);
+          ok = ok_tri && ok_ref;
+        },
+        [&]() { return tri_miss(tg, ok, F); });
+    if (!ok) {
       if (st) st->feats.push_back(FeatDebug{(*it1)->featid, {0, 0, 0}, 1, -1.0});
+      if (dbg) dbg->record(0, FeatDebug{(*it1)->featid, {0, 0, 0}, 1, -1.0});
       (*it1)->to_delete = true;
       it1 = feature_vec.erase(it1);
       continue;
@@ -342,8 +421,25 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
     }
     Mat H_f, H_x, res;
     std::vector<Ref> Hx_order;
-    UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
-    UpdaterHelper::nullspace_project_inplace(H_f, H_x, res);
+    double chi2 = 0;
+    const SteerTarget *tg = dbg ? dbg->target(0, feat.featid) : nullptr;
+    steer_stage(
+        dbg, tg, 0, feat.featid, 1, kTolChi2,
+        [&]() {
+          H_f = Mat();
+          H_x = Mat();
+          res = Mat();
+          Hx_order.clear();
+          UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
+          UpdaterHelper::nullspace_project_inplace(H_f, H_x, res);
+          Mat P_marg = StateHelper::get_marginal_covariance(s, Hx_order);
+          Mat S = H_x * P_marg * H_x.T();
+          for (int i = 0; i < S.r; i++) S(i, i) += sigma_pix_sq;
+          Mat sol = res;
+          llt_solve(S, sol);
+          chi2 = dot(res, sol);
+        },
+        [&]() { return chi2_miss(tg, chi2); });
     if (const char *dump = std::getenv("ORC_DUMP")) {  // debug: projected rows per feature
       FILE *fp = std::fopen(dump, "ab");
       std::vector<double> hdr = {(double)feat.featid, (double)H_x.r, (double)H_x.c};
@@ -356,17 +452,12 @@ int UpdaterMSCKF::update(State &s, std::vector<FeatP> &feature_vec, UpdateStats 
       }
       std::fclose(fp);
     }
-    Mat P_marg = StateHelper::get_marginal_covariance(s, Hx_order);
-    Mat S = H_x * P_marg * H_x.T();
-    for (int i = 0; i < S.r; i++) S(i, i) += sigma_pix_sq;
-    Mat sol = res;
-    llt_solve(S, sol);
-    double chi2 = dot(res, sol);
     double chi2_check = (res.r < 500) ? chi_squared_table[res.r] : chi2_quantile95(res.r);
-    if (st) {
+    {
       FeatDebug d{(*it2)->featid, {(*it2)->p_FinG[0], (*it2)->p_FinG[1], (*it2)->p_FinG[2]}, 0, chi2};
       if (chi2 > chi2_mult * chi2_check) d.status = 3;
-      st->feats.push_back(d);
+      if (st) st->feats.push_back(d);
+      if (dbg) dbg->record(0, d);
     }
     if (chi2 > chi2_mult * chi2_check) {
       (*it2)->to_delete = true;
@@ -428,11 +519,21 @@ int UpdaterSLAM::delayed_init(State &s, std::vector<FeatP> &feature_vec) {
   ClonesCam clones_cam = make_clones_cam(s);
   auto it1 = feature_vec.begin();
   while (it1 != feature_vec.end()) {
-    bool ok_tri = init.o.fi_triangulate_1d ? init.single_triangulation_1d(**it1, clones_cam)
-                                           : init.single_triangulation(**it1, clones_cam);
-    bool ok_ref = true;
-    if (init.o.fi_refine_features) ok_ref = init.single_gaussnewton(**it1, clones_cam);
-    if (!ok_tri || !ok_ref) {
+    bool ok = false;
+    Feature &F = **it1;
+    const SteerTarget *tg = dbg ? dbg->target(2, F.featid) : nullptr;
+    steer_stage(
+        dbg, tg, 2, F.featid, 0, kTolP,
+        [&]() {
+          bool ok_tri = init.o.fi_triangulate_1d ? init.single_triangulation_1d(F, clones_cam)
+                                                 : init.single_triangulation(F, clones_cam);
+          bool ok_ref = true;
+          if (init.o.fi_refine_features) ok_ref = init.single_gaussnewton(F, clones_cam);
+          ok = ok_tri && ok_ref;
+        },
+        [&]() { return tri_miss(tg, ok, F); });
+    if (!ok) {
+      if (dbg) dbg->record(2, FeatDebug{(*it1)->featid, {0, 0, 0}, 1, 0.0});
       (*it1)->to_delete = true;
       it1 = feature_vec.erase(it1);
       continue;
@@ -458,16 +559,31 @@ int UpdaterSLAM::delayed_init(State &s, std::vector<FeatP> &feature_vec) {
     }
     Mat H_f, H_x, res;
     std::vector<Ref> Hx_order;
-    UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
-    if (feat_rep == ANCHORED_INVERSE_DEPTH_SINGLE) {
-      Mat H_xf(H_x.r, H_x.c + 1);
-      H_xf.set_block(0, 0, H_x);
-      H_xf.set_block(0, H_x.c, H_f.block(0, H_f.c - 1, H_f.r, 1));
-      Mat H_fb = H_f.block(0, 0, H_f.r, H_f.c - 1);
-      UpdaterHelper::nullspace_project_inplace(H_fb, H_xf, res);
-      H_x = H_xf.block(0, 0, H_xf.r, H_xf.c - 1);
-      H_f = H_xf.block(0, H_xf.c - 1, H_xf.r, 1);
-    }
+    double chi2 = 0;
+    const SteerTarget *tg = dbg ? dbg->target(2, feat.featid) : nullptr;
+    steer_stage(
+        dbg, tg, 2, feat.featid, 1, kTolChi2,
+        [&]() {
+          H_f = Mat();
+          H_x = Mat();
+          res = Mat();
+          Hx_order.clear();
+          UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
+          if (feat_rep == ANCHORED_INVERSE_DEPTH_SINGLE) {
+            Mat H_xf(H_x.r, H_x.c + 1);
+            H_xf.set_block(0, 0, H_x);
+            H_xf.set_block(0, H_x.c, H_f.block(0, H_f.c - 1, H_f.r, 1));
+            Mat H_fb = H_f.block(0, 0, H_f.r, H_f.c - 1);
+            UpdaterHelper::nullspace_project_inplace(H_fb, H_xf, res);
+            H_x = H_xf.block(0, 0, H_xf.r, H_xf.c - 1);
+            H_f = H_xf.block(0, H_xf.c - 1, H_xf.r, 1);
+          }
+          if (dbg) {  // initialize's chi2 on copies (the state is not touched)
+            Mat a = H_x, b = H_f, r = res, Hup, resup;
+            chi2 = StateHelper::initialize_split(s, Hx_order, a, b, sigma_pix_sq, r, Hup, resup);
+          }
+        },
+        [&]() { return chi2_miss(tg, chi2); });
     int landmark_size = (feat_rep == ANCHORED_INVERSE_DEPTH_SINGLE) ? 1 : 3;
     auto landmark = std::make_shared<Var>(K_LANDMARK, landmark_size, landmark_size);
     landmark->featid = feat.featid;
@@ -483,7 +599,10 @@ int UpdaterSLAM::delayed_init(State &s, std::vector<FeatP> &feature_vec) {
       landmark->set_from_xyz(feat.p_FinG_fej, true);
     }
     int st = 0;
-    if (StateHelper::initialize(s, landmark, Hx_order, H_x, H_f, sigma_pix_sq, res, chi2_mult, &st)) {
+    const Mat p_tri = (*it2)->p_FinG;
+    const bool init_ok = StateHelper::initialize(s, landmark, Hx_order, H_x, H_f, sigma_pix_sq, res, chi2_mult, &st);
+    if (dbg) dbg->record(2, FeatDebug{feat.featid, {p_tri[0], p_tri[1], p_tri[2]}, init_ok ? 0 : 3, chi2});
+    if (init_ok) {
       if (st < 0) return UVIO_HP_E_NUMERIC;
       s.features_SLAM.insert({(*it2)->featid, landmark});
       (*it2)->to_delete = true;
@@ -543,30 +662,41 @@ int UpdaterSLAM::update(State &s, std::vector<FeatP> &feature_vec) {
       feat.p_FinG = landmark->get_xyz(false);
       feat.p_FinG_fej = landmark->get_xyz(true);
     }
-    Mat H_f, H_x, res;
-    std::vector<Ref> Hx_order;
-    UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
-    Mat H_xf;
-    if (landmark->rep == ANCHORED_INVERSE_DEPTH_SINGLE) {
-      H_xf = Mat(H_x.r, H_x.c + 1);
-      H_xf.set_block(0, 0, H_x);
-      H_xf.set_block(0, H_x.c, H_f.block(0, H_f.c - 1, H_f.r, 1));
-      Mat H_fb = H_f.block(0, 0, H_f.r, H_f.c - 1);
-      UpdaterHelper::nullspace_project_inplace(H_fb, H_xf, res);
-    } else {
-      H_xf = Mat(H_x.r, H_x.c + H_f.c);
-      H_xf.set_block(0, 0, H_x);
-      H_xf.set_block(0, H_x.c, H_f);
-    }
-    std::vector<Ref> Hxf_order = Hx_order;
-    Hxf_order.push_back(ref_of(landmark));
-    Mat P_marg = StateHelper::get_marginal_covariance(s, Hxf_order);
-    Mat S = H_xf * P_marg * H_xf.T();
-    for (int i = 0; i < S.r; i++) S(i, i) += sigma_pix_sq;
-    Mat sol = res;
-    llt_solve(S, sol);
-    double chi2 = dot(res, sol);
+    Mat H_f, H_x, res, H_xf;
+    std::vector<Ref> Hx_order, Hxf_order;
+    double chi2 = 0;
+    const SteerTarget *tg = dbg ? dbg->target(1, feat.featid) : nullptr;
+    steer_stage(
+        dbg, tg, 1, feat.featid, 1, kTolChi2,
+        [&]() {
+          H_f = Mat();
+          H_x = Mat();
+          res = Mat();
+          Hx_order.clear();
+          UpdaterHelper::get_feature_jacobian_full(s, feat, H_f, H_x, res, Hx_order);
+          if (landmark->rep == ANCHORED_INVERSE_DEPTH_SINGLE) {
+            H_xf = Mat(H_x.r, H_x.c + 1);
+            H_xf.set_block(0, 0, H_x);
+            H_xf.set_block(0, H_x.c, H_f.block(0, H_f.c - 1, H_f.r, 1));
+            Mat H_fb = H_f.block(0, 0, H_f.r, H_f.c - 1);
+            UpdaterHelper::nullspace_project_inplace(H_fb, H_xf, res);
+          } else {
+            H_xf = Mat(H_x.r, H_x.c + H_f.c);
+            H_xf.set_block(0, 0, H_x);
+            H_xf.set_block(0, H_x.c, H_f);
+          }
+          Hxf_order = Hx_order;
+          Hxf_order.push_back(ref_of(landmark));
+          Mat P_marg = StateHelper::get_marginal_covariance(s, Hxf_order);
+          Mat S = H_xf * P_marg * H_xf.T();
+          for (int i = 0; i < S.r; i++) S(i, i) += sigma_pix_sq;
+          Mat sol = res;
+          llt_solve(S, sol);
+          chi2 = dot(res, sol);
+        },
+        [&]() { return chi2_miss(tg, chi2); });
     double chi2_check = (res.r < 500) ? chi_squared_table[res.r] : chi2_quantile95(res.r);
+    if (dbg) dbg->record(1, FeatDebug{feat.featid, {0, 0, 0}, chi2 > chi2_mult * chi2_check ? 3 : 0, chi2});
     if (chi2 > chi2_mult * chi2_check) {
       landmark->fail_count++;
       (*it2)->to_delete = true;

@@ -14,18 +14,21 @@ chunk build (>= 256 features), k_gemm_HPg_tiled (m >= 4096 stacked rows), k_gram
 information-form Cholesky factors of n > 135 columns.  Lock-step as in test_gpu_parity.py: before every
 frame the oracle adopts the device's mean / FEJ values / covariance, both process the same frame.
 
-Tolerances: the per-frame bounds of test_gpu_parity.py (triangulation 1e-9 m, chi2 1e-11 relative, no
-accept / reject flip, state and covariance 1e-10 relative) at every size, although the oracle compresses
-the ~80k stacked rows of cfg4 / cfg5 with Givens rotations (UpdaterHelper.cpp:456-487) while the device
-forms their Gram in information form.  Measured on MI355X (r02c): worst P 1.2e-12 (cfg4,
-800 features x 52 measurements), 1.9e-13 (cfg5), 6.8e-13 (cfg3); worst state 2.2e-14.
+Tolerances: the per-frame bounds of test_gpu_parity.py on EVERY frame (triangulation 1e-9 m, chi2 1e-11
+relative, no accept / reject flip, state and covariance 1e-10 relative), with the oracle's rounding-tie
+steering (test_gpu_parity.py docstring, oracle/src/flip.h): a feature on which the device and the oracle
+disagree must be explained by ONE float cast within 1e-10 relative of its rounding midpoint, and with that
+cast rounded the device's way the frame must meet the strict bounds.  The oracle compresses the ~80k stacked
+rows of cfg4 / cfg5 with Givens rotations (UpdaterHelper.cpp:456-487) while the device forms their Gram in
+information form.  Measured on MI355X (r02c): worst P 1.2e-12 (cfg4, 800 features x 52
+measurements), 1.9e-13 (cfg5), 6.8e-13 (cfg3); worst state 2.2e-14.
 """
 import os
 
 import numpy as np
 import pytest
 
-from test_gpu_parity import _compare_feats, _rel, _snap
+from test_gpu_parity import _check_lockstep, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -40,51 +43,25 @@ def _bench():
 
 
 def _lockstep(opts, sim, n_frames, renderer=None, after_init=None):
-    import uvio_amd as U
-    from oracle import oracle as O
-    g, o = U.VioManager(opts), O.OracleManager(opts)
-    steps = []
-
-    def before(nf, t):
-        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
-
-    def after(nf, t):
-        steps.append((_snap(g), _snap(o)))
-
-    sim.run([g, o], n_frames=n_frames, before_frame=before, on_frame=after, renderer=renderer, after_init=after_init)
-    g.close()
-    return steps
+    return run_lockstep(opts, sim, n_frames, renderer=renderer, after_init=after_init)
 
 
 def _stats(steps, max_clones):
-    """per-frame worst differences; frames with the full window counted"""
+    """per-frame summary; frames with the full window"""
     rows = []
     for k, (a, b) in enumerate(steps):
-        assert a["x"].shape == b["x"].shape and a["P"].shape == b["P"].shape, k
-        for key in ("n_msckf", "n_slam", "n_slam_delayed"):
-            assert a["timing"][key] == b["timing"][key], (k, key, a["timing"][key], b["timing"][key])
-        p, c = _compare_feats(a["feats"], b["feats"])
-        rows.append((k, a["timing"]["n_clones"], a["timing"]["n_msckf"], p, c, _rel(a["x"], b["x"]), _rel(a["P"], b["P"])))
+        rows.append((k, a["timing"]["n_clones"], a["timing"]["n_msckf"], a["timing"]["n_slam"],
+                     a["timing"]["n_slam_delayed"]))
     full = [r for r in rows if r[1] >= max_clones + 1 and r[2] > 0]
     for r in rows:
-        print("frame %3d clones %3d msckf %5d  p %.1e chi2 %.1e x %.1e P %.1e" % r)
+        print("frame %3d clones %3d msckf %5d slam %3d delayed %3d" % r)
     return rows, full
 
 
-def _check(rows, full, min_full=3, p_tol=1e-9, c_tol=1e-11, x_tol=1e-10, P_tol=1e-10, max_flips=2):
+def _check(steps, full, min_full=3):
     assert len(full) >= min_full, "only %d lock-step frames with the full clone window" % len(full)
-    flips = [r for r in rows if r[3] > p_tol or r[4] > c_tol]
-    assert len(flips) <= max_flips, flips
-    for r in rows:
-        if r in flips:
-            # one float ulp of a predicted pixel flipped (test_gpu_parity.py docstring).  At these sizes the
-            # flipped pixel can sit in a delayed initialization, whose new landmark then enters x and P: one
-            # ulp of a ~500 px coordinate is 6e-5 px, 3e-7 in normalized units at f ~ 190, and along the
-            # depth of a d = 5 m point seen over a 0.1 m baseline d^2/b x 3e-7 ~ 7.5e-5 m.  Measured on
-            # MI355X (cfg3, frame 21, 172 MSCKF features): p 3.2e-6 m, chi2 1.5e-6, x 1.4e-7, P 5.1e-7.
-            assert r[3] < 1e-4 and r[4] < 1e-4 and r[5] < 1e-6 and r[6] < 1e-5, r
-        else:
-            assert r[5] < x_tol and r[6] < P_tol, r
+    worst = _check_lockstep(steps)
+    print("worst", worst)
 
 
 def test_lockstep_cfg1_mono_images():
@@ -98,7 +75,7 @@ def test_lockstep_cfg1_mono_images():
     rows, full = _stats(steps, opts.max_clone_size)
     assert steps[-1][0]["P"].shape[0] >= 15 + 1 + 14 + 6 * 11  # one camera's 14 calibration dims
     assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 0
-    _check(rows, full)
+    _check(steps, full)
 
 
 def test_lockstep_cfg3_baseline_size():
@@ -111,7 +88,7 @@ def test_lockstep_cfg3_baseline_size():
     steps = _lockstep(opts, sim, n, renderer=SceneRenderer(opts, device="cuda"))
     rows, full = _stats(steps, opts.max_clone_size)
     assert max(r[2] for r in rows) >= 100
-    _check(rows, full)
+    _check(steps, full)
 
 
 def test_lockstep_cfg4_baseline_size():
@@ -124,7 +101,7 @@ def test_lockstep_cfg4_baseline_size():
     rows, full = _stats(steps, opts.max_clone_size)
     assert max(r[2] for r in rows) == 800  # direct-to-staging tables, chunked build, tiled T GEMM, MFMA Gram
     assert max(a["timing"]["msckf_rows"] for a, _ in steps) >= 8192
-    _check(rows, full)
+    _check(steps, full)
 
 
 def test_lockstep_cfg5_baseline_size():
@@ -137,7 +114,7 @@ def test_lockstep_cfg5_baseline_size():
     rows, full = _stats(steps, opts.max_clone_size)
     assert max(r[2] for r in rows) == 1500
     assert steps[-1][0]["P"].shape[0] >= 15 + 24 + 1 + 56 + 6 * 31 + 20
-    _check(rows, full)
+    _check(steps, full)
 
 
 def _iros_anchors():
@@ -182,4 +159,4 @@ def test_lockstep_iros_2023_uvio():
     # 2 unfixed anchors x 5 appended after their initialization
     assert steps[-1][0]["P"].shape[0] >= 15 + 14 + 10 + 6 * 10
     assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 50
-    _check(rows, full)
+    _check(steps, full)

@@ -1,5 +1,5 @@
 """GPU parity on the BASELINE.json configs 3-5: the HIP path against the oracle in
-lock-step (tolerances and the float-flip rule as in test_gpu_parity.py) on streams shaped like
+lock-step (tolerances and the rounding-tie steering as in test_gpu_parity.py) on streams shaped like
 
   cfg3  configs/tum_vi            stereo equidistant (fisheye) 512x512, T_cam_imu calibration
   cfg4  configs/uzhfpv_outdoor_45 stereo equidistant 640x480, extrinsics not calibrated, sigma_px 1.5
@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from test_gpu_parity import _check_lockstep, _rel, _snap
+from test_gpu_parity import _check_lockstep, _rel, _snap, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -28,23 +28,10 @@ def _cfg(name):
 
 
 def _lockstep(opts, n_frames, anchors=False, **simkw):
-    import uvio_amd as U
-    from oracle import oracle as O
     from uvio_amd.sim import SimStream
     anc = [opts.anchors[i] for i in range(opts.n_anchors)] if anchors else None
     s = SimStream(opts, duration=n_frames / opts.track_frequency + 1.2, seed=5, anchors=anc, **simkw)
-    g, o = U.VioManager(opts), O.OracleManager(opts)
-    steps = []
-
-    def before(nf, t):
-        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
-
-    def after(nf, t):
-        steps.append((_snap(g), _snap(o)))
-
-    s.run([g, o], n_frames=n_frames, before_frame=before, on_frame=after)
-    g.close()
-    return steps
+    return run_lockstep(opts, s, n_frames)
 
 
 def test_lockstep_cfg3_tum_vi_fisheye():

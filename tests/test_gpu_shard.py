@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from test_gpu_parity import _check_lockstep, _rel, _snap
+from test_gpu_parity import _check_lockstep, _rel, _snap, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -39,17 +39,9 @@ def test_sharded_world1_rccl_lockstep():
     from uvio_amd.manager import shard_unique_id
     opts = _opts(U)
     s = _stream(opts)
-    g, o = U.VioManager(opts), O.OracleManager(opts)
+    g = U.VioManager(opts)
     g.enable_feature_sharding(0, 1, backend="rccl", unique_id=shard_unique_id(), min_features=1)
-    steps = []
-
-    def before(nf, t):
-        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
-
-    def after(nf, t):
-        steps.append((_snap(g), _snap(o)))
-
-    s.run([g, o], n_frames=N_FRAMES, before_frame=before, on_frame=after)
+    steps = run_lockstep(opts, s, N_FRAMES, mgr=g)
     g.close()
     assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 300
     _check_lockstep(steps)

@@ -116,18 +116,12 @@ def test_lockstep_images(euroc_yaml):
     from oracle import oracle as O
     opts, s, r = _setup(euroc_yaml, 30, init_max_features=200, max_msckf_in_update=200, max_slam_features=25,
                         max_slam_in_update=25, dt_slam_delay=1.0)
-    g, o = U.VioManager(opts), O.OracleManager(opts)
-    steps = []
     bad = [0]
 
-    def before(nf, t):
-        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
-
-    def after(nf, t):
+    def extra(g, o, a, b):
         bad[0] += _compare_tracks(g, o, [0, 1])[1]
-        steps.append((P._snap(g), P._snap(o)))
 
-    s.run([g, o], n_frames=30, before_frame=before, on_frame=after, renderer=r)
+    steps = P.run_lockstep(opts, s, 30, renderer=r, extra=extra)
     assert bad[0] == 0
     assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 0
     assert sum(a["timing"]["n_slam_delayed"] for a, _ in steps) > 0

@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from test_gpu_parity import _check_lockstep, _rel, _snap
+from test_gpu_parity import _check_lockstep, _rel, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -24,22 +24,9 @@ EUROC = os.path.join(ROOT, "configs", "euroc_mav", "estimator_config.yaml")
 
 
 def _lockstep(opts, sim, n, renderer=None, after_init=None):
-    import uvio_amd as U
-    from oracle import oracle as O
-    g, o = U.VioManager(opts), O.OracleManager(opts)
-    steps = []
-
-    def before(nf, t):
-        o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
-
-    def after(nf, t):
-        a, b = _snap(g), _snap(o)
+    def extra(g, o, a, b):
         a["active"], b["active"] = g.get_active_tracks(), o.get_active_tracks()
-        steps.append((a, b))
-
-    sim.run([g, o], n_frames=n, before_frame=before, on_frame=after, renderer=renderer, after_init=after_init)
-    g.close()
-    return steps
+    return run_lockstep(opts, sim, n, renderer=renderer, after_init=after_init, extra=extra)
 
 
 def _check_active(steps, min_tracks=20):

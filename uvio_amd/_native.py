@@ -130,6 +130,7 @@ SIGNATURES = [
     ("get_tracks", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(C.c_float), _I, _P(_I)]),
     ("get_pyramid", _I, [C.c_void_p, _I, _I, _P(_I), _P(_I), _P(C.c_uint8), _P(C.c_int16), C.c_size_t]),
     ("debug_last_msckf", _I, [C.c_void_p, _P(C.c_uint64), _P(_D), _P(_I), _P(_D), _I, _P(_I)]),
+    ("debug_frame_feats", _I, [C.c_void_p, _P(_I), _P(C.c_uint64), _P(_D), _P(_I), _P(_D), _I, _P(_I)]),
     ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("msckf_compressed_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("compress", _I, [_P(_D), _I, _I, _P(_D)]),

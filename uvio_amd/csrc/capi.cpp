@@ -285,6 +285,24 @@ int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *statu
   return 0;
 }
 
+int uvio_hp_debug_frame_feats(uvio_hp_t *h, int *kind, uint64_t *ids, double *pG, int *status, double *chi2, int cap,
+                              int *n) {
+  if (!h || !n) return UVIO_HP_E_ARG;
+  int k = 0;
+  for (const auto &kd : h->e->frame_feats_) {
+    if (k < cap) {
+      kind[k] = kd.first;
+      ids[k] = kd.second.id;
+      for (int j = 0; j < 3; j++) pG[3 * k + j] = kd.second.p_FinG[j];
+      status[k] = kd.second.status;
+      chi2[k] = kd.second.chi2;
+    }
+    k++;
+  }
+  *n = k;
+  return 0;
+}
+
 int uvio_hp_shard_unique_id(uint8_t id[128]) {
   if (!id) return UVIO_HP_E_ARG;
   std::string err;

@@ -313,6 +313,9 @@ class Engine {
   };
   std::vector<FeatDebug> last_msckf_;
   std::vector<FeatDebug> last_upd_;  // the last SLAM update / delayed initialization, per feature
+  // every updater's per-feature results of the current frame: (kind 0 MSCKF / 1 SLAM update / 2 delayed
+  // initialization, result), cleared when the frame's update stage begins (lock-step parity tests)
+  std::vector<std::pair<int, FeatDebug>> frame_feats_;
 
   // updater-level entry points (engine_api.cpp; include/uvio_hp.h "Updater-level boundary")
   enum ApiUpdater { API_MSCKF = 0, API_SLAM = 1, API_DELAYED = 2 };

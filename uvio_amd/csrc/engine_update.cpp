@@ -292,6 +292,7 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
                            double track_wait) {
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
+  frame_feats_.clear();
   timing_.tracking = secs(rT1, rT2);
   timing_.device_syncs = track_syncs;
   timing_.sync_wait = track_wait;
@@ -1022,6 +1023,7 @@ int Engine::msckf_update(std::vector<FeatP> &fv) {
     for (size_t i = 0; i < outs.size(); i++) {
       last_msckf_.push_back(FeatDebug{fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
                                       outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+      frame_feats_.push_back({0, last_msckf_.back()});
       fv[i]->to_delete = true;
       for (int k = 0; k < 3; k++) fv[i]->p_FinG[k] = outs[i].p_FinG[k], fv[i]->p_FinA[k] = outs[i].p_FinA[k];
       if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
@@ -1110,6 +1112,7 @@ int Engine::slam_update(std::vector<FeatP> &fv) {
     int acc = 0;
     for (size_t i = 0; i < outs.size(); i++) {
       last_upd_.push_back(FeatDebug{fv[i]->featid, {0.0, 0.0, 0.0}, outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+      frame_feats_.push_back({1, last_upd_.back()});
       fv[i]->to_delete = true;
       if (outs[i].status == 3) slam_.at(fv[i]->featid)->fail_count++;
       if (outs[i].status == 0) acc++;
@@ -1170,6 +1173,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     if (tri[i].status == 1 || tri[i].status == 2) {
       f->to_delete = true;
       last_upd_.push_back(FeatDebug{f->featid, {0.0, 0.0, 0.0}, tri[i].status, 0.0});
+      frame_feats_.push_back({2, FeatDebug{f->featid, {0.0, 0.0, 0.0}, 1, 0.0}});
       continue;
     }
     // anchor (host rule, identical to the kernel's) and triangulated position
@@ -1254,6 +1258,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     }
     last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,
                                   nup > 0 ? d_.dx_host[N0 + 3] : 0.0});
+    frame_feats_.push_back({2, last_upd_.back()});
     if (accepted) {
       slam_.insert({f->featid, lm});
     } else {

@@ -185,6 +185,7 @@ int Engine::msckf_update_sharded(std::vector<FeatP> &fv) {
       const FeatP &f = fv[lo + i];
       last_msckf_.push_back(FeatDebug{f->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
                                       outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+      frame_feats_.push_back({0, last_msckf_.back()});
       for (int k = 0; k < 3; k++) f->p_FinG[k] = outs[i].p_FinG[k], f->p_FinA[k] = outs[i].p_FinA[k];
     }
     for (auto &f : fv) f->to_delete = true;

@@ -383,6 +383,22 @@ class VioManager:
         k = n.value
         return ids[:k].copy(), pG[:k].copy(), st[:k].copy(), c2[:k].copy()
 
+    def debug_frame_feats(self):
+        """Per-feature results of every updater call of the last frame: (kind, ids, p_FinG, status, chi2);
+        kind 0 MSCKF update, 1 SLAM update, 2 delayed initialization."""
+        cap = 16384
+        kind = np.zeros(cap, dtype=np.int32)
+        ids = np.zeros(cap, dtype=np.uint64)
+        pG = np.zeros((cap, 3))
+        st = np.zeros(cap, dtype=np.int32)
+        c2 = np.zeros(cap)
+        n = C.c_int()
+        self._check(self._call("debug_frame_feats", self._h, kind.ctypes.data_as(C.POINTER(C.c_int)),
+                               ids.ctypes.data_as(C.POINTER(C.c_uint64)), _dp(pG), st.ctypes.data_as(C.POINTER(C.c_int)),
+                               _dp(c2), cap, C.byref(n)), "debug_frame_feats")
+        k = min(n.value, cap)
+        return kind[:k].copy(), ids[:k].copy(), pG[:k].copy(), st[:k].copy(), c2[:k].copy()
+
     def get_active_tracks(self):
         """VioManager::get_active_tracks: (time, {featid: p_FinG}, {featid: (u, v, depth)})."""
         cap = 16384

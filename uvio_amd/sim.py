@@ -278,10 +278,13 @@ class SimStream:
         ev.sort(key=lambda e: (e[1] + (0.0 if e[0] == "imu" else lag), order[e[0]]))
         return ev
 
-    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None, renderer=None):
+    def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None, renderer=None,
+            before_feed=None):
         """Drive one manager (or a list of managers in lock-step): initialize from ground truth at t0, then
         feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed,
-        after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init).  With a
+        after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init), before_feed(mgr)
+        right before each manager's camera feed (lock-step steering: the oracle, fed after the device, learns
+        the device's results of the same frame).  With a
         renderer (uvio_amd.render.SceneRenderer) the managers get images (feed_measurement_camera)
         instead of the simulated tracks."""
         mgrs = mgr if isinstance(mgr, (list, tuple)) else [mgr]
@@ -307,10 +310,14 @@ class SimStream:
                 if renderer is not None:
                     imgs = [renderer.render(k, *self.camera_pose(i, k), frame_seed=i).cpu().numpy() for k in range(self.K)]
                     for m in mgrs:
+                        if before_feed is not None:
+                            before_feed(m)
                         m.feed_measurement_camera(t, list(range(self.K)), imgs)
                 else:
                     fr = self.frames[i]
                     for m in mgrs:
+                        if before_feed is not None:
+                            before_feed(m)
                         m.feed_measurement_simulation(t, list(range(self.K)), fr)
                 nf += 1
                 if on_frame is not None:
