@@ -197,8 +197,16 @@ def pmc_files(workload):
     return [os.path.join("profiles", f) for f in names]
 
 
-def pmc_class_traffic(workload, kernels):
-    """(HBM bytes per launch of the kernel class, source file) from the newest PMC summary holding it."""
+# the kernels one timed "launch" of a class (one HIP-event pair around a launch chain, kprof.h) contains exactly
+# once: their PMC launch count is the class's group count
+CLASS_GROUP_KERNELS = {"feature": ["k_feature"], "chi2": ["k_chi2"], "gram": ["k_gram", "k_gram_mfma"],
+                       "ekf_update": ["k_ekf_fact", "k_info_cholZ"], "ldl": ["k_ekf_fact"], "lk": ["k_lk"],
+                       "pyramid": ["k_hist_multi"]}
+
+
+def pmc_class_traffic(workload, name, kernels):
+    """(HBM bytes per launch group of the kernel class, source file) from the newest PMC summary holding it:
+    the members' summed bytes over the number of groups (CLASS_GROUP_KERNELS)."""
     for path in pmc_files(workload):
         try:
             with open(os.path.join(ROOT, path)) as f:
@@ -206,11 +214,11 @@ def pmc_class_traffic(workload, kernels):
         except (OSError, KeyError, ValueError):
             continue
         hit = [n for n in kernels if n in k]
-        if not hit:
+        groups = sum(k[n]["launches"] for n in CLASS_GROUP_KERNELS.get(name, kernels[:1]) if n in k)
+        if not hit or groups == 0:
             continue
-        # per launch of the class: the members' bytes over the launches of the class's first member present
         tot = sum(k[n]["traffic"] * k[n]["launches"] for n in hit)
-        return tot / max(k[hit[0]]["launches"], 1), path
+        return tot / groups, path
     return None, None
 
 
@@ -281,7 +289,7 @@ def roofline_entry(name, st, wl):
         per = st["bytes"] / n
         achieved = per / avg / 1e9 if avg > 0 else 0.0
         peak, unit = HBM_PEAK_GBS, "GB/s"
-    traffic, src = pmc_class_traffic(wl, st["kernels"])
+    traffic, src = pmc_class_traffic(wl, name, st["kernels"])
     return {"kernel": name, "kernels": st["kernels"], "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak, "traffic": traffic, "traffic_source": src, "launches": st["launches"],
             "avg_launch_us": avg * 1e6, ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per,
@@ -301,8 +309,9 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
     ap.add_argument("--shard", action="store_true", help="feature sharding also at N = 1 (RCCL world of 1)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
-    ap.add_argument("--ktime-period", type=int, default=10,
-                    help="kernel-class event timing on every k-th frame of the timed region (0 = off)")
+    ap.add_argument("--ktime-period", type=int, default=None,
+                    help="kernel-class event timing on every k-th frame of the timed region (0 = off; default: every "
+                         "frame for --steps <= 50, else every 10th)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -320,6 +329,8 @@ def main():
         wl = "cfg2" if world == 1 else ("cfg4" if world <= 4 else "cfg5")
     if args.cpu_frames is None:
         args.cpu_frames = CPU_FRAMES[wl]
+    if args.ktime_period is None:
+        args.ktime_period = 1 if args.steps <= 50 else 10
     # stdout carries exactly the one JSON line: whatever the libraries print (RCCL's version banner at
     # communicator creation, ...) goes to stderr
     sys.stdout.flush()

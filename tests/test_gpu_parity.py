@@ -126,7 +126,7 @@ class Steps(list):
 STEER_MARGIN = 1e-10  # an explained disagreement: one cast within this relative distance of its rounding tie
 
 
-def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None, steer=True, mgr=None):
+def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None, steer=True, mgr=None, pre_frame=None):
     """Device and oracle on the same stream: before every frame the oracle adopts the device's state; right
     before its feed it gets the device's per-feature results of that frame (rounding-tie steering)."""
     import uvio_amd as U
@@ -137,6 +137,8 @@ def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None
 
     def before(nf, t):
         o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
+        if pre_frame is not None:
+            pre_frame(nf, t, g, o)
 
     def before_feed(m):
         if steer and m is o:
@@ -252,6 +254,33 @@ def test_lockstep_slam_parity(euroc_yaml):
     steps = _lockstep(opts, 30, spawn=80, frac_long=0.3)
     assert sum(a["timing"]["n_slam"] for a, _ in steps) > 0
     assert sum(a["timing"]["n_slam_delayed"] for a, _ in steps) > 0
+    _check_lockstep(steps)
+
+
+def test_out_of_order_frame_lockstep(euroc_yaml):
+    """VioManager.cpp:330-334: a camera frame older than the state is tracked into the feature database and
+    then dropped (here: E_ORDER).  Its measurements leave tracks out of time order in the database; the
+    later frames' selection / cleanup must still follow the reference's linear scans (the device's
+    MeasList falls back from its binary searches), in lock-step with the oracle."""
+    import uvio_amd as U
+    opts = U.load_options(euroc_yaml, max_msckf_in_update=100, max_slam_features=20, max_slam_in_update=10,
+                          dt_slam_delay=0.3)
+    n = 30
+    s = _sim(opts, n, spawn=80, frac_long=0.3)
+    cams = list(range(s.K))
+    hit = []
+
+    def stale(nf, t, g, o):
+        if nf in (12, 18):
+            i = int(np.argmin(np.abs(np.asarray(s.cam_t) - t)))
+            for m in (g, o):
+                with pytest.raises(RuntimeError, match="E_ORDER"):
+                    m.feed_measurement_simulation(s.cam_t[i - 3], cams, s.frames[i - 3])
+            hit.append(nf)
+
+    steps = run_lockstep(opts, s, n, pre_frame=stale)
+    assert hit == [12, 18]
+    assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 100
     _check_lockstep(steps)
 
 

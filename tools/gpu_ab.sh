@@ -9,9 +9,9 @@ for wl in "$@"; do
     # ABBA: the arm that runs first alternates, so an order effect hits both arms alike
     if [ $((i % 2)) = 1 ]; then
       timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
-      UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
+      UVIO_HP_AB_OLD=1 UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
     else
-      UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
+      UVIO_HP_AB_OLD=1 UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
       timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
     fi
   done

@@ -156,19 +156,25 @@ ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, _P(_D), C.c_size_t, C.c_void_p)
 EXPORTED = ["uvio_hp_" + s[0] for s in SIGNATURES]
 
 
-MISSING = set()  # entry points an overriding UVIO_HP_LIB (an older build in an A/B run) does not export
+MISSING = set()  # entry points an older build under UVIO_HP_AB_OLD=1 (A/B runs, tools/gpu_ab.sh) does not export
 
 
 def bind(lib, prefix, names=None):
+    """Bind the declared signatures; a missing entry point raises, except in an explicit A/B run against an
+    older build (UVIO_HP_AB_OLD=1 with UVIO_HP_LIB), where it is recorded in MISSING and reported."""
+    ab_old = os.environ.get("UVIO_HP_AB_OLD") == "1" and "UVIO_HP_LIB" in os.environ
     for name, res, args in SIGNATURES:
         if names is not None and name not in names:
             continue
-        if "UVIO_HP_LIB" in os.environ and prefix == "uvio_hp_" and not hasattr(lib, prefix + name):
+        if ab_old and prefix == "uvio_hp_" and not hasattr(lib, prefix + name):
             MISSING.add(name)
             continue
         f = getattr(lib, prefix + name)
         f.restype = res
         f.argtypes = args
+    if MISSING:
+        import sys
+        sys.stderr.write("uvio_amd: A/B library %s lacks %s\n" % (os.environ["UVIO_HP_LIB"], ", ".join(sorted(MISSING))))
     return lib
 
 

@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <unordered_map>
+#include <algorithm>
 #include <vector>
 
 #include "hp_common.h"
@@ -56,7 +57,9 @@ struct FeatMeas {
 // once the dead prefix outgrows the live part -- so the per-frame cleanup touches no measurement data.
 struct MeasList {
   std::vector<FeatMeas> v;
-  size_t b = 0;  // first live entry
+  size_t b = 0;         // first live entry
+  bool sorted = true;   // live entries in non-decreasing time (every in-order stream); the time searches
+                        // (contains / drop_through) fall back to the reference's linear scans otherwise
   using iterator = std::vector<FeatMeas>::iterator;
   using const_iterator = std::vector<FeatMeas>::const_iterator;
   size_t size() const { return v.size() - b; }
@@ -70,13 +73,43 @@ struct MeasList {
   iterator end() { return v.end(); }
   const_iterator begin() const { return v.begin() + (std::ptrdiff_t)b; }
   const_iterator end() const { return v.end(); }
-  void push_back(const FeatMeas &x) { v.push_back(x); }
+  void push_back(const FeatMeas &x) {
+    if (v.size() > b && x.t < v.back().t) sorted = false;
+    v.push_back(x);
+  }
+  // a live entry at time t (FeatureDatabase::features_containing's std::find, FeatureDatabase.cpp:169-208)
+  bool contains(double t) const {
+    if (sorted) {
+      auto it = std::lower_bound(begin(), end(), t, [](const FeatMeas &x, double tt) { return x.t < tt; });
+      return it != end() && it->t == t;
+    }
+    for (auto it = begin(); it != end(); ++it)
+      if (it->t == t) return true;
+    return false;
+  }
+  // remove every live entry at or before t (Feature::clean_older_measurements, Feature.cpp:85-104)
+  void drop_through(double t) {
+    if (sorted) {
+      auto it = std::upper_bound(begin(), end(), t, [](double tt, const FeatMeas &x) { return tt < x.t; });
+      drop_front((size_t)(it - begin()));
+      return;
+    }
+    size_t w = b;
+    for (size_t i = b; i < v.size(); i++)
+      if (!(v[i].t <= t)) v[w++] = v[i];
+    v.resize(w);
+    if (v.size() == b) clear();
+  }
+  void clear() {
+    v.clear();
+    b = 0;
+    sorted = true;
+  }
   iterator erase(iterator first, iterator last) { return v.erase(first, last); }
   void drop_front(size_t k) {  // remove the k oldest live entries
     b += k;
     if (b == v.size()) {
-      v.clear();
-      b = 0;
+      clear();
     } else if (b > 32 && 2 * b > v.size()) {
       v.erase(v.begin(), v.begin() + (std::ptrdiff_t)b);
       b = 0;
@@ -198,6 +231,7 @@ struct DeviceBufs {
   int *hidx_pre = nullptr, *hidx_pre_h = nullptr;
   std::vector<int> pre_hidx;  // columns of the pending prefactor (empty: none)
   int pre_N = -1;
+  long long pre_epoch = -1;  // Engine::p_epoch_ when the prefactor was enqueued
 };
 
 class Engine {
@@ -255,6 +289,10 @@ class Engine {
   CamParams cams_[UVIO_HP_MAX_CAMS];
   std::vector<VarP> vars_;
   int N_ = 0;
+  // bumped by every write of P (propagation, clone, marginalization, EKF updates, initialization, uploads):
+  // a side-stream prefactor is only used when P is unchanged since it was enqueued
+  long long p_epoch_ = 0;
+  double early_prop_s_ = 0.0;  // host time of a propagation run inside the tracker's wait (feed_camera)
   // ---- propagator ----
   std::mutex imu_mtx_;
   std::vector<ImuSample> imu_data_;

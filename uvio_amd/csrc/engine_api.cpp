@@ -45,6 +45,7 @@ int Engine::api_set_state(const double *val, const double *fej, int len, const d
       for (int i = 0; i < 8; i++) cams_[c.first].v[i] = c.second->val[i];
   HP_HIP(hipMemcpy2DAsync(d_.P, sizeof(double) * d_.ldp, P, sizeof(double) * ld, sizeof(double) * N, N,
                           hipMemcpyHostToDevice, d_.stream));
+  ++p_epoch_;
   dev_sync();
   return 0;
 }

@@ -832,7 +832,13 @@ int Engine::zupt_try_update(double timestamp) {
   for (int j = 0; j < m; j++) {
     double d = S[(size_t)j * m + j];
     for (int k = 0; k < j; k++) d -= L[(size_t)j * m + k] * L[(size_t)j * m + k];
-    if (!(d > 0)) return 0;
+    if (!(d > 0)) {
+      // S not positive definite (the reference's LLT result is undefined there): take the reference's
+      // rejection path, which also resets the ZUPT bookkeeping (UpdaterZeroVelocity.cpp:240-245)
+      last_zupt_state_timestamp_ = 0.0;
+      last_zupt_count_ = 0;
+      return 0;
+    }
     L[(size_t)j * m + j] = std::sqrt(d);
     for (int i = j + 1; i < m; i++) {
       double v = S[(size_t)i * m + j];

@@ -74,22 +74,16 @@ void MeasList::keep_if_valid(const std::vector<double> &valid) {
   for (size_t i = b; i < v.size(); i++)
     if (std::binary_search(valid.begin(), valid.end(), v[i].t)) v[w++] = v[i];
   v.resize(w);
-  if (v.size() == b) {
-    v.clear();
-    b = 0;
-  }
+  if (v.size() == b) clear();
 }
 // Feature::clean_old_measurements (Feature.cpp:37-60): keep the measurements at the given (sorted) times
 void Feature::clean_old_measurements(const std::vector<double> &valid) {
   for (auto &c : tracks) c.m.keep_if_valid(valid);
 }
 // Feature::clean_older_measurements (Feature.cpp:85-104): drop every measurement at or before t.  A camera's
-// measurements are appended in time order, so they form a prefix, found by binary search.
+// measurements of an in-order stream form a prefix, found by binary search (MeasList::drop_through).
 void Feature::clean_older_measurements(double t) {
-  for (auto &c : tracks) {
-    auto it = std::upper_bound(c.m.begin(), c.m.end(), t, [](double tt, const FeatMeas &x) { return tt < x.t; });
-    c.m.drop_front((size_t)(it - c.m.begin()));
-  }
+  for (auto &c : tracks) c.m.drop_through(t);
 }
 
 static VarP mk(VKind k, int size, int vlen) { return std::make_shared<Var>(k, size, vlen); }
@@ -343,6 +337,7 @@ void Engine::alloc_device() {
 void Engine::upload_P_full(const std::vector<double> &Ph, int N) {
   HP_HIP(hipMemcpy2DAsync(d_.P, sizeof(double) * d_.ldp, Ph.data(), sizeof(double) * N, sizeof(double) * N, N,
                           hipMemcpyHostToDevice, d_.stream));
+  ++p_epoch_;
   dev_sync();
 }
 void Engine::download_P(std::vector<double> &Ph) {
@@ -418,7 +413,7 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
     int bound;
   } info[KC_COUNT] = {
       {"feature", "k_feature", 1},
-      {"chi2", "k_gemm_HPg,k_gemm_HPg_tiled,k_chi2", 1},
+      {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
       {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm,k_info_cholZ,k_trinv16,"
                      "k_trsm_lt,k_info_P",
@@ -470,6 +465,7 @@ void Engine::cov_propagate(int s0, int p, const std::vector<int> &iold, const st
   const int *drows = rows ? stage(rows->data(), rows->size()) : nullptr;
   stage_flush();
   launch_cov_propagate(d_.stream, d_.P, d_.ldp, N_, s0, p, diold, q, dPhi, dQ, d_.T, drows);
+  ++p_epoch_;
 }
 
 void Engine::check_neg_diag(const char *who) {
@@ -492,6 +488,7 @@ VarP Engine::clone_imu_pose(const double *dnc, bool do_dt, const double *staged)
     }
   }
   launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, ddnc, do_dt ? 1 : 0);
+  ++p_epoch_;
   VarP pose = mk(V_POSE, 6, 7);
   for (int k = 0; k < 7; k++) pose->val[k] = imu_->val[k], pose->fej[k] = imu_->fej[k];
   pose->id = N_;
@@ -505,6 +502,7 @@ void Engine::marginalize(const VarP &m) {
   int m0 = m->id, ms = m->size;
   launch_marginalize(d_.stream, d_.P, d_.P2, d_.ldp, N_, m0, ms);
   std::swap(d_.P, d_.P2);
+  ++p_epoch_;
   std::vector<VarP> keep;
   for (auto &v : vars_)
     if (v != m) {
@@ -552,6 +550,7 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
     d_.ekf.ldt = ldh;
     launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, Hdev, ldh, r, n, hidx_dev, resdev, res_stride, sigma2, d_.ekf);
     d_.ekf.Tall = nullptr;
+    ++p_epoch_;
   }
   kprof_.credit(KC_EKF, ekf_flops(N_, n, r), ekf_bytes(N_, n, r));
   read_dx("EKFUpdate");
@@ -561,7 +560,9 @@ void Engine::ekf_update_rows(const double *Hdev, int ldh, int r, int n, const st
 // EKF update from the Gram partials of a stacked batch (compressed path, m > n)
 void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, double sigma2,
                              const std::function<bool()> &apply, const int *gate, const double *partials) {
-  const bool pre = d_.pre_N == N_ && d_.pre_hidx == hidx;  // the prefactor of these columns is in flight
+  // the prefactor of these columns is in flight and P is unchanged since it was enqueued
+  const bool inflight = d_.pre_N >= 0;
+  const bool pre = inflight && d_.pre_N == N_ && d_.pre_hidx == hidx && d_.pre_epoch == p_epoch_;
   d_.pre_hidx.clear();
   d_.pre_N = -1;
   d_.ekf.gate = gate;
@@ -571,11 +572,14 @@ void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, doubl
     KScope ks(&kprof_, KC_EKF);
     launch_ekf_info_post(d_.stream, d_.P, d_.ldp, N_, G, nch, n, sigma2, d_.R, d_.ekf);
   } else {
+    // a stale prefactor still writes the factor scratch on the side stream: order the full update after it
+    if (inflight) HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
     const int *dh = stage(hidx.data(), (size_t)n);
     stage_flush();
     KScope ks(&kprof_, KC_EKF);
     launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, G, nch, n, dh, sigma2, d_.R, d_.ekf);
   }
+  ++p_epoch_;
   // the timed launches: without the side-stream prefactor (Cholesky of P_II, n^3 / 3, and V, N n^2) when it ran
   const double fl = ekf_flops(N_, n, n) - (pre ? (double)n * n * n / 3.0 + (double)N_ * n * n : 0.0);
   kprof_.credit(KC_EKF, fl, ekf_bytes(N_, n, n));
@@ -599,6 +603,7 @@ void Engine::info_prefactor(const std::vector<int> &hidx) {
   HP_HIP(hipEventRecord(d_.ev_aux_out, d_.aux));
   d_.pre_hidx = hidx;
   d_.pre_N = N_;
+  d_.pre_epoch = p_epoch_;
 }
 
 // StateHelper::set_initial_covariance (StateHelper.cpp:199-223).  Start-up only (initialize_with_gt,

@@ -1,6 +1,7 @@
 // Engine: per-frame manager logic (VioManager.cpp:166-651, UVioManager.cpp:61-344), feature database
 // (FeatureDatabase.cpp:59-263) and the update orchestration (UpdaterMSCKF.cpp:58-295,
 // UpdaterSLAM.cpp:61-647, UpdaterUWB.cpp:53-90) over the device kernels.
+#include <exception>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -168,6 +169,7 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
                             const float *uv) {
   stage_ = "feed_simulation";
   auto rT1 = clk::now();
+  early_prop_s_ = 0.0;
   frame_begin();
   std::vector<int> camids, cam_of;
   for (int i = 0; i < ncam; i++) {
@@ -257,14 +259,24 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
   // tracking and the propagation (no zero-velocity check, no UWB range before t), the host computes it
   // while the frame's LK + RANSAC are on the device and enqueues its launches behind them: the same
   // launches in the same stream order, the host's share hidden under the tracker's wait.
+  // An exception of the early propagation is held until the tracker has finished its frame (results
+  // consumed, buffers flipped) and rethrown then; its host time is booked as propagation, not tracking.
   bool early = false;
   int early_rc = 0;
+  std::exception_ptr early_exc;
   std::function<void()> in_flight;
+  early_prop_s_ = 0.0;
   if (propagation_can_precede_tracking(t))
     in_flight = [&, t]() {
       HPROF("prop");
       early = true;
-      early_rc = propagate_and_clone(t);
+      auto p0 = clk::now();
+      try {
+        early_rc = propagate_and_clone(t);
+      } catch (...) {
+        early_exc = std::current_exception();
+      }
+      early_prop_s_ = secs(p0, clk::now());
     };
   {
     HPROF("track.feed");
@@ -275,6 +287,7 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
         },
         std::move(in_flight));
   }
+  if (early_exc) std::rethrow_exception(early_exc);
   if (early && early_rc) return early_rc;
   return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait);
 }
@@ -293,7 +306,7 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
   frame_feats_.clear();
-  timing_.tracking = secs(rT1, rT2);
+  timing_.tracking = secs(rT1, rT2) - early_prop_s_;
   timing_.device_syncs = track_syncs;
   timing_.sync_wait = track_wait;
   if (!is_initialized_) return UVIO_HP_E_STATE;
@@ -359,7 +372,8 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   if (o_.record_timing >= 2) dev_sync();
   auto rT3 = clk::now();
   timing_.timestamp = t;
-  timing_.propagation = secs(rT2, rT3);
+  timing_.propagation = secs(rT2, rT3) + early_prop_s_;  // + the propagation run during the tracking wait
+  early_prop_s_ = 0.0;
   timing_.n_clones = (int)clones_.size();
   timing_.cov_dim = N_;
   if ((int)clones_.size() < std::min(o_.max_clone_size, 5)) return 0;
@@ -394,9 +408,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
         }
         if (do_marg)
           for (auto &p : f.tracks) {
-            // time-ordered: binary search for the marginalized clone's time
-            auto it = std::lower_bound(p.m.begin(), p.m.end(), mt, [](const FeatMeas &x, double tt) { return x.t < tt; });
-            has = it != p.m.end() && it->t == mt;
+            has = p.m.contains(mt);  // binary search on an in-order track
             if (has) break;
           }
         all[i].second = (uint8_t)((newer ? 0 : 1) | (has ? 2 : 0));
@@ -1223,6 +1235,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     const int N0 = N_;
     launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, nullptr, s2, d_.ekf, d_.fout,
                            nullptr, d_.ekf.dx + N0 + 5);
+    ++p_epoch_;
     const double *resinit = d_.dx_host + N0 + 5;
     bool accepted = false;
     const int nup = 2 * b.feats[0].nmeas - 3;
@@ -1516,6 +1529,7 @@ int Engine::uwb_update_single(size_t anchor_id, double range) {
   double chi2 = res * res / Sval;
   if (chi2 > o_.uwb_chi2_multipler * chi2_table_[1]) return 0;
   launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, dH + n, 1, d_.ekf);
+  ++p_epoch_;
   read_dx("UWB EKFUpdate");
   apply_dx(d_.dx_host);
   return 1;
