@@ -151,6 +151,7 @@ typedef struct {
   int device_syncs;
   double sync_wait;
   int zupt;  /* 1: this frame ended in a zero-velocity update (UpdaterZeroVelocity::try_update accepted) */
+  int n_anchor_change;  /* SLAM landmarks re-anchored by UpdaterSLAM::change_anchors this frame (UpdaterSLAM.cpp:481-503) */
 } uvio_hp_timing_t;
 
 /* Live device timing of the kernel classes the benchmark prices against a roofline (HIP events on the

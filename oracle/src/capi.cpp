@@ -218,7 +218,10 @@ int orc_propagate_and_clone(orc_handle *h, double t) {
   if (!h->m.prop.propagate_and_clone(h->m.state, t, &st)) return st ? st : UVIO_HP_E_NUMERIC;
   return 0;
 }
-int orc_slam_change_anchors(orc_handle *h) { return h->m.slam.change_anchors(h->m.state); }
+int orc_slam_change_anchors(orc_handle *h) {
+  int r = h->m.slam.change_anchors(h->m.state);
+  return r < 0 ? r : 0;
+}
 int orc_marginalize_slam(orc_handle *h) {
   StateHelper::marginalize_slam(h->m.state);
   return 0;

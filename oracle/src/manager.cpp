@@ -312,6 +312,7 @@ int Manager::do_feature_propagate_update(double t, const std::vector<int> &camid
   db.cleanup();
   rc = slam.change_anchors(state);
   if (rc < 0) return rc;
+  timing.n_anchor_change = rc;
   if ((int)state.clones.size() > state.opt.max_clone_size) db.cleanup_measurements(state.margtimestep());
   StateHelper::marginalize_old_clone(state);
   auto rT7 = clk::now();

@@ -728,6 +728,7 @@ int UpdaterSLAM::update(State &s, std::vector<FeatP> &feature_vec) {
 // UpdaterSLAM.cpp:481-503
 int UpdaterSLAM::change_anchors(State &s) {
   if ((int)s.clones.size() <= s.opt.max_clone_size) return 0;
+  int changed = 0;
   double marg_timestep = s.margtimestep();
   for (auto &f : s.features_SLAM) {
     if (f.second->rep == GLOBAL_3D || f.second->rep == GLOBAL_FULL_INVERSE_DEPTH) continue;
@@ -735,9 +736,10 @@ int UpdaterSLAM::change_anchors(State &s) {
     if (f.second->anchor_time == marg_timestep) {
       int r = perform_anchor_change(s, f.second, s.timestamp, f.second->anchor_cam);
       if (r < 0) return r;
+      changed++;
     }
   }
-  return 0;
+  return changed;
 }
 
 // UpdaterSLAM.cpp:505-647

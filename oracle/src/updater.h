@@ -89,7 +89,7 @@ struct UpdaterSLAM {
   UpdaterSLAM(const uvio_hp_options_t &o);
   int delayed_init(State &s, std::vector<FeatP> &feature_vec);
   int update(State &s, std::vector<FeatP> &feature_vec);
-  int change_anchors(State &s);
+  int change_anchors(State &s);  // landmarks re-anchored (>= 0), < 0 on a numeric error
   int perform_anchor_change(State &s, VarP landmark, double new_anchor_timestamp, size_t new_cam_id);
 };
 

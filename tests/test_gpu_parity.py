@@ -219,6 +219,7 @@ def _check_lockstep(steps, max_events=None):
         assert a["timing"]["n_msckf"] == b["timing"]["n_msckf"]
         assert a["timing"]["n_slam"] == b["timing"]["n_slam"]
         assert a["timing"]["n_slam_delayed"] == b["timing"]["n_slam_delayed"]
+        assert a["timing"]["n_anchor_change"] == b["timing"]["n_anchor_change"]
         p, c = _compare_feats(a["feats"], b["feats"])
         p2, c2 = _compare_frame(a["frame"], b["frame"])
         x, P = _rel(a["x"], b["x"]), _rel(a["P"], b["P"])
@@ -254,6 +255,8 @@ def test_lockstep_slam_parity(euroc_yaml):
     steps = _lockstep(opts, 30, spawn=80, frac_long=0.3)
     assert sum(a["timing"]["n_slam"] for a, _ in steps) > 0
     assert sum(a["timing"]["n_slam_delayed"] for a, _ in steps) > 0
+    # UpdaterSLAM::change_anchors (UpdaterSLAM.cpp:481-647) re-anchored landmarks on both sides
+    assert sum(a["timing"]["n_anchor_change"] for a, _ in steps) > 0
     _check_lockstep(steps)
 
 

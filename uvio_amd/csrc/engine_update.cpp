@@ -1459,6 +1459,7 @@ int Engine::slam_change_anchors() {
       b_phi.push_back(rowv);
     }
     lm->anchor_time = timestamp_;
+    timing_.n_anchor_change++;
     lm->set_xyz(p_new, false);
     lm->set_xyz(p_new_fej, true);
   }
