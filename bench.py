@@ -16,18 +16,20 @@ frames); the line reports the effective warm-up and whether steady state was rea
 Multi-GPU (--gpus N > 1; launched either by torch.distributed.run, or by this script itself, which then
 spawns N worker processes before any GPU call): the north star's feature-sharded update --
 every rank runs the same stream and each MSCKF update's per-feature linearization, chi2 gate and Gram are
-split across the ranks with one RCCL all-reduce; cfg4 (UZH-FPV, 25 clones x 800 features) at N <= 4 and
-cfg5 (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value = frames of
-the one stream / wall time).  --replicas instead runs one independent estimator per GPU (weak scaling).
+split across the ranks with one RCCL all-reduce; cfg4t (UZH-FPV, 25 clones x 800 features per update) at
+N <= 4 and cfg5t (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value =
+frames of the one stream / wall time).  --replicas instead runs one independent estimator per GPU (weak).
 
 Other workloads (--workload, SURVEY.md §8 cfg 1-5; parity-test cases and stress lines):
   cfg1  EuRoC MH_01-shaped MONO 752x480 images (configs/euroc_mav, max_cameras 1), 11 clones, <= 100 MSCKF
   cfg3  TUM-VI room1-shaped stereo fisheye 512x512 images (configs/tum_vi), 20 clones, 400 tracks per
         camera, <= 400 MSCKF + 50 SLAM (LDS-tiled KLT stress)
-  cfg4  UZH-FPV outdoor_45-shaped stereo fisheye rig (configs/uzhfpv_outdoor_45), 25 clones, 800 MSCKF
-        features per update, each seen in all 26 clones x 2 cameras (TrackSIM feed: the backend stress case)
-  cfg5  rpng_sim 4-camera rig + 6 UWB anchors (configs/rpng_sim_uwb), IMU intrinsics + g-sensitivity
-        calibrated, 30 clones, 1500 MSCKF features per update (each in one camera), UWB ranges at 10 Hz
+  cfg4  UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images (configs/uzhfpv_outdoor_45), 25 clones,
+        800 tracks, <= 800 MSCKF + 50 SLAM
+  cfg5  rpng_sim 4-camera 752x480 images, each camera tracked on its own (configs/rpng_sim_uwb), + 6 UWB
+        anchors at 10 Hz, IMU intrinsics + g-sensitivity calibrated, 30 clones, 1500 tracks
+  cfg4t / cfg5t  the backend stress at BASELINE's feature counts: TrackSIM feed with 800 / 1500 MSCKF features
+        per update, each seen in every clone (26 clones x 2 cameras / 31 clones x 1 of 4 cameras)
 
 roofline: live HIP-event timing of the kernel classes (uvio_hp_set_kernel_timing) over the timed region;
 achieved = algorithmic FLOPs (FP64 classes) or bytes (tracker classes) of the class's launches (SURVEY.md
@@ -70,20 +72,34 @@ WORKLOADS = {
                   max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
              dict(spawn=4),
              "cfg3 TUM-VI room1-shaped stereo fisheye 512x512 images, 20 clones, 400 tracks/cam, <=400 MSCKF + 50 SLAM"),
-    "cfg4": ("uzhfpv_outdoor_45", "tracks",
-             dict(max_clone_size=25, max_msckf_in_update=800, max_slam_features=50, max_slam_in_update=25,
-                  dt_slam_delay=1.0),
-             dict(spawn=800, frac_lost=0.0, frac_long=0.02),
-             "cfg4 UZH-FPV outdoor_45-shaped stereo fisheye 640x480 tracks, 25 clones, 800 MSCKF feats x 52 meas"),
-    "cfg5": ("rpng_sim_uwb", "tracks",
-             dict(max_clone_size=30, max_msckf_in_update=1500, max_slam_features=50, max_slam_in_update=25,
-                  dt_slam_delay=1.0),
-             dict(spawn=1500, frac_lost=0.0, frac_long=0.02, uwb=True),
-             "cfg5 rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
+    "cfg4": ("uzhfpv_outdoor_45", "images",
+             dict(max_clone_size=25, init_max_features=800, num_pts=400, max_msckf_in_update=800, max_slam_features=50,
+                  max_slam_in_update=25, dt_slam_delay=1.0),
+             dict(spawn=4),
+             "cfg4 UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images, 25 clones, 800 tracks (400/cam), "
+             "<=800 MSCKF + 50 SLAM"),
+    "cfg5": ("rpng_sim_uwb", "images",
+             dict(max_clone_size=30, init_max_features=1500, num_pts=375, max_msckf_in_update=1500,
+                  max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
+             dict(spawn=4, uwb=True),
+             "cfg5 rpng_sim 4-cam 752x480 images (each camera tracked on its own) + 6 UWB anchors (2 fixed), IMU "
+             "intrinsics, 30 clones, 1500 tracks (375/cam), <=1500 MSCKF + 50 SLAM"),
+    # the backend stress at the BASELINE feature counts: every MSCKF update holds 800 / 1500 features seen in
+    # every clone (TrackSIM feed); the feature-sharded multi-GPU lines run these
+    "cfg4t": ("uzhfpv_outdoor_45", "tracks",
+              dict(max_clone_size=25, max_msckf_in_update=800, max_slam_features=50, max_slam_in_update=25,
+                   dt_slam_delay=1.0),
+              dict(spawn=800, frac_lost=0.0, frac_long=0.02),
+              "cfg4t UZH-FPV outdoor_45-shaped stereo fisheye 640x480 tracks, 25 clones, 800 MSCKF feats x 52 meas"),
+    "cfg5t": ("rpng_sim_uwb", "tracks",
+              dict(max_clone_size=30, max_msckf_in_update=1500, max_slam_features=50, max_slam_in_update=25,
+                   dt_slam_delay=1.0),
+              dict(spawn=1500, frac_lost=0.0, frac_long=0.02, uwb=True),
+              "cfg5t rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
 }
 
 # oracle frames in the cpu_baseline sample (~10-30 s of single-core CPU work per workload)
-CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg3": 60, "cfg4": 3, "cfg5": 2}
+CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg3": 60, "cfg4": 20, "cfg5": 10, "cfg4t": 3, "cfg5t": 2}
 
 
 def workload_options(U, name):
@@ -190,10 +206,14 @@ class Driver:
                 return t
 
 
-# committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py), newest first
+# committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py), newest first.  cfg4 / cfg5 were
+# TrackSIM workloads before r03b (now cfg4t / cfg5t): their older summaries do not describe the image workloads
+PMC_MIN_TAG = {"cfg4": "r03b", "cfg5": "r03b"}
+
+
 def pmc_files(workload):
-    names = sorted((f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc_traffic_%s.json" % workload)),
-                   reverse=True)
+    names = sorted((f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_pmc_traffic_%s.json" % workload)
+                    and f >= PMC_MIN_TAG.get(workload, "")), reverse=True)
     return [os.path.join("profiles", f) for f in names]
 
 
@@ -305,7 +325,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=None,
                     help="timed oracle frames for cpu_baseline (0 = skip; default: ~10-30 s of CPU work per workload)")
     ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto",
-                    help="auto: cfg2 at 1 GPU, feature-sharded cfg4 at 2-4 GPUs, cfg5 beyond")
+                    help="auto: cfg2 at 1 GPU, feature-sharded cfg4t at 2-4 GPUs, cfg5t beyond")
     ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
     ap.add_argument("--shard", action="store_true", help="feature sharding also at N = 1 (RCCL world of 1)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
@@ -326,7 +346,7 @@ def main():
     shard = (world > 1 and not args.replicas) or args.shard
     wl = args.workload
     if wl == "auto":
-        wl = "cfg2" if world == 1 else ("cfg4" if world <= 4 else "cfg5")
+        wl = "cfg2" if world == 1 else ("cfg4t" if world <= 4 else "cfg5t")
     if args.cpu_frames is None:
         args.cpu_frames = CPU_FRAMES[wl]
     if args.ktime_period is None:

@@ -65,6 +65,23 @@ def test_lockstep_cfg5_four_cameras_uwb_imu_intrinsics():
     _check_lockstep(steps)
 
 
+def test_lockstep_images_cfg5_four_cameras():
+    """The full image path on the 4-camera rig (each camera tracked on its own, batched on the device) with
+    UWB ranges and IMU intrinsics: track -> propagate -> MSCKF / SLAM / delayed init / UWB, lock-step."""
+    import uvio_amd as U
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(_cfg("rpng_sim_uwb"), init_max_features=600, max_msckf_in_update=150, max_slam_features=20,
+                          max_slam_in_update=10, dt_slam_delay=0.5, min_dist_to_use_uwb=0.05)
+    anc = [opts.anchors[i] for i in range(opts.n_anchors)]
+    n = 24
+    s = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, anchors=anc, spawn=4)
+    steps = run_lockstep(opts, s, n, renderer=SceneRenderer(opts, device="cuda"))
+    assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 100
+    assert sum(a["timing"]["n_slam_delayed"] for a, _ in steps) > 0
+    _check_lockstep(steps)
+
+
 def test_cfg5_long_run_matches_oracle_counts():
     """cfg5 shape past the clone-window fill (max_clones 30) with SLAM promotion and UWB: both run on their
     own; the update sets must agree frame by frame while the states stay close."""

@@ -278,7 +278,9 @@ def test_out_of_order_frame_lockstep(euroc_yaml):
             i = int(np.argmin(np.abs(np.asarray(s.cam_t) - t)))
             for m in (g, o):
                 with pytest.raises(RuntimeError, match="E_ORDER"):
-                    m.feed_measurement_simulation(s.cam_t[i - 3], cams, s.frames[i - 3])
+                    # between two earlier frames: no clone has this time, so the stale measurements only
+                    # break the tracks' time order (duplicate clone times would be a different case)
+                    m.feed_measurement_simulation(0.5 * (s.cam_t[i - 3] + s.cam_t[i - 4]), cams, s.frames[i - 3])
             hit.append(nf)
 
     steps = run_lockstep(opts, s, n, pre_frame=stale)

@@ -90,6 +90,41 @@ def test_tracks_bit_exact(euroc_yaml, stereo):
     assert bad == 0, (bad, total)
 
 
+def test_tracks_bit_exact_four_cameras():
+    """The 4-camera rpng_sim rig (configs/rpng_sim_uwb, use_stereo 0: each camera tracked on its own,
+    TrackKLT.cpp:85-89) on rendered 752x480 frames, one camera masked: every camera's ids and uv equal
+    the oracle's after every frame.  The device runs the cameras' detections and temporal matchings as
+    one batch; the ids follow the cameras' order, as in the oracle's serial loop."""
+    import uvio_amd as U
+    from oracle import oracle as O
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    cfg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "rpng_sim_uwb",
+                       "estimator_config.yaml")
+    opts = U.load_options(cfg, init_max_features=800)
+    assert opts.num_cameras == 4 and not opts.use_stereo
+    n = 16
+    s = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=10)
+    r = SceneRenderer(opts, device="cuda")
+    g, o = U.VioManager(opts), O.OracleManager(opts)
+    cams = [0, 1, 2, 3]
+    mask = np.zeros((opts.cams[2].height, opts.cams[2].width), dtype=np.uint8)
+    mask[:120, :] = 255
+    masks = [None, None, mask, None]
+    total = bad = 0
+    per_cam = np.zeros(4, dtype=int)
+    for i, t, imgs in _frames(s, r, cams, n):
+        g.feed_measurement_camera(t, cams, imgs, masks=masks, allow_uninit=True)
+        o.feed_measurement_camera(t, cams, imgs, masks=masks, allow_uninit=True)
+        nt, b = _compare_tracks(g, o, cams)
+        total += nt
+        bad += b
+        for c in cams:
+            per_cam[c] += len(o.get_tracks(c)[0])
+    assert np.all(per_cam > n * 40), per_cam  # every camera keeps tracks
+    assert bad == 0, (bad, total)
+
+
 def test_tracks_mono_masked(euroc_yaml):
     """Monocular feed with a user mask (TrackKLT mask path: kept points, grid cells, griding)."""
     import uvio_amd as U

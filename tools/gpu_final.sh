@@ -8,7 +8,7 @@ cd $R && mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg2_bench.json 2> $O/cfg2.err
-for wl in cfg3 cfg4 cfg5; do
+for wl in cfg3 cfg4 cfg5 cfg4t cfg5t; do
   timeout -k 10 400 python -u bench.py --workload $wl > $O/${TAG}_${wl}_bench.json 2> $O/$wl.err
 done
 export TMPDIR=/tmp

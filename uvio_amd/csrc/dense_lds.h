@@ -124,6 +124,33 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 // the tiles of one row block, or the tile pairs of one row chunk -- land on the same XCD and share the
 // operand rows it has cached instead of each XCD fetching them again.  Only placement changes: every work
 // index is computed exactly as before.
+__device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Accumulate one 16x16 tile over k in [0, kend): acc += sum_k A(r16, k) B(k, r16) with the operands fetched
+// through the callables (k = 4 s + kq); the loads of eight k-slabs are issued before their MFMAs, so a
+// chunk costs one memory round trip.  (32-slab chunks measured slower in k_ekf_MS / k_ekf_WP: 24.4 / 10.3
+// against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
+template <class LA, class LB>
+__device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
+  constexpr int U = 8;
+  for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
+    double a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int k = k0 + 4 * u + kq;
+      const bool in = k < kend;
+      a[u] = in ? la(k) : 0.0;
+      b[u] = in ? lb(k) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (k0 + 4 * u < kend) acc = mfma4(a[u], b[u], acc);
+  }
+  return acc;
+}
+
 __device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, x = orig % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;

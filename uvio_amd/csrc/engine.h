@@ -232,7 +232,17 @@ struct DeviceBufs {
   std::vector<int> pre_hidx;  // columns of the pending prefactor (empty: none)
   int pre_N = -1;
   long long pre_epoch = -1;  // Engine::p_epoch_ when the prefactor was enqueued
+  // delayed-initialization chain (Engine::slam_delayed_init): per candidate one region of chain_stride doubles
+  // [dx (N) | chi2, accepted | init residual (3) | accepted, negative diagonals], chain_k candidates per chain,
+  // mirrored in pinned memory
+  double *chain = nullptr, *chain_host = nullptr;
+  int chain_k = 0;
+  size_t chain_stride = 0;
 };
+
+// algorithmic FP64 FLOPs / bytes of one EKFUpdate (engine_state.cpp)
+double ekf_flops(double N, double n, double r);
+double ekf_bytes(double N, double n, double r);
 
 class Engine {
  public:
@@ -516,6 +526,10 @@ class Engine {
   // wait = false: only enqueue (kernels + result readback); the caller's next device sync completes it and
   // finish_batch then fills outs
   // chi2 = false: the feature kernel only (delayed init gates on its own update factor instead)
+  DBatchParams batch_params(const Batch &b, double sigma_pix_sq, double chi2_mult) const;
+  // one chain of delayed initializations: fv[idx[0..]] (triangulated) linearized, initialized and updated on
+  // the device one after the other, one host wait at the end
+  int slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t> &idx, int rep, double s2);
   int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs,
                 bool chi2 = true);
   void finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs);

@@ -224,13 +224,14 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
   if (d_.shard_host) hipHostFree(d_.shard_host);
   if (d_.stg_h) hipHostFree(d_.stg_h);
   if (d_.hidx_pre_h) hipHostFree(d_.hidx_pre_h);
+  if (d_.chain_host) hipHostFree(d_.chain_host);
   if (d_.ev_aux_in) hipEventDestroy(d_.ev_aux_in);
   if (d_.ev_aux_out) hipEventDestroy(d_.ev_aux_out);
   if (d_.aux) hipStreamDestroy(d_.aux);
@@ -312,6 +313,10 @@ void Engine::alloc_device() {
   dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
+  d_.chain_k = std::max(1, std::min(std::max(o_.max_slam_features, 1), 64));
+  d_.chain_stride = (size_t)cap + 16;
+  dalloc(&d_.chain, (size_t)d_.chain_k * d_.chain_stride);
+  HP_HIP(hipHostMalloc((void **)&d_.chain_host, sizeof(double) * d_.chain_k * d_.chain_stride, hipHostMallocDefault));
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
   for (int i = 1; i < 1000; i++) chi2_table_[i] = chi2_quantile95(i);
   HP_HIP(hipMemcpy(d_.chi2, chi2_table_.data(), 1000 * sizeof(double), hipMemcpyHostToDevice));
@@ -415,7 +420,7 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"feature", "k_feature", 1},
       {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
-      {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm,k_info_cholZ,k_trinv16,"
+      {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm_mfma,k_info_cholZ,k_trinv16,"
                      "k_trsm_lt,k_info_P",
        1},
       {"ldl", "k_ekf_fact", 1},

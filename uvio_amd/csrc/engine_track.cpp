@@ -55,12 +55,12 @@ struct Tracker::Bufs {
   int cap = 0, maxcells = 0, kmax = 0;
   char *dmem = nullptr, *hmem = nullptr;
   size_t mirror = 0;  // bytes [0, mirror) of the device block are mirrored in pinned host memory
-  // device (host mirror: hp(x)); the matching inputs [p0 | sub] x 2 slots and outputs [p1 | st | mask] x 2
-  // are contiguous so each direction is one copy per frame
-  float *p0[2], *p1[2], *p0n[2], *p1n[2];
-  uint8_t *st[2], *mask[2];
-  int *sub[2], *nm[2], *good[2];
-  double *F[2];
+  // device (host mirror: hp(x)); the matching inputs [p0 | sub] x kMaxCams slots and outputs
+  // [p1 | st | mask] x kMaxCams are contiguous so each direction is one copy per frame
+  float *p0[kMaxCams], *p1[kMaxCams], *p0n[kMaxCams], *p1n[kMaxCams];
+  uint8_t *st[kMaxCams], *mask[kMaxCams];
+  int *sub[kMaxCams], *nm[kMaxCams], *good[kMaxCams];
+  double *F[kMaxCams];
   int *cells, *fastn;
   float *fast, *det, *det1, *spmask;
   uint8_t *detst;
@@ -166,15 +166,15 @@ void Tracker::ensure_cap(int n) {
     b.dmem = b.hmem = nullptr;
   }
   int cap = std::max(n, 2 * b.cap);
-  size_t ncell = (size_t)b.maxcells;
+  size_t ncell = (size_t)b.maxcells * kMaxCams;  // the grid cells of every camera of one feed
   for (int pass = 0; pass < 2; pass++) {
     Arena d;
     if (pass == 1) d.base = b.dmem;
-    for (int k = 0; k < 2; k++) {  // matching inputs of both slots: one upload
+    for (int k = 0; k < kMaxCams; k++) {  // matching inputs of every slot: one upload
       b.p0[k] = d.take<float>(2 * cap);
       b.sub[k] = d.take<int>(7 * kRansacIters);
     }
-    for (int k = 0; k < 2; k++) {  // matching outputs of both slots: one readback
+    for (int k = 0; k < kMaxCams; k++) {  // matching outputs of every slot: one readback
       b.p1[k] = d.take<float>(2 * cap);
       b.st[k] = d.take<uint8_t>(cap);
       b.mask[k] = d.take<uint8_t>(cap);
@@ -186,7 +186,7 @@ void Tracker::ensure_cap(int n) {
     b.det1 = d.take<float>(2 * cap);
     b.detst = d.take<uint8_t>(cap);
     const size_t mirror = d.off;
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < kMaxCams; k++) {
       b.p0n[k] = d.take<float>(2 * cap);
       b.p1n[k] = d.take<float>(2 * cap);
       b.nm[k] = d.take<int>(kRansacIters);
@@ -341,12 +341,13 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
     launch_pyramids(s_, job);
   }
   if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
-  if (ncam == 1) {
-    feed_monocular(t, cam_ids[0], db);
-  } else if (ncam == 2 && use_stereo_) {
+  if (ncam == 2 && use_stereo_) {
     feed_stereo(t, cam_ids[0], cam_ids[1], db);
+  } else if (ncam > 2 && use_stereo_) {
+    // TrackKLT.cpp:90-93: more than two images with use_stereo is an error (std::exit in the reference)
+    throw HpError(UVIO_HP_E_ARG, "more than 2 images in one feed with use_stereo");
   } else {
-    for (int k = 0; k < ncam; k++) feed_monocular(t, cam_ids[k], db);
+    feed_multi(t, cam_ids, ncam, db);  // mono, or binocular tracking of each camera on its own
   }
   in_flight_ = nullptr;  // not reached (no matching this frame): the caller does that work afterwards
   // pyr_last / mask_last <- this frame's (every TrackKLT path ends this way)
@@ -359,13 +360,13 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
 }
 
 // ---------------------------------------------------------------- detection
-void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &boxes,
-                      const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
-                      std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st) {
-  out.clear();
-  if (valid.empty()) return;
+// Grider_GRID::perform_griding + cornerSubPix for the requests of several cameras at once: the FAST
+// scores / top-k of every camera's valid cells in one launch pair and one readback, the sub-pixel
+// refinement of every camera's kept corners in one launch and one readback.  With lk_to (one request
+// only) the refined points are also tracked into that pyramid (TrackKLT.cpp:640-655).
+void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vector<KeyPt> *lk_pts,
+                            std::vector<uint8_t> *lk_st) {
   Bufs &b = *b_;
-  const int W = p.w[0], H = p.h[0];
   int gx = grid_x_, gy = grid_y_;
   if (num_features_ < gx * gy) {
     double ratio = (double)gx / (double)gy;
@@ -373,86 +374,153 @@ void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_m
     gx = (int)std::ceil(gy * ratio);
   }
   const int nfg = b.kmax;
-  const int size_x = W / gx, size_y = H / gy;
-  int nc = 0;
-  for (auto &g : valid) {
-    int x = g.first * size_x, y = g.second * size_y;
-    if (x + size_x > W || y + size_y > H) continue;
-    b.hp(b.cells)[2 * nc] = x;
-    b.hp(b.cells)[2 * nc + 1] = y;
-    nc++;
+  FastJob fj{};
+  int nc = 0, nf = 0;
+  std::vector<int> req_cam(nr, -1), cell0(nr, 0);
+  for (int r = 0; r < nr; r++) {
+    GridReq &q = reqs[r];
+    q.out.clear();
+    const int W = q.p->w[0], H = q.p->h[0];
+    const int size_x = W / gx, size_y = H / gy;
+    cell0[r] = nc;
+    for (auto &g : q.valid) {
+      int x = g.first * size_x, y = g.second * size_y;
+      if (x + size_x > W || y + size_y > H) continue;
+      b.hp(b.cells)[2 * nc] = x;
+      b.hp(b.cells)[2 * nc + 1] = y;
+      nc++;
+    }
+    if (nc == cell0[r]) continue;
+    req_cam[r] = nf;
+    fj.img[nf] = q.p->img[0];
+    fj.score[nf] = cs_[q.cam].d_score;
+    fj.w[nf] = W;
+    fj.sw[nf] = size_x;
+    fj.sh[nf] = size_y;
+    fj.cell_end[nf] = nc;
+    nf++;
   }
   if (nc == 0) return;
+  fj.ncam = nf;
   HP_HIP(hipMemcpyAsync(b.cells, b.hp(b.cells), 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
-  launch_fast_cells(s_, p.img[0], W, H, b.cells, nc, size_x, size_y, threshold_, nfg, b.fast, b.fastn, cs_[cam].d_score);
+  launch_fast_multi(s_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
   HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, s_));
   sync();
   const int *h_fastn = b.hp(b.fastn);
   const float *h_fast = b.hp(b.fast);
   const int d = min_px_dist_;
-  for (int c = 0; c < nc; c++)
-    for (int i = 0; i < h_fastn[c]; i++) {
-      const float *f = h_fast + ((size_t)c * nfg + i) * 3;
-      KeyPt k{f[0], f[1], f[2]};
-      if ((int)k.x < 0 || (int)k.x > W || (int)k.y < 0 || (int)k.y > H) continue;
-      if (mask_px(user_mask, W, (int)k.x, (int)k.y) > 127 || in_boxes(boxes, d, (int)k.x, (int)k.y)) continue;
-      out.push_back(k);
-    }
-  if (out.empty()) return;
-  const int n = (int)out.size();
-  ensure_cap(n);
+  int total = 0;
+  for (int r = 0; r < nr; r++) {
+    GridReq &q = reqs[r];
+    if (req_cam[r] < 0) continue;
+    const int W = q.p->w[0], H = q.p->h[0];
+    for (int c = cell0[r]; c < fj.cell_end[req_cam[r]]; c++)
+      for (int i = 0; i < h_fastn[c]; i++) {
+        const float *f = h_fast + ((size_t)c * nfg + i) * 3;
+        KeyPt k{f[0], f[1], f[2]};
+        if ((int)k.x < 0 || (int)k.x > W || (int)k.y < 0 || (int)k.y > H) continue;
+        if (mask_px(*q.user_mask, W, (int)k.x, (int)k.y) > 127 || in_boxes(*q.boxes, d, (int)k.x, (int)k.y)) continue;
+        q.out.push_back(k);
+      }
+    total += (int)q.out.size();
+  }
+  if (total == 0) return;
+  ensure_cap(total);
   float *h_det = b.hp(b.det), *h_det1 = b.hp(b.det1);
   const uint8_t *h_detst = b.hp(b.detst);
-  for (int i = 0; i < n; i++) {
-    h_det[2 * i] = out[i].x;
-    h_det[2 * i + 1] = out[i].y;
+  SubpixJob sj{};
+  int np = 0;
+  for (int r = 0; r < nr; r++) {
+    GridReq &q = reqs[r];
+    if (q.out.empty()) continue;
+    for (auto &k : q.out) {
+      h_det[2 * np] = k.x;
+      h_det[2 * np + 1] = k.y;
+      np++;
+    }
+    sj.img[sj.ncam] = q.p->img[0];
+    sj.w[sj.ncam] = q.p->w[0];
+    sj.h[sj.ncam] = q.p->h[0];
+    sj.end[sj.ncam] = np;
+    sj.ncam++;
   }
-  HP_HIP(hipMemcpyAsync(b.det, h_det, 2 * n * sizeof(float), hipMemcpyHostToDevice, s_));
-  launch_subpix(s_, p.img[0], W, H, b.det, n, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
-  if (lk_to) {
+  HP_HIP(hipMemcpyAsync(b.det, h_det, 2 * np * sizeof(float), hipMemcpyHostToDevice, s_));
+  launch_subpix_multi(s_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
+  const bool do_lk = lk_to && nr == 1;
+  if (do_lk) {
     LkSlots lk{};
-    lk.prev[0] = p;
+    lk.prev[0] = *reqs[0].p;
     lk.next[0] = *lk_to;
     lk.p0[0] = b.det;
     lk.p1[0] = b.det1;
     lk.st[0] = b.detst;
-    lk.n[0] = n;
+    lk.n[0] = np;
     lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
     {
       KScope ks(kp_, KC_LK);
       launch_lk(s_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
     }
-    HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + n), hipMemcpyDeviceToHost, s_));
+    HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + np), hipMemcpyDeviceToHost, s_));
   } else {
-    HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s_));
+    HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * np * sizeof(float), hipMemcpyDeviceToHost, s_));
   }
   sync();
-  for (int i = 0; i < n; i++) {
-    out[i].x = h_det[2 * i];
-    out[i].y = h_det[2 * i + 1];
-  }
-  if (lk_to) {
-    lk_pts->resize(n);
-    lk_st->resize(n);
-    for (int i = 0; i < n; i++) {
-      (*lk_pts)[i] = KeyPt{h_det1[2 * i], h_det1[2 * i + 1], out[i].response};
+  int at = 0;
+  for (int r = 0; r < nr; r++)
+    for (auto &k : reqs[r].out) {
+      k.x = h_det[2 * at];
+      k.y = h_det[2 * at + 1];
+      at++;
+    }
+  if (do_lk) {
+    lk_pts->resize(np);
+    lk_st->resize(np);
+    for (int i = 0; i < np; i++) {
+      (*lk_pts)[i] = KeyPt{h_det1[2 * i], h_det1[2 * i + 1], reqs[0].out[i].response};
       (*lk_st)[i] = h_detst[i];
     }
   }
 }
 
-// TrackKLT::perform_detection_monocular (TrackKLT.cpp:395-528)
-void Tracker::detect_monocular(int cam, const DPyr &p, const std::vector<uint8_t> &mask0, std::vector<KeyPt> &pts0,
-                               std::vector<size_t> &ids0) {
+void Tracker::griding(int cam, const DPyr &p, const std::vector<uint8_t> &user_mask, const std::vector<int> &boxes,
+                      const std::vector<std::pair<int, int>> &valid, std::vector<KeyPt> &out, const DPyr *lk_to,
+                      std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st) {
+  out.clear();
+  if (valid.empty()) return;
+  GridReq q{cam, &p, &user_mask, &boxes, valid, {}};
+  griding_multi(&q, 1, lk_to, lk_pts, lk_st);
+  out.swap(q.out);
+}
+
+// TrackKLT::perform_detection_monocular (TrackKLT.cpp:395-528) of one camera, split around the device
+// griding so that the cameras of one feed share its launches: pre keeps the tracked points that pass the
+// edge / occupancy / mask tests and lists the cells that need corners, post adds the new corners that
+// keep the minimum distance and numbers them (++currid, in camera order: the serial schedule's ids).
+struct Tracker::MonoDet {
+  int cam;
+  const DPyr *p;
+  const std::vector<uint8_t> *mask;
+  std::vector<KeyPt> pts;
+  std::vector<size_t> ids;
+  int scw = 0, sch = 0;
+  std::vector<uint8_t> close;
+  bool run = false;
+  std::vector<int> boxes;
+  GridReq g;
+};
+
+void Tracker::detect_mono_pre(MonoDet &m) {
+  const DPyr &p = *m.p;
+  const std::vector<uint8_t> &mask0 = *m.mask;
   const int W = p.w[0], H = p.h[0], d = min_px_dist_;
   const int scw = (int)((float)W / (float)d), sch = (int)((float)H / (float)d);
   Occupancy close(scw, sch), grid(grid_x_, grid_y_);
   const float size_x = (float)W / (float)grid_x_, size_y = (float)H / (float)grid_y_;
-  std::vector<int> boxes;
   std::vector<KeyPt> kp;
   std::vector<size_t> kid;
-  for (size_t i = 0; i < pts0.size(); i++) {
-    const KeyPt &k = pts0[i];
+  m.boxes.clear();
+  for (size_t i = 0; i < m.pts.size(); i++) {
+    const KeyPt &k = m.pts[i];
     const int x = (int)k.x, y = (int)k.y, edge = 10;
     if (x < edge || x >= W - edge || y < edge || y >= H - edge) continue;
     const int xc = (int)(k.x / (float)d), yc = (int)(k.y / (float)d);
@@ -464,32 +532,60 @@ void Tracker::detect_monocular(int cam, const DPyr &p, const std::vector<uint8_t
     close.at(xc, yc) = 255;
     if (grid.at(xg, yg) < 255) grid.at(xg, yg) += 1;
     if (x - d >= 0 && x + d < W && y - d >= 0 && y + d < H) {
-      boxes.push_back(x);
-      boxes.push_back(y);
+      m.boxes.push_back(x);
+      m.boxes.push_back(y);
     }
     kp.push_back(k);
-    kid.push_back(ids0[i]);
+    kid.push_back(m.ids[i]);
   }
-  pts0.swap(kp);
-  ids0.swap(kid);
-  const int needed = num_features_ - (int)pts0.size();
+  m.pts.swap(kp);
+  m.ids.swap(kid);
+  m.scw = scw;
+  m.sch = sch;
+  m.close.swap(close.d);
+  m.g = GridReq{m.cam, m.p, m.mask, &m.boxes, {}, {}};
+  const int needed = num_features_ - (int)m.pts.size();
+  m.run = false;
   if (needed < std::min(20, (int)(kMinFeatPercent * num_features_))) return;
   const int nfg = (int)((double)num_features_ / (double)(grid_x_ * grid_y_)) + 1;
   const int nfg_req = std::max(1, (int)(kMinFeatPercent * nfg));
-  std::vector<std::pair<int, int>> valid;
   for (int x = 0; x < grid_x_; x++)
     for (int y = 0; y < grid_y_; y++)
-      if ((int)grid.at(x, y) < nfg_req && (int)mask_cell(mask0, W, H, x, y, grid_x_, grid_y_) != 255) valid.emplace_back(x, y);
-  std::vector<KeyPt> ext;
-  griding(cam, p, mask0, boxes, valid, ext, nullptr, nullptr, nullptr);
-  for (auto &k : ext) {
+      if ((int)grid.at(x, y) < nfg_req && (int)mask_cell(mask0, W, H, x, y, grid_x_, grid_y_) != 255)
+        m.g.valid.emplace_back(x, y);
+  m.run = !m.g.valid.empty();
+}
+
+void Tracker::detect_mono_post(MonoDet &m) {
+  if (!m.run) return;
+  const int d = min_px_dist_;
+  for (auto &k : m.g.out) {
     const int xg = (int)(k.x / (float)d), yg = (int)(k.y / (float)d);
-    if (xg < 0 || xg >= scw || yg < 0 || yg >= sch) continue;
-    if (close.at(xg, yg) > 127) continue;
-    close.at(xg, yg) = 255;
-    pts0.push_back(k);
-    ids0.push_back(++currid);
+    if (xg < 0 || xg >= m.scw || yg < 0 || yg >= m.sch) continue;
+    uint8_t &cl = m.close[(size_t)yg * m.scw + xg];
+    if (cl > 127) continue;
+    cl = 255;
+    m.pts.push_back(k);
+    m.ids.push_back(++currid);
   }
+}
+
+// perform_detection_monocular of several cameras: host passes per camera, one shared device griding
+void Tracker::detect_mono_multi(MonoDet *m, int n) {
+  std::vector<GridReq> reqs;
+  std::vector<int> who;
+  for (int k = 0; k < n; k++) {
+    detect_mono_pre(m[k]);
+    if (m[k].run) {
+      reqs.push_back(m[k].g);
+      who.push_back(k);
+    }
+  }
+  if (!reqs.empty()) {
+    griding_multi(reqs.data(), (int)reqs.size(), nullptr, nullptr, nullptr);
+    for (size_t r = 0; r < reqs.size(); r++) m[who[r]].g.out.swap(reqs[r].out);
+  }
+  for (int k = 0; k < n; k++) detect_mono_post(m[k]);
 }
 
 // TrackKLT::perform_detection_stereo (TrackKLT.cpp:530-827)
@@ -650,7 +746,7 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
   Bufs &b = *b_;
   LkSlots lk{};
   RansacSlots rs{};
-  int ns = 0, lo = 2, hi = -1;
+  int ns = 0, lo = kMaxCams, hi = -1;
   for (int k = 0; k < nj; k++) {
     const MatchJob &j = jobs[k];
     if (!j.run) continue;
@@ -725,51 +821,82 @@ void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1,
 }
 
 // ---------------------------------------------------------------- per-frame logic
-// TrackKLT::feed_monocular (TrackKLT.cpp:96-200)
-void Tracker::feed_monocular(double t, int cam, const DbSink &db) {
-  CamState &c = cs_[cam];
-  const DPyr &pn = c.pyr[1 - c.last], &pl = c.pyr[c.last];
-  if (c.pts_last.empty()) {
-    std::vector<KeyPt> good;
-    std::vector<size_t> gid;
-    detect_monocular(cam, pn, c.mask_new, good, gid);
-    c.pts_last = good;
-    c.ids_last = gid;
-    return;
-  }
-  std::vector<KeyPt> pts_old = c.pts_last;
-  std::vector<size_t> ids_old = c.ids_last;
-  detect_monocular(cam, pl, c.mask_last, pts_old, ids_old);
-  MatchJob j;
-  ensure_cap((int)pts_old.size());
-  match_prepare(0, pl, pn, cam, cam, pts_old, j);
-  match_run(&j, 1);
-  std::vector<KeyPt> pts_new = pts_old;
-  std::vector<uint8_t> mask_ll;
-  match_collect(0, j, pts_new, mask_ll);
-  if (mask_ll.empty()) {
-    c.pts_last.clear();
-    c.ids_last.clear();
-    return;
-  }
-  const int W = pn.w[0], H = pn.h[0];
-  std::vector<KeyPt> good;
-  std::vector<size_t> gid;
-  for (size_t i = 0; i < pts_new.size(); i++) {
-    if (pts_new[i].x < 0 || pts_new[i].y < 0 || (int)pts_new[i].x >= W || (int)pts_new[i].y >= H) continue;
-    if (mask_px(c.mask_new, W, (int)pts_new[i].x, (int)pts_new[i].y) > 127) continue;
-    if (mask_ll[i]) {
-      good.push_back(pts_new[i]);
-      gid.push_back(ids_old[i]);
+// TrackKLT::feed_monocular (TrackKLT.cpp:96-200) of the n cameras of one feed.  The reference runs the
+// cameras' feed_monocular side by side (TrackKLT.cpp:85-89, parallel_for_ over the images, one atomic
+// currid); here their detections share one device griding, their temporal matchings one LK + RANSAC launch
+// pair and one readback, and the ids and database inserts follow the camera order -- the schedule in
+// which the cameras run one after the other (the reference's threads may interleave the ids of
+// different cameras; any interleaving is a valid run of it).
+void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
+  std::vector<MonoDet> det(n);
+  std::vector<bool> first(n);
+  for (int k = 0; k < n; k++) {
+    CamState &c = cs_[cams[k]];
+    first[k] = c.pts_last.empty();
+    det[k].cam = cams[k];
+    if (first[k]) {  // no tracks yet: detect on this frame and keep them
+      det[k].p = &c.pyr[1 - c.last];
+      det[k].mask = &c.mask_new;
+    } else {
+      det[k].p = &c.pyr[c.last];
+      det[k].mask = &c.mask_last;
+      det[k].pts = c.pts_last;
+      det[k].ids = c.ids_last;
     }
   }
-  for (size_t i = 0; i < good.size(); i++) {
-    float un, vn;
-    cam_undistort_f(cams_[cam], good[i].x, good[i].y, un, vn);
-    db(gid[i], t, cam, good[i].x, good[i].y, un, vn);
+  detect_mono_multi(det.data(), n);
+  std::vector<MatchJob> jobs;
+  std::vector<int> who;
+  size_t most = 0;
+  for (int k = 0; k < n; k++) {
+    CamState &c = cs_[cams[k]];
+    if (first[k]) {
+      c.pts_last = det[k].pts;
+      c.ids_last = det[k].ids;
+      continue;
+    }
+    most = std::max(most, det[k].pts.size());
+    who.push_back(k);
   }
-  c.pts_last.swap(good);
-  c.ids_last.swap(gid);
+  if (who.empty()) return;
+  ensure_cap((int)most);  // no reallocation between the slots
+  jobs.resize(who.size());
+  for (size_t j = 0; j < who.size(); j++) {
+    CamState &c = cs_[cams[who[j]]];
+    match_prepare((int)j, c.pyr[c.last], c.pyr[1 - c.last], cams[who[j]], cams[who[j]], det[who[j]].pts, jobs[j]);
+  }
+  match_run(jobs.data(), (int)jobs.size());
+  for (size_t j = 0; j < who.size(); j++) {
+    const int k = who[j], cam = cams[k];
+    CamState &c = cs_[cam];
+    const DPyr &pn = c.pyr[1 - c.last];
+    std::vector<KeyPt> pts_new = det[k].pts;
+    std::vector<uint8_t> mask_ll;
+    match_collect((int)j, jobs[j], pts_new, mask_ll);
+    if (mask_ll.empty()) {
+      c.pts_last.clear();
+      c.ids_last.clear();
+      continue;
+    }
+    const int W = pn.w[0], H = pn.h[0];
+    std::vector<KeyPt> good;
+    std::vector<size_t> gid;
+    for (size_t i = 0; i < pts_new.size(); i++) {
+      if (pts_new[i].x < 0 || pts_new[i].y < 0 || (int)pts_new[i].x >= W || (int)pts_new[i].y >= H) continue;
+      if (mask_px(c.mask_new, W, (int)pts_new[i].x, (int)pts_new[i].y) > 127) continue;
+      if (mask_ll[i]) {
+        good.push_back(pts_new[i]);
+        gid.push_back(det[k].ids[i]);
+      }
+    }
+    for (size_t i = 0; i < good.size(); i++) {
+      float un, vn;
+      cam_undistort_f(cams_[cam], good[i].x, good[i].y, un, vn);
+      db(gid[i], t, cam, good[i].x, good[i].y, un, vn);
+    }
+    c.pts_last.swap(good);
+    c.ids_last.swap(gid);
+  }
 }
 
 // TrackKLT::feed_stereo (TrackKLT.cpp:202-393)

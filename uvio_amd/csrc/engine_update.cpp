@@ -813,6 +813,32 @@ void Engine::add_features_to_batch(Batch &b, const std::vector<FeatP> &fv, size_
   }
 }
 
+DBatchParams Engine::batch_params(const Batch &b, double sigma_pix_sq, double chi2_mult) const {
+  DBatchParams bp{};
+  bp.nfeat = (int)b.feats.size();
+  bp.n_canon = b.n_canon;
+  bp.ldh = d_.ldh;
+  bp.ldp = d_.ldp;
+  bp.sigma_pix_sq = sigma_pix_sq;
+  bp.chi2_mult = chi2_mult;
+  bp.do_fej = o_.do_fej;
+  bp.calib_ext = o_.do_calib_camera_pose;
+  bp.calib_intr = o_.do_calib_camera_intrinsics;
+  bp.fi_max_runs = o_.fi_max_runs;
+  bp.fi_refine = o_.fi_refine_features;
+  bp.fi_tri1d = o_.fi_triangulate_1d;
+  bp.fi_init_lamda = o_.fi_init_lamda;
+  bp.fi_max_lamda = o_.fi_max_lamda;
+  bp.fi_min_dx = o_.fi_min_dx;
+  bp.fi_min_dcost = o_.fi_min_dcost;
+  bp.fi_lam_mult = o_.fi_lam_mult;
+  bp.fi_min_dist = o_.fi_min_dist;
+  bp.fi_max_dist = o_.fi_max_dist;
+  bp.fi_max_baseline = o_.fi_max_baseline;
+  bp.fi_max_cond = o_.fi_max_cond_number;
+  return bp;
+}
+
 // Upload a batch, run the per-feature kernel and (optionally) compression; results in outs.
 // Returns the number of stacked rows written to H_all.
 int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs,
@@ -845,28 +871,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
   if (b.meas_dev && b.stg_epoch != d_.stg_epoch && d_.stg_used > (size_t)((const char *)b.meas_dev - d_.stg_d))
     throw HpError(UVIO_HP_E_CAPACITY, "upload staging ring restarted inside one launch group (UVIO_HP_STAGE_BYTES too small)");
   b.hidx_dev = t_hidx;
-  DBatchParams bp{};
-  bp.nfeat = nf;
-  bp.n_canon = b.n_canon;
-  bp.ldh = d_.ldh;
-  bp.ldp = d_.ldp;
-  bp.sigma_pix_sq = sigma_pix_sq;
-  bp.chi2_mult = chi2_mult;
-  bp.do_fej = o_.do_fej;
-  bp.calib_ext = o_.do_calib_camera_pose;
-  bp.calib_intr = o_.do_calib_camera_intrinsics;
-  bp.fi_max_runs = o_.fi_max_runs;
-  bp.fi_refine = o_.fi_refine_features;
-  bp.fi_tri1d = o_.fi_triangulate_1d;
-  bp.fi_init_lamda = o_.fi_init_lamda;
-  bp.fi_max_lamda = o_.fi_max_lamda;
-  bp.fi_min_dx = o_.fi_min_dx;
-  bp.fi_min_dcost = o_.fi_min_dcost;
-  bp.fi_lam_mult = o_.fi_lam_mult;
-  bp.fi_min_dist = o_.fi_min_dist;
-  bp.fi_max_dist = o_.fi_max_dist;
-  bp.fi_max_baseline = o_.fi_max_baseline;
-  bp.fi_max_cond = o_.fi_max_cond_number;
+  DBatchParams bp = batch_params(b, sigma_pix_sq, chi2_mult);
   const char *mdump = (mode == 0) ? std::getenv("UVIO_HP_MEAS_DUMP") : nullptr;  // debug only
   if (mdump) HP_HIP(hipMalloc(&bp.dbg, sizeof(double) * 8 * b.n_meas()));
   const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
@@ -1180,6 +1185,7 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     // triangulation only: the rows and chi2 come from the per-feature mode-3 linearization below
     run_batch(b, 2, s2, o_.slam_chi2_multipler, true, tri, false);
   }
+  std::vector<size_t> cand;
   for (size_t i = 0; i < fv.size(); i++) {
     FeatP &f = fv[i];
     if (tri[i].status == 1 || tri[i].status == 2) {
@@ -1195,89 +1201,163 @@ int Engine::slam_delayed_init(std::vector<FeatP> &fv) {
     f->anchor_cam_id = (int)anchor_cam;
     f->anchor_clone_timestamp = f->find(anchor_cam)->m.back().t;
     for (int k = 0; k < 3; k++) f->p_FinA[k] = tri[i].p_FinA[k], f->p_FinG[k] = tri[i].p_FinG[k];
-    // 2) linearize at the current state (mode 3 = given triangulation, nullspace-split rows)
+    cand.push_back(i);
+  }
+  // 2) per candidate, in order: linearize at the current state, initialize_invertible, the EKF update of the
+  // remaining rows behind StateHelper::initialize's chi2 test -- as device chains of up to chain_k candidates
+  for (size_t c0 = 0; c0 < cand.size(); c0 += (size_t)d_.chain_k) {
+    std::vector<size_t> part(cand.begin() + c0, cand.begin() + std::min(cand.size(), c0 + (size_t)d_.chain_k));
+    HPROF("di.chain");
+    int rc = slam_delayed_chain(fv, part, rep, s2);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// The delayed initializations of one frame (StateHelper::initialize per candidate, StateHelper.cpp:393-482)
+// as one device chain with one host wait.  Candidate j is linearized (mode 3: at the batch triangulation,
+// the current clone / camera values), its landmark is appended by initialize_invertible in a FIXED slot
+// N0 + 3 j, its remaining rows update the state behind the chi2 test of their own factor (the S of
+// StateHelper::initialize's test, StateHelper.cpp:451-470, is the S the update factors), and k_chain_apply
+// then either moves the device clone / camera tables by the update's dx (the next candidate linearizes at
+// the updated state, as the reference's loop does) or clears the slot of a rejected candidate: a zero slot
+// has zero rows in every later M and K, so it changes nothing until the host marginalizes it afterwards
+// (StateHelper::marginalize, the same exact copy-compaction as any other variable).  The host then replays
+// the candidates in order from one readback: landmark values (H_finit^-1 times the init residual), the
+// updates' dx on its mean, the landmark set.
+int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t> &idx, int rep, double s2) {
+  const int K = (int)idx.size();
+  if (K == 0) return 0;
+  const int N0 = N_;
+  if (N0 + 3 * K > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
+  Batch b;
+  {
+    HPROF("di.prep");
+    build_clone_cam_tables(b, false);
+    for (size_t i : idx)
+      add_feature(this, fv[i], 3, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+  }
+  if ((int)b.feats.size() > d_.max_feat || (int)b.n_meas() > d_.max_meas_total || (int)b.n_vars() > d_.max_vars_total ||
+      b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol)
+    throw HpError(UVIO_HP_E_CAPACITY, "delayed-initialization chain exceeds device capacity");
+  for (int j = 0; j < K; j++) {  // mode 3 linearizes at the batch triangulation (p_in = p_FinA, p_in_fej = p_FinG)
+    const FeatP &f = fv[idx[j]];
+    for (int k = 0; k < 3; k++) b.feats[j].p_in[k] = f->p_FinA[k], b.feats[j].p_in_fej[k] = f->p_FinG[k];
+    if (b.feats[j].nmeas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
+  }
+  // the pose values behind the clone / camera tables (k_chain_apply updates them in place)
+  std::vector<DPoseVal> cv(b.clones.size()), camv(b.cams.size());
+  {
+    size_t s = 0;
+    for (auto &c : clones_) {
+      for (int k = 0; k < 4; k++) cv[s].q[k] = c.second->val[k];
+      for (int k = 0; k < 3; k++) cv[s].p[k] = c.second->val[4 + k];
+      cv[s].pid = c.second->id;
+      s++;
+    }
+    for (size_t c = 0; c < camv.size(); c++) {
+      const VarP &pose = calib_pose_.at((int)c);
+      for (int k = 0; k < 4; k++) camv[c].q[k] = pose->val[k];
+      for (int k = 0; k < 3; k++) camv[c].p[k] = pose->val[4 + k];
+      camv[c].pid = pose->id;
+    }
+  }
+  const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
+  const DMeas *t_meas = stage(b.meas.data(), b.meas.size());
+  const DVar *t_vars = stage(b.vars.data(), b.vars.size());
+  DClone *t_clones = const_cast<DClone *>(stage(b.clones.data(), b.clones.size()));
+  DCam *t_cams = const_cast<DCam *>(stage(b.cams.data(), b.cams.size()));
+  DPoseVal *t_cv = const_cast<DPoseVal *>(stage(cv.data(), cv.size()));
+  DPoseVal *t_camv = const_cast<DPoseVal *>(stage(camv.data(), camv.size()));
+  const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
+  stage_flush();
+  DBatchParams bp = batch_params(b, s2, o_.slam_chi2_multipler);
+  bp.nfeat = 1;
+  const int n = b.n_canon;
+  const size_t st = d_.chain_stride;
+  {
+    HPROF("di.enqueue");
+    for (int j = 0; j < K; j++) {
+      const DFeat &F = b.feats[j];
+      const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
+      {
+        KScope ks(&kprof_, KC_FEATURE);
+        launch_feature_linearize(d_.stream, bp, t_feats + j, t_meas, t_vars, t_clones, t_cams, d_.P, d_.chi2, d_.H,
+                                 d_.fout + j, F.nmeas, F.nf);
+      }
+      EkfScratch sc = d_.ekf;
+      sc.dx = d_.chain + (size_t)j * st;
+      double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
+      // initialize_invertible with rows 0..2 (H_Linv from the feature's H_finit); its residual column lands in
+      // the candidate's region behind the chi2 gate's [chi2, accepted]
+      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, t_hidx, nullptr, s2, sc, d_.fout + j, nullptr,
+                             sc.dx + Ni + 5);
+      if (nup > 0) {
+        sc.chi2_gate = d_.acc;
+        sc.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * F.nmeas, 999)];
+        sc.gate = nullptr;
+        KScope ks(&kprof_, KC_EKF);
+        launch_ekf_update(d_.stream, d_.P, d_.ldp, Ni + 3, Hrow + 3 * (size_t)d_.ldh, d_.ldh, nup, n, t_hidx,
+                          Hrow + 3 * (size_t)d_.ldh + n, d_.ldh, s2, sc);
+      }
+      if (nup > 0) kprof_.credit(KC_EKF, ekf_flops(Ni + 3, n, nup), ekf_bytes(Ni + 3, n, nup));
+      launch_chain_apply(d_.stream, d_.fout + j, nup > 0 ? d_.acc : nullptr, nup > 0 ? sc.neg : nullptr,
+                         nup > 0 ? sc.dx : nullptr, t_clones, t_cv, (int)b.clones.size(), t_cams, t_camv,
+                         (int)b.cams.size(), o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, d_.P, d_.ldp, Ni + 3,
+                         Ni, sc.dx + Ni + 8);
+    }
+    ++p_epoch_;
+    HP_HIP(hipMemcpyAsync(d_.chain_host, d_.chain, sizeof(double) * st * K, hipMemcpyDeviceToHost, d_.stream));
+    HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * K, hipMemcpyDeviceToHost, d_.stream));
+    d_.fout_pending = 0;
+  }
+  dev_sync();
+  // replay on the host mean, candidate by candidate
+  HPROF("di.replay");
+  N_ = N0 + 3 * K;
+  std::vector<int> dead;
+  for (int j = 0; j < K; j++) {
+    FeatP &f = fv[idx[j]];
+    const DFeat &F = b.feats[j];
+    const DFeatOut &o1 = d_.fout_host[j];
+    const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
+    const double *base = d_.chain_host + (size_t)j * st;
+    if (base[Ni + 9] > 0.5) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+    const bool accepted = base[Ni + 8] > 0.5;
+    f->to_delete = true;
+    last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,
+                                  nup > 0 ? base[Ni + 3] : 0.0});
+    frame_feats_.push_back({2, last_upd_.back()});
+    if (!accepted) {
+      dead.push_back(Ni);
+      continue;
+    }
     VarP lm = std::make_shared<Var>(V_LANDMARK, 3, 3);
     lm->featid = f->featid;
     lm->rep = rep;
     lm->unique_cam = f->anchor_cam_id;
     lm->anchor_cam = f->anchor_cam_id;
     lm->anchor_time = f->anchor_clone_timestamp;
-    bool relr = (rep == 2 || rep == 4);
+    const bool relr = (rep == 2 || rep == 4);
     lm->set_xyz(relr ? f->p_FinA : f->p_FinG, false);
     lm->set_xyz(relr ? f->p_FinA : f->p_FinG, true);
-    Batch b;
-    {
-      HPROF("di.prep");
-      build_clone_cam_tables(b, false);
-      add_feature(this, f, 3, rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
-    }
-    // mode 3: linearize at the batch triangulation (p_in = p_FinA, p_in_fej = p_FinG), as the reference
-    // triangulates the whole batch before the per-feature initialize loop
-    for (int k = 0; k < 3; k++) b.feats[0].p_in[k] = f->p_FinA[k], b.feats[0].p_in_fej[k] = f->p_FinG[k];
-    // The chi2 test of StateHelper::initialize (StateHelper.cpp:451-470) is decided on the device: the
-    // batch's accepted count (d_.acc) gates initialize_invertible and the EKF update enqueued right
-    // behind it, and the host learns the decision with the update's dx (one wait per feature).  The
-    // landmark is appended tentatively and withdrawn when the feature was rejected (nothing was written).
-    // The chi2 of StateHelper::initialize uses S = H_up P_up H_up^T + R_up, exactly the S the EKF update
-    // of the same rows factors, so the test runs on that factor (chi2 = |L^-1 r_up|^2, dof = all rows)
-    // instead of a separate chi2 kernel: the feature kernel alone linearizes.
-    std::vector<DFeatOut> o1;
-    {
-      HPROF("di.run_batch");
-      run_batch(b, 3, s2, o_.slam_chi2_multipler, false, o1, false);
-    }
-    // 3) initialize_invertible with rows 0..2 (H_Linv = H_finit^-1 formed on the device from HfR), EKF
-    // update with rows 3..
-    int n = b.n_canon;
-    if (N_ + 3 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
-    // the residual column of rows 0..2 lands behind the chi2 gate's [chi2, accepted] (dx[N+3], dx[N+4] once
-    // the landmark is appended) and comes back with the update's dx readback
-    const int N0 = N_;
-    launch_init_invertible(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, n, b.hidx_dev, nullptr, s2, d_.ekf, d_.fout,
-                           nullptr, d_.ekf.dx + N0 + 5);
-    ++p_epoch_;
-    const double *resinit = d_.dx_host + N0 + 5;
-    bool accepted = false;
-    const int nup = 2 * b.feats[0].nmeas - 3;
-    auto land = [&]() {
-      finish_batch(b, 3, o1);
-      // [chi2, accepted] of the update factor's gate land at dx[N], dx[N+1] (N with the landmark)
-      accepted = (o1[0].status == 0) && (nup <= 0 || d_.dx_host[N_ + 1] > 0.5);
-      if (!accepted) return false;  // the device skipped the update; the landmark slot is withdrawn
-      double HLinv[9], dl[3];
-      inv3_cofactor(o1[0].HfR, HLinv);  // the device's formula: identical H_Linv
-      for (int a = 0; a < 3; a++)
-        dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
-      lm->update(dl);
-      return true;
-    };
-    lm->id = N_;
+    lm->id = Ni;
     vars_.push_back(lm);
-    N_ += 3;
-    f->to_delete = true;
-    HPROF("di.ekf");
-    if (nup > 0) {
-      struct GateScope {  // the chi2 gate applies to this update only, also when it throws
-        EkfScratch &e;
-        ~GateScope() { e.chi2_gate = nullptr; }
-      } scope{d_.ekf};
-      d_.ekf.chi2_gate = d_.acc;
-      d_.ekf.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * b.feats[0].nmeas, 999)];
-      ekf_update_rows(d_.H + (size_t)3 * d_.ldh, d_.ldh, nup, n, b.hidx, d_.H + 3 * (size_t)d_.ldh + n, d_.ldh, s2,
-                      b.hidx_dev, land, d_.acc);
-    } else {
-      read_dx("initialize_invertible");  // the batch results and the residual column
-      land();
-    }
-    last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,
-                                  nup > 0 ? d_.dx_host[N0 + 3] : 0.0});
-    frame_feats_.push_back({2, last_upd_.back()});
-    if (accepted) {
-      slam_.insert({f->featid, lm});
-    } else {
-      vars_.pop_back();
-      N_ = N0;
-    }
+    double HLinv[9], dl[3];
+    inv3_cofactor(o1.HfR, HLinv);  // the device's formula: identical H_Linv
+    const double *resinit = base + Ni + 5;
+    for (int a = 0; a < 3; a++)
+      dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
+    lm->update(dl);
+    if (nup > 0) apply_dx(base);
+    slam_.insert({f->featid, lm});
+  }
+  // the rejected candidates' (zeroed) slots leave the covariance, last first
+  for (size_t k = dead.size(); k-- > 0;) {
+    VarP ph = std::make_shared<Var>(V_LANDMARK, 3, 3);
+    ph->id = dead[k];
+    vars_.push_back(ph);
+    marginalize(ph);
   }
   return 0;
 }

@@ -180,6 +180,20 @@ void launch_ekf_M(hipStream_t s, const double *P, int ldp, int N, const double *
 void launch_init_invertible(hipStream_t s, double *P, int ldp, int N, const double *Hx, int ldh, int n,
                             const int *hidx, const double *HLinv, double s2, EkfScratch &sc,
                             const DFeatOut *fout = nullptr, const int *gate = nullptr, double *resout = nullptr);
+// the JPL pose value behind a clone / camera-extrinsic table entry (PoseJPL: q_GtoI / q_ItoC, position) and its
+// covariance id, updated on the device inside a delayed-initialization chain
+struct DPoseVal {
+  double q[4], p[3];
+  int pid, pad;
+};
+// One step of a delayed-initialization chain (Engine::slam_delayed_init): the candidate's acceptance
+// (linearization status, and with update rows the chi2 gate of its factor) into out[0], the update's
+// negative-diagonal count into out[1]; accepted with an update (dx): the clone / camera tables the next
+// candidate is linearized against get the update (Var::update + quat_2_Rot, the host's formulas);
+// rejected: the appended landmark slot's rows / columns (slot .. slot+2 over [0, Ntot)) are zeroed.
+void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, const int *neg, const double *dx,
+                        DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
+                        int calib_intr, double *P, int ldp, int Ntot, int slot, double *out);
 double chi2_quantile95(int dof);
 
 // ---- VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388) on the device ----
@@ -278,22 +292,38 @@ struct DecimateJob {
   int ncam;
 };
 void launch_decimate(hipStream_t s, const DecimateJob &job);
-// FAST on ncell cells (cells: x0, y0 pairs) of sw x sh; out: ncell x kmax x (x, y, response), out_n: per cell;
-// score_map: w x h u8 scratch
+// FAST on the grid cells of up to kMaxCams images in one launch pair: cells (x0, y0 pairs) of camera k are
+// [cell_end[k-1], cell_end[k]), each sw[k] x sh[k] of image img[k] (row length w[k]); out: ncell x kmax x
+// (x, y, response), out_n: per cell; score[k]: w[k] x h u8 scratch of camera k
+struct FastJob {
+  const uint8_t *img[kMaxCams];
+  uint8_t *score[kMaxCams];
+  int w[kMaxCams], sw[kMaxCams], sh[kMaxCams], cell_end[kMaxCams];
+  int ncam;
+};
+void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n);
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
                        int kmax, float *out, int *out_n, uint8_t *score_map);
-// cornerSubPix in place on n points (x, y); mask: (2 win + 1)^2 weights
+// cornerSubPix in place on the points (x, y) of up to kMaxCams images: points [end[k-1], end[k]) lie in img[k]
+// (w[k] x h[k]); mask: (2 win + 1)^2 weights
+struct SubpixJob {
+  const uint8_t *img[kMaxCams];
+  int w[kMaxCams], h[kMaxCams], end[kMaxCams];
+  int ncam;
+};
+void launch_subpix_multi(hipStream_t s, const SubpixJob &job, float *pts, const float *mask, int win, int max_iters,
+                         double eps2);
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2);
-// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW for up to 2 point sets in one launch: slot k tracks
+// calcOpticalFlowPyrLK with OPTFLOW_USE_INITIAL_FLOW for up to kMaxCams point sets in one launch: slot k tracks
 // n[k] points p0[k] from prev[k] into next[k]; the initial guess is p1[k] (or p0[k] when init_from_p0),
 // the result goes to p1[k], the status to st[k]
 struct LkSlots {
-  DPyr prev[2], next[2];
-  const float *p0[2];
-  float *p1[2];
-  uint8_t *st[2];
-  int n[2];
+  DPyr prev[kMaxCams], next[kMaxCams];
+  const float *p0[kMaxCams];
+  float *p1[kMaxCams];
+  uint8_t *st[kMaxCams];
+  int n[kMaxCams];
   // optional: algorithmic bytes of the launch accumulated on the device (SURVEY.md §8(d) LK term:
   // 256 (5 + iterations) per point and pyramid level visited)
   unsigned long long *bytes = nullptr;
@@ -304,15 +334,15 @@ void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_le
 // host-drawn subsets sub (max_iters x 7): hypotheses in parallel, sequential adaptive selection, inlier
 // mask.  t = thr^2 (float), scratch p0n / p1n (2n), F (27 max_iters), nm (max_iters), good (3 max_iters)
 struct RansacSlots {
-  CamParams c0[2], c1[2];
-  const float *p0[2], *p1[2];
-  float *p0n[2], *p1n[2];
-  const int *sub[2];
-  double *F[2];
-  int *nm[2], *good[2];
-  uint8_t *mask[2];
-  float t[2];
-  int n[2];
+  CamParams c0[kMaxCams], c1[kMaxCams];
+  const float *p0[kMaxCams], *p1[kMaxCams];
+  float *p0n[kMaxCams], *p1n[kMaxCams];
+  const int *sub[kMaxCams];
+  double *F[kMaxCams];
+  int *nm[kMaxCams], *good[kMaxCams];
+  uint8_t *mask[kMaxCams];
+  float t[kMaxCams];
+  int n[kMaxCams];
 };
 void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf);
 

@@ -496,39 +496,63 @@ void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, in
 // Cholesky factor of a singular Gram does.  The eigenvalues of G P_II + s2 I are >= s2, so the LU solve
 // below is well conditioned.
 
-// full symmetric G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk order)
+// full symmetric G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk order).
+// One workgroup row per G row a: thread b >= a reads the partials' (a, b) entries (coalesced along the row,
+// only the written upper triangle is fetched) and writes G[a][b] and G[b][a].
 __global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ partials, int nch, int ncol,
                                                      double *__restrict__ G, int *zero) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (zero && e == 0) *zero = 0;  // the update's negative-diagonal count
-  if (e >= ncol * ncol) return;
-  int a = e / ncol, b = e % ncol;
-  int u = (a <= b) ? a * ncol + b : b * ncol + a;
+  const int a = blockIdx.y, b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero && a == 0 && b == 0) *zero = 0;  // the update's negative-diagonal count
+  if (b < a || b >= ncol) return;
+  const size_t u = (size_t)a * ncol + b, stride = (size_t)ncol * ncol;
   double acc = 0.0;
-  for (int c = 0; c < nch; c++) acc += partials[(size_t)c * ncol * ncol + u];
-  G[e] = acc;
+  int c = 0;
+  for (; c + 4 <= nch; c += 4) {  // four loads in flight, the sum in chunk order
+    const double p0 = partials[c * stride + u], p1 = partials[(c + 1) * stride + u];
+    const double p2 = partials[(c + 2) * stride + u], p3 = partials[(c + 3) * stride + u];
+    acc += p0;
+    acc += p1;
+    acc += p2;
+    acc += p3;
+  }
+  for (; c < nch; c++) acc += partials[c * stride + u];
+  G[u] = acc;
+  G[(size_t)b * ncol + a] = acc;
 }
 
-// C (m x n) = op(A) op(B), 16x16 tiles; op(X) = X or X^T.  Small dense products of the info path.
-__global__ void __launch_bounds__(256) k_gemm(int ta, int tb, int m, int n, int k, const double *__restrict__ A,
-                                              int lda, const double *__restrict__ B, int ldb, double *__restrict__ C,
-                                              int ldc) {
-  __shared__ double As[16][17];
-  __shared__ double Bs[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
-  double acc = 0.0;
-  for (int k0 = 0; k0 < k; k0 += 16) {
-    int ai = i0 + ty, ak = k0 + tx;
-    As[ty][tx] = (ai < m && ak < k) ? (ta ? A[(size_t)ak * lda + ai] : A[(size_t)ai * lda + ak]) : 0.0;
-    int bk = k0 + ty, bj = j0 + tx;
-    Bs[ty][tx] = (bk < k && bj < n) ? (tb ? B[(size_t)bj * ldb + bk] : B[(size_t)bk * ldb + bj]) : 0.0;
-    __syncthreads();
+// C (m x n) = op(A) op(B); op(X) = X or X^T.  The small dense products of the information form (E = L^T G L,
+// (n+1)^2 with n ~ 100-243) on the matrix cores: one 16 x 16 output tile per wave (v_mfma_f64_16x16x4f64,
+// eight k-slabs loaded ahead of their MFMAs).  tri = 1: B is lower triangular (k >= j0 only), tri = 2:
+// op(A) is upper triangular (k >= i0 only) -- the zero blocks of the triangular factor are skipped.
+constexpr int kGemmWaves = 4;
+__global__ void __launch_bounds__(64 * kGemmWaves) k_gemm_mfma(int ta, int tb, int tri, int m, int n, int k,
+                                                              const double *__restrict__ A, int lda,
+                                                              const double *__restrict__ B, int ldb,
+                                                              double *__restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int ntj = (n + 15) / 16;
+  const int tile = blockIdx.x * kGemmWaves + wid, ti = tile / ntj, tj = tile - ti * ntj;
+  const int i0 = 16 * ti, j0 = 16 * tj;
+  if (i0 >= m) return;  // a whole wave (no barriers in this kernel)
+  const int ia = min(i0 + r16, m - 1), jb = min(j0 + r16, n - 1);
+  const bool iv = i0 + r16 < m, jv = j0 + r16 < n;
+  const int kbeg = tri == 1 ? j0 : tri == 2 ? i0 : 0;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  acc = tile_chain(
+      kbeg, k, kq, [&](int kk) { return iv ? (ta ? A[(size_t)kk * lda + ia] : A[(size_t)ia * lda + kk]) : 0.0; },
+      [&](int kk) { return jv ? (tb ? B[(size_t)jb * ldb + kk] : B[(size_t)kk * ldb + jb]) : 0.0; }, acc);
 #pragma unroll
-    for (int kk = 0; kk < 16; kk++) acc += As[ty][kk] * Bs[kk][tx];
-    __syncthreads();
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    if (row < m && col < n) C[(size_t)row * ldc + col] = acc[q];
   }
-  if (i0 + ty < m && j0 + tx < n) C[(size_t)(i0 + ty) * ldc + j0 + tx] = acc;
+}
+static void launch_gemm_mfma(hipStream_t s, int ta, int tb, int tri, int m, int n, int k, const double *A, int lda,
+                             const double *B, int ldb, double *C, int ldc) {
+  const int tiles = ((m + 15) / 16) * ((n + 15) / 16);
+  hipLaunchKernelGGL(k_gemm_mfma, dim3((tiles + kGemmWaves - 1) / kGemmWaves), dim3(64 * kGemmWaves), 0, s, ta, tb, tri,
+                     m, n, k, A, lda, B, ldb, C, ldc);
 }
 
 // Single-workgroup Cholesky factors of the information-form update (dense_lds.h ldl_wave: one wave
@@ -649,44 +673,75 @@ static int info_chol_mode(int nrows, int n, size_t *bytes) {
 
 // P[i][j] -= sum_k V[i][k] V[j][k] - s2 sum_k X[i][k] X[j][k]  for j >= i, mirrored;  dx = X w;
 // negative-diagonal count.   (P+ = P - V (I - s2 Z^-1) V^T, see launch_ekf_info)
+// Grid over the upper 16 x 16 tile pairs (bi <= bj) of P, 4 waves: wave w accumulates both products over the
+// k-slabs w, w + 4, ... on the matrix cores (four slabs' loads issued ahead of their MFMAs), the waves' partial
+// tiles are added in LDS in a fixed order.
 __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ V,
                                                 const double *__restrict__ X, int n, double s2,
-                                                const double *__restrict__ w, double *__restrict__ dx, int *neg, const int *gate) {
+                                                const double *__restrict__ w, double *__restrict__ dx, int *neg,
+                                                const int *gate, int nb) {
   if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
-  __shared__ double Vi[16][17], Vj[16][17], Xi[16][17], Xj[16][17];
-  int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  int bi = blockIdx.y, bj = blockIdx.x;
-  if (bj < bi) return;
-  int i0 = bi * 16, j0 = bj * 16;
-  double av = 0.0, ax = 0.0;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    bool kin = k0 + tx < n;
-    Vi[ty][tx] = (i0 + ty < N && kin) ? V[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
-    Vj[ty][tx] = (j0 + ty < N && kin) ? V[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
-    Xi[ty][tx] = (i0 + ty < N && kin) ? X[(size_t)(i0 + ty) * n + k0 + tx] : 0.0;
-    Xj[ty][tx] = (j0 + ty < N && kin) ? X[(size_t)(j0 + ty) * n + k0 + tx] : 0.0;
-    __syncthreads();
+  __shared__ double red[2][4][256];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  int b = blockIdx.x, bi = 0;
+  while (b >= nb - bi) {
+    b -= nb - bi;
+    bi++;
+  }
+  const int bj = bi + b;
+  // this thread's P element, fetched before the products so its latency is hidden
+  const int ei = threadIdx.x >> 4, ej = threadIdx.x & 15;
+  const int gi = 16 * bi + ei, gj = 16 * bj + ej;
+  const bool pw = gi < N && gj < N && (bi < bj || ej >= ei);
+  const double pv = pw ? P[(size_t)gi * ldp + gj] : 0.0;
+  const int ri = 16 * bi + r16, rj = 16 * bj + r16;
+  const bool vi = ri < N, vj = rj < N;
+  const double *Vi = V + (size_t)min(ri, N - 1) * n, *Vj = V + (size_t)min(rj, N - 1) * n;
+  const double *Xi = X + (size_t)min(ri, N - 1) * n, *Xj = X + (size_t)min(rj, N - 1) * n;
+  dbl4 av = {0.0, 0.0, 0.0, 0.0}, ax = {0.0, 0.0, 0.0, 0.0};
+  constexpr int U = 4;
+  for (int k0 = 4 * wid; k0 < n; k0 += 16 * U) {
+    double a0[U], b0[U], a1[U], b1[U];
 #pragma unroll
-    for (int kk = 0; kk < 16; kk++) {
-      av += Vi[ty][kk] * Vj[tx][kk];
-      ax += Xi[ty][kk] * Xj[tx][kk];
+    for (int u = 0; u < U; u++) {
+      const int k = k0 + 16 * u + kq;
+      const bool in = k < n;
+      a0[u] = (in && vi) ? Vi[k] : 0.0;
+      b0[u] = (in && vj) ? Vj[k] : 0.0;
+      a1[u] = (in && vi) ? Xi[k] : 0.0;
+      b1[u] = (in && vj) ? Xj[k] : 0.0;
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (k0 + 16 * u < n) {
+        av = mfma4(a0[u], b0[u], av);
+        ax = mfma4(a1[u], b1[u], ax);
+      }
   }
-  int i = i0 + ty, j = j0 + tx;
-  if (i < N && j < N && j >= i) {
-    double v = P[(size_t)i * ldp + j] - (av - s2 * ax);
-    P[(size_t)i * ldp + j] = v;
-    P[(size_t)j * ldp + i] = v;
-    if (i == j && v < 0.0) atomicAdd(neg, 1);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    red[0][wid][(kq + 4 * q) * 16 + r16] = av[q];
+    red[1][wid][(kq + 4 * q) * 16 + r16] = ax[q];
   }
-  if (bi == bj && ty == 0) {
-    int row = i0 + tx;
-    if (row < N) {
-      double a = 0.0;
-      for (int k = 0; k < n; k++) a += X[(size_t)row * n + k] * w[k];
-      dx[row] = a;
-    }
+  __syncthreads();
+  if (pw) {
+    const int e = threadIdx.x;
+    const double sv = (red[0][0][e] + red[0][1][e]) + (red[0][2][e] + red[0][3][e]);
+    const double sx = (red[1][0][e] + red[1][1][e]) + (red[1][2][e] + red[1][3][e]);
+    const double v = pv - (sv - s2 * sx);
+    P[(size_t)gi * ldp + gj] = v;
+    P[(size_t)gj * ldp + gi] = v;
+    if (gi == gj && v < 0.0) atomicAdd(neg, 1);
+  }
+  if (bi == bj && wid == 1) {
+    const int i = lane >> 2, part = lane & 3, row = 16 * bi + i;
+    double a = 0.0;
+    if (row < N)
+      for (int k = part; k < n; k += 4) a += X[(size_t)row * n + k] * w[k];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (part == 0 && row < N) dx[row] = a;
   }
 }
 
@@ -717,23 +772,22 @@ void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, 
 void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
                           double sigma2, double *Gbuf, EkfScratch &sc) {
   const int na = n + 1;
-  hipLaunchKernelGGL(k_gram_reduce, dim3((na * na + 255) / 256), dim3(256), 0, s, partials, nch, na, Gbuf, sc.neg);
+  hipLaunchKernelGGL(k_gram_reduce, dim3((na + 255) / 256, na), dim3(256), 0, s, partials, nch, na, Gbuf, sc.neg);
   double *Laug = sc.S;                            // (n+1)^2
   double *Lf = Laug + (size_t)na * na;            // n^2   L_P
   double *T1 = Lf + (size_t)n * n;                // (n+1)^2
   double *E = T1 + (size_t)na * na;               // (n+1)^2
   double *Uf = E + (size_t)na * na;               // n^2   U   (5 (n+1)^2 in total)
   double *w = sc.y;
-  dim3 g((na + 15) / 16, (na + 15) / 16);
-  hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 0, 0, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug
-  hipLaunchKernelGGL(k_gemm, g, dim3(256), 0, s, 1, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
+  launch_gemm_mfma(s, 0, 0, 1, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug (Laug lower triangular)
+  launch_gemm_mfma(s, 1, 0, 2, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
   hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2);
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
-  int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_info_P, dim3(nb, nb), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg,
-                     sc.gate);
+  const int nb = (N + 15) / 16;
+  hipLaunchKernelGGL(k_info_P, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx,
+                     sc.neg, sc.gate, nb);
 }
 
 void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,

@@ -17,39 +17,13 @@
 //
 // MFMA operand layout (f64 16x16x4): A (16x4) lane l holds A[l & 15][l >> 4]; B (4x16) lane l holds
 // B[l >> 4][l & 15]; C/D register q of lane l is D[(l >> 4) + 4 q][l & 15].
+#include <algorithm>
 #include <stdexcept>
 
 #include "dense_lds.h"
 #include "kernels.h"
 
 namespace uvhp {
-
-__device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// Accumulate one 16x16 tile over k in [0, kend): acc += sum_k A(r16, k) B(k, r16) with the operands fetched
-// through the callables (k = 4 s + kq); the loads of eight k-slabs are issued before their MFMAs, so a
-// chunk costs one memory round trip.  (32-slab chunks measured slower in k_ekf_MS / k_ekf_WP: 24.4 / 10.3
-// against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
-template <class LA, class LB>
-__device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
-  constexpr int U = 8;
-  for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
-    double a[U], b[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int k = k0 + 4 * u + kq;
-      const bool in = k < kend;
-      a[u] = in ? la(k) : 0.0;
-      b[u] = in ? lb(k) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (k0 + 4 * u < kend) acc = mfma4(a[u], b[u], acc);
-  }
-  return acc;
-}
 
 // ---------------------------------------------------------------------------------------------------
 // K1: M (blocks 0 .. nbM-1) and S_up (blocks nbM .. nbM + ceil(r/16) - 1; none when Sup is null)
@@ -325,6 +299,60 @@ __global__ void __launch_bounds__(256) k_ekf_WP(double *__restrict__ P, int ldp,
     a += __shfl_xor(a, 2, 64);
     if (part == 0 && 16 * bi + i < N) dx[16 * bi + i] = a;
   }
+}
+
+// Delayed-initialization chain step (kernels.h launch_chain_apply).  Block 0 updates the tables (one thread
+// per clone / camera) when the candidate was accepted; every block clears a rejected candidate's slot.
+__global__ void __launch_bounds__(256) k_chain_apply(const DFeatOut *__restrict__ fout, const int *__restrict__ gate,
+                                                     const int *__restrict__ neg, const double *__restrict__ dx,
+                                                     DClone *__restrict__ clones, DPoseVal *__restrict__ cv, int ncl,
+                                                     DCam *__restrict__ cams, DPoseVal *__restrict__ camv, int ncam,
+                                                     int calib_ext, int calib_intr, double *__restrict__ P, int ldp,
+                                                     int Ntot, int slot, double *__restrict__ out) {
+  const bool acc = fout->status == 0 && (!gate || *gate != 0);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!acc) {
+    for (int e = t; e < 3 * Ntot; e += gridDim.x * blockDim.x) {
+      const int i = e / 3, a = e - 3 * i;
+      P[(size_t)(slot + a) * ldp + i] = 0.0;
+      P[(size_t)i * ldp + slot + a] = 0.0;
+    }
+  } else if (blockIdx.x == 0 && dx) {
+    if (t < ncl) {  // PoseJPL::update of clone t, then the table's R_GtoI / p_IinG
+      DPoseVal &v = cv[t];
+      const double *d = dx + v.pid;
+      quat_boxplus(v.q, d);
+      for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
+      quat_2_Rot(v.q, clones[t].R);
+      for (int k = 0; k < 3; k++) clones[t].p[k] = v.p[k];
+    } else if (t < ncl + ncam) {
+      const int c = t - ncl;
+      DCam &dc = cams[c];
+      if (calib_ext && dc.pid_ext >= 0) {
+        DPoseVal &v = camv[c];
+        const double *d = dx + v.pid;
+        quat_boxplus(v.q, d);
+        for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
+        quat_2_Rot(v.q, dc.R_ItoC);
+        for (int k = 0; k < 3; k++) dc.p_IinC[k] = v.p[k];
+      }
+      if (calib_intr && dc.pid_intr >= 0)
+        for (int k = 0; k < 8; k++) dc.cam.v[k] += dx[dc.pid_intr + k];
+    }
+  }
+  if (t == 0) {
+    out[0] = acc ? 1.0 : 0.0;
+    out[1] = neg ? (double)*neg : 0.0;
+  }
+}
+
+void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, const int *neg, const double *dx,
+                        DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
+                        int calib_intr, double *P, int ldp, int Ntot, int slot, double *out) {
+  if (ncl + ncam > 256) throw std::runtime_error("delayed-init chain: more clones + cameras than one workgroup");
+  const int nb = std::max(1, std::min(16, (3 * Ntot + 255) / 256));
+  hipLaunchKernelGGL(k_chain_apply, dim3(nb), dim3(256), 0, s, fout, gate, neg, dx, clones, cv, ncl, cams, camv, ncam,
+                     calib_ext, calib_intr, P, ldp, Ntot, slot, out);
 }
 
 static void ensure_ekf_lds_attrs() {

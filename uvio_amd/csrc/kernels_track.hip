@@ -371,9 +371,17 @@ __device__ int fast_corner_score(const uint8_t *p, int ld, int thr) {
 // interior pixel stay inside the cell) into an image-sized u8 map.  Grid (cell, band of kFastBand rows)
 // so a few cells still spread over many CUs.
 constexpr int kFastBand = 8;
-__global__ void __launch_bounds__(256) k_fast_score(const uint8_t *__restrict__ img, int w, const int *__restrict__ cells,
-                                                    int sw, int sh, int thr, uint8_t *__restrict__ score) {
+__device__ __forceinline__ int fast_cam(const FastJob &job, int c) {
+  int k = 0;
+  while (k < job.ncam - 1 && c >= job.cell_end[k]) k++;
+  return k;
+}
+__global__ void __launch_bounds__(256) k_fast_score(FastJob job, const int *__restrict__ cells, int thr) {
   const int c = blockIdx.x, i0 = blockIdx.y * kFastBand;
+  const int k = fast_cam(job, c);
+  const uint8_t *__restrict__ img = job.img[k];
+  uint8_t *__restrict__ score = job.score[k];
+  const int w = job.w[k], sw = job.sw[k], sh = job.sh[k];
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
   const int rows = min(kFastBand, sh - i0);
   for (int e = threadIdx.x; e < rows * sw; e += blockDim.x) {
@@ -393,16 +401,18 @@ __host__ __device__ inline int fast_max_cand(int sw, int sh) { return ((sw + 1) 
 __host__ __device__ inline size_t fast_lds_bytes(int sw, int sh) {
   return (size_t)fast_max_cand(sw, sh) * 8 + (((size_t)sw * sh + 15) & ~(size_t)15);
 }
-__global__ void __launch_bounds__(kFastThreads) k_fast_select(const uint8_t *__restrict__ scmap, int w,
-                                                              const int *__restrict__ cells, int sw, int sh, int kmax,
+__global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const int *__restrict__ cells, int kmax,
                                                               float *__restrict__ out, int *__restrict__ out_n) {
   extern __shared__ int lds_fast[];
+  const int c = blockIdx.x;
+  const int cam = fast_cam(job, c);
+  const uint8_t *__restrict__ scmap = job.score[cam];
+  const int w = job.w[cam], sw = job.sw[cam], sh = job.sh[cam];
   const int kFastMaxCand = fast_max_cand(sw, sh);
   const int area = sw * sh;
   int *cand_idx = lds_fast, *cand_s = lds_fast + kFastMaxCand;
   uint8_t *score = (uint8_t *)(cand_s + kFastMaxCand);
   __shared__ int ncand;
-  const int c = blockIdx.x;
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
   if (threadIdx.x == 0) ncand = 0;
   for (int e = threadIdx.x; e < area; e += blockDim.x) {
@@ -502,9 +512,8 @@ __device__ __forceinline__ float px_clamped(const uint8_t *img, int w, int h, in
 // terms in LDS; lane 0 then accumulates them in the oracle's raster order (the double sums are
 // order-sensitive), so the result is bit-identical to the sequential cornerSubPix.
 constexpr int kSubpixMaxWin = 5, kSubpixMargin = 3;
-__global__ void __launch_bounds__(64) k_subpix(const uint8_t *__restrict__ img, int w, int h, float *__restrict__ pts,
-                                               int n, const float *__restrict__ mask, int win, int max_iters,
-                                               double eps2) {
+__global__ void __launch_bounds__(64) k_subpix(SubpixJob job, float *__restrict__ pts, const float *__restrict__ mask,
+                                               int win, int max_iters, double eps2) {
   constexpr int kBw = 2 * kSubpixMaxWin + 3, kT = (2 * kSubpixMaxWin + 1) * (2 * kSubpixMaxWin + 1);
   constexpr int kTile = kBw + 1 + 2 * kSubpixMargin;
   __shared__ float tile[kTile * kTile];  // clamped image neighbourhood (u8 as float)
@@ -514,7 +523,11 @@ __global__ void __launch_bounds__(64) k_subpix(const uint8_t *__restrict__ img, 
   __shared__ float cur[2];
   __shared__ int done;
   const int p = blockIdx.x, lane = threadIdx.x;
-  if (p >= n) return;
+  int cam = 0;
+  while (cam < job.ncam - 1 && p >= job.end[cam]) cam++;
+  if (p >= job.end[cam]) return;
+  const uint8_t *__restrict__ img = job.img[cam];
+  const int w = job.w[cam], h = job.h[cam];
   const int win_w = 2 * win + 1, bw = win_w + 2, nt = win_w * win_w, S = bw + 1 + 2 * kSubpixMargin;
   const float cTx = pts[2 * p], cTy = pts[2 * p + 1];
   if (lane == 0) {
@@ -1029,25 +1042,56 @@ void launch_pyramid(hipStream_t s, DPyr &p) {
   }
 }
 
+void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n) {
+  if (job.ncam <= 0 || job.ncam > kMaxCams) return;
+  const int ncell = job.cell_end[job.ncam - 1];
+  if (ncell <= 0) return;
+  size_t lds = 0;
+  int shmax = 0;
+  for (int k = 0; k < job.ncam; k++) {
+    if (kmax > kFastMaxK || job.sw[k] * job.sh[k] > 65536)
+      throw std::runtime_error("FAST cell / per-cell count beyond the kernel's limits");
+    lds = max(lds, fast_lds_bytes(job.sw[k], job.sh[k]));
+    shmax = max(shmax, job.sh[k]);
+  }
+  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_select, (int)lds) < (int)lds)
+    throw std::runtime_error("FAST cell too large for LDS");
+  hipLaunchKernelGGL(k_fast_score, dim3(ncell, (shmax + kFastBand - 1) / kFastBand), dim3(256), 0, s, job, cells, thr);
+  hipLaunchKernelGGL(k_fast_select, dim3(ncell), dim3(kFastThreads), lds, s, job, cells, kmax, out, out_n);
+}
+
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
                        int kmax, float *out, int *out_n, uint8_t *score_map) {
   (void)h;
-  if (ncell <= 0) return;
-  const size_t lds = fast_lds_bytes(sw, sh);
-  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_select, (int)lds) < (int)lds)
-    throw std::runtime_error("FAST cell too large for LDS");
-  if (kmax > kFastMaxK || sw * sh > 65536) throw std::runtime_error("FAST cell / per-cell count beyond the kernel's limits");
-  hipLaunchKernelGGL(k_fast_score, dim3(ncell, (sh + kFastBand - 1) / kFastBand), dim3(256), 0, s, img, w, cells, sw, sh,
-                     thr, score_map);
-  hipLaunchKernelGGL(k_fast_select, dim3(ncell), dim3(kFastThreads), lds, s, score_map, w, cells, sw, sh, kmax, out,
-                     out_n);
+  FastJob job{};
+  job.img[0] = img;
+  job.score[0] = score_map;
+  job.w[0] = w;
+  job.sw[0] = sw;
+  job.sh[0] = sh;
+  job.cell_end[0] = ncell;
+  job.ncam = 1;
+  launch_fast_multi(s, job, cells, thr, kmax, out, out_n);
+}
+
+void launch_subpix_multi(hipStream_t s, const SubpixJob &job, float *pts, const float *mask, int win, int max_iters,
+                         double eps2) {
+  if (job.ncam <= 0 || job.ncam > kMaxCams) return;
+  const int n = job.end[job.ncam - 1];
+  if (n <= 0) return;
+  if (win > kSubpixMaxWin) throw std::runtime_error("cornerSubPix window larger than the kernel's LDS patch");
+  hipLaunchKernelGGL(k_subpix, dim3(n), dim3(64), 0, s, job, pts, mask, win, max_iters, eps2);
 }
 
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
                    int max_iters, double eps2) {
-  if (n <= 0) return;
-  if (win > kSubpixMaxWin) throw std::runtime_error("cornerSubPix window larger than the kernel's LDS patch");
-  hipLaunchKernelGGL(k_subpix, dim3(n), dim3(64), 0, s, img, w, h, pts, n, mask, win, max_iters, eps2);
+  SubpixJob job{};
+  job.img[0] = img;
+  job.w[0] = w;
+  job.h[0] = h;
+  job.end[0] = n;
+  job.ncam = 1;
+  launch_subpix_multi(s, job, pts, mask, win, max_iters, eps2);
 }
 
 void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,

@@ -91,11 +91,23 @@ class Tracker {
   void sync();
   const std::vector<int> &subsets(int count);
 
-  void feed_monocular(double t, int cam, const DbSink &db);
+  // one Grider_GRID request: camera, pyramid, user mask, min-distance boxes, cells to fill -> corners
+  struct GridReq {
+    int cam;
+    const DPyr *p;
+    const std::vector<uint8_t> *user_mask;
+    const std::vector<int> *boxes;
+    std::vector<std::pair<int, int>> valid;
+    std::vector<KeyPt> out;
+  };
+  struct MonoDet;
+
+  void feed_multi(double t, const int *cams, int n, const DbSink &db);
   void feed_stereo(double t, int cl, int cr, const DbSink &db);
-  // detection on pyramid `p` of camera `cam` (user mask `mask`); kept / new points in pts / ids
-  void detect_monocular(int cam, const DPyr &p, const std::vector<uint8_t> &mask, std::vector<KeyPt> &pts,
-                        std::vector<size_t> &ids);
+  void detect_mono_pre(MonoDet &m);
+  void detect_mono_post(MonoDet &m);
+  void detect_mono_multi(MonoDet *m, int n);
+  void griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vector<KeyPt> *lk_pts, std::vector<uint8_t> *lk_st);
   void detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, const std::vector<uint8_t> &m0,
                      const std::vector<uint8_t> &m1, std::vector<KeyPt> &pts0, std::vector<KeyPt> &pts1,
                      std::vector<size_t> &ids0, std::vector<size_t> &ids1);

@@ -24,6 +24,13 @@ def load_options(yaml_path=None, **overrides):
     return opts
 
 
+def _mask_ptrs(masks, ncam):
+    """per-camera u8 masks (None: no mask for that camera) -> (kept arrays, uint8_t*[ncam])"""
+    mk = [None if m is None else np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
+    ptrs = [C.POINTER(C.c_uint8)() if m is None else m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in mk]
+    return mk, (C.POINTER(C.c_uint8) * ncam)(*ptrs)
+
+
 def apply_overrides(opts, overrides):
     for k, v in overrides.items():
         if not hasattr(opts, k):
@@ -196,8 +203,7 @@ class VioManager:
         strides = (C.c_int * ncam)(*[im.strides[0] for im in imgs])
         mptr = None
         if masks is not None:
-            mk = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
-            mptr = (C.POINTER(C.c_uint8) * ncam)(*[m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in mk])
+            mk, mptr = _mask_ptrs(masks, ncam)
         rc = self._call("feed_camera", self._h, C.c_double(t), ncam, cam, ptrs, strides, mptr)
         if rc == N.E_STATE and allow_uninit:
             return rc
@@ -218,8 +224,7 @@ class VioManager:
         strides = (C.c_int * ncam)(*[im.stride(0) for im in images])
         mptr = None
         if masks is not None:
-            mk = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
-            mptr = (C.POINTER(C.c_uint8) * ncam)(*[m.ctypes.data_as(C.POINTER(C.c_uint8)) for m in mk])
+            mk, mptr = _mask_ptrs(masks, ncam)
         rc = self._call("feed_camera_device", self._h, C.c_double(t), ncam, cam, ptrs, strides, mptr)
         if rc == N.E_STATE and allow_uninit:
             return rc
