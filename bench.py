@@ -99,6 +99,7 @@ WORKLOADS = {
 }
 
 # oracle frames in the cpu_baseline sample (~10-30 s of single-core CPU work per workload)
+CPU_CV_THREADS = 4  # num_opencv_threads of every reference config
 CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg3": 60, "cfg4": 20, "cfg5": 10, "cfg4t": 3, "cfg5t": 2}
 
 
@@ -507,6 +508,10 @@ def main():
 def cpu_baseline(opts, wl, warmup, frames, dev_frames):
     """oracle/ (the CPU restatement) on the same stream (rank 0's), one thread, bounded sample."""
     from oracle import oracle as O
+    # the reference's configs run OpenCV on num_opencv_threads = 4 (config/*/estimator_config.yaml:87-89): the
+    # oracle's restated parallel OpenCV calls (LK per point, pyrDown / Scharr per row) use as many; the estimator
+    # itself is single-threaded in the reference
+    threads = O.set_threads(CPU_CV_THREADS)
     sim = make_stream(opts, warmup + frames + 2, seed=5, workload=wl)
     host = None
     if dev_frames is not None:
@@ -521,10 +526,11 @@ def cpu_baseline(opts, wl, warmup, frames, dev_frames):
     for _ in range(frames):
         drv.step()
     dt = time.perf_counter() - t0
-    return {"value": frames / dt, "unit": "frames/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
-            "sample": "%d frames of the %s %s stream after %d warm-up frames, oracle/liboracle.so (g++ -O3, one "
-                      "thread: the reference estimator is single-threaded; its tracker's cv::parallel_for_ is not "
-                      "restated)" % (frames, wl, "image" if dev_frames is not None else "track", warmup)}
+    O.set_threads(1)
+    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "sample": "%d frames of the %s %s stream after %d warm-up frames, oracle/liboracle.so (g++ -O3): the "
+                      "tracker's OpenCV-parallel calls on %d threads (num_opencv_threads), the estimator on one (as "
+                      "the reference)" % (frames, wl, "image" if dev_frames is not None else "track", warmup, threads)}
 
 
 if __name__ == "__main__":

@@ -129,6 +129,11 @@ typedef struct {
    * 631-644); the file is recreated at uvio_hp_create */
   int record_timing_information;
   char record_timing_filepath[256];
+  /* InertialInitializerOptions (InertialInitializerOptions.h:64-76): the static initializer's window (also
+   * the IMU kept before initialization, VioManager.cpp:174-176), accelerometer excitation threshold, rest
+   * disparity threshold; init_dyn_use selects the dynamic initializer, which is not built */
+  double init_window_time, init_imu_thresh, init_max_disparity;
+  int init_dyn_use;
 } uvio_hp_options_t;
 
 /* Per-frame stage timings in seconds, the reference CSV schema

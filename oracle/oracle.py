@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 _ORC_NAMES = ["create", "destroy", "initialize_with_gt", "feed_imu", "feed_simulation", "feed_uwb", "init_anchors",
               "get_imu_state", "get_cov_dim", "get_cov", "get_state_vector", "get_timing", "get_clone_times",
               "ekf_update", "compress", "debug_last_msckf", "debug_frame_feats", "get_fej_vector",
-              "msckf_compressed_update", "feed_camera", "get_tracks", "get_pyramid", "get_active_tracks"]
+              "msckf_compressed_update", "feed_camera", "get_tracks", "get_pyramid", "get_active_tracks", "initialized"]
 
 _lib = None
 
@@ -56,6 +56,7 @@ def load():
         lib.orc_set_steer.argtypes = [C.c_void_p, C.c_int, C.c_int, i32p, u64p, dp, i32p, dp]
         lib.orc_get_steer_log.argtypes = [C.c_void_p, i32p, u64p, i32p, C.POINTER(C.c_int64), dp, dp, dp, i32p, i32p,
                                           C.c_int, i32p]
+        lib.orc_static_initialize.argtypes = [C.POINTER(N.Options), C.c_int, dp, dp, dp, C.c_int, dp, dp]
         lib.orc_chi2_quantile95.restype = C.c_double
         lib.orc_chi2_quantile95.argtypes = [C.c_int]
         lib.orc_camera_distort.argtypes = [C.POINTER(N.Camera), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -154,6 +155,26 @@ class OracleManager(VioManager):
 
 def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def set_threads(n):
+    """threads of the restated OpenCV calls (num_opencv_threads: LK per point, pyrDown / Scharr per row)"""
+    lib = load()
+    lib.orc_set_threads.argtypes = [C.c_int]
+    return lib.orc_set_threads(int(n))
+
+
+def static_initialize(opts, t, wm, am, wait_for_jerk):
+    """StaticInitializer::initialize (StaticInitializer.cpp:37-165) on one IMU buffer: (t_init, state16) or None."""
+    lib = load()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    wm = np.ascontiguousarray(wm, dtype=np.float64)
+    am = np.ascontiguousarray(am, dtype=np.float64)
+    ti = C.c_double()
+    x = np.zeros(16)
+    ok = lib.orc_static_initialize(C.byref(opts), len(t), _dp(t), _dp(wm), _dp(am), int(bool(wait_for_jerk)), C.byref(ti),
+                                   _dp(x))
+    return (ti.value, x) if ok else None
 
 
 def chi2_quantile95(dof):

@@ -77,6 +77,26 @@ int orc_init_anchors(orc_handle *h, int n, const uvio_hp_anchor_t *a) {
   std::vector<uvio_hp_anchor_t> v(a, a + n);
   return h->m.init_anchors(v);
 }
+// StaticInitializer::initialize alone on an IMU window (CPU tests of its branches): 1 initialized (state16 =
+// q p v bg ba, *t the state time), 0 not
+int orc_static_initialize(const uvio_hp_options_t *opts, int n, const double *t, const double *wm, const double *am,
+                          int wait_for_jerk, double *t_init, double state16[16]) {
+  InertialInitializer ini(*opts);
+  for (int i = 0; i < n; i++) {
+    ImuData d;
+    d.t = t[i];
+    for (int k = 0; k < 3; k++) d.wm[k] = wm[3 * i + k], d.am[k] = am[3 * i + k];
+    ini.imu_data.push_back(d);
+  }
+  Mat cov, x;
+  if (!ini.static_initialize(t_init, cov, x, wait_for_jerk != 0)) return 0;
+  for (int k = 0; k < 16; k++) state16[k] = x[k];
+  return 1;
+}
+int orc_initialized(orc_handle *h, int *out) {
+  *out = h->m.is_initialized ? 1 : 0;
+  return 0;
+}
 int orc_get_imu_state(orc_handle *h, double *t, double out[16]) {
   *t = h->m.state.timestamp;
   for (int k = 0; k < 16; k++) out[k] = h->m.state.imu->val[k];
@@ -297,6 +317,12 @@ int orc_compress(const double *A, int m, int n, double *R_out) {
 }
 
 double orc_chi2_quantile95(int dof) { return chi2_quantile95(dof); }
+
+// threads of the restated OpenCV calls (num_opencv_threads; 1 = serial)
+int orc_set_threads(int n) {
+  set_cv_threads(n);
+  return cv_threads();
+}
 
 // per-feature results of every updater call of the last frame (include/uvio_hp.h uvio_hp_debug_frame_feats)
 int orc_debug_frame_feats(orc_handle *h, int *kind, uint64_t *ids, double *pG, int *status, double *chi2, int cap,

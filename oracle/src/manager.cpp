@@ -11,7 +11,7 @@ using clk = std::chrono::steady_clock;
 static double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
 Manager::Manager(const uvio_hp_options_t &opt)
-    : o(opt), state(opt), prop(opt), msckf(opt), slam(opt), uwb(opt), currid(4 * (size_t)opt.max_aruco_features + 1) {
+    : o(opt), state(opt), prop(opt), msckf(opt), slam(opt), uwb(opt), initializer(opt), currid(4 * (size_t)opt.max_aruco_features + 1) {
   msckf.dbg = &fdbg;
   slam.dbg = &fdbg;
   tracker.num_features = (int)std::floor((double)opt.init_max_features / (double)opt.num_cameras);
@@ -59,7 +59,7 @@ void Manager::initialize_with_gt(const double x[17]) {
 void Manager::feed_imu(double t, const double wm[3], const double am[3]) {
   double oldest_time = state.margtimestep();
   if (oldest_time > state.timestamp) oldest_time = -1;
-  if (!is_initialized) oldest_time = t - 2.0 + state.calib_dt->val[0] - 0.10;
+  if (!is_initialized) oldest_time = t - o.init_window_time + state.calib_dt->val[0] - 0.10;
   ImuData d;
   d.t = t;
   for (int k = 0; k < 3; k++) {
@@ -67,6 +67,7 @@ void Manager::feed_imu(double t, const double wm[3], const double am[3]) {
     d.am[k] = am[k];
   }
   prop.feed_imu(d, oldest_time);
+  if (!is_initialized) initializer.feed_imu(d, oldest_time);
   if (is_initialized && zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) zupt->feed_imu(d, oldest_time);
 }
 
@@ -143,12 +144,32 @@ int Manager::feed_simulation(double t, const std::vector<int> &camids,
   return after_tracking(t, camids, rT1);
 }
 
-int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1) {
+// VioManagerHelper.cpp:78-190 (the thread's body, run inline: use_multi_threading_subs off)
+bool Manager::try_to_initialize() {
+  double timestamp = 0;
+  Mat covariance, imu_state;
+  bool wait_for_jerk = (zupt == nullptr);
+  if (!initializer.initialize(db, &timestamp, covariance, imu_state, wait_for_jerk)) return false;
+  for (int k = 0; k < 16; k++) state.imu->val[k] = state.imu->fej[k] = imu_state[k];
+  StateHelper::set_initial_covariance(state, covariance, {ref_of(state.imu)});
+  state.timestamp = timestamp;
+  startup_time = timestamp;
+  db.cleanup_measurements(state.timestamp);
+  tracker.num_features = (int)std::floor((double)o.num_pts / (double)o.num_cameras);
+  if (norm(state.imu->vel()) > o.zupt_max_velocity) has_moved_since_zupt = true;
+  return true;
+}
+
+int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, bool try_init) {
   auto rT2 = clk::now();
   timing = uvio_hp_timing_t{};
   timing.tracking = secs(rT1, rT2);
   fdbg.feats.clear();
-  if (!is_initialized) return UVIO_HP_E_STATE;
+  // VioManager.cpp:308-317 (camera frames only; a simulated frame needs an initialized filter, :236-240)
+  if (!is_initialized) {
+    if (!try_init || !try_to_initialize()) return UVIO_HP_E_STATE;
+    is_initialized = true;
+  }
   // UVioManager.cpp:147-162 / VioManager.cpp:291-307: zero-velocity update; on success the frame ends here
   if (zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) {
     if (state.timestamp != t) {
@@ -187,7 +208,7 @@ int Manager::feed_camera(double t, const std::vector<int> &camids, const std::ve
                          const std::vector<GrayImg> &masks) {
   auto rT1 = clk::now();
   tracker.feed(t, camids, imgs, masks, db);
-  return after_tracking(t, camids, rT1);
+  return after_tracking(t, camids, rT1, true);
 }
 
 // VioManager.cpp:323-651

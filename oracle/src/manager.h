@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 
+#include "init.h"
 #include "propagator.h"
 #include "tracker.h"
 #include "updater.h"
@@ -32,6 +33,7 @@ struct Manager {
   UpdaterSLAM slam;
   UpdaterUWB uwb;
   FeatureDatabase db;
+  InertialInitializer initializer;  // VioManager.cpp:150-153 (static initializer, init.h)
   TrackKLT tracker;
   size_t currid;
   bool is_initialized = false;
@@ -67,7 +69,10 @@ struct Manager {
   int do_feature_propagate_update(double t, const std::vector<int> &camids);
   int do_uwb_propagate_update(const UwbMsg &m);
   // UVioManager.cpp:147-205 after the tracker: ZUPT, UWB ranges, feature propagate / update
-  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1);
+  int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1,
+                     bool try_init = false);
+  // VioManager::try_to_initialize (VioManagerHelper.cpp:78-190), single-threaded
+  bool try_to_initialize();
   void retriangulate_active_tracks(double t, const std::vector<int> &camids);
 };
 

@@ -4,11 +4,94 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 #include "feat.h"
 
 namespace orc {
+
+// cv::parallel_for_ stand-in for the CPU baseline: the reference's configs run OpenCV with
+// num_opencv_threads 4 (config/*/estimator_config.yaml:87-89), and calcOpticalFlowPyrLK (per point),
+// pyrDown and the Scharr derivatives (per row) are the parallel OpenCV calls of the KLT front-end.
+// Work items are independent, so the results do not depend on the thread count (tests compare 1 vs 4).
+namespace {
+struct CvPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  const std::function<void(size_t, size_t)> *job = nullptr;
+  size_t n = 0, chunks = 0, next = 0, done = 0;
+  long gen = 0;
+  bool stop = false;
+  ~CvPool() { resize(0); }
+  void resize(int k) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+    th.clear();
+    stop = false;
+    for (int i = 0; i < k; i++) th.emplace_back([this] { loop(); });
+  }
+  void loop() {
+    long seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return stop || (job && gen != seen); });
+      if (stop) return;
+      seen = gen;
+      work(l);
+    }
+  }
+  // claims chunks until none is left (called with the lock held)
+  void work(std::unique_lock<std::mutex> &l) {
+    while (next < chunks) {
+      const size_t c = next++;
+      const auto *f = job;
+      const size_t lo = n * c / chunks, hi = n * (c + 1) / chunks;
+      l.unlock();
+      (*f)(lo, hi);
+      l.lock();
+      if (++done == chunks) done_cv.notify_all();
+    }
+  }
+  void run(size_t count, const std::function<void(size_t, size_t)> &f) {
+    std::unique_lock<std::mutex> l(mu);
+    job = &f;
+    n = count;
+    chunks = std::min(count, (size_t)(4 * (th.size() + 1)));
+    next = done = 0;
+    gen++;
+    cv.notify_all();
+    work(l);
+    done_cv.wait(l, [&] { return done == chunks; });
+    job = nullptr;
+  }
+};
+CvPool g_pool;
+int g_threads = 1;
+}  // namespace
+
+void set_cv_threads(int k) {
+  k = std::max(1, k);
+  if (k == g_threads) return;
+  g_pool.resize(k - 1);
+  g_threads = k;
+}
+int cv_threads() { return g_threads; }
+void cv_parallel_for(size_t n, const std::function<void(size_t, size_t)> &f) {
+  if (g_threads <= 1 || n < 2) {
+    if (n) f(0, n);
+    return;
+  }
+  g_pool.run(n, f);
+}
 
 static inline int reflect101(int p, int n) {
   if (n == 1) return 0;
@@ -50,33 +133,37 @@ GrayImg pyr_down(const GrayImg &src) {
   dst.h = (src.h + 1) / 2;
   dst.d.resize((size_t)dst.w * dst.h);
   static const int k[5] = {1, 4, 6, 4, 1};
-  for (int y = 0; y < dst.h; y++)
-    for (int x = 0; x < dst.w; x++) {
-      int acc = 0;
-      for (int i = 0; i < 5; i++) {
-        int sy = reflect101(2 * y + i - 2, src.h);
-        int row = 0;
-        for (int j = 0; j < 5; j++) row += k[j] * src.at(reflect101(2 * x + j - 2, src.w), sy);
-        acc += k[i] * row;
+  cv_parallel_for((size_t)dst.h, [&](size_t y0, size_t y1) {
+    for (int y = (int)y0; y < (int)y1; y++)
+      for (int x = 0; x < dst.w; x++) {
+        int acc = 0;
+        for (int i = 0; i < 5; i++) {
+          int sy = reflect101(2 * y + i - 2, src.h);
+          int row = 0;
+          for (int j = 0; j < 5; j++) row += k[j] * src.at(reflect101(2 * x + j - 2, src.w), sy);
+          acc += k[i] * row;
+        }
+        dst.d[(size_t)y * dst.w + x] = (uint8_t)((acc + 128) >> 8);
       }
-      dst.d[(size_t)y * dst.w + x] = (uint8_t)((acc + 128) >> 8);
-    }
+  });
   return dst;
 }
 
 // calcSharrDeriv (lkpyramid.cpp): dx = [3 10 3]^T (x) [-1 0 1], dy = its transpose, reflect-101 borders
 std::vector<int16_t> scharr_deriv(const GrayImg &s) {
   std::vector<int16_t> d((size_t)s.w * s.h * 2);
-  for (int y = 0; y < s.h; y++) {
-    int y0 = reflect101(y - 1, s.h), y2 = reflect101(y + 1, s.h);
-    auto t0 = [&](int x) { return (s.at(x, y0) + s.at(x, y2)) * 3 + s.at(x, y) * 10; };
-    auto t1 = [&](int x) { return s.at(x, y2) - s.at(x, y0); };
-    for (int x = 0; x < s.w; x++) {
-      int xm = reflect101(x - 1, s.w), xp = reflect101(x + 1, s.w);
-      d[((size_t)y * s.w + x) * 2] = (int16_t)(t0(xp) - t0(xm));
-      d[((size_t)y * s.w + x) * 2 + 1] = (int16_t)((t1(xp) + t1(xm)) * 3 + t1(x) * 10);
+  cv_parallel_for((size_t)s.h, [&](size_t ya, size_t yb) {
+    for (int y = (int)ya; y < (int)yb; y++) {
+      int y0 = reflect101(y - 1, s.h), y2 = reflect101(y + 1, s.h);
+      auto t0 = [&](int x) { return (s.at(x, y0) + s.at(x, y2)) * 3 + s.at(x, y) * 10; };
+      auto t1 = [&](int x) { return s.at(x, y2) - s.at(x, y0); };
+      for (int x = 0; x < s.w; x++) {
+        int xm = reflect101(x - 1, s.w), xp = reflect101(x + 1, s.w);
+        d[((size_t)y * s.w + x) * 2] = (int16_t)(t0(xp) - t0(xm));
+        d[((size_t)y * s.w + x) * 2 + 1] = (int16_t)((t1(xp) + t1(xm)) * 3 + t1(x) * 10);
+      }
     }
-  }
+  });
   return d;
 }
 
@@ -269,11 +356,13 @@ void lk_track(const Pyramid &prev, const Pyramid &next, const std::vector<KeyPt>
   const int W_BITS = 14;
   const float FLT_SCALE = 1.f / (1 << 20);
   const float crit_eps = eps * eps;
-  std::vector<int> Iw((size_t)win * win), dIx((size_t)win * win), dIy((size_t)win * win);
   for (int level = maxL; level >= 0; level--) {
     const GrayImg &I = prev.img[level], &J = next.img[level];
     const auto &dI = prev.deriv[level];
-    for (size_t pi = 0; pi < n; pi++) {
+    // calcOpticalFlowPyrLK: parallel_for_ over the points of each level (lkpyramid.cpp LKTrackerInvoker)
+    cv_parallel_for(n, [&](size_t plo, size_t phi) {
+    std::vector<int> Iw((size_t)win * win), dIx((size_t)win * win), dIy((size_t)win * win);
+    for (size_t pi = plo; pi < phi; pi++) {
       float sc = (float)(1. / (1 << level));
       float prx = p0[pi].x * sc, pry = p0[pi].y * sc;
       float nx, ny;
@@ -369,6 +458,7 @@ void lk_track(const Pyramid &prev, const Pyramid &next, const std::vector<KeyPt>
         pdy = dy;
       }
     }
+    });
   }
 }
 

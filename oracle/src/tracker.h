@@ -12,6 +12,7 @@
 // float vs int accumulation of LK sums), this file fixes one deterministic choice and the device
 // follows the same choice: equal responses keep raster order; LK sums are exact integers.
 #pragma once
+#include <functional>
 #include <cstdint>
 #include <unordered_map>
 #include <vector>
@@ -49,6 +50,10 @@ std::vector<KeyPt> fast_roi(const GrayImg &img, int x0, int y0, int w, int h, in
 // cv::cornerSubPix(win 5x5, zeroZone -1, 20 iterations, eps 1e-3)
 void corner_subpix(const GrayImg &img, std::vector<KeyPt> &pts, int win, int max_iters, double eps);
 // cv::calcOpticalFlowPyrLK(win, maxLevel, COUNT|EPS 30 / 0.01, OPTFLOW_USE_INITIAL_FLOW, minEig 1e-4)
+// cv::parallel_for_ stand-in (tracker.cpp): thread count of the OpenCV calls, a parallel loop over [0, n)
+void set_cv_threads(int k);
+int cv_threads();
+void cv_parallel_for(size_t n, const std::function<void(size_t, size_t)> &f);
 void lk_track(const Pyramid &prev, const Pyramid &next, const std::vector<KeyPt> &p0, std::vector<KeyPt> &p1,
               std::vector<uint8_t> &status, int win, int max_level, int max_iters, float eps);
 // cv::findFundamentalMat(FM_RANSAC, thr, 0.999) mask (7-point RANSAC, cv::RNG((uint64)-1))

@@ -115,7 +115,7 @@ def _free_run(opts, n_frames, **simkw):
 def _snap(m):
     x, meta = m.get_state_vector()
     return {"x": x, "meta": meta, "P": m.get_cov(), "timing": m.get_timing(), "imu": m.get_imu_state()[1],
-            "feats": m.debug_last_msckf(), "frame": m.debug_frame_feats()}
+            "feats": m.debug_last_msckf(), "frame": m.debug_frame_feats(), "init": m.initialized()}
 
 
 class Steps(list):
@@ -126,9 +126,12 @@ class Steps(list):
 STEER_MARGIN = 1e-10  # an explained disagreement: one cast within this relative distance of its rounding tie
 
 
-def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None, steer=True, mgr=None, pre_frame=None):
+def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None, steer=True, mgr=None, pre_frame=None,
+                 init="gt"):
     """Device and oracle on the same stream: before every frame the oracle adopts the device's state; right
-    before its feed it gets the device's per-feature results of that frame (rounding-tie steering)."""
+    before its feed it gets the device's per-feature results of that frame (rounding-tie steering).  With
+    init="static" both start uninitialized and run their own static initializers; the oracle adopts the
+    device's state only once the device is initialized (the initialization frame itself is independent)."""
     import uvio_amd as U
     from oracle import oracle as O
     g = mgr if mgr is not None else U.VioManager(opts)
@@ -136,6 +139,8 @@ def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None
     steps = Steps()
 
     def before(nf, t):
+        if init == "static" and not g.initialized():
+            return
         o.set_state(g.get_state_vector()[0], g.get_fej_vector(), g.get_cov())
         if pre_frame is not None:
             pre_frame(nf, t, g, o)
@@ -151,7 +156,7 @@ def run_lockstep(opts, sim, n_frames, renderer=None, after_init=None, extra=None
         steps.append((a, b))
 
     sim.run([g, o], n_frames=n_frames, before_frame=before, before_feed=before_feed, on_frame=after,
-            renderer=renderer, after_init=after_init)
+            renderer=renderer, after_init=after_init, init=init)
     steps.steer = o.steer_log()
     if mgr is None:
         g.close()
@@ -220,6 +225,7 @@ def _check_lockstep(steps, max_events=None):
         assert a["timing"]["n_slam"] == b["timing"]["n_slam"]
         assert a["timing"]["n_slam_delayed"] == b["timing"]["n_slam_delayed"]
         assert a["timing"]["n_anchor_change"] == b["timing"]["n_anchor_change"]
+        assert a["init"] == b["init"], ("initialized differs", k)
         p, c = _compare_feats(a["feats"], b["feats"])
         p2, c2 = _compare_frame(a["frame"], b["frame"])
         x, P = _rel(a["x"], b["x"]), _rel(a["P"], b["P"])

@@ -321,3 +321,34 @@ def test_ransac_needs_seven_points():
     rng = np.random.default_rng(6)
     x0, x1, _ = _two_views(rng, 6)
     assert O.ransac_mask(x0, x1, 0.01).sum() == 0
+
+
+def test_oracle_tracker_threads_give_identical_tracks(euroc_yaml):
+    """The CPU baseline runs the restated OpenCV calls (LK per point, pyrDown / Scharr per row) on
+    num_opencv_threads = 4 threads, as the reference's configs do (config/euroc_mav/estimator_config.yaml:89):
+    every work item is independent, so the tracks must not depend on the thread count."""
+    import uvio_amd as U
+    from oracle import oracle as O
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(euroc_yaml, init_max_features=200)
+    n = 6
+    sim = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=4)
+    r = SceneRenderer(opts, device="cpu")
+    frames = [[r.render(k, *sim.camera_pose(i, k), frame_seed=i).numpy() for k in range(2)] for i in range(n)]
+    runs = []
+    for threads in (1, 4):
+        assert O.set_threads(threads) == threads
+        o = O.OracleManager(opts)
+        tr = []
+        for i in range(n):
+            o.feed_measurement_camera(sim.cam_t[i], [0, 1], frames[i], allow_uninit=True)
+            tr.append([o.get_tracks(c) for c in (0, 1)])
+        runs.append(tr)
+    O.set_threads(1)
+    total = 0
+    for a, b in zip(*runs):
+        for (ia, ua), (ib, ub) in zip(a, b):
+            assert np.array_equal(ia, ib) and np.array_equal(ua, ub)
+            total += len(ia)
+    assert total > 200

@@ -1,0 +1,147 @@
+"""Static initializer (StaticInitializer.cpp:37-165 via InertialInitializer.cpp:73-147 and
+VioManagerHelper.cpp:78-190): the oracle restatement against an independent numpy statement of the same
+formulas, its branches (rest / jerk / moving / short buffer), and a resting image stream that starts the
+filter without initialize_with_gt.  CPU only; the device engine is checked against the oracle in
+tests/test_gpu_static_init.py."""
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+IROS = os.path.join(ROOT, "configs", "iros_2023_uvio", "estimator_config.yaml")
+EUROC = os.path.join(ROOT, "configs", "euroc_mav", "estimator_config.yaml")
+
+
+def _numpy_static(opts, t, wm, am, wait_for_jerk):
+    """StaticInitializer::initialize restated in numpy: (t_init, q_GtoI, bg, ba) or None."""
+    w = opts.init_window_time
+    if len(t) < 2 or t[-1] - t[0] < w:
+        return None
+    newest = t[-1]
+    m10 = (t > newest - 0.5 * w) & (t <= newest)
+    m21 = (t > newest - w) & (t <= newest - 0.5 * w)
+    if m10.sum() < 2 or m21.sum() < 2:
+        return None
+
+    def stats(m):
+        a = am[m].mean(axis=0)
+        return a, np.sqrt(np.sum((am[m] - a) ** 2) / (m.sum() - 1))
+
+    a10, v10 = stats(m10)
+    a21, v21 = stats(m21)
+    thr = opts.init_imu_thresh
+    if wait_for_jerk and (v10 < thr or v21 > thr):
+        return None
+    if not wait_for_jerk and (v10 > thr or v21 > thr):
+        return None
+    z = a21 / np.linalg.norm(a21)
+    x = np.array([1.0, 0.0, 0.0]) - z * z[0]
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    y /= np.linalg.norm(y)
+    R_GtoI = np.stack([x, y, z], axis=1)
+    ba = a21 - opts.gravity_mag * z  # R_GtoI e_z = z
+    return t[m21][-1], R_GtoI, wm[m21].mean(axis=0), ba
+
+
+def _imu(rng, n, rate=200.0, t0=0.3, g=9.81, tilt=(0.1, -0.05), noise=0.02, bg=(1e-3, -2e-3, 5e-4),
+         ba=(0.02, -0.01, 0.03)):
+    t = t0 + np.arange(n) / rate
+    gI = g * np.array([np.sin(tilt[1]), -np.sin(tilt[0]) * np.cos(tilt[1]), np.cos(tilt[0]) * np.cos(tilt[1])])
+    am = gI + np.array(ba) + noise * rng.standard_normal((n, 3))
+    wm = np.array(bg) + 1e-3 * rng.standard_normal((n, 3))
+    return t, wm, am
+
+
+def _quat_R(q):
+    from uvio_amd.sim import quat_2_rot
+    return quat_2_rot(np.asarray(q))
+
+
+def test_static_initializer_branches_match_numpy():
+    import uvio_amd as U
+    from oracle import oracle as O
+    opts = U.load_options(EUROC)
+    assert opts.init_window_time == 2.0 and opts.init_imu_thresh == 1.5 and opts.init_max_disparity == 10.0
+    rng = np.random.default_rng(3)
+    t, wm, am = _imu(rng, 600)
+    # at rest, not waiting for a jerk (ZUPT configs): initialized, values as the numpy statement
+    r = O.static_initialize(opts, t, wm, am, wait_for_jerk=False)
+    e = _numpy_static(opts, t, wm, am, False)
+    assert r is not None and e is not None
+    t_init, x = r
+    assert t_init == e[0]
+    np.testing.assert_allclose(_quat_R(x[:4]), e[1], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(x[4:10], 0.0, atol=0)
+    np.testing.assert_allclose(x[10:13], e[2], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(x[13:16], e[3], rtol=0, atol=1e-12)
+    assert x[3] >= 0 and abs(np.linalg.norm(x[:4]) - 1) < 1e-14
+    # gravity is aligned: R_GtoI e_z is the measured specific force direction, so the accel bias is along it
+    assert abs(np.dot(_quat_R(x[:4])[:, 2], am.mean(0) / np.linalg.norm(am.mean(0))) - 1) < 1e-6
+    # waiting for a jerk at rest: no excitation in the newest half
+    assert O.static_initialize(opts, t, wm, am, wait_for_jerk=True) is None
+    assert _numpy_static(opts, t, wm, am, True) is None
+    # a jerk in the newest half (window 1to0) with the older half at rest: initialized from the older half
+    amj = am.copy()
+    newest = t[-1]
+    jerk = t > newest - 0.5 * opts.init_window_time
+    amj[jerk] += 3.0 * rng.standard_normal((jerk.sum(), 3))
+    r = O.static_initialize(opts, t, wm, amj, wait_for_jerk=True)
+    e = _numpy_static(opts, t, wm, amj, True)
+    assert r is not None and e is not None
+    np.testing.assert_allclose(_quat_R(r[1][:4]), e[1], atol=1e-12)
+    np.testing.assert_allclose(r[1][13:16], e[3], atol=1e-12)
+    # ... but not when not waiting for one (the platform moves)
+    assert O.static_initialize(opts, t, wm, amj, wait_for_jerk=False) is None
+    # moving during the older half: never
+    amm = am.copy()
+    old = (t > newest - opts.init_window_time) & ~jerk
+    amm[old] += 3.0 * rng.standard_normal((old.sum(), 3))
+    assert O.static_initialize(opts, t, wm, amm, wait_for_jerk=True) is None
+    assert O.static_initialize(opts, t, wm, amm, wait_for_jerk=False) is None
+    # a buffer shorter than the window
+    assert O.static_initialize(opts, t[:300], wm[:300], am[:300], wait_for_jerk=False) is None
+
+
+def test_oracle_starts_from_rest_on_images():
+    """iros_2023_uvio (ZUPT on, so no jerk is awaited): a platform at rest, mono downsampled images.  The
+    filter stays uninitialized until the initializer's IMU window spans init_window_time, then initializes
+    on its own at the first such frame (the disparity test sees a still platform), and estimates gravity."""
+    import uvio_amd as U
+    from oracle import oracle as O
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(IROS, init_max_features=100, use_uwb=0)
+    assert opts.try_zupt == 1 and opts.init_window_time == 1.0
+    n = 14
+    sim = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=4, static_for=5.0)
+    o = O.OracleManager(opts)
+    states = []
+
+    def on_frame(nf, t):
+        states.append((t, o.initialized(), o.get_imu_state(), o.get_timing()))
+
+    sim.run(o, n_frames=n, on_frame=on_frame, renderer=SceneRenderer(opts, device="cpu"), init="static")
+    flags = [s[1] for s in states]
+    assert not flags[0] and flags[-1], flags
+    k = flags.index(True)
+    assert all(flags[k:])
+    # the first frame at which (a) the initializer's IMU window (trimmed at t - w - 0.1 + dt) spans the
+    # window and (b) the disparity test has tracks with two observations in the older half: TrackKLT writes
+    # no observation for the first image (it only detects), so the tracks' observations start at frame 1
+    lag = 1.0 / sim.imu_rate + 1e-9
+    w = opts.init_window_time
+    for i, (t, ok, _, _) in enumerate(states[:k + 1]):
+        m = (sim.imu_t >= sim.t0 - 0.4) & (sim.imu_t <= t + lag)
+        m &= sim.imu_t >= t - w - 0.10 + opts.calib_camimu_dt
+        e = _numpy_static(opts, sim.imu_t[m], sim.wm[m], sim.am[m], False)
+        two_old = sim.cam_t[2] < t - 0.5 * w
+        assert (e is not None and two_old) == (i == k), (i, k)
+    # after initialization the filter runs: the state is at the frame time, gravity matches the truth
+    t, _, (ts, x), timing = states[-1]
+    assert ts == t and timing["n_clones"] >= 1
+    gt = sim.gt_state(t)
+    Rg, Re = _quat_R(gt[1:5]), _quat_R(x[:4])
+    ang = np.arccos(np.clip(np.dot(Rg[:, 2], Re[:, 2]), -1, 1))
+    assert ang < 0.02, ang
+    assert np.linalg.norm(x[7:10]) < 0.05

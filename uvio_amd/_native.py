@@ -59,6 +59,8 @@ class Options(C.Structure):
         ("zupt_noise_multiplier", C.c_double), ("zupt_max_disparity", C.c_double),
         ("zupt_only_at_beginning", C.c_int), ("use_klt", C.c_int), ("use_aruco", C.c_int),
         ("record_timing_information", C.c_int), ("record_timing_filepath", C.c_char * 256),
+        ("init_window_time", C.c_double), ("init_imu_thresh", C.c_double), ("init_max_disparity", C.c_double),
+        ("init_dyn_use", C.c_int),
     ]
 
 

@@ -20,6 +20,7 @@ SOURCES = [
     "engine_state.cpp",
     "engine_prop.cpp",
     "engine_update.cpp",
+    "engine_chain.cpp", "engine_init.cpp",
     "engine_track.cpp",
     "engine_retri.cpp",
     "engine_api.cpp",

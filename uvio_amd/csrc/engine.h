@@ -14,6 +14,7 @@
 #include <mutex>
 #include <unordered_map>
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "hp_common.h"
@@ -238,8 +239,16 @@ struct DeviceBufs {
   double *chain = nullptr, *chain_host = nullptr;
   int chain_k = 0;
   size_t chain_stride = 0;
+  int fout_cap = 0;            // per-feature result slots in fout / fout_host (one frame chain's batches)
+  char *frame = nullptr;       // the frame chain's device state: clone / camera tables, pose values, mirror
+  size_t frame_bytes = 0;
 };
 
+// the per-feature measurement / variable tables of one feature in the reference iteration order (engine_update.cpp)
+class Engine;
+void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
+                 std::map<double, int> &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
+                 std::vector<DMeas> &meas, std::vector<DVar> &vars, int &rows, const Var *landmark, int landmark_canon);
 // algorithmic FP64 FLOPs / bytes of one EKFUpdate (engine_state.cpp)
 double ekf_flops(double N, double n, double r);
 double ekf_bytes(double N, double n, double r);
@@ -437,6 +446,13 @@ class Engine {
                                   const std::vector<double> &R, const std::vector<double> &res);
   void set_initial_covariance(const std::vector<double> &cov, const std::vector<VarP> &order);
 
+  // start-up from rest (engine_init.cpp): the InertialInitializer's IMU buffer (fed until initialized,
+  // VioManager.cpp:180-182), FeatureDatabase::cleanup_measurements, and the initializers
+  std::vector<ImuSample> init_imu_;
+  void db_cleanup_measurements(double t);
+  bool static_initialize(bool wait_for_jerk, double *t_init, std::vector<double> &cov);
+  bool try_to_initialize();
+
   // UpdaterZeroVelocity (UpdaterZeroVelocity.cpp:65-329; VioManager.cpp:160, 186-188, 294-307, 360)
   std::vector<ImuSample> zupt_imu_;
   bool zupt_have_last_off_ = false;
@@ -458,7 +474,7 @@ class Engine {
 
   // updates
   int after_tracking(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT1,
-                     int track_syncs = 0, double track_wait = 0.0);
+                     int track_syncs = 0, double track_wait = 0.0, bool try_init = false);
   int do_feature_propagate_update(double t, const std::vector<int> &camids, std::chrono::steady_clock::time_point rT2);
   int msckf_update(std::vector<FeatP> &feats);
   void gram(int m, int ncol, int *nch);
@@ -519,6 +535,7 @@ class Engine {
     size_t n_meas() const { return meas_dev ? n_meas_dev : meas.size(); }
     size_t n_vars() const { return vars_dev ? n_vars_dev : vars.size(); }
     std::map<double, int> slot_of_time;
+    int fout_off = 0;  // its per-feature results in d_.fout / d_.fout_host start here
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);
   void add_feature_to_batch(Batch &b, const FeatP &f, int mode, int rep);
@@ -530,6 +547,16 @@ class Engine {
   // one chain of delayed initializations: fv[idx[0..]] (triangulated) linearized, initialized and updated on
   // the device one after the other, one host wait at the end
   int slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t> &idx, int rep, double s2);
+  // the frame's UpdaterMSCKF::update, UpdaterSLAM::update chunks and delayed_init as one device chain with one
+  // host wait (engine_chain.cpp)
+  int update_frame(std::vector<FeatP> &msckf, std::vector<FeatP> &slam_upd, std::vector<FeatP> &delayed);
+  struct ChainItem;
+  double chain_times_[3] = {0, 0, 0};  // host seconds of the chain's MSCKF / SLAM / delayed-init parts
+  // UVIO_HP_NO_CHAIN set when the engine is created: the updaters one after the other with their host waits
+  // (A/B runs and diagnostics)
+  const bool no_chain_ = std::getenv("UVIO_HP_NO_CHAIN") != nullptr;
+  // 3-wide variables (zeroed landmark slots) at the given covariance offsets leave P in one compaction
+  void marginalize_slots(std::vector<int> slots);
   int run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult, bool wait, std::vector<DFeatOut> &outs,
                 bool chi2 = true);
   void finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs);

@@ -1,0 +1,519 @@
+// The frame's update as one device chain (VioManager.cpp:498-547: UpdaterMSCKF::update, UpdaterSLAM::update in
+// chunks of max_slam_in_update, UpdaterSLAM::delayed_init).
+//
+// Each reference updater linearizes at the state the previous one left: the SLAM chunk after the MSCKF update,
+// the next chunk after it, every delayed initialization after the one before.  Here the host builds every
+// batch's tables up front from the frame's selection and enqueues all of it on the library stream; the state
+// the linearizations read lives on the device for the length of the chain:
+//   * the clone / camera tables (DClone, DCam) with the JPL pose values behind them (DPoseVal) and an additive
+//     mirror of the mean indexed by covariance id (the SLAM landmarks' values), all in one dedicated buffer;
+//   * after every update k_chain_apply moves them by the update's dx with the host's own formulas
+//     (Var::update, quat_2_Rot; the same FP64 operations in the same order), gated by the update's acceptance;
+//   * the delayed initialization's batch triangulation feeds its per-candidate linearization on the device
+//     (DBatchParams::tri_in), each candidate's landmark goes into a fixed slot N0 + 3 j whose rows are zeroed
+//     when the candidate is rejected (zero rows of P make zero rows of every later M and K), and the host
+//     compacts the zeroed slots away afterwards in one gather.
+// Every update writes its dx into its own region of d_.chain; after ONE wait the host replays the updaters in
+// order on its mean (per-feature results, dx, landmark creation, fail counts), exactly the sequence the
+// reference applies.  The batches' decisions (accepted rows, chi2, LM status) never need the host in between.
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "engine.h"
+#include "hprof.h"
+
+namespace uvhp {
+
+using clk = std::chrono::steady_clock;
+static double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+void Engine::marginalize_slots(std::vector<int> slots) {
+  if (slots.empty()) return;
+  std::sort(slots.begin(), slots.end());
+  std::vector<int> src;
+  src.reserve(N_);
+  size_t k = 0;
+  for (int i = 0; i < N_; i++) {
+    while (k < slots.size() && i >= slots[k] + 3) k++;
+    if (k < slots.size() && i >= slots[k] && i < slots[k] + 3) continue;
+    src.push_back(i);
+  }
+  const int Nn = (int)src.size();
+  const int *dsrc = stage(src.data(), src.size());
+  stage_flush();
+  launch_compact(d_.stream, d_.P, d_.P2, d_.ldp, Nn, dsrc);
+  std::swap(d_.P, d_.P2);
+  ++p_epoch_;
+  for (auto &v : vars_) {
+    int shift = 0;
+    for (int s : slots)
+      if (v->id > s) shift += 3;
+    v->id -= shift;
+  }
+  N_ = Nn;
+}
+
+// one enqueued batch of the chain and what its replay needs
+struct Engine::ChainItem {
+  int kind = 0;  // 0 MSCKF, 1 SLAM chunk, 2 delayed-init triangulation, 3 delayed-init candidates
+  Engine::Batch b;
+  std::vector<FeatP> fv;
+  int region = -1;  // d_.chain region of its update (-1: none enqueued)
+  int m = 0;        // stacked rows
+};
+
+int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, std::vector<FeatP> &delayed) {
+  stage_ = "update chain";
+  last_msckf_.clear();
+  last_upd_.clear();
+  std::vector<double> clonetimes;
+  for (auto &c : clones_) clonetimes.push_back(c.first);
+  // ---- 0) each updater's measurement cleaning (UpdaterMSCKF.cpp:69-86, UpdaterSLAM.cpp:68-84 / 262-283);
+  // the clone set does not change during the updates, so all three lists are cleaned up front.  The SLAM
+  // list is split into its max_slam_in_update chunks first (VioManager.cpp:533-545) and each chunk is
+  // cleaned on its own, as UpdaterSLAM::update does: a feature left without measurements shrinks its chunk,
+  // it does not pull the next chunk's features forward
+  {
+    std::vector<uint8_t> few(up.size());
+    pool_.parallel_for(up.size(), 64, [&](size_t b0, size_t e0) {
+      for (size_t i = b0; i < e0; i++) {
+        up[i]->clean_old_measurements(clonetimes);
+        few[i] = up[i]->count() < 2;
+      }
+    });
+    std::vector<FeatP> keep;
+    for (size_t i = 0; i < up.size(); i++) {
+      if (few[i])
+        up[i]->to_delete = true;
+      else
+        keep.push_back(up[i]);
+    }
+    up.swap(keep);
+  }
+  std::vector<std::vector<FeatP>> slam_chunks;
+  {
+    const size_t chunk = (size_t)std::max(o_.max_slam_in_update, 1);
+    std::vector<FeatP> all;
+    for (size_t c0 = 0; c0 < slam_upd.size(); c0 += chunk) {
+      std::vector<FeatP> keep;
+      for (size_t i = c0; i < std::min(slam_upd.size(), c0 + chunk); i++) {
+        FeatP &f = slam_upd[i];
+        f->clean_old_measurements(clonetimes);
+        if (f->count() < 1)
+          f->to_delete = true;
+        else
+          keep.push_back(f);
+      }
+      all.insert(all.end(), keep.begin(), keep.end());
+      if (!keep.empty()) slam_chunks.push_back(std::move(keep));
+    }
+    slam_upd.swap(all);
+  }
+  {
+    std::vector<FeatP> keep;
+    for (auto &f : delayed) {
+      f->clean_old_measurements(clonetimes);
+      if (f->count() < 2)
+        f->to_delete = true;
+      else
+        keep.push_back(f);
+    }
+    delayed.swap(keep);
+  }
+  if (up.empty() && slam_upd.empty() && delayed.empty()) return 0;
+  if (!up.empty() && o_.feat_rep_msckf != 0 && o_.feat_rep_msckf != 4)
+    throw HpError(UVIO_HP_E_CONFIG, "feat_rep_msckf: only GLOBAL_3D / ANCHORED_MSCKF_INVERSE_DEPTH are implemented");
+  const int rep_slam = o_.feat_rep_slam;
+  if (!delayed.empty() && rep_slam != 0 && rep_slam != 2 && rep_slam != 4)
+    throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
+  for (auto &f : slam_upd) {
+    const VarP &lm = slam_.at(f->featid);
+    if (lm->rep != 0 && lm->rep != 2 && lm->rep != 4)
+      throw HpError(UVIO_HP_E_CONFIG, "feat_rep_slam: representation not implemented");
+  }
+  const int N0 = N_;
+  const int K = (int)delayed.size();
+  if (N0 + 3 * K > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
+
+  // ---- 1) the frame state on the device
+  DClone *fr_cl;
+  DCam *fr_cam;
+  DPoseVal *fr_cv, *fr_camv;
+  double *fr_xv;
+  int ncl, ncam;
+  {
+    HPROF("chain.state");
+    Batch base;
+    build_clone_cam_tables(base, false);
+    ncl = (int)base.clones.size();
+    ncam = (int)base.cams.size();
+    std::vector<DPoseVal> cv(ncl), camv(ncam);
+    int s = 0;
+    for (auto &c : clones_) {
+      for (int k = 0; k < 4; k++) cv[s].q[k] = c.second->val[k];
+      for (int k = 0; k < 3; k++) cv[s].p[k] = c.second->val[4 + k];
+      cv[s].pid = c.second->id;
+      s++;
+    }
+    for (int c = 0; c < ncam; c++) {
+      const VarP &pose = calib_pose_.at(c);
+      for (int k = 0; k < 4; k++) camv[c].q[k] = pose->val[k];
+      for (int k = 0; k < 3; k++) camv[c].p[k] = pose->val[4 + k];
+      camv[c].pid = pose->id;
+    }
+    std::vector<double> xv((size_t)d_.ldp, 0.0);
+    for (auto &kv : slam_)
+      for (int k = 0; k < kv.second->size; k++) xv[(size_t)kv.second->id + k] = kv.second->val[k];
+    // one contiguous blob, staged and copied into the dedicated buffer (the ring may restart during the chain)
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_cam = al(sizeof(DClone) * ncl), o_cv = o_cam + al(sizeof(DCam) * ncam),
+                 o_camv = o_cv + al(sizeof(DPoseVal) * ncl), o_xv = o_camv + al(sizeof(DPoseVal) * ncam),
+                 bytes = o_xv + sizeof(double) * xv.size();
+    if (bytes > d_.frame_bytes) throw HpError(UVIO_HP_E_CAPACITY, "update chain state exceeds its buffer");
+    std::vector<char> blob(bytes, 0);
+    std::memcpy(blob.data(), base.clones.data(), sizeof(DClone) * ncl);
+    std::memcpy(blob.data() + o_cam, base.cams.data(), sizeof(DCam) * ncam);
+    std::memcpy(blob.data() + o_cv, cv.data(), sizeof(DPoseVal) * ncl);
+    std::memcpy(blob.data() + o_camv, camv.data(), sizeof(DPoseVal) * ncam);
+    std::memcpy(blob.data() + o_xv, xv.data(), sizeof(double) * xv.size());
+    const char *staged = stage(blob.data(), blob.size());
+    stage_flush();
+    HP_HIP(hipMemcpyAsync(d_.frame, staged, bytes, hipMemcpyDeviceToDevice, d_.stream));
+    fr_cl = (DClone *)d_.frame;
+    fr_cam = (DCam *)(d_.frame + o_cam);
+    fr_cv = (DPoseVal *)(d_.frame + o_cv);
+    fr_camv = (DPoseVal *)(d_.frame + o_camv);
+    fr_xv = (double *)(d_.frame + o_xv);
+  }
+  std::vector<std::unique_ptr<ChainItem>> items;
+  int fo = 0, nreg = 0;
+  const size_t st = d_.chain_stride;
+  auto new_region = [&]() {
+    if (nreg >= d_.chain_k) throw HpError(UVIO_HP_E_CAPACITY, "update chain: too many updates in one frame");
+    return nreg++;
+  };
+  auto region = [&](int r) { return d_.chain + (size_t)r * st; };
+  // stage a batch's tables and launch its feature kernel (+ the chi2 group); results at d_.fout + b.fout_off
+  auto enqueue_batch = [&](ChainItem &it, int mode, double s2, double mult, bool chi2, const DFeatOut *tri) {
+    Batch &b = it.b;
+    const int nf = (int)b.feats.size();
+    if (nf > d_.max_feat || (int)b.n_meas() > d_.max_meas_total || (int)b.n_vars() > d_.max_vars_total ||
+        b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol)
+      throw HpError(UVIO_HP_E_CAPACITY, "update batch exceeds device capacity");
+    if (fo + nf > d_.fout_cap) throw HpError(UVIO_HP_E_CAPACITY, "update chain: per-feature results exceed capacity");
+    int max_meas = 0, max_nf = 0;
+    for (auto &F : b.feats) {
+      max_meas = std::max(max_meas, F.nmeas);
+      max_nf = std::max(max_nf, F.nf);
+    }
+    if (max_meas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
+    b.fout_off = fo;
+    fo += nf;
+    const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
+    const DMeas *t_meas = b.meas_dev ? b.meas_dev : stage(b.meas.data(), b.meas.size());
+    const DVar *t_vars = b.vars_dev ? b.vars_dev : stage(b.vars.data(), b.vars.size());
+    const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
+    stage_flush();
+    if (b.meas_dev && b.stg_epoch != d_.stg_epoch && d_.stg_used > (size_t)((const char *)b.meas_dev - d_.stg_d))
+      throw HpError(UVIO_HP_E_CAPACITY, "upload staging ring restarted inside one launch group (UVIO_HP_STAGE_BYTES too small)");
+    b.hidx_dev = t_hidx;
+    b.chi2 = chi2;
+    DBatchParams bp = batch_params(b, s2, mult);
+    bp.xv = fr_xv;
+    bp.tri_in = tri;
+    {
+      KScope ks(&kprof_, KC_FEATURE);
+      launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H,
+                               d_.fout + b.fout_off, max_meas, max_nf);
+    }
+    if (chi2) {
+      int max_rows_f = 0;
+      for (auto &F : b.feats) max_rows_f = std::max(max_rows_f, (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas);
+      KScope ks(&kprof_, KC_CHI2);
+      launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout + b.fout_off,
+                        max_rows_f, d_.acc, d_.R);
+    }
+    it.m = b.rows;
+    return t_feats;
+  };
+  // the EKF update of a batch's stacked rows (direct, or information form on their Gram), gated by the batch's
+  // accepted count, dx into a fresh region; then the state tables move by it
+  auto enqueue_update = [&](ChainItem &it, double s2) {
+    Batch &b = it.b;
+    const int m = b.rows, n = b.n_canon, ncol = n + 1;
+    it.region = new_region();
+    EkfScratch sc = d_.ekf;
+    sc.dx = region(it.region);
+    sc.gate = d_.acc;
+    if (m > n || m > kMaxEkfRows) {
+      int nch = 0;
+      gram(m, ncol, &nch);
+      const bool inflight = d_.pre_N >= 0;
+      const bool pre = inflight && d_.pre_N == N_ && d_.pre_hidx == b.hidx && d_.pre_epoch == p_epoch_;
+      d_.pre_hidx.clear();
+      d_.pre_N = -1;
+      if (pre) {
+        HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
+        KScope ks(&kprof_, KC_EKF);
+        launch_ekf_info_post(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, s2, d_.R, sc);
+      } else {
+        if (inflight) HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
+        KScope ks(&kprof_, KC_EKF);
+        launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.partials, nch, n, b.hidx_dev, s2, d_.R, sc);
+      }
+      const double fl = ekf_flops(N_, n, n) - (pre ? (double)n * n * n / 3.0 + (double)N_ * n * n : 0.0);
+      kprof_.credit(KC_EKF, fl, ekf_bytes(N_, n, n));
+    } else {
+      sc.Tall = d_.Tall;
+      sc.ldt = d_.ldh;
+      KScope ks(&kprof_, KC_EKF);
+      launch_ekf_update(d_.stream, d_.P, d_.ldp, N_, d_.H, d_.ldh, m, n, b.hidx_dev, d_.H + n, d_.ldh, s2, sc);
+      kprof_.credit(KC_EKF, ekf_flops(N_, n, m), ekf_bytes(N_, n, m));
+    }
+    ++p_epoch_;
+    launch_chain_apply(d_.stream, nullptr, d_.acc, sc.neg, sc.dx, fr_cl, fr_cv, ncl, fr_cam, fr_camv, ncam,
+                       o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, fr_xv, N_, d_.P, d_.ldp, N_, -1,
+                       sc.dx + N_ + 8);
+  };
+
+  // ---- 2) UpdaterMSCKF::update
+  auto tm0 = clk::now();
+  if (!up.empty()) {
+    HPROF("chain.msckf");
+    auto it = std::make_unique<ChainItem>();
+    it->kind = 0;
+    it->fv = up;
+    build_clone_cam_tables(it->b, false);
+    add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
+    PrefactorJoin pj(this);
+    if (it->b.rows > it->b.n_canon || it->b.rows > kMaxEkfRows) info_prefactor(it->b.hidx);
+    const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
+    enqueue_batch(*it, 0, s2, o_.msckf_chi2_multipler, true, nullptr);
+    if (it->m >= 1) enqueue_update(*it, s2);
+    items.push_back(std::move(it));
+  }
+  auto tm1 = clk::now();
+  // ---- 3) UpdaterSLAM::update in chunks of max_slam_in_update (VioManager.cpp:533-545)
+  {
+    HPROF("chain.slam");
+    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+    for (auto &ch : slam_chunks) {
+      auto it = std::make_unique<ChainItem>();
+      it->kind = 1;
+      it->fv = ch;
+      Batch &b = it->b;
+      build_clone_cam_tables(b, true);
+      std::vector<int> lm_canon;
+      for (auto &f : it->fv) {
+        const VarP &lm = slam_.at(f->featid);
+        lm_canon.push_back(b.n_canon);
+        for (int k = 0; k < lm->size; k++) b.hidx.push_back(lm->id + k);
+        b.n_canon += lm->size;
+      }
+      for (size_t i = 0; i < it->fv.size(); i++) {
+        const VarP &lm = slam_.at(it->fv[i]->featid);
+        add_feature(this, it->fv[i], 1, lm->rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows,
+                    lm.get(), lm_canon[i]);
+      }
+      PrefactorJoin pj(this);
+      if (b.rows > b.n_canon || b.rows > kMaxEkfRows) info_prefactor(b.hidx);
+      enqueue_batch(*it, 1, s2, o_.slam_chi2_multipler, true, nullptr);
+      if (it->m >= 1) enqueue_update(*it, s2);
+      items.push_back(std::move(it));
+    }
+  }
+  auto tm2 = clk::now();
+  // ---- 4) UpdaterSLAM::delayed_init: batch triangulation, then per candidate (fixed slot N0 + 3 j) the
+  // linearization at the current state, initialize_invertible and the chi2-gated update of the other rows
+  ChainItem *tri = nullptr, *cand = nullptr;
+  if (K > 0) {
+    HPROF("chain.delayed");
+    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+    auto ti = std::make_unique<ChainItem>();
+    ti->kind = 2;
+    ti->fv = delayed;
+    build_clone_cam_tables(ti->b, false);
+    for (auto &f : delayed)
+      add_feature(this, f, 2, rep_slam, o_, ti->b.cams, ti->b.slot_of_time, ti->b.clones, ti->b.feats, ti->b.meas,
+                  ti->b.vars, ti->b.rows, nullptr, -1);
+    enqueue_batch(*ti, 2, s2, o_.slam_chi2_multipler, false, nullptr);
+    tri = ti.get();
+    items.push_back(std::move(ti));
+    auto ci = std::make_unique<ChainItem>();
+    ci->kind = 3;
+    ci->fv = delayed;
+    Batch &b = ci->b;
+    build_clone_cam_tables(b, false);
+    for (auto &f : delayed)
+      add_feature(this, f, 3, rep_slam, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows, nullptr, -1);
+    if (b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol || (int)b.n_meas() > d_.max_meas_total ||
+        (int)b.n_vars() > d_.max_vars_total)
+      throw HpError(UVIO_HP_E_CAPACITY, "delayed-initialization chain exceeds device capacity");
+    if (fo + K > d_.fout_cap) throw HpError(UVIO_HP_E_CAPACITY, "update chain: per-feature results exceed capacity");
+    b.fout_off = fo;
+    fo += K;
+    const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
+    const DMeas *t_meas = stage(b.meas.data(), b.meas.size());
+    const DVar *t_vars = stage(b.vars.data(), b.vars.size());
+    const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
+    stage_flush();
+    b.hidx_dev = t_hidx;
+    b.chi2 = false;
+    DBatchParams bp = batch_params(b, s2, o_.slam_chi2_multipler);
+    bp.nfeat = 1;
+    bp.gate_out = d_.acc;  // triangulation ok and linearized: gates initialize_invertible and the update
+    const int n = b.n_canon;
+    const DFeatOut *tri_out = d_.fout + tri->b.fout_off;
+    DFeatOut *fo3 = d_.fout + b.fout_off;
+    cand = ci.get();
+    ci->region = nreg;
+    for (int j = 0; j < K; j++) {
+      const DFeat &F = b.feats[j];
+      if (F.nmeas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
+      const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
+      bp.tri_in = tri_out + j;
+      {
+        KScope ks(&kprof_, KC_FEATURE);
+        launch_feature_linearize(d_.stream, bp, t_feats + j, t_meas, t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H, fo3 + j,
+                                 F.nmeas, F.nf);
+      }
+      EkfScratch sc = d_.ekf;
+      sc.dx = region(new_region());
+      double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
+      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, t_hidx, nullptr, s2, sc, fo3 + j, d_.acc,
+                             sc.dx + Ni + 5);
+      if (nup > 0) {
+        sc.chi2_gate = d_.acc;
+        sc.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * F.nmeas, 999)];
+        sc.gate = nullptr;
+        KScope ks(&kprof_, KC_EKF);
+        launch_ekf_update(d_.stream, d_.P, d_.ldp, Ni + 3, Hrow + 3 * (size_t)d_.ldh, d_.ldh, nup, n, t_hidx,
+                          Hrow + 3 * (size_t)d_.ldh + n, d_.ldh, s2, sc);
+        kprof_.credit(KC_EKF, ekf_flops(Ni + 3, n, nup), ekf_bytes(Ni + 3, n, nup));
+      }
+      launch_chain_apply(d_.stream, fo3 + j, d_.acc, nup > 0 ? sc.neg : nullptr, nup > 0 ? sc.dx : nullptr, fr_cl, fr_cv,
+                         ncl, fr_cam, fr_camv, ncam, o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, nullptr, 0,
+                         d_.P, d_.ldp, Ni + 3, Ni, sc.dx + Ni + 8);
+    }
+    ++p_epoch_;
+    items.push_back(std::move(ci));
+  }
+  // ---- 5) one readback: every update's region and every batch's per-feature results
+  {
+    HPROF("chain.wait");
+    if (nreg > 0)
+      HP_HIP(hipMemcpyAsync(d_.chain_host, d_.chain, sizeof(double) * st * nreg, hipMemcpyDeviceToHost, d_.stream));
+    if (fo > 0) HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * fo, hipMemcpyDeviceToHost, d_.stream));
+    d_.fout_pending = 0;
+    dev_sync();
+  }
+  auto tm3 = clk::now();
+  // ---- 6) replay on the host mean, in the reference's order
+  HPROF("chain.replay");
+  auto neg_check = [&](const double *base, int N) {
+    if (base[N + 9] > 0.5) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+  };
+  std::vector<DFeatOut> outs;
+  for (auto &itp : items) {
+    ChainItem &it = *itp;
+    if (it.kind == 0) {
+      finish_batch(it.b, 0, outs);
+      int acc = 0, acc_rows = 0;
+      for (size_t i = 0; i < outs.size(); i++) {
+        last_msckf_.push_back(FeatDebug{it.fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
+                                        outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+        frame_feats_.push_back({0, last_msckf_.back()});
+        it.fv[i]->to_delete = true;
+        for (int k = 0; k < 3; k++) it.fv[i]->p_FinG[k] = outs[i].p_FinG[k], it.fv[i]->p_FinA[k] = outs[i].p_FinA[k];
+        if (outs[i].status == 0) acc++, acc_rows += outs[i].rows;
+      }
+      timing_.msckf_rows = acc_rows;
+      timing_.msckf_cols = it.b.n_canon;
+      if (it.region >= 0) {
+        const double *base = d_.chain_host + (size_t)it.region * st;
+        neg_check(base, N_);
+        if (acc > 0) apply_dx(base);
+      }
+    } else if (it.kind == 1) {
+      finish_batch(it.b, 1, outs);
+      last_upd_.clear();
+      int acc = 0;
+      for (size_t i = 0; i < outs.size(); i++) {
+        last_upd_.push_back(FeatDebug{it.fv[i]->featid, {0.0, 0.0, 0.0}, outs[i].status == 2 ? 1 : outs[i].status, outs[i].chi2});
+        frame_feats_.push_back({1, last_upd_.back()});
+        it.fv[i]->to_delete = true;
+        if (outs[i].status == 3) slam_.at(it.fv[i]->featid)->fail_count++;
+        if (outs[i].status == 0) acc++;
+      }
+      if (it.region >= 0) {
+        const double *base = d_.chain_host + (size_t)it.region * st;
+        neg_check(base, N_);
+        if (acc > 0) apply_dx(base);
+      }
+    } else if (it.kind == 3) {
+      std::vector<DFeatOut> touts;
+      finish_batch(tri->b, 2, touts);
+      finish_batch(it.b, 3, outs);
+      last_upd_.clear();
+      N_ = N0 + 3 * K;
+      std::vector<int> dead;
+      for (int j = 0; j < K; j++) {
+        FeatP &f = it.fv[j];
+        const int Ni = N0 + 3 * j, nup = 2 * it.b.feats[j].nmeas - 3;
+        f->to_delete = true;
+        if (touts[j].status == 1 || touts[j].status == 2) {
+          last_upd_.push_back(FeatDebug{f->featid, {0.0, 0.0, 0.0}, touts[j].status, 0.0});
+          frame_feats_.push_back({2, FeatDebug{f->featid, {0.0, 0.0, 0.0}, 1, 0.0}});
+          dead.push_back(Ni);
+          continue;
+        }
+        // anchor (host rule, identical to the kernel's) and the triangulated position
+        f->anchor_cam_id = it.b.feats[j].anchor_cam;
+        f->anchor_clone_timestamp = f->find((size_t)f->anchor_cam_id)->m.back().t;
+        for (int k = 0; k < 3; k++) f->p_FinA[k] = touts[j].p_FinA[k], f->p_FinG[k] = touts[j].p_FinG[k];
+        const double *base = d_.chain_host + (size_t)(it.region + j) * st;
+        if (base[Ni + 9] > 0.5) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
+        const bool accepted = base[Ni + 8] > 0.5;
+        last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,
+                                      nup > 0 ? base[Ni + 3] : 0.0});
+        frame_feats_.push_back({2, last_upd_.back()});
+        if (!accepted) {
+          dead.push_back(Ni);
+          continue;
+        }
+        VarP lm = std::make_shared<Var>(V_LANDMARK, 3, 3);
+        lm->featid = f->featid;
+        lm->rep = rep_slam;
+        lm->unique_cam = f->anchor_cam_id;
+        lm->anchor_cam = f->anchor_cam_id;
+        lm->anchor_time = f->anchor_clone_timestamp;
+        const bool relr = (rep_slam == 2 || rep_slam == 4);
+        lm->set_xyz(relr ? f->p_FinA : f->p_FinG, false);
+        lm->set_xyz(relr ? f->p_FinA : f->p_FinG, true);
+        lm->id = Ni;
+        vars_.push_back(lm);
+        double HLinv[9], dl[3];
+        inv3_cofactor(outs[j].HfR, HLinv);  // the device's formula: identical H_Linv
+        const double *resinit = base + Ni + 5;
+        for (int a = 0; a < 3; a++)
+          dl[a] = HLinv[3 * a] * resinit[0] + HLinv[3 * a + 1] * resinit[1] + HLinv[3 * a + 2] * resinit[2];
+        lm->update(dl);
+        if (nup > 0) apply_dx(base);
+        slam_.insert({f->featid, lm});
+      }
+      marginalize_slots(dead);  // the rejected candidates' zeroed slots
+    }
+  }
+  auto tm4 = clk::now();
+  chain_times_[0] = secs(tm0, tm1);
+  chain_times_[1] = secs(tm1, tm2);
+  chain_times_[2] = secs(tm2, tm4);
+  (void)tm3;
+  return 0;
+}
+
+}  // namespace uvhp

@@ -224,7 +224,7 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
@@ -307,13 +307,15 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   d_.dx_bytes = sizeof(double) * (cap + 16);
-  HP_HIP(hipMalloc((void **)&d_.dxneg, d_.dx_bytes + sizeof(DFeatOut) * maxf));
+  // one frame chain holds the MSCKF batch, the SLAM chunks and the delayed initialization's two passes
+  d_.fout_cap = maxf + 3 * std::max(o_.max_slam_features, 0) + 64;
+  HP_HIP(hipMalloc((void **)&d_.dxneg, d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap));
   d_.fout = (DFeatOut *)((char *)d_.dxneg + d_.dx_bytes);
   dalloc(&d_.acc, 4);
   dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
-  d_.chain_k = std::max(1, std::min(std::max(o_.max_slam_features, 1), 64));
+  d_.chain_k = std::max(o_.max_slam_features, 1) + std::max(o_.max_slam_features, 1) / std::max(o_.max_slam_in_update, 1) + 4;
   d_.chain_stride = (size_t)cap + 16;
   dalloc(&d_.chain, (size_t)d_.chain_k * d_.chain_stride);
   HP_HIP(hipHostMalloc((void **)&d_.chain_host, sizeof(double) * d_.chain_k * d_.chain_stride, hipHostMallocDefault));
@@ -323,14 +325,17 @@ void Engine::alloc_device() {
   // pinned staging: batch upload + small downloads
   d_.pin_bytes = sizeof(DFeat) * maxf + sizeof(DMeas) * d_.max_meas_total + sizeof(DVar) * d_.max_vars_total +
                  sizeof(DClone) * (C + 4) + sizeof(DCam) * UVIO_HP_MAX_CAMS + sizeof(int) * (d_.max_ncol + d_.max_rows) +
-                 sizeof(double) * (cap + 16) + sizeof(DFeatOut) * maxf + sizeof(double) * 16 + 4096;
+                 sizeof(double) * (cap + 16) + sizeof(DFeatOut) * d_.fout_cap + sizeof(double) * 16 + 4096;
   HP_HIP(hipHostMalloc(&d_.pin, d_.pin_bytes, hipHostMallocDefault));
   char *pb = (char *)d_.pin + d_.pin_bytes -
-             (d_.dx_bytes + sizeof(DFeatOut) * maxf + sizeof(double) * 16 + 64);
+             (d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap + sizeof(double) * 16 + 64);
   d_.neg_host = (int *)pb;  // same layout as dxneg
   d_.dx_host = (double *)(pb + sizeof(double));
   d_.fout_host = (DFeatOut *)(pb + d_.dx_bytes);
-  d_.aux_host = (double *)(pb + d_.dx_bytes + sizeof(DFeatOut) * maxf);
+  d_.aux_host = (double *)(pb + d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap);
+  d_.frame_bytes = sizeof(DClone) * (C + 4) + sizeof(DCam) * UVIO_HP_MAX_CAMS + sizeof(DPoseVal) * (C + 4 + UVIO_HP_MAX_CAMS) +
+                   sizeof(double) * cap + 1024;
+  dalloc(&d_.frame, d_.frame_bytes);
   // upload staging (batch tables, Phi / Q, column maps)
   d_.stg_cap = d_.pin_bytes + 2 * 64 * 64 * sizeof(double) + 64 * 1024;
   // test hook: a smaller ring recycles every few batches (tests/test_gpu_configs.py staging test)

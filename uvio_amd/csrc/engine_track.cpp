@@ -124,6 +124,24 @@ Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t 
   HP_HIP(hipMemsetAsync(d_lk_bytes_, 0, sizeof(unsigned long long), s_));
 }
 
+void Tracker::set_num_features(int n) {
+  if (n <= 0) throw HpError(UVIO_HP_E_CONFIG, "tracker: num features must be positive");
+  num_features_ = n;
+  int gx = grid_x_, gy = grid_y_;
+  if (num_features_ < gx * gy) {
+    double ratio = (double)gx / (double)gy;
+    gy = (int)std::ceil(std::sqrt(num_features_ / ratio));
+    gx = (int)std::ceil(gy * ratio);
+  }
+  const int kmax = (int)((double)num_features_ / (double)(gx * gy)) + 1;
+  const int cap = std::max(b_->cap, 8 * num_features_);
+  if (kmax != b_->kmax || cap > b_->cap) {  // the per-cell FAST top-k table is sized by kmax: reallocate
+    b_->kmax = kmax;
+    b_->cap = 0;
+    ensure_cap(cap);
+  }
+}
+
 unsigned long long Tracker::lk_bytes() {
   unsigned long long v = 0;
   HP_HIP(hipMemcpyAsync(&v, d_lk_bytes_, sizeof(v), hipMemcpyDeviceToHost, s_));

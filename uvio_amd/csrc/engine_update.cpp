@@ -72,26 +72,28 @@ void Engine::initialize_with_gt(const double x[17]) {
   timestamp_ = x[0];
   startup_time_ = x[0];
   is_initialized_ = true;
-  // FeatureDatabase::cleanup_measurements(t)
-  for (auto it = db_.begin(); it != db_.end();) {
-    it->second->clean_older_measurements(timestamp_);
-    if (it->second->count() < 1)
-      it = db_erase(it);
-    else
-      it++;
-  }
+  db_cleanup_measurements(timestamp_);
+  std::lock_guard<std::mutex> lk(imu_mtx_);
+  init_imu_.clear();
 }
 
 // VioManager.cpp:166-189 + Propagator::feed_imu (Propagator.h:65-91)
 void Engine::feed_imu(double t, const double wm[3], const double am[3]) {
   double oldest = margtimestep();
   if (oldest > timestamp_) oldest = -1;
-  if (!is_initialized_) oldest = t - 2.0 + calib_dt_->val[0] - 0.10;
+  if (!is_initialized_) oldest = t - o_.init_window_time + calib_dt_->val[0] - 0.10;
   ImuSample s;
   s.t = t;
   for (int k = 0; k < 3; k++) s.wm[k] = wm[k], s.am[k] = am[k];
   std::lock_guard<std::mutex> lk(imu_mtx_);
   imu_data_.push_back(s);
+  // InertialInitializer::feed_imu (InertialInitializer.cpp:49-71): its age test reads the new message's
+  // time, so the buffer is emptied only by a message older than oldest (never, in time order); the
+  // window is trimmed in InertialInitializer::initialize
+  if (!is_initialized_) {
+    init_imu_.push_back(s);
+    if (oldest != -1 && t < oldest) init_imu_.clear();
+  }
   double cut = oldest - 0.10;
   // UpdaterZeroVelocity::feed_imu (VioManager.cpp:186-188; UpdaterZeroVelocity.h:77-107)
   if (is_initialized_ && o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
@@ -289,7 +291,7 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
   }
   if (early_exc) std::rethrow_exception(early_exc);
   if (early && early_rc) return early_rc;
-  return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait);
+  return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait, true);
 }
 
 // the conditions under which after_tracking's first state change is propagate_and_clone(t)
@@ -302,14 +304,16 @@ bool Engine::propagation_can_precede_tracking(double t) const {
 }
 
 int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, int track_syncs,
-                           double track_wait) {
+                           double track_wait, bool try_init) {
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
   frame_feats_.clear();
   timing_.tracking = secs(rT1, rT2) - early_prop_s_;
   timing_.device_syncs = track_syncs;
   timing_.sync_wait = track_wait;
-  if (!is_initialized_) return UVIO_HP_E_STATE;
+  // VioManager.cpp:308-317: a camera frame before initialization tries the initializer (the simulated
+  // feed requires an initialized filter, VioManager.cpp:236-240)
+  if (!is_initialized_ && !(try_init && try_to_initialize())) return UVIO_HP_E_STATE;
   // zero-velocity update (UVioManager.cpp:147-162, VioManager.cpp:291-307): on success the frame ends here
   if (o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
     if (timestamp_ != t) did_zupt_update_ = zupt_try_update(t) == 1;
@@ -495,21 +499,36 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     a.first += secs(t_sel, clk::now());
     a.second++;
   }
-  int rc = msckf_update(up);
-  if (rc) return rc;
-  auto rT4 = clk::now();
-  while (!slam_upd.empty()) {
-    size_t k = std::min((size_t)std::max(o_.max_slam_in_update, 1), slam_upd.size());
-    std::vector<FeatP> tmp(slam_upd.begin(), slam_upd.begin() + k);
-    slam_upd.erase(slam_upd.begin(), slam_upd.begin() + k);
-    rc = slam_update(tmp);
-    if (rc) return rc;
-  }
-  auto rT5 = clk::now();
   timing_.n_slam_delayed = (int)slam_delayed.size();
-  rc = slam_delayed_init(slam_delayed);
-  if (rc) return rc;
-  auto rT6 = clk::now();
+  int rc = 0;
+  auto rT4 = clk::now(), rT5 = rT4, rT6 = rT4;
+  if (!shard_.enabled && !no_chain_) {
+    // the three updaters as one device chain with one host wait (engine_chain.cpp)
+    rc = update_frame(up, slam_upd, slam_delayed);
+    if (rc) return rc;
+    rT6 = clk::now();
+    timing_.msckf_update = chain_times_[0];
+    timing_.slam_update = chain_times_[1];
+    timing_.slam_delayed = chain_times_[2];
+  } else {
+    rc = msckf_update(up);
+    if (rc) return rc;
+    rT4 = clk::now();
+    while (!slam_upd.empty()) {
+      size_t k = std::min((size_t)std::max(o_.max_slam_in_update, 1), slam_upd.size());
+      std::vector<FeatP> tmp(slam_upd.begin(), slam_upd.begin() + k);
+      slam_upd.erase(slam_upd.begin(), slam_upd.begin() + k);
+      rc = slam_update(tmp);
+      if (rc) return rc;
+    }
+    rT5 = clk::now();
+    rc = slam_delayed_init(slam_delayed);
+    if (rc) return rc;
+    rT6 = clk::now();
+    timing_.msckf_update = secs(rT3, rT4);
+    timing_.slam_update = secs(rT4, rT5);
+    timing_.slam_delayed = secs(rT5, rT6);
+  }
   HPROF("marg.total");
   {
     HPROF("marg.retri");
@@ -548,9 +567,6 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   marginalize_old_clone();
   if (o_.record_timing >= 2) dev_sync();
   auto rT7 = clk::now();
-  timing_.msckf_update = secs(rT3, rT4);
-  timing_.slam_update = secs(rT4, rT5);
-  timing_.slam_delayed = secs(rT5, rT6);
   timing_.marg = secs(rT6, rT7);
   timing_.n_slam = (int)slam_.size();
   timing_.cov_dim = N_;
@@ -635,7 +651,7 @@ void Engine::build_clone_cam_tables(Batch &b, bool include_landmarks) {
 
 // Builds the per-feature measurement / variable tables in the reference iteration order
 // (get_feature_jacobian_full's x_order, UpdaterHelper.cpp:200-262) and appends them to the batch.
-static void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
+void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
                         std::map<double, int> &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
                         std::vector<DMeas> &meas, std::vector<DVar> &vars, int &rows, const Var *landmark,
                         int landmark_canon) {
@@ -939,7 +955,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
 // group's event timing
 void Engine::finish_batch(Batch &b, int mode, std::vector<DFeatOut> &outs) {
   const int nf = (int)b.feats.size();
-  outs.assign(d_.fout_host, d_.fout_host + nf);
+  outs.assign(d_.fout_host + b.fout_off, d_.fout_host + b.fout_off + nf);
   if (b.finished) return;
   b.finished = true;
   if (b.evtimed) {
@@ -1273,6 +1289,7 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
   stage_flush();
   DBatchParams bp = batch_params(b, s2, o_.slam_chi2_multipler);
   bp.nfeat = 1;
+  bp.gate_out = d_.acc;  // the candidate's linearization status: gates initialize_invertible and its update
   const int n = b.n_canon;
   const size_t st = d_.chain_stride;
   {
@@ -1290,7 +1307,7 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
       double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
       // initialize_invertible with rows 0..2 (H_Linv from the feature's H_finit); its residual column lands in
       // the candidate's region behind the chi2 gate's [chi2, accepted]
-      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, t_hidx, nullptr, s2, sc, d_.fout + j, nullptr,
+      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, t_hidx, nullptr, s2, sc, d_.fout + j, d_.acc,
                              sc.dx + Ni + 5);
       if (nup > 0) {
         sc.chi2_gate = d_.acc;
@@ -1301,10 +1318,10 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
                           Hrow + 3 * (size_t)d_.ldh + n, d_.ldh, s2, sc);
       }
       if (nup > 0) kprof_.credit(KC_EKF, ekf_flops(Ni + 3, n, nup), ekf_bytes(Ni + 3, n, nup));
-      launch_chain_apply(d_.stream, d_.fout + j, nup > 0 ? d_.acc : nullptr, nup > 0 ? sc.neg : nullptr,
-                         nup > 0 ? sc.dx : nullptr, t_clones, t_cv, (int)b.clones.size(), t_cams, t_camv,
-                         (int)b.cams.size(), o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, d_.P, d_.ldp, Ni + 3,
-                         Ni, sc.dx + Ni + 8);
+      launch_chain_apply(d_.stream, d_.fout + j, d_.acc, nup > 0 ? sc.neg : nullptr, nup > 0 ? sc.dx : nullptr,
+                         t_clones, t_cv, (int)b.clones.size(), t_cams, t_camv, (int)b.cams.size(),
+                         o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, nullptr, 0, d_.P, d_.ldp, Ni + 3, Ni,
+                         sc.dx + Ni + 8);
     }
     ++p_epoch_;
     HP_HIP(hipMemcpyAsync(d_.chain_host, d_.chain, sizeof(double) * st * K, hipMemcpyDeviceToHost, d_.stream));

@@ -91,6 +91,12 @@ struct DBatchParams {
   double fi_min_dist, fi_max_dist, fi_max_baseline, fi_max_cond;
   double *dbg;         // optional per-measurement debug record (8 doubles each), nullptr in production
   long long *dbg_ts;   // optional per-feature phase timestamps (8 per feature), nullptr in production
+  // device-chained updates (Engine::update_frame): mode 3 takes its triangulation from tri_in[f] (a failed
+  // one fails the feature); mode 1 takes its landmark from the additive mirror xv (indexed by covariance id,
+  // kept current by k_chain_apply); gate_out (one-feature batches) <- the feature's status == 0
+  const DFeatOut *tri_in;
+  const double *xv;
+  int *gate_out;
 };
 
 // ---- launch wrappers (all asynchronous on `s`) ----
@@ -102,6 +108,8 @@ void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p
 void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt);
 // StateHelper::marginalize (StateHelper.cpp:271-339): Pout <- P without rows/cols [m0, m0+ms)
 void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, int N, int m0, int ms);
+// Pout (Nn x Nn) <- P[src, src]: several variables marginalized at once (src: the kept indices, device)
+void launch_compact(hipStream_t s, const double *P, double *Pout, int ld, int Nn, const int *src);
 // diagonal check: writes count of negative diagonal entries to *neg (device int)
 void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg);
 
@@ -186,14 +194,15 @@ struct DPoseVal {
   double q[4], p[3];
   int pid, pad;
 };
-// One step of a delayed-initialization chain (Engine::slam_delayed_init): the candidate's acceptance
-// (linearization status, and with update rows the chi2 gate of its factor) into out[0], the update's
-// negative-diagonal count into out[1]; accepted with an update (dx): the clone / camera tables the next
-// candidate is linearized against get the update (Var::update + quat_2_Rot, the host's formulas);
-// rejected: the appended landmark slot's rows / columns (slot .. slot+2 over [0, Ntot)) are zeroed.
+// One step of a device update chain (Engine::update_frame, Engine::slam_delayed_chain): the update's acceptance
+// (fout's linearization status if given, the gate if given: accepted rows / the chi2 test of its factor) into
+// out[0], its negative-diagonal count into out[1]; accepted with an update (dx): the clone / camera tables
+// the next batch is linearized against get the update (Var::update + quat_2_Rot, the host's formulas) and the
+// additive mirror xv[0, Nx) += dx; rejected with slot >= 0: the appended landmark slot's rows / columns
+// (slot .. slot+2 over [0, Ntot)) are zeroed.
 void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, const int *neg, const double *dx,
                         DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
-                        int calib_intr, double *P, int ldp, int Ntot, int slot, double *out);
+                        int calib_intr, double *xv, int Nx, double *P, int ldp, int Ntot, int slot, double *out);
 double chi2_quantile95(int dof);
 
 // ---- VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388) on the device ----

@@ -123,6 +123,18 @@ void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, in
   hipLaunchKernelGGL(k_marginalize, dim3((Nn + 127) / 128, Nn), dim3(128), 0, s, P, Pout, ld, N, m0, ms);
 }
 
+// several variables at once: Po (Nn x Nn) = P[src, src] (P is exactly symmetric: both triangles are written
+// with the same values by every update, so the gather equals the sequence of single marginalizations)
+__global__ void k_compact(const double *__restrict__ P, double *__restrict__ Po, int ld, int Nn, const int *__restrict__ src) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y;
+  if (j >= Nn || i >= Nn) return;
+  Po[(size_t)i * ld + j] = P[(size_t)src[i] * ld + src[j]];
+}
+void launch_compact(hipStream_t s, const double *P, double *Pout, int ld, int Nn, const int *src) {
+  if (Nn <= 0) return;
+  hipLaunchKernelGGL(k_compact, dim3((Nn + 127) / 128, Nn), dim3(128), 0, s, P, Pout, ld, Nn, src);
+}
+
 __global__ void k_check_diag(const double *__restrict__ P, int ld, int N, int *neg) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < N && P[(size_t)i * ld + i] < 0.0) atomicAdd(neg, 1);

@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(512) k_ekf_fact(const double *__restrict__ Sup
     }
     for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
     if (threadIdx.x == 0) {
-      const int acc = !(s > chi2_thr);
+      // the incoming gate (the feature's linearization succeeded) AND the test
+      const int acc = (*chi2_gate != 0) && !(s > chi2_thr);
       *chi2_gate = acc;
       gate_out[0] = s;
       gate_out[1] = acc;
@@ -307,17 +308,22 @@ __global__ void __launch_bounds__(256) k_chain_apply(const DFeatOut *__restrict_
                                                      const int *__restrict__ neg, const double *__restrict__ dx,
                                                      DClone *__restrict__ clones, DPoseVal *__restrict__ cv, int ncl,
                                                      DCam *__restrict__ cams, DPoseVal *__restrict__ camv, int ncam,
-                                                     int calib_ext, int calib_intr, double *__restrict__ P, int ldp,
-                                                     int Ntot, int slot, double *__restrict__ out) {
-  const bool acc = fout->status == 0 && (!gate || *gate != 0);
+                                                     int calib_ext, int calib_intr, double *__restrict__ xv, int Nx,
+                                                     double *__restrict__ P, int ldp, int Ntot, int slot,
+                                                     double *__restrict__ out) {
+  const bool acc = (!fout || fout->status == 0) && (!gate || *gate != 0);
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (!acc) {
-    for (int e = t; e < 3 * Ntot; e += gridDim.x * blockDim.x) {
-      const int i = e / 3, a = e - 3 * i;
-      P[(size_t)(slot + a) * ldp + i] = 0.0;
-      P[(size_t)i * ldp + slot + a] = 0.0;
-    }
-  } else if (blockIdx.x == 0 && dx) {
+    if (slot >= 0)
+      for (int e = t; e < 3 * Ntot; e += gridDim.x * blockDim.x) {
+        const int i = e / 3, a = e - 3 * i;
+        P[(size_t)(slot + a) * ldp + i] = 0.0;
+        P[(size_t)i * ldp + slot + a] = 0.0;
+      }
+  } else if (dx && xv) {  // the additive mirror (landmarks): Var::update of a vector, val += dx
+    for (int e = t; e < Nx; e += gridDim.x * blockDim.x) xv[e] += dx[e];
+  }
+  if (acc && blockIdx.x == 0 && dx) {
     if (t < ncl) {  // PoseJPL::update of clone t, then the table's R_GtoI / p_IinG
       DPoseVal &v = cv[t];
       const double *d = dx + v.pid;
@@ -348,11 +354,11 @@ __global__ void __launch_bounds__(256) k_chain_apply(const DFeatOut *__restrict_
 
 void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, const int *neg, const double *dx,
                         DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
-                        int calib_intr, double *P, int ldp, int Ntot, int slot, double *out) {
-  if (ncl + ncam > 256) throw std::runtime_error("delayed-init chain: more clones + cameras than one workgroup");
-  const int nb = std::max(1, std::min(16, (3 * Ntot + 255) / 256));
+                        int calib_intr, double *xv, int Nx, double *P, int ldp, int Ntot, int slot, double *out) {
+  if (ncl + ncam > 256) throw std::runtime_error("update chain: more clones + cameras than one workgroup");
+  const int nb = std::max(1, std::min(16, (std::max(3 * Ntot, Nx) + 255) / 256));
   hipLaunchKernelGGL(k_chain_apply, dim3(nb), dim3(256), 0, s, fout, gate, neg, dx, clones, cv, ncl, cams, camv, ncam,
-                     calib_ext, calib_intr, P, ldp, Ntot, slot, out);
+                     calib_ext, calib_intr, xv, Nx, P, ldp, Ntot, slot, out);
 }
 
 static void ensure_ekf_lds_attrs() {

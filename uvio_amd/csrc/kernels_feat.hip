@@ -263,12 +263,30 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   }
   if (tid == 0) {
     sh.status = 0;
+    double pin[3], pinf[3];
+    for (int k = 0; k < 3; k++) pin[k] = F.p_in[k], pinf[k] = F.p_in_fej[k];
+    if (F.mode == 3 && bp.tri_in) {  // the chained batch triangulation (p_FinA, p_FinG)
+      const DFeatOut &t = bp.tri_in[f];
+      for (int k = 0; k < 3; k++) pin[k] = t.p_FinA[k], pinf[k] = t.p_FinG[k];
+      if (t.status == 1 || t.status == 2) sh.status = 1;
+    }
+    if (F.mode == 1 && bp.xv && F.lm_pid >= 0) {  // Landmark::get_xyz of the current value (Landmark.cpp:26-63)
+      const double *v = bp.xv + F.lm_pid;
+      if (F.rep == 4) {
+        pin[0] = (1 / v[2]) * v[0];
+        pin[1] = (1 / v[2]) * v[1];
+        pin[2] = 1 / v[2];
+        for (int k = 0; k < 3; k++) pinf[k] = pin[k];  // the reference ignores the fej value here
+      } else {
+        for (int k = 0; k < 3; k++) pin[k] = v[k];
+      }
+    }
     for (int k = 0; k < 3; k++) {
-      sh.p_FinA[k] = F.p_in[k];
-      sh.p_FinA_fej[k] = F.p_in_fej[k];
-      sh.p_FinG[k] = (F.mode == 3) ? F.p_in_fej[k] : F.p_in[k];
-      sh.p_FinG_fej[k] = F.p_in_fej[k];
-      if (F.mode == 3) sh.p_FinA_fej[k] = F.p_in[k];
+      sh.p_FinA[k] = pin[k];
+      sh.p_FinA_fej[k] = pinf[k];
+      sh.p_FinG[k] = (F.mode == 3) ? pinf[k] : pin[k];
+      sh.p_FinG_fej[k] = pinf[k];
+      if (F.mode == 3) sh.p_FinA_fej[k] = pin[k];
     }
   }
   __syncthreads();
@@ -746,6 +764,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
     o.status = status;
     o.rows = status == 0 ? nrows_out : 0;
     out[f] = o;
+    if (bp.gate_out) *bp.gate_out = (status == 0) ? 1 : 0;
   }
   FEAT_TS(7)
 #undef FEAT_TS

@@ -328,6 +328,11 @@ void options_default(uvio_hp_options_t *o) {
   o->use_aruco = 0;
   o->record_timing_information = 0;
   std::snprintf(o->record_timing_filepath, sizeof(o->record_timing_filepath), "%s", "ov_msckf_timing.txt");
+  // InertialInitializerOptions.h:64-76
+  o->init_window_time = 1.0;
+  o->init_imu_thresh = 1.0;
+  o->init_max_disparity = 1.0;
+  o->init_dyn_use = 0;
 }
 
 int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
@@ -395,6 +400,10 @@ int options_load(const char *path, uvio_hp_options_t *o, std::string *err) {
   est.get({"num_pts"}, o->num_pts);
   est.get({"fast_threshold"}, o->fast_threshold);
   est.get({"init_max_features"}, o->init_max_features);
+  est.get({"init_window_time"}, o->init_window_time);
+  est.get({"init_imu_thresh"}, o->init_imu_thresh);
+  est.get({"init_max_disparity"}, o->init_max_disparity);
+  est.getb({"init_dyn_use"}, o->init_dyn_use);
   est.get({"grid_x"}, o->grid_x);
   est.get({"grid_y"}, o->grid_y);
   est.get({"min_px_dist"}, o->min_px_dist);

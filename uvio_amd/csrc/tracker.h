@@ -43,6 +43,8 @@ class Tracker {
   bool last_pyramid(int cam, int level, int *w, int *h, std::vector<uint8_t> *img, std::vector<int16_t> *der);
 
   size_t currid;
+  // TrackBase::set_num_features (TrackBase.h:152): after an initializer succeeds (VioManagerHelper.cpp:124)
+  void set_num_features(int n);
   int device_syncs = 0;     // host waits in the last feed
   double sync_wait = 0.0;   // seconds blocked in them
   // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand

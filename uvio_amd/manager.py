@@ -325,6 +325,12 @@ class VioManager:
         return bool(a.value)
 
     # ---- getters ----
+    def initialized(self):
+        """VioManager::initialized (VioManager.h:99): initialize_with_gt ran or an initializer succeeded."""
+        out = C.c_int()
+        self._check(self._call("initialized", self._h, C.byref(out)), "initialized")
+        return bool(out.value)
+
     def get_imu_state(self):
         t = C.c_double()
         out = np.zeros(16)

@@ -279,16 +279,23 @@ class SimStream:
         return ev
 
     def run(self, mgr, n_frames=None, on_frame=None, start_frame=0, before_frame=None, after_init=None, renderer=None,
-            before_feed=None):
+            before_feed=None, init="gt"):
         """Drive one manager (or a list of managers in lock-step): initialize from ground truth at t0, then
         feed IMU / UWB / camera in time order.  before_frame(nf, t) runs before each camera feed,
         after_init(mgr) right after the ground-truth initialization (e.g. UWB anchor init), before_feed(mgr)
         right before each manager's camera feed (lock-step steering: the oracle, fed after the device, learns
         the device's results of the same frame).  With a
         renderer (uvio_amd.render.SceneRenderer) the managers get images (feed_measurement_camera)
-        instead of the simulated tracks."""
+        instead of the simulated tracks.  init="static" skips the ground-truth initialization: the camera
+        feeds then run the managers' own initializer (VioManager::try_to_initialize, a stream that starts at
+        rest) until it succeeds; after_init is not called."""
         mgrs = mgr if isinstance(mgr, (list, tuple)) else [mgr]
+        static = init == "static"
+        if static and renderer is None:
+            raise ValueError("init='static' needs camera images (the simulated feed requires an initialized filter)")
         for m in mgrs:
+            if static:
+                continue
             m.initialize_with_gt(self.gt_state(self.t0))
             if after_init is not None:
                 after_init(m)
@@ -312,7 +319,7 @@ class SimStream:
                     for m in mgrs:
                         if before_feed is not None:
                             before_feed(m)
-                        m.feed_measurement_camera(t, list(range(self.K)), imgs)
+                        m.feed_measurement_camera(t, list(range(self.K)), imgs, allow_uninit=static)
                 else:
                     fr = self.frames[i]
                     for m in mgrs:
