@@ -67,6 +67,14 @@ WORKLOADS = {
                   dt_slam_delay=1.0),
              dict(spawn=4),
              "cfg2 EuRoC V1_02-shaped stereo 752x480 images, 11 clones, <=200 MSCKF + 50 SLAM"),
+    # cfg2 with real track loss: 400 stereo tracks over a scene whose texture panels redraw every 4 frames
+    # (render.py churn), so each update holds 100+ lost / marginalized MSCKF features
+    "cfg2l": ("euroc_mav", "images",
+              dict(init_max_features=800, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
+                   dt_slam_delay=1.0),
+              dict(spawn=4, churn=4),
+              "cfg2l EuRoC V1_02-shaped stereo 752x480 images with track loss (scene churn 1/4 per frame), 400 "
+              "tracks, 11 clones, <=200 MSCKF + 50 SLAM"),
     "cfg3": ("tum_vi", "images",
              dict(max_clone_size=20, init_max_features=800, num_pts=400, max_msckf_in_update=400,
                   max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
@@ -100,7 +108,7 @@ WORKLOADS = {
 
 # oracle frames in the cpu_baseline sample (~10-30 s of single-core CPU work per workload)
 CPU_CV_THREADS = 4  # num_opencv_threads of every reference config
-CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg3": 60, "cfg4": 20, "cfg5": 10, "cfg4t": 3, "cfg5t": 2}
+CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg2l": 60, "cfg3": 60, "cfg4": 20, "cfg5": 10, "cfg4t": 3, "cfg5t": 2}
 
 
 def workload_options(U, name):
@@ -118,8 +126,11 @@ def make_stream(opts, n_frames, seed, workload="cfg2"):
     anchors = None
     if kw.pop("uwb", False):
         anchors = [opts.anchors[i] for i in range(opts.n_anchors)]
+    churn = kw.pop("churn", 0)
     # image workloads: the simulated tracks are not used (the images are); keep their generation small
-    return SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, anchors=anchors, **kw)
+    sim = SimStream(opts, duration=n_frames / opts.track_frequency + 1.0, seed=seed, anchors=anchors, **kw)
+    sim.churn = churn  # scene churn of the rendered images (render.py)
+    return sim
 
 
 class Frames:
@@ -129,7 +140,7 @@ class Frames:
         import torch
         from uvio_amd.render import SceneRenderer
         self.sim, self.device, self.torch = sim, device, torch
-        self.r = SceneRenderer(sim.opts, device=device)
+        self.r = SceneRenderer(sim.opts, device=device, churn=getattr(sim, "churn", 0))
         self.cache = {}
 
     def __getitem__(self, i):
@@ -408,7 +419,7 @@ def main():
 
     acc = {"rows": 0, "n_msckf": 0, "n_slam": 0, "cols": 0, "cov_dim": 0, "tracking_s": 0.0, "syncs": 0,
            "sync_wait": 0.0}
-    stages = ("propagation", "msckf_update", "slam_update", "slam_delayed", "marg", "total")
+    stages = ("propagation", "msckf_update", "slam_update", "slam_delayed", "marg", "total", "chain_wait")
     stage_s = dict.fromkeys(stages, 0.0)
     est_p, est_q, gt_p, gt_q = [], [], [], []
     mgr.set_kernel_timing(args.ktime_period)

@@ -157,6 +157,10 @@ typedef struct {
   double sync_wait;
   int zupt;  /* 1: this frame ended in a zero-velocity update (UpdaterZeroVelocity::try_update accepted) */
   int n_anchor_change;  /* SLAM landmarks re-anchored by UpdaterSLAM::change_anchors this frame (UpdaterSLAM.cpp:481-503) */
+  /* the per-frame device update chain (MSCKF, SLAM chunks, delayed initialization enqueued back to back, DESIGN.md
+   * §4): seconds of its single wait for the device plus the host replay of the results.  The chain books this
+   * time in slam_delayed (the last stage); msckf_update / slam_update hold the host enqueue times of theirs */
+  double chain_wait;
 } uvio_hp_timing_t;
 
 /* Live device timing of the kernel classes the benchmark prices against a roofline (HIP events on the

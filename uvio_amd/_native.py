@@ -71,7 +71,8 @@ class Timing(C.Structure):
                 ("n_slam_delayed", C.c_int), ("n_clones", C.c_int), ("cov_dim", C.c_int),
                 ("msckf_rows", C.c_int), ("msckf_cols", C.c_int), ("k_feat_launches", C.c_int),
                 ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double), ("device_syncs", C.c_int),
-                ("sync_wait", C.c_double), ("zupt", C.c_int), ("n_anchor_change", C.c_int)]
+                ("sync_wait", C.c_double), ("zupt", C.c_int), ("n_anchor_change", C.c_int),
+                ("chain_wait", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -403,6 +403,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     items.push_back(std::move(ci));
   }
   // ---- 5) one readback: every update's region and every batch's per-feature results
+  const auto tw = clk::now();
   {
     HPROF("chain.wait");
     if (nreg > 0)
@@ -512,6 +513,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
   chain_times_[0] = secs(tm0, tm1);
   chain_times_[1] = secs(tm1, tm2);
   chain_times_[2] = secs(tm2, tm4);
+  timing_.chain_wait = secs(tw, tm4);
   (void)tm3;
   return 0;
 }

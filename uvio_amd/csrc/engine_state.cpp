@@ -430,7 +430,7 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
        1},
       {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
-      {"pyramid", "k_hist_multi,k_eq_scharr_multi,k_pyr_scharr_multi", 0},
+      {"pyramid", "k_hist_multi,k_pyr_pair", 0},
   };
   if (flush) {
     HP_HIP(hipStreamSynchronize(d_.stream));

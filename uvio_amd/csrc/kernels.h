@@ -274,11 +274,6 @@ struct DPyr {
   int w[kMaxPyrLevels], h[kMaxPyrLevels];
   int levels;
 };
-// equalizeHist (or copy when !equalize) of src (row stride `stride`) into dst (packed); hist: 256 u32
-void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride, int equalize, unsigned *hist,
-                     uint8_t *dst);
-// pyrDown + Scharr for every level of p (level 0 image already written)
-void launch_pyramid(hipStream_t s, DPyr &p);
 // one frame's cameras at once: equalizeHist (or copy) of src[c] (row stride stride[c]) into level 0 of
 // p[c], then every level's pyrDown + Scharr; hist[c]: 256 u32 scratch per camera
 struct PyrJob {

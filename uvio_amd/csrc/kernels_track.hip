@@ -1,9 +1,9 @@
 // KLT front-end kernels (TrackKLT.cpp:34-886, Grider_GRID.h:74-180 over the OpenCV primitives they
 // call; restated in oracle/src/tracker.cpp).  Byte / integer work throughout
 // except cornerSubPix (double) and the LK float tail; every result is bit-identical to the oracle:
-//   k_hist + k_equalize      equalizeHist: LDS histogram, LUT per workgroup from the global counts
-//   k_pyrdown                pyrDown 5x5 (sum + 128) >> 8, reflect-101
-//   k_scharr                 Scharr dx/dy int16, reflect-101 (calcSharrDeriv)
+//   k_hist_multi + k_pyr_pair  equalizeHist (LDS histogram, LUT per workgroup from the global counts),
+//                            pyrDown 5x5 (sum + 128) >> 8 and Scharr dx/dy int16 (calcSharrDeriv), reflect-101,
+//                            two pyramid levels per launch
 //   k_fast_cells             FAST-9 + 3x3 NMS + top-k per grid cell (one workgroup per valid cell)
 //   k_subpix                 cornerSubPix, one thread per point (sequential sums = oracle order)
 //   k_lk                     pyramidal LK, one wavefront per point, exact integer window sums
@@ -22,110 +22,169 @@ __device__ __forceinline__ int reflect101(int p, int n) {
   return p;
 }
 
-// ---------------------------------------------------------------- equalizeHist
-__global__ void __launch_bounds__(256) k_hist(const uint8_t *__restrict__ img, int w, int h, int stride,
-                                              unsigned *__restrict__ hist) {
-  __shared__ unsigned hs[256];
-  hs[threadIdx.x] = 0;
-  __syncthreads();
-  const int n = w * h;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    int y = e / w, x = e - y * w;
-    atomicAdd(&hs[img[(size_t)y * stride + x]], 1u);
-  }
-  __syncthreads();
-  if (hs[threadIdx.x]) atomicAdd(&hist[threadIdx.x], hs[threadIdx.x]);
+// ---------------------------------------------------------------- fused multi-camera pyramid
+// All cameras of a frame in one launch per stage (blockIdx.z = camera), TWO pyramid levels per launch:
+//   k_hist_multi              histograms of the input images
+//   k_pyr_pair<true>  (l = 0) level 0 = LUT(src) (the LUT from the histogram scan) and level 1
+//   k_pyr_pair<false> (l = 2) level 2 = pyrDown(level 1) and level 3; (l = 4) level 4
+// A workgroup owns a 64 x 16 tile of level l and the 32 x 8 tile of level l+1 below it.  Level l is built in
+// LDS over the tile plus a 4-pixel margin (each cell the value at the reflect-101 coordinate, so the margin
+// holds exactly the neighbours calcSharrDeriv and the next pyrDown read); level l's pixels and Scharr
+// derivatives are written from LDS four pixels per thread (one 4-byte image store, one 16-byte derivative
+// store), then level l+1 (+1 halo, reflect-101 in its own size) is reduced from the same LDS block and
+// written with its derivatives.  Level l+1 is never read back for level l+2's margin inside the launch, and
+// level l is not re-read from memory for level l+1: 4 launches per frame (with the histogram) instead of 6,
+// same bits as one pyrDown + Scharr per level.
+constexpr int kPW = 64, kPH = 16, kPM = 4;           // level-l tile and LDS margin
+constexpr int kWW = kPW + 2 * kPM, kWH = kPH + 2 * kPM;  // LDS window of level l: 72 x 24
+constexpr int kQW = kPW / 2, kQH = kPH / 2;          // level-(l+1) tile: 32 x 8
+
+__device__ __forceinline__ void scharr_at(const uint8_t *t, int ld, int x, int y, int16_t &dx, int16_t &dy) {
+  // (x, y): the pixel's cell; the 3x3 neighbourhood is in t
+  const uint8_t *rm = t + (y - 1) * ld, *r0 = t + y * ld, *rp = t + (y + 1) * ld;
+  const int t0m = (rm[x - 1] + rp[x - 1]) * 3 + r0[x - 1] * 10, t0p = (rm[x + 1] + rp[x + 1]) * 3 + r0[x + 1] * 10;
+  const int t1m = rp[x - 1] - rm[x - 1], t1p = rp[x + 1] - rm[x + 1], t1 = rp[x] - rm[x];
+  dx = (int16_t)(t0p - t0m);
+  dy = (int16_t)((t1p + t1m) * 3 + t1 * 10);
 }
 
-__global__ void __launch_bounds__(256) k_equalize(const uint8_t *__restrict__ src, int w, int h, int stride,
-                                                  const unsigned *__restrict__ hist, int equalize,
-                                                  uint8_t *__restrict__ dst) {
-  // LUT of EqualizeHistLut_Invoker from an inclusive LDS scan of the counts (blockDim == 256)
-  __shared__ uint8_t lut[256];
-  __shared__ int scan[256];
-  __shared__ int first;
-  const int t = threadIdx.x;
-  if (!equalize) {
-    lut[t] = (uint8_t)t;
-  } else {
-    const int hv = (int)hist[t];
-    scan[t] = hv;
-    if (t == 0) first = 256;
-    __syncthreads();
-    if (hv) atomicMin(&first, t);
-    for (int o = 1; o < 256; o <<= 1) {
-      int v = (t >= o) ? scan[t - o] : 0;
-      __syncthreads();
-      scan[t] += v;
-      __syncthreads();
-    }
-    const int i0 = first, total = w * h, h0 = (int)hist[i0];
-    if (h0 == total) {
-      lut[t] = (uint8_t)i0;
-    } else if (t <= i0) {
-      lut[t] = 0;
-    } else {
-      float scale = __fdiv_rn(256 - 1.f, (float)(total - h0));
-      int sum = scan[t] - scan[i0];
-      int r = (int)rintf(__fmul_rn((float)sum, scale));
-      lut[t] = (uint8_t)min(255, max(0, r));
-    }
-  }
-  __syncthreads();
-  const int n = w * h;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    int y = e / w, x = e - y * w;
-    dst[e] = lut[src[(size_t)y * stride + x]];
-  }
-}
-
-// ---------------------------------------------------------------- pyramid
-__global__ void k_pyrdown(const uint8_t *__restrict__ src, int sw, int sh, uint8_t *__restrict__ dst, int dw, int dh) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
-  if (x >= dw || y >= dh) return;
-  const int k[5] = {1, 4, 6, 4, 1};
+__device__ __forceinline__ int pyrdown_at(const uint8_t *src, int sw, int sh, int ld, int x, int y) {
+  const int k5[5] = {1, 4, 6, 4, 1};
   int xs[5];
 #pragma unroll
   for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
   int acc = 0;
 #pragma unroll
   for (int i = 0; i < 5; i++) {
-    const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * sw;
+    const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * ld;
     int r = 0;
 #pragma unroll
-    for (int j = 0; j < 5; j++) r += k[j] * row[xs[j]];
-    acc += k[i] * r;
+    for (int j = 0; j < 5; j++) r += k5[j] * row[xs[j]];
+    acc += k5[i] * r;
   }
-  dst[(size_t)y * dw + x] = (uint8_t)((acc + 128) >> 8);
+  return (acc + 128) >> 8;
 }
 
-__global__ void k_scharr(const uint8_t *__restrict__ s, int w, int h, int16_t *__restrict__ d) {
-  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
-  if (x >= w || y >= h) return;
-  const uint8_t *r0 = s + (size_t)reflect101(y - 1, h) * w, *r1 = s + (size_t)y * w, *r2 = s + (size_t)reflect101(y + 1, h) * w;
-  int xm = reflect101(x - 1, w), xp = reflect101(x + 1, w);
-  int t0m = (r0[xm] + r2[xm]) * 3 + r1[xm] * 10, t0p = (r0[xp] + r2[xp]) * 3 + r1[xp] * 10;
-  int t1m = r2[xm] - r0[xm], t1p = r2[xp] - r0[xp], t1 = r2[x] - r0[x];
-  d[((size_t)y * w + x) * 2] = (int16_t)(t0p - t0m);
-  d[((size_t)y * w + x) * 2 + 1] = (int16_t)((t1p + t1m) * 3 + t1 * 10);
+// level `l`'s owned pixels (4 per thread) and derivatives from the LDS window
+__device__ __forceinline__ void write_level(const uint8_t *win, int x0, int y0, int w, int h, uint8_t *img,
+                                            int16_t *der) {
+  const int t = threadIdx.x, ty = t >> 4, tx = (t & 15) * 4;
+  const int gy = y0 + ty, gx = x0 + tx;
+  if (gy >= h || gx >= w) return;
+  const int cy = ty + kPM, cx = tx + kPM;
+  uint8_t v[4];
+  int16_t d[8];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = win[cy * kWW + cx + k];
+    scharr_at(win, kWW, cx + k, cy, d[2 * k], d[2 * k + 1]);
+  }
+  const size_t o = (size_t)gy * w + gx;
+  if (gx + 3 < w && (w & 3) == 0) {
+    *(uchar4 *)(img + o) = make_uchar4(v[0], v[1], v[2], v[3]);
+    short4 lo = make_short4(d[0], d[1], d[2], d[3]), hi = make_short4(d[4], d[5], d[6], d[7]);
+    int4 pk;
+    pk.x = (int)(((unsigned)(uint16_t)lo.y << 16) | (uint16_t)lo.x);
+    pk.y = (int)(((unsigned)(uint16_t)lo.w << 16) | (uint16_t)lo.z);
+    pk.z = (int)(((unsigned)(uint16_t)hi.y << 16) | (uint16_t)hi.x);
+    pk.w = (int)(((unsigned)(uint16_t)hi.w << 16) | (uint16_t)hi.z);
+    *(int4 *)(der + 2 * o) = pk;
+  } else {
+    for (int k = 0; k < 4 && gx + k < w; k++) {
+      img[o + k] = v[k];
+      der[2 * (o + k)] = d[2 * k];
+      der[2 * (o + k) + 1] = d[2 * k + 1];
+    }
+  }
 }
 
-// ---------------------------------------------------------------- fused multi-camera pyramid
-// All cameras of a frame in one launch per stage (blockIdx.z = camera):
-//   k_hist_multi               histograms of the input images
-//   k_eq_scharr_multi          LUT from the histogram scan, level 0 = LUT(src), Scharr of level 0
-//   k_pyr_scharr_multi(l)      level l = pyrDown(level l-1), Scharr of level l
-// A 32x8 output tile plus a 1-pixel halo (reflect-101 coordinates, so the halo holds exactly the
-// neighbours calcSharrDeriv reads) is built in LDS and the derivatives come out of LDS: 6 launches per
-// frame for all levels of all cameras instead of 11 per camera, same bits as k_pyrdown + k_scharr.
-constexpr int kTW = 32, kTH = 8;
-
-__device__ __forceinline__ void scharr_from_tile(const uint8_t (*t)[kTW + 2], int tx, int ty, int16_t *d) {
-  const int xm = tx, x = tx + 1, xp = tx + 2, ym = ty, y = ty + 1, yp = ty + 2;
-  const int t0m = (t[ym][xm] + t[yp][xm]) * 3 + t[y][xm] * 10, t0p = (t[ym][xp] + t[yp][xp]) * 3 + t[y][xp] * 10;
-  const int t1m = t[yp][xm] - t[ym][xm], t1p = t[yp][xp] - t[ym][xp], t1 = t[yp][x] - t[ym][x];
-  d[0] = (int16_t)(t0p - t0m);
-  d[1] = (int16_t)((t1p + t1m) * 3 + t1 * 10);
+template <bool EQ>
+__global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
+  __shared__ uint8_t lut[256];
+  __shared__ int scan[256];
+  __shared__ int first;
+  __shared__ uint8_t win[kWH * kWW];
+  __shared__ uint8_t q[(kQH + 2) * (kQW + 2)];
+  const int c = blockIdx.z, t = threadIdx.x;
+  const DPyr &p = job.p[c];
+  if (l >= p.levels) return;
+  const int w = p.w[l], h = p.h[l];
+  const int ntx = (w + kPW - 1) / kPW;
+  const int x0 = (blockIdx.x % ntx) * kPW, y0 = (blockIdx.x / ntx) * kPH;
+  if (y0 >= h) return;
+  if constexpr (EQ) {
+    // LUT of EqualizeHistLut_Invoker from an inclusive LDS scan of the counts (blockDim == 256)
+    if (!job.equalize) {
+      lut[t] = (uint8_t)t;
+    } else {
+      const unsigned *hist = job.hist[c];
+      const int hv = (int)hist[t];
+      scan[t] = hv;
+      if (t == 0) first = 256;
+      __syncthreads();
+      if (hv) atomicMin(&first, t);
+      for (int o = 1; o < 256; o <<= 1) {
+        int v = (t >= o) ? scan[t - o] : 0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+      }
+      const int i0 = first, total = w * h, h0 = (int)hist[i0];
+      if (h0 == total) {
+        lut[t] = (uint8_t)i0;
+      } else if (t <= i0) {
+        lut[t] = 0;
+      } else {
+        float scale = __fdiv_rn(256 - 1.f, (float)(total - h0));
+        int sum = scan[t] - scan[i0];
+        int r = (int)rintf(__fmul_rn((float)sum, scale));
+        lut[t] = (uint8_t)min(255, max(0, r));
+      }
+    }
+    __syncthreads();
+  }
+  // level l over the window (reflect-101 coordinates)
+  const uint8_t *src = EQ ? job.src[c] : p.img[l - 1];
+  const int sld = EQ ? job.stride[c] : p.w[l - 1];
+  for (int e = t; e < kWH * kWW; e += 256) {
+    const int wy = e / kWW, wx = e - wy * kWW;
+    const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
+    if constexpr (EQ)
+      win[e] = lut[src[(size_t)gy * sld + gx]];
+    else
+      win[e] = (uint8_t)pyrdown_at(src, p.w[l - 1], p.h[l - 1], sld, gx, gy);
+  }
+  __syncthreads();
+  write_level(win, x0, y0, w, h, (uint8_t *)p.img[l], (int16_t *)p.der[l]);
+  if (l + 1 >= p.levels) return;
+  // level l+1: the 32 x 8 tile + 1 halo, each cell pyrDown of the window at its reflect-101 coordinate
+  const int dw = p.w[l + 1], dh = p.h[l + 1], qx0 = x0 / 2, qy0 = y0 / 2;
+  if (qy0 >= dh || qx0 >= dw) return;
+  const int k5[5] = {1, 4, 6, 4, 1};
+  for (int e = t; e < (kQH + 2) * (kQW + 2); e += 256) {
+    const int ty = e / (kQW + 2), tx = e - ty * (kQW + 2);
+    const int x = reflect101(qx0 + tx - 1, dw), y = reflect101(qy0 + ty - 1, dh);
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      // level-l row 2y + i - 2 (the window cell holds its reflect-101 value)
+      const uint8_t *row = win + (2 * y + i - 2 - (y0 - kPM)) * kWW - (x0 - kPM);
+      int r = 0;
+#pragma unroll
+      for (int j = 0; j < 5; j++) r += k5[j] * row[2 * x + j - 2];
+      acc += k5[i] * r;
+    }
+    q[e] = (uint8_t)((acc + 128) >> 8);
+  }
+  __syncthreads();
+  const int tx = t & (kQW - 1), ty = t / kQW, gx = qx0 + tx, gy = qy0 + ty;
+  if (gx < dw && gy < dh) {
+    const size_t o = (size_t)gy * dw + gx;
+    ((uint8_t *)p.img[l + 1])[o] = q[(ty + 1) * (kQW + 2) + tx + 1];
+    int16_t dx, dy;
+    scharr_at(q, kQW + 2, tx + 1, ty + 1, dx, dy);
+    *(int *)((int16_t *)p.der[l + 1] + 2 * o) = (int)(((unsigned)(uint16_t)dy << 16) | (uint16_t)dx);
+  }
 }
 
 __global__ void __launch_bounds__(256) k_hist_multi(PyrJob job) {
@@ -144,130 +203,41 @@ __global__ void __launch_bounds__(256) k_hist_multi(PyrJob job) {
   if (hs[threadIdx.x]) atomicAdd(&job.hist[c][threadIdx.x], hs[threadIdx.x]);
 }
 
-__global__ void __launch_bounds__(256) k_eq_scharr_multi(PyrJob job) {
-  __shared__ uint8_t lut[256];
-  __shared__ int scan[256];
-  __shared__ int first;
-  __shared__ uint8_t tile[kTH + 2][kTW + 2];
-  const int c = blockIdx.z, t = threadIdx.x;
-  const DPyr &p = job.p[c];
-  const int w = p.w[0], h = p.h[0], stride = job.stride[c];
-  const uint8_t *src = job.src[c];
-  // LUT of EqualizeHistLut_Invoker (as k_equalize)
-  if (!job.equalize) {
-    lut[t] = (uint8_t)t;
-  } else {
-    const unsigned *hist = job.hist[c];
-    const int hv = (int)hist[t];
-    scan[t] = hv;
-    if (t == 0) first = 256;
-    __syncthreads();
-    if (hv) atomicMin(&first, t);
-    for (int o = 1; o < 256; o <<= 1) {
-      int v = (t >= o) ? scan[t - o] : 0;
-      __syncthreads();
-      scan[t] += v;
-      __syncthreads();
-    }
-    const int i0 = first, total = w * h, h0 = (int)hist[i0];
-    if (h0 == total) {
-      lut[t] = (uint8_t)i0;
-    } else if (t <= i0) {
-      lut[t] = 0;
-    } else {
-      float scale = __fdiv_rn(256 - 1.f, (float)(total - h0));
-      int sum = scan[t] - scan[i0];
-      int r = (int)rintf(__fmul_rn((float)sum, scale));
-      lut[t] = (uint8_t)min(255, max(0, r));
-    }
-  }
-  __syncthreads();
-  const int ntx = (w + kTW - 1) / kTW;
-  const int x0 = (blockIdx.x % ntx) * kTW, y0 = (blockIdx.x / ntx) * kTH;
-  if (y0 >= h) return;
-  for (int e = t; e < (kTW + 2) * (kTH + 2); e += blockDim.x) {
-    const int ty = e / (kTW + 2), tx = e - ty * (kTW + 2);
-    const int gx = reflect101(x0 + tx - 1, w), gy = reflect101(y0 + ty - 1, h);
-    tile[ty][tx] = lut[src[(size_t)gy * stride + gx]];
-  }
-  __syncthreads();
-  const int tx = t % kTW, ty = t / kTW, gx = x0 + tx, gy = y0 + ty;
-  if (gx < w && gy < h) {
-    ((uint8_t *)p.img[0])[(size_t)gy * w + gx] = tile[ty + 1][tx + 1];
-    scharr_from_tile(tile, tx, ty, (int16_t *)p.der[0] + ((size_t)gy * w + gx) * 2);
-  }
-}
-
-__global__ void __launch_bounds__(256) k_pyr_scharr_multi(PyrJob job, int l) {
-  __shared__ uint8_t tile[kTH + 2][kTW + 2];
-  const int c = blockIdx.z, t = threadIdx.x;
-  const DPyr &p = job.p[c];
-  if (l >= p.levels) return;
-  const int sw = p.w[l - 1], sh = p.h[l - 1], dw = p.w[l], dh = p.h[l];
-  const uint8_t *src = p.img[l - 1];
-  const int ntx = (dw + kTW - 1) / kTW;
-  const int x0 = (blockIdx.x % ntx) * kTW, y0 = (blockIdx.x / ntx) * kTH;
-  if (y0 >= dh) return;
-  const int k5[5] = {1, 4, 6, 4, 1};
-  for (int e = t; e < (kTW + 2) * (kTH + 2); e += blockDim.x) {
-    const int ty = e / (kTW + 2), tx = e - ty * (kTW + 2);
-    const int x = reflect101(x0 + tx - 1, dw), y = reflect101(y0 + ty - 1, dh);
-    int xs[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
-    int acc = 0;
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * sw;
-      int r = 0;
-#pragma unroll
-      for (int j = 0; j < 5; j++) r += k5[j] * row[xs[j]];
-      acc += k5[i] * r;
-    }
-    tile[ty][tx] = (uint8_t)((acc + 128) >> 8);
-  }
-  __syncthreads();
-  const int tx = t % kTW, ty = t / kTW, gx = x0 + tx, gy = y0 + ty;
-  if (gx < dw && gy < dh) {
-    ((uint8_t *)p.img[l])[(size_t)gy * dw + gx] = tile[ty + 1][tx + 1];
-    scharr_from_tile(tile, tx, ty, (int16_t *)p.der[l] + ((size_t)gy * dw + gx) * 2);
-  }
-}
-
 void launch_pyramids(hipStream_t s, const PyrJob &job) {
   if (job.ncam <= 0) return;
-  int w0 = 0, h0 = 0, maxl = 0;
-  for (int c = 0; c < job.ncam; c++) {
-    w0 = max(w0, job.p[c].w[0]);
-    h0 = max(h0, job.p[c].h[0]);
-    maxl = max(maxl, job.p[c].levels);
-  }
-  if (job.equalize) {
-    for (int c = 0; c < job.ncam; c++)
-      if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
-    hipLaunchKernelGGL(k_hist_multi, dim3(min(256, (w0 * h0 + 4095) / 4096), 1, job.ncam), dim3(256), 0, s, job);
-  }
-  const int t0 = ((w0 + kTW - 1) / kTW) * ((h0 + kTH - 1) / kTH);
-  hipLaunchKernelGGL(k_eq_scharr_multi, dim3(t0, 1, job.ncam), dim3(256), 0, s, job);
-  for (int l = 1; l < maxl; l++) {
+  int maxl = 0;
+  for (int c = 0; c < job.ncam; c++) maxl = max(maxl, job.p[c].levels);
+  auto tiles = [&](int l) {
     int wl = 0, hl = 0;
     for (int c = 0; c < job.ncam; c++)
       if (l < job.p[c].levels) {
         wl = max(wl, job.p[c].w[l]);
         hl = max(hl, job.p[c].h[l]);
       }
-    const int tl = ((wl + kTW - 1) / kTW) * ((hl + kTH - 1) / kTH);
-    hipLaunchKernelGGL(k_pyr_scharr_multi, dim3(tl, 1, job.ncam), dim3(256), 0, s, job, l);
+    return ((wl + kPW - 1) / kPW) * ((hl + kPH - 1) / kPH);
+  };
+  if (job.equalize) {
+    int w0 = 0, h0 = 0;
+    for (int c = 0; c < job.ncam; c++) w0 = max(w0, job.p[c].w[0]), h0 = max(h0, job.p[c].h[0]);
+    for (int c = 0; c < job.ncam; c++)
+      if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
+    hipLaunchKernelGGL(k_hist_multi, dim3(min(256, (w0 * h0 + 4095) / 4096), 1, job.ncam), dim3(256), 0, s, job);
   }
+  hipLaunchKernelGGL(k_pyr_pair<true>, dim3(tiles(0), 1, job.ncam), dim3(256), 0, s, job, 0);
+  for (int l = 2; l < maxl; l += 2)
+    hipLaunchKernelGGL(k_pyr_pair<false>, dim3(tiles(l), 1, job.ncam), dim3(256), 0, s, job, l);
 }
 
 double pyramid_bytes(const PyrJob &job) {
+  // histogram pass reads the input; every pair launch reads its source (the input, or level l-1) once and
+  // writes its two levels' images and derivatives
   double b = 0.0;
   for (int c = 0; c < job.ncam; c++) {
     const DPyr &p = job.p[c];
     const double a0 = (double)p.w[0] * p.h[0];
-    b += (job.equalize ? a0 : 0.0) + a0 + a0 + 4.0 * a0;  // histogram read, source read, level 0 + Scharr
-    for (int l = 1; l < p.levels; l++) b += (double)p.w[l - 1] * p.h[l - 1] + 5.0 * p.w[l] * p.h[l];
+    b += (job.equalize ? a0 : 0.0) + a0;
+    for (int l = 0; l < p.levels; l++) b += 5.0 * p.w[l] * p.h[l];
+    for (int l = 2; l < p.levels; l += 2) b += (double)p.w[l - 1] * p.h[l - 1];
   }
   return b;
 }
@@ -617,10 +587,41 @@ __device__ __forceinline__ int der_px(const int16_t *d, int w, int h, int x, int
   return d[((size_t)y * w + x) * 2 + c];
 }
 __device__ __forceinline__ int descale(long long x, int n) { return (int)((x + (1ll << (n - 1))) >> n); }
-__device__ __forceinline__ long long wave_sum_ll(long long v) {
+// Exact wave sums of integer partials through DPP instead of six ds_bpermute rounds: every partial and every
+// total here is an integer below 2^53 in magnitude, so the FP64 adds are exact in any order (LK window sums:
+// |partial| < 2^32, |total| < 2^38).  Within a row of 16 lanes: quad_perm xor 1, xor 2, row_half_mirror,
+// row_mirror (each lane then holds its row's sum); across rows: row_bcast15 / row_bcast31 into row 3 and
+// v_readlane of lane 63.  The whole wave must be active.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, ROWMASK, 0xf, false);
+  const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+template <int N>
+__device__ __forceinline__ void wave_sum_exact(long long (&v)[N]) {
+  double d[N];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  for (int k = 0; k < N; k++) d[k] = (double)v[k];
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0xB1>(d[k]);   // quad_perm [1, 0, 3, 2]
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x4E>(d[k]);   // quad_perm [2, 3, 0, 1]
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x141>(d[k]);  // row_half_mirror
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x140>(d[k]);  // row_mirror
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x142, 0xa>(d[k]);  // row_bcast15 -> rows 1, 3
+#pragma unroll
+  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x143, 0xc>(d[k]);  // row_bcast31 -> rows 2, 3
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, d[k]);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, 63), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), 63);
+    v[k] = (long long)__builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+  }
 }
 
 constexpr int kLkMargin = 4, kLkMaxWin = 16, kLkMaxTile = kLkMaxWin + 1 + 2 * kLkMargin;
@@ -701,9 +702,13 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
         sA22 += (long long)iyv * iyv;
       }
     }
-    sA11 = wave_sum_ll(sA11);
-    sA12 = wave_sum_ll(sA12);
-    sA22 = wave_sum_ll(sA22);
+    {
+      long long s3[3] = {sA11, sA12, sA22};
+      wave_sum_exact<3>(s3);
+      sA11 = s3[0];
+      sA12 = s3[1];
+      sA22 = s3[2];
+    }
     const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
     float D = A11 * A22 - A12 * A12;
     const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
@@ -751,8 +756,12 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
           ib2 += (long long)diff * dIy[q];
         }
       }
-      ib1 = wave_sum_ll(ib1);
-      ib2 = wave_sum_ll(ib2);
+      {
+        long long s2[2] = {ib1, ib2};
+        wave_sum_exact<2>(s2);
+        ib1 = s2[0];
+        ib2 = s2[1];
+      }
       const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
       const float dx = (A12 * b2 - A22 * b1) * D;
       const float dy = (A12 * b1 - A11 * b2) * D;
@@ -1023,25 +1032,6 @@ __global__ void __launch_bounds__(256) k_ransac_select(RansacSlots job, int max_
 }
 
 // ---------------------------------------------------------------- launch wrappers
-void launch_equalize(hipStream_t s, const uint8_t *src, int w, int h, int stride, int equalize, unsigned *hist,
-                     uint8_t *dst) {
-  int blocks = min(256, (w * h + 4095) / 4096);
-  if (equalize) {
-    if (hipMemsetAsync(hist, 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
-    hipLaunchKernelGGL(k_hist, dim3(blocks), dim3(256), 0, s, src, w, h, stride, hist);
-  }
-  hipLaunchKernelGGL(k_equalize, dim3(blocks), dim3(256), 0, s, src, w, h, stride, hist, equalize, dst);
-}
-
-void launch_pyramid(hipStream_t s, DPyr &p) {
-  for (int l = 0; l < p.levels; l++) {
-    dim3 b(32, 8), g((p.w[l] + 31) / 32, (p.h[l] + 7) / 8);
-    if (l > 0)
-      hipLaunchKernelGGL(k_pyrdown, g, b, 0, s, p.img[l - 1], p.w[l - 1], p.h[l - 1], (uint8_t *)p.img[l], p.w[l], p.h[l]);
-    hipLaunchKernelGGL(k_scharr, g, b, 0, s, p.img[l], p.w[l], p.h[l], (int16_t *)p.der[l]);
-  }
-}
-
 void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n) {
   if (job.ncam <= 0 || job.ncam > kMaxCams) return;
   const int ncell = job.cell_end[job.ncam - 1];

@@ -17,7 +17,7 @@ enum KClass {
   KC_EKF,          // one EKFUpdate (direct or information form): every kernel of the update chain
   KC_LDL,          // k_ekf_fact: LDL^T / Cholesky (+ inverse) of the innovation covariance (inside KC_EKF)
   KC_LK,           // k_lk: pyramidal LK
-  KC_PYR,          // k_hist_multi + k_eq_scharr_multi + k_pyr_scharr_multi: equalizeHist + pyramid + Scharr
+  KC_PYR,          // k_hist_multi + k_pyr_pair: equalizeHist + pyramid + Scharr
   KC_COUNT
 };
 

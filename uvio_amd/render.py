@@ -9,6 +9,11 @@ little seeded sensor noise.  Rays come from inverting the camera's distortion on
 where the estimator's distort() predicts them.
 
 Rendering runs on torch (the GPU when present) so a few hundred stereo frames take seconds.
+
+churn > 0 (track-loss streams): every face is cut into PANEL x PANEL m panels, and each panel redraws its
+texture (tile values, tile-grid offset, noise) every `churn` frames at its own random phase, so about
+1/churn of the scene changes under the tracks each frame.  A track on a redrawn panel loses its corner:
+KLT drifts or fails and the RANSAC step drops it, as on real footage with occlusions and motion blur.
 """
 import numpy as np
 import torch
@@ -16,6 +21,7 @@ import torch
 ROOM_MIN = (-9.0, -9.0, -2.0)
 ROOM_MAX = (9.0, 9.0, 4.5)
 TILE = 0.25
+PANEL = 1.0
 
 
 def _undistort_grid(cam):
@@ -54,9 +60,10 @@ def _hash2(a, b, seed):
 
 
 class SceneRenderer:
-    def __init__(self, opts, device=None, seed=1234):
+    def __init__(self, opts, device=None, seed=1234, churn=0):
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
         self.seed = seed
+        self.churn = int(churn)
         self.rays = []
         self.sizes = []
         for i in range(opts.num_cameras):
@@ -78,18 +85,29 @@ class SceneRenderer:
         self.lo = torch.tensor(ROOM_MIN, dtype=torch.float32, device=self.device)
         self.hi = torch.tensor(ROOM_MAX, dtype=torch.float32, device=self.device)
 
-    def _texture(self, face, s, t):
+    def _texture(self, face, s, t, frame=0):
+        seed = torch.full_like(face, self.seed)
+        if self.churn > 0:
+            # the panel's redraw epoch: floor((frame + phase) / churn), phase a per-panel hash in [0, churn)
+            pi = torch.floor(s / PANEL).to(torch.int64) + 4096 * face
+            pj = torch.floor(t / PANEL).to(torch.int64)
+            phase = torch.floor(_hash2(pi, pj, self.seed + 3) * self.churn).to(torch.int64)
+            epoch = torch.div(frame + phase, self.churn, rounding_mode="floor")
+            seed = seed + 7919 * epoch
+            # a new tile-grid offset per epoch moves the panel's corners
+            s = s + TILE * _hash2(pi, pj, seed + 5)
+            t = t + TILE * _hash2(pj, pi, seed + 11)
         si = torch.floor(s / TILE).to(torch.int64)
         ti = torch.floor(t / TILE).to(torch.int64)
-        base = 35.0 + 185.0 * _hash2(si + 1000 * face, ti, self.seed)
+        base = 35.0 + 185.0 * _hash2(si + 1000 * face, ti, seed)
         # value noise at 1/4 tile for LK texture
         fs, ft = s / (TILE / 4), t / (TILE / 4)
         i0, j0 = torch.floor(fs).to(torch.int64), torch.floor(ft).to(torch.int64)
         a, b = fs - i0, ft - j0
-        n00 = _hash2(i0, j0, self.seed + 7 + face)
-        n10 = _hash2(i0 + 1, j0, self.seed + 7 + face)
-        n01 = _hash2(i0, j0 + 1, self.seed + 7 + face)
-        n11 = _hash2(i0 + 1, j0 + 1, self.seed + 7 + face)
+        n00 = _hash2(i0, j0, seed + 7 + face)
+        n10 = _hash2(i0 + 1, j0, seed + 7 + face)
+        n01 = _hash2(i0, j0 + 1, seed + 7 + face)
+        n11 = _hash2(i0 + 1, j0 + 1, seed + 7 + face)
         n = (1 - a) * (1 - b) * n00 + a * (1 - b) * n10 + (1 - a) * b * n01 + a * b * n11
         return base + 36.0 * (n - 0.5)
 
@@ -112,7 +130,7 @@ class SceneRenderer:
         # in-plane coordinates of each face
         ax0 = torch.where(axis == 0, P[..., 1], P[..., 0])
         ax1 = torch.where(axis == 2, P[..., 1], P[..., 2])
-        img = self._texture(face, ax0, ax1)
+        img = self._texture(face, ax0, ax1, frame_seed)
         g = torch.Generator(device=self.device)
         g.manual_seed(int(self.seed * 1000003 + frame_seed * 7 + k))
         img = img + 2.0 * torch.randn(img.shape, generator=g, device=self.device)
