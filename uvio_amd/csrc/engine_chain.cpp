@@ -64,6 +64,12 @@ struct Engine::ChainItem {
   std::vector<FeatP> fv;
   int region = -1;  // d_.chain region of its update (-1: none enqueued)
   int m = 0;        // stacked rows
+  // the batch's staged tables (device addresses after the flush)
+  bool staged = false;
+  const DFeat *t_feats = nullptr;
+  const DMeas *t_meas = nullptr;
+  const DVar *t_vars = nullptr;
+  const int *t_hidx = nullptr;
 };
 
 int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, std::vector<FeatP> &delayed) {
@@ -139,18 +145,17 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
   const int K = (int)delayed.size();
   if (N0 + 3 * K > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
 
-  // ---- 1) the frame state on the device
-  DClone *fr_cl;
-  DCam *fr_cam;
-  DPoseVal *fr_cv, *fr_camv;
-  double *fr_xv;
-  int ncl, ncam;
+  // ---- 1) host side first: the frame state blob and every batch's tables (the large MSCKF batches write
+  // theirs straight into the staging ring while they are built)
+  double t_build[3] = {0, 0, 0}, t_launch[3] = {0, 0, 0};
+  auto tm0 = clk::now();
+  Batch base;
+  build_clone_cam_tables(base, false);
+  const int ncl = (int)base.clones.size(), ncam = (int)base.cams.size();
+  std::vector<char> blob;
+  size_t o_cam, o_cv, o_camv, o_xv;
   {
     HPROF("chain.state");
-    Batch base;
-    build_clone_cam_tables(base, false);
-    ncl = (int)base.clones.size();
-    ncam = (int)base.cams.size();
     std::vector<DPoseVal> cv(ncl), camv(ncam);
     int s = 0;
     for (auto &c : clones_) {
@@ -168,28 +173,82 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     std::vector<double> xv((size_t)d_.ldp, 0.0);
     for (auto &kv : slam_)
       for (int k = 0; k < kv.second->size; k++) xv[(size_t)kv.second->id + k] = kv.second->val[k];
-    // one contiguous blob, staged and copied into the dedicated buffer (the ring may restart during the chain)
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
-    const size_t o_cam = al(sizeof(DClone) * ncl), o_cv = o_cam + al(sizeof(DCam) * ncam),
-                 o_camv = o_cv + al(sizeof(DPoseVal) * ncl), o_xv = o_camv + al(sizeof(DPoseVal) * ncam),
-                 bytes = o_xv + sizeof(double) * xv.size();
+    o_cam = al(sizeof(DClone) * ncl);
+    o_cv = o_cam + al(sizeof(DCam) * ncam);
+    o_camv = o_cv + al(sizeof(DPoseVal) * ncl);
+    o_xv = o_camv + al(sizeof(DPoseVal) * ncam);
+    const size_t bytes = o_xv + sizeof(double) * xv.size();
     if (bytes > d_.frame_bytes) throw HpError(UVIO_HP_E_CAPACITY, "update chain state exceeds its buffer");
-    std::vector<char> blob(bytes, 0);
+    blob.assign(bytes, 0);
     std::memcpy(blob.data(), base.clones.data(), sizeof(DClone) * ncl);
     std::memcpy(blob.data() + o_cam, base.cams.data(), sizeof(DCam) * ncam);
     std::memcpy(blob.data() + o_cv, cv.data(), sizeof(DPoseVal) * ncl);
     std::memcpy(blob.data() + o_camv, camv.data(), sizeof(DPoseVal) * ncam);
     std::memcpy(blob.data() + o_xv, xv.data(), sizeof(double) * xv.size());
-    const char *staged = stage(blob.data(), blob.size());
-    stage_flush();
-    HP_HIP(hipMemcpyAsync(d_.frame, staged, bytes, hipMemcpyDeviceToDevice, d_.stream));
-    fr_cl = (DClone *)d_.frame;
-    fr_cam = (DCam *)(d_.frame + o_cam);
-    fr_cv = (DPoseVal *)(d_.frame + o_cv);
-    fr_camv = (DPoseVal *)(d_.frame + o_camv);
-    fr_xv = (double *)(d_.frame + o_xv);
   }
+  // the blob goes into the ring ahead of the MSCKF tables and is copied to its own buffer once on the device
+  // (the ring may restart while later batches are staged)
+  const char *blob_staged = stage(blob.data(), blob.size());
+  const long long blob_epoch = d_.stg_epoch;
   std::vector<std::unique_ptr<ChainItem>> items;
+  ChainItem *msk = nullptr, *tri = nullptr, *cand = nullptr;
+  std::vector<ChainItem *> slam_items;
+  auto stage_item = [&](ChainItem &it) {
+    Batch &b = it.b;
+    it.t_feats = stage(b.feats.data(), b.feats.size());
+    it.t_meas = b.meas_dev ? b.meas_dev : stage(b.meas.data(), b.meas.size());
+    it.t_vars = b.vars_dev ? b.vars_dev : stage(b.vars.data(), b.vars.size());
+    it.t_hidx = stage(b.hidx.data(), b.hidx.size());
+    b.hidx_dev = it.t_hidx;
+    it.staged = true;
+  };
+  // the bytes a group of batches adds to the ring: staged together (one copy) when they fit behind what it
+  // holds, else each right before its launches (enqueue_batch)
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  auto stage_group = [&](const std::vector<ChainItem *> &g) {
+    size_t need = 0;
+    for (ChainItem *it : g) {
+      const Batch &b = it->b;
+      need += al(sizeof(DFeat) * b.feats.size()) + al(sizeof(int) * b.hidx.size());
+      if (!b.meas_dev) need += al(sizeof(DMeas) * b.meas.size());
+      if (!b.vars_dev) need += al(sizeof(DVar) * b.vars.size());
+    }
+    if (d_.stg_used + need > d_.stg_cap) return;
+    for (ChainItem *it : g) stage_item(*it);
+  };
+  // ---- 1a) UpdaterMSCKF's batch: built, staged with the blob, and launched before the rest is built (the host
+  // builds the SLAM / delayed-initialization batches while the device runs the MSCKF update)
+  if (!up.empty()) {
+    HPROF("chain.msckf.build");
+    auto it = std::make_unique<ChainItem>();
+    it->kind = 0;
+    it->fv = up;
+    build_clone_cam_tables(it->b, false);
+    add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
+    msk = it.get();
+    items.push_back(std::move(it));
+    stage_group({msk});
+  }
+  char *const frame = d_.frame;
+  {
+    HPROF("chain.stage");
+    if (d_.stg_epoch != blob_epoch) {
+      // the ring restarted after the blob was staged: it is on the device (the restart flushed it and waited);
+      // copied out before anything staged since then is flushed over it
+      HP_HIP(hipMemcpyAsync(frame, blob_staged, blob.size(), hipMemcpyDeviceToDevice, d_.stream));
+      stage_flush();
+    } else {
+      stage_flush();
+      HP_HIP(hipMemcpyAsync(frame, blob_staged, blob.size(), hipMemcpyDeviceToDevice, d_.stream));
+    }
+  }
+  t_build[0] = secs(tm0, clk::now());
+  DClone *fr_cl = (DClone *)frame;
+  DCam *fr_cam = (DCam *)(frame + o_cam);
+  DPoseVal *fr_cv = (DPoseVal *)(frame + o_cv), *fr_camv = (DPoseVal *)(frame + o_camv);
+  double *fr_xv = (double *)(frame + o_xv);
+
   int fo = 0, nreg = 0;
   const size_t st = d_.chain_stride;
   auto new_region = [&]() {
@@ -197,8 +256,8 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     return nreg++;
   };
   auto region = [&](int r) { return d_.chain + (size_t)r * st; };
-  // stage a batch's tables and launch its feature kernel (+ the chi2 group); results at d_.fout + b.fout_off
-  auto enqueue_batch = [&](ChainItem &it, int mode, double s2, double mult, bool chi2, const DFeatOut *tri) {
+  // a batch's feature kernel (+ the chi2 group); results at d_.fout + b.fout_off
+  auto enqueue_batch = [&](ChainItem &it, int mode, double s2, double mult, bool chi2, const DFeatOut *tri_in) {
     Batch &b = it.b;
     const int nf = (int)b.feats.size();
     if (nf > d_.max_feat || (int)b.n_meas() > d_.max_meas_total || (int)b.n_vars() > d_.max_vars_total ||
@@ -213,32 +272,29 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     if (max_meas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
     b.fout_off = fo;
     fo += nf;
-    const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
-    const DMeas *t_meas = b.meas_dev ? b.meas_dev : stage(b.meas.data(), b.meas.size());
-    const DVar *t_vars = b.vars_dev ? b.vars_dev : stage(b.vars.data(), b.vars.size());
-    const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
-    stage_flush();
+    if (!it.staged) {
+      stage_item(it);
+      stage_flush();
+    }
     if (b.meas_dev && b.stg_epoch != d_.stg_epoch && d_.stg_used > (size_t)((const char *)b.meas_dev - d_.stg_d))
       throw HpError(UVIO_HP_E_CAPACITY, "upload staging ring restarted inside one launch group (UVIO_HP_STAGE_BYTES too small)");
-    b.hidx_dev = t_hidx;
     b.chi2 = chi2;
     DBatchParams bp = batch_params(b, s2, mult);
     bp.xv = fr_xv;
-    bp.tri_in = tri;
+    bp.tri_in = tri_in;
     {
       KScope ks(&kprof_, KC_FEATURE);
-      launch_feature_linearize(d_.stream, bp, t_feats, t_meas, t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H,
+      launch_feature_linearize(d_.stream, bp, it.t_feats, it.t_meas, it.t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H,
                                d_.fout + b.fout_off, max_meas, max_nf);
     }
     if (chi2) {
       int max_rows_f = 0;
       for (auto &F : b.feats) max_rows_f = std::max(max_rows_f, (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas);
       KScope ks(&kprof_, KC_CHI2);
-      launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout + b.fout_off,
+      launch_chi2_batch(d_.stream, bp, it.t_feats, d_.P, it.t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout + b.fout_off,
                         max_rows_f, d_.acc, d_.R);
     }
     it.m = b.rows;
-    return t_feats;
   };
   // the EKF update of a batch's stacked rows (direct, or information form on their Gram), gated by the batch's
   // accepted count, dx into a fresh region; then the state tables move by it
@@ -280,59 +336,43 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
                        sc.dx + N_ + 8);
   };
 
-  // ---- 2) UpdaterMSCKF::update
-  auto tm0 = clk::now();
-  if (!up.empty()) {
+  // ---- 3) UpdaterMSCKF::update
+  auto tl0 = clk::now();
+  if (msk) {
     HPROF("chain.msckf");
-    auto it = std::make_unique<ChainItem>();
-    it->kind = 0;
-    it->fv = up;
-    build_clone_cam_tables(it->b, false);
-    add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
     PrefactorJoin pj(this);
-    if (it->b.rows > it->b.n_canon || it->b.rows > kMaxEkfRows) info_prefactor(it->b.hidx);
+    if (msk->b.rows > msk->b.n_canon || msk->b.rows > kMaxEkfRows) info_prefactor(msk->b.hidx);
     const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
-    enqueue_batch(*it, 0, s2, o_.msckf_chi2_multipler, true, nullptr);
-    if (it->m >= 1) enqueue_update(*it, s2);
+    enqueue_batch(*msk, 0, s2, o_.msckf_chi2_multipler, true, nullptr);
+    if (msk->m >= 1) enqueue_update(*msk, s2);
+  }
+  // ---- 1b) the SLAM chunks' and the delayed initialization's batches (host, while the MSCKF update runs)
+  auto tb1 = clk::now();
+  for (auto &ch : slam_chunks) {
+    HPROF("chain.slam.build");
+    auto it = std::make_unique<ChainItem>();
+    it->kind = 1;
+    it->fv = ch;
+    Batch &b = it->b;
+    build_clone_cam_tables(b, true);
+    std::vector<int> lm_canon;
+    for (auto &f : it->fv) {
+      const VarP &lm = slam_.at(f->featid);
+      lm_canon.push_back(b.n_canon);
+      for (int k = 0; k < lm->size; k++) b.hidx.push_back(lm->id + k);
+      b.n_canon += lm->size;
+    }
+    for (size_t i = 0; i < it->fv.size(); i++) {
+      const VarP &lm = slam_.at(it->fv[i]->featid);
+      add_feature(this, it->fv[i], 1, lm->rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows,
+                  lm.get(), lm_canon[i]);
+    }
+    slam_items.push_back(it.get());
     items.push_back(std::move(it));
   }
-  auto tm1 = clk::now();
-  // ---- 3) UpdaterSLAM::update in chunks of max_slam_in_update (VioManager.cpp:533-545)
-  {
-    HPROF("chain.slam");
-    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
-    for (auto &ch : slam_chunks) {
-      auto it = std::make_unique<ChainItem>();
-      it->kind = 1;
-      it->fv = ch;
-      Batch &b = it->b;
-      build_clone_cam_tables(b, true);
-      std::vector<int> lm_canon;
-      for (auto &f : it->fv) {
-        const VarP &lm = slam_.at(f->featid);
-        lm_canon.push_back(b.n_canon);
-        for (int k = 0; k < lm->size; k++) b.hidx.push_back(lm->id + k);
-        b.n_canon += lm->size;
-      }
-      for (size_t i = 0; i < it->fv.size(); i++) {
-        const VarP &lm = slam_.at(it->fv[i]->featid);
-        add_feature(this, it->fv[i], 1, lm->rep, o_, b.cams, b.slot_of_time, b.clones, b.feats, b.meas, b.vars, b.rows,
-                    lm.get(), lm_canon[i]);
-      }
-      PrefactorJoin pj(this);
-      if (b.rows > b.n_canon || b.rows > kMaxEkfRows) info_prefactor(b.hidx);
-      enqueue_batch(*it, 1, s2, o_.slam_chi2_multipler, true, nullptr);
-      if (it->m >= 1) enqueue_update(*it, s2);
-      items.push_back(std::move(it));
-    }
-  }
-  auto tm2 = clk::now();
-  // ---- 4) UpdaterSLAM::delayed_init: batch triangulation, then per candidate (fixed slot N0 + 3 j) the
-  // linearization at the current state, initialize_invertible and the chi2-gated update of the other rows
-  ChainItem *tri = nullptr, *cand = nullptr;
+  auto tb2 = clk::now();
   if (K > 0) {
-    HPROF("chain.delayed");
-    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+    HPROF("chain.delayed.build");
     auto ti = std::make_unique<ChainItem>();
     ti->kind = 2;
     ti->fv = delayed;
@@ -340,7 +380,6 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     for (auto &f : delayed)
       add_feature(this, f, 2, rep_slam, o_, ti->b.cams, ti->b.slot_of_time, ti->b.clones, ti->b.feats, ti->b.meas,
                   ti->b.vars, ti->b.rows, nullptr, -1);
-    enqueue_batch(*ti, 2, s2, o_.slam_chi2_multipler, false, nullptr);
     tri = ti.get();
     items.push_back(std::move(ti));
     auto ci = std::make_unique<ChainItem>();
@@ -353,45 +392,78 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     if (b.rows > d_.max_rows || b.n_canon + 1 > d_.max_ncol || (int)b.n_meas() > d_.max_meas_total ||
         (int)b.n_vars() > d_.max_vars_total)
       throw HpError(UVIO_HP_E_CAPACITY, "delayed-initialization chain exceeds device capacity");
+    for (int j = 0; j < K; j++)
+      if (b.feats[j].nmeas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
+    cand = ci.get();
+    items.push_back(std::move(ci));
+  }
+  {
+    HPROF("chain.stage");
+    std::vector<ChainItem *> g(slam_items);
+    if (tri) g.push_back(tri);
+    if (cand) g.push_back(cand);
+    stage_group(g);
+    stage_flush();
+  }
+  auto tb3 = clk::now();
+  t_build[1] = secs(tb1, tb2);
+  t_build[2] = secs(tb2, tb3);
+  auto tl1 = clk::now();
+  // ---- 4) UpdaterSLAM::update in chunks of max_slam_in_update (VioManager.cpp:533-545)
+  {
+    HPROF("chain.slam");
+    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+    for (ChainItem *it : slam_items) {
+      PrefactorJoin pj(this);
+      if (it->b.rows > it->b.n_canon || it->b.rows > kMaxEkfRows) info_prefactor(it->b.hidx);
+      enqueue_batch(*it, 1, s2, o_.slam_chi2_multipler, true, nullptr);
+      if (it->m >= 1) enqueue_update(*it, s2);
+    }
+  }
+  auto tl2 = clk::now();
+  // ---- 5) UpdaterSLAM::delayed_init: batch triangulation, then per candidate (fixed slot N0 + 3 j) the
+  // linearization at the current state, initialize_invertible and the chi2-gated update of the other rows
+  if (K > 0) {
+    HPROF("chain.delayed");
+    const double s2 = o_.slam_sigma_pix * o_.slam_sigma_pix;
+    enqueue_batch(*tri, 2, s2, o_.slam_chi2_multipler, false, nullptr);
+    Batch &b = cand->b;
     if (fo + K > d_.fout_cap) throw HpError(UVIO_HP_E_CAPACITY, "update chain: per-feature results exceed capacity");
     b.fout_off = fo;
     fo += K;
-    const DFeat *t_feats = stage(b.feats.data(), b.feats.size());
-    const DMeas *t_meas = stage(b.meas.data(), b.meas.size());
-    const DVar *t_vars = stage(b.vars.data(), b.vars.size());
-    const int *t_hidx = stage(b.hidx.data(), b.hidx.size());
-    stage_flush();
-    b.hidx_dev = t_hidx;
+    if (!cand->staged) {
+      stage_item(*cand);
+      stage_flush();
+    }
     b.chi2 = false;
     DBatchParams bp = batch_params(b, s2, o_.slam_chi2_multipler);
     bp.nfeat = 1;
     bp.gate_out = d_.acc;  // triangulation ok and linearized: gates initialize_invertible and the update
+    bp.xv = fr_xv;
     const int n = b.n_canon;
     const DFeatOut *tri_out = d_.fout + tri->b.fout_off;
     DFeatOut *fo3 = d_.fout + b.fout_off;
-    cand = ci.get();
-    ci->region = nreg;
+    cand->region = nreg;
     for (int j = 0; j < K; j++) {
       const DFeat &F = b.feats[j];
-      if (F.nmeas > kMaxMeasPerFeat) throw HpError(UVIO_HP_E_CAPACITY, "too many measurements per feature");
       const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
       bp.tri_in = tri_out + j;
       {
         KScope ks(&kprof_, KC_FEATURE);
-        launch_feature_linearize(d_.stream, bp, t_feats + j, t_meas, t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H, fo3 + j,
-                                 F.nmeas, F.nf);
+        launch_feature_linearize(d_.stream, bp, cand->t_feats + j, cand->t_meas, cand->t_vars, fr_cl, fr_cam, d_.P,
+                                 d_.chi2, d_.H, fo3 + j, F.nmeas, F.nf);
       }
       EkfScratch sc = d_.ekf;
       sc.dx = region(new_region());
       double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
-      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, t_hidx, nullptr, s2, sc, fo3 + j, d_.acc,
+      launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, cand->t_hidx, nullptr, s2, sc, fo3 + j, d_.acc,
                              sc.dx + Ni + 5);
       if (nup > 0) {
         sc.chi2_gate = d_.acc;
         sc.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * F.nmeas, 999)];
         sc.gate = nullptr;
         KScope ks(&kprof_, KC_EKF);
-        launch_ekf_update(d_.stream, d_.P, d_.ldp, Ni + 3, Hrow + 3 * (size_t)d_.ldh, d_.ldh, nup, n, t_hidx,
+        launch_ekf_update(d_.stream, d_.P, d_.ldp, Ni + 3, Hrow + 3 * (size_t)d_.ldh, d_.ldh, nup, n, cand->t_hidx,
                           Hrow + 3 * (size_t)d_.ldh + n, d_.ldh, s2, sc);
         kprof_.credit(KC_EKF, ekf_flops(Ni + 3, n, nup), ekf_bytes(Ni + 3, n, nup));
       }
@@ -400,8 +472,11 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
                          d_.P, d_.ldp, Ni + 3, Ni, sc.dx + Ni + 8);
     }
     ++p_epoch_;
-    items.push_back(std::move(ci));
   }
+  auto tl3 = clk::now();
+  t_launch[0] = secs(tl0, tb1);
+  t_launch[1] = secs(tl1, tl2);
+  t_launch[2] = secs(tl2, tl3);
   // ---- 5) one readback: every update's region and every batch's per-feature results
   const auto tw = clk::now();
   {
@@ -510,9 +585,10 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     }
   }
   auto tm4 = clk::now();
-  chain_times_[0] = secs(tm0, tm1);
-  chain_times_[1] = secs(tm1, tm2);
-  chain_times_[2] = secs(tm2, tm4);
+  // each updater's host time: its tables + its launches; the one wait and the replay go with the last
+  chain_times_[0] = t_build[0] + t_launch[0];
+  chain_times_[1] = t_build[1] + t_launch[1];
+  chain_times_[2] = t_build[2] + t_launch[2] + secs(tw, tm4);
   timing_.chain_wait = secs(tw, tm4);
   (void)tm3;
   return 0;

@@ -38,6 +38,7 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 constexpr int kPW = 64, kPH = 16, kPM = 4;           // level-l tile and LDS margin
 constexpr int kWW = kPW + 2 * kPM, kWH = kPH + 2 * kPM;  // LDS window of level l: 72 x 24
 constexpr int kQW = kPW / 2, kQH = kPH / 2;          // level-(l+1) tile: 32 x 8
+constexpr int kSW = 2 * kWW + 4, kSH = 2 * kWH + 4;  // level l-1 source of the window (pyrDown taps): 148 x 52
 
 __device__ __forceinline__ void scharr_at(const uint8_t *t, int ld, int x, int y, int16_t &dx, int16_t &dy) {
   // (x, y): the pixel's cell; the 3x3 neighbourhood is in t
@@ -46,23 +47,6 @@ __device__ __forceinline__ void scharr_at(const uint8_t *t, int ld, int x, int y
   const int t1m = rp[x - 1] - rm[x - 1], t1p = rp[x + 1] - rm[x + 1], t1 = rp[x] - rm[x];
   dx = (int16_t)(t0p - t0m);
   dy = (int16_t)((t1p + t1m) * 3 + t1 * 10);
-}
-
-__device__ __forceinline__ int pyrdown_at(const uint8_t *src, int sw, int sh, int ld, int x, int y) {
-  const int k5[5] = {1, 4, 6, 4, 1};
-  int xs[5];
-#pragma unroll
-  for (int j = 0; j < 5; j++) xs[j] = reflect101(2 * x + j - 2, sw);
-  int acc = 0;
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    const uint8_t *row = src + (size_t)reflect101(2 * y + i - 2, sh) * ld;
-    int r = 0;
-#pragma unroll
-    for (int j = 0; j < 5; j++) r += k5[j] * row[xs[j]];
-    acc += k5[i] * r;
-  }
-  return (acc + 128) >> 8;
 }
 
 // level `l`'s owned pixels (4 per thread) and derivatives from the LDS window
@@ -105,6 +89,7 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   __shared__ int first;
   __shared__ uint8_t win[kWH * kWW];
   __shared__ uint8_t q[(kQH + 2) * (kQW + 2)];
+  __shared__ uint8_t srcs[EQ ? 1 : kSH * kSW];
   const int c = blockIdx.z, t = threadIdx.x;
   const DPyr &p = job.p[c];
   if (l >= p.levels) return;
@@ -146,13 +131,39 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   // level l over the window (reflect-101 coordinates)
   const uint8_t *src = EQ ? job.src[c] : p.img[l - 1];
   const int sld = EQ ? job.stride[c] : p.w[l - 1];
-  for (int e = t; e < kWH * kWW; e += 256) {
-    const int wy = e / kWW, wx = e - wy * kWW;
-    const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
-    if constexpr (EQ)
+  if constexpr (EQ) {
+    for (int e = t; e < kWH * kWW; e += 256) {
+      const int wy = e / kWW, wx = e - wy * kWW;
+      const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
       win[e] = lut[src[(size_t)gy * sld + gx]];
-    else
-      win[e] = (uint8_t)pyrdown_at(src, p.w[l - 1], p.h[l - 1], sld, gx, gy);
+    }
+  } else {
+    // level l-1 over every pyrDown tap of the window, at virtual coordinates (each cell the value at its
+    // reflect-101 coordinate in level l-1).  Every window cell that is read later (rows / columns up to one
+    // past the level's edge: reflected by at most 3) has its taps inside this block; the deeper-reflected
+    // margin cells nothing reads are clamped into it
+    const int sw = p.w[l - 1], sh = p.h[l - 1], sx0 = 2 * (x0 - kPM) - 2, sy0 = 2 * (y0 - kPM) - 2;
+    for (int e = t; e < kSH * kSW; e += 256) {
+      const int sy = e / kSW, sx = e - sy * kSW;
+      srcs[e] = src[(size_t)reflect101(sy0 + sy, sh) * sld + reflect101(sx0 + sx, sw)];
+    }
+    __syncthreads();
+    const int k5[5] = {1, 4, 6, 4, 1};
+    for (int e = t; e < kWH * kWW; e += 256) {
+      const int wy = e / kWW, wx = e - wy * kWW;
+      const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
+      const int ry = min(max(2 * gy - 2 - sy0, 0), kSH - 5), rx = min(max(2 * gx - 2 - sx0, 0), kSW - 5);
+      int acc = 0;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        const uint8_t *row = srcs + (ry + i) * kSW + rx;
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 5; j++) r += k5[j] * row[j];
+        acc += k5[i] * r;
+      }
+      win[e] = (uint8_t)((acc + 128) >> 8);
+    }
   }
   __syncthreads();
   write_level(win, x0, y0, w, h, (uint8_t *)p.img[l], (int16_t *)p.der[l]);

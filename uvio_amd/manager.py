@@ -364,9 +364,13 @@ class VioManager:
         return out[:ln.value].copy()
 
     def get_timing(self):
+        return self.get_timing_raw().as_dict()
+
+    def get_timing_raw(self):
+        """the timing struct itself (uvio_hp_timing_t); .as_dict() gives get_timing()'s dict"""
         t = N.Timing()
         self._check(self._call("get_timing", self._h, C.byref(t)), "get_timing")
-        return t.as_dict()
+        return t
 
     def set_kernel_timing(self, period=1):
         """Live per-class device timing of the roofline kernels (HIP events, include/uvio_hp.h): the launches
