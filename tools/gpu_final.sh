@@ -8,9 +8,10 @@ cd $R && mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg2_bench.json 2> $O/cfg2.err
-for wl in cfg3 cfg4 cfg5 cfg4t cfg5t; do
+for wl in cfg2l cfg3 cfg4 cfg5 cfg4t cfg5t; do
   timeout -k 10 400 python -u bench.py --workload $wl > $O/${TAG}_${wl}_bench.json 2> $O/$wl.err
 done
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg2_bench_driver_form.json 2> $O/cfg2_driver.err
 export TMPDIR=/tmp
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof2 -o run -- python3 $R/bench.py --cpu-frames 0 > $O/prof2.log 2>&1)
 python tools/prof_summary.py $O/prof2/run_kernel_trace.csv > $O/${TAG}_cfg2_per_frame.txt

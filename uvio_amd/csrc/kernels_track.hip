@@ -11,6 +11,7 @@
 //   k_ransac_hyp / _select   7-point RANSAC: all hypotheses in parallel, then the sequential
 //                            adaptive-iteration scan of RANSACPointSetRegistrator::run on one lane
 #include <stdexcept>
+#include <utility>
 
 #include "kernels.h"
 
@@ -35,11 +36,14 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 // written with its derivatives.  Level l+1 is never read back for level l+2's margin inside the launch, and
 // level l is not re-read from memory for level l+1: 4 launches per frame (with the histogram) instead of 6,
 // same bits as one pyrDown + Scharr per level.
-constexpr int kPW = 64, kPH = 16, kPM = 4;           // level-l tile and LDS margin
-constexpr int kWW = kPW + 2 * kPM, kWH = kPH + 2 * kPM;  // LDS window of level l: 72 x 24
-constexpr int kQW = kPW / 2, kQH = kPH / 2;          // level-(l+1) tile: 32 x 8
-constexpr int kSW = 2 * kWW + 4, kSH = 2 * kWH + 4;  // level l-1 source of the window (pyrDown taps): 148 x 52
-
+constexpr int kPM = 4;  // LDS margin of the level-l window
+// tile geometry of one pair launch: the level-l tile PW x PH (PW * PH / 256 pixels per thread), its window with
+// the margin, the level-(l+1) tile under it and the level l-1 source of the window's pyrDown taps
+template <int PW, int PH>
+struct PairTile {
+  static constexpr int WW = PW + 2 * kPM, WH = PH + 2 * kPM, QW = PW / 2, QH = PH / 2;
+  static constexpr int SW = 2 * WW + 4, SH = 2 * WH + 4, PPT = PW * PH / 256;
+};
 __device__ __forceinline__ void scharr_at(const uint8_t *t, int ld, int x, int y, int16_t &dx, int16_t &dy) {
   // (x, y): the pixel's cell; the 3x3 neighbourhood is in t
   const uint8_t *rm = t + (y - 1) * ld, *r0 = t + y * ld, *rp = t + (y + 1) * ld;
@@ -49,53 +53,57 @@ __device__ __forceinline__ void scharr_at(const uint8_t *t, int ld, int x, int y
   dy = (int16_t)((t1p + t1m) * 3 + t1 * 10);
 }
 
-// level `l`'s owned pixels (4 per thread) and derivatives from the LDS window
+// level `l`'s owned pixels (PPT consecutive per thread) and derivatives from the LDS window
+template <int PW, int PH>
 __device__ __forceinline__ void write_level(const uint8_t *win, int x0, int y0, int w, int h, uint8_t *img,
                                             int16_t *der) {
-  const int t = threadIdx.x, ty = t >> 4, tx = (t & 15) * 4;
+  using T = PairTile<PW, PH>;
+  constexpr int PPT = T::PPT, TPR = PW / PPT;  // pixels per thread, threads per tile row
+  const int t = threadIdx.x, ty = t / TPR, tx = (t % TPR) * PPT;
   const int gy = y0 + ty, gx = x0 + tx;
-  if (gy >= h || gx >= w) return;
+  if (ty >= PH || gy >= h || gx >= w) return;
   const int cy = ty + kPM, cx = tx + kPM;
-  uint8_t v[4];
-  int16_t d[8];
+  uint8_t v[PPT];
+  int16_t d[2 * PPT];
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    v[k] = win[cy * kWW + cx + k];
-    scharr_at(win, kWW, cx + k, cy, d[2 * k], d[2 * k + 1]);
+  for (int k = 0; k < PPT; k++) {
+    v[k] = win[cy * T::WW + cx + k];
+    scharr_at(win, T::WW, cx + k, cy, d[2 * k], d[2 * k + 1]);
   }
   const size_t o = (size_t)gy * w + gx;
-  if (gx + 3 < w && (w & 3) == 0) {
-    *(uchar4 *)(img + o) = make_uchar4(v[0], v[1], v[2], v[3]);
-    short4 lo = make_short4(d[0], d[1], d[2], d[3]), hi = make_short4(d[4], d[5], d[6], d[7]);
-    int4 pk;
-    pk.x = (int)(((unsigned)(uint16_t)lo.y << 16) | (uint16_t)lo.x);
-    pk.y = (int)(((unsigned)(uint16_t)lo.w << 16) | (uint16_t)lo.z);
-    pk.z = (int)(((unsigned)(uint16_t)hi.y << 16) | (uint16_t)hi.x);
-    pk.w = (int)(((unsigned)(uint16_t)hi.w << 16) | (uint16_t)hi.z);
-    *(int4 *)(der + 2 * o) = pk;
-  } else {
-    for (int k = 0; k < 4 && gx + k < w; k++) {
-      img[o + k] = v[k];
-      der[2 * (o + k)] = d[2 * k];
-      der[2 * (o + k) + 1] = d[2 * k + 1];
+  if constexpr (PPT == 4) {
+    if (gx + 3 < w && (w & 3) == 0) {
+      *(uchar4 *)(img + o) = make_uchar4(v[0], v[1], v[2], v[3]);
+      int4 pk;
+      pk.x = (int)(((unsigned)(uint16_t)d[1] << 16) | (uint16_t)d[0]);
+      pk.y = (int)(((unsigned)(uint16_t)d[3] << 16) | (uint16_t)d[2]);
+      pk.z = (int)(((unsigned)(uint16_t)d[5] << 16) | (uint16_t)d[4]);
+      pk.w = (int)(((unsigned)(uint16_t)d[7] << 16) | (uint16_t)d[6]);
+      *(int4 *)(der + 2 * o) = pk;
+      return;
     }
+  }
+  for (int k = 0; k < PPT && gx + k < w; k++) {
+    img[o + k] = v[k];
+    *(int *)(der + 2 * (o + k)) = (int)(((unsigned)(uint16_t)d[2 * k + 1] << 16) | (uint16_t)d[2 * k]);
   }
 }
 
-template <bool EQ>
+template <bool EQ, int PW, int PH>
 __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
+  using T = PairTile<PW, PH>;
   __shared__ uint8_t lut[256];
   __shared__ int scan[256];
   __shared__ int first;
-  __shared__ uint8_t win[kWH * kWW];
-  __shared__ uint8_t q[(kQH + 2) * (kQW + 2)];
-  __shared__ uint8_t srcs[EQ ? 1 : kSH * kSW];
+  __shared__ uint8_t win[T::WH * T::WW];
+  __shared__ uint8_t q[(T::QH + 2) * (T::QW + 2)];
+  __shared__ uint8_t srcs[EQ ? 1 : T::SH * T::SW];
   const int c = blockIdx.z, t = threadIdx.x;
   const DPyr &p = job.p[c];
   if (l >= p.levels) return;
   const int w = p.w[l], h = p.h[l];
-  const int ntx = (w + kPW - 1) / kPW;
-  const int x0 = (blockIdx.x % ntx) * kPW, y0 = (blockIdx.x / ntx) * kPH;
+  const int ntx = (w + PW - 1) / PW;
+  const int x0 = (blockIdx.x % ntx) * PW, y0 = (blockIdx.x / ntx) * PH;
   if (y0 >= h) return;
   if constexpr (EQ) {
     // LUT of EqualizeHistLut_Invoker from an inclusive LDS scan of the counts (blockDim == 256)
@@ -132,8 +140,8 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   const uint8_t *src = EQ ? job.src[c] : p.img[l - 1];
   const int sld = EQ ? job.stride[c] : p.w[l - 1];
   if constexpr (EQ) {
-    for (int e = t; e < kWH * kWW; e += 256) {
-      const int wy = e / kWW, wx = e - wy * kWW;
+    for (int e = t; e < T::WH * T::WW; e += 256) {
+      const int wy = e / T::WW, wx = e - wy * T::WW;
       const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
       win[e] = lut[src[(size_t)gy * sld + gx]];
     }
@@ -143,20 +151,20 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
     // past the level's edge: reflected by at most 3) has its taps inside this block; the deeper-reflected
     // margin cells nothing reads are clamped into it
     const int sw = p.w[l - 1], sh = p.h[l - 1], sx0 = 2 * (x0 - kPM) - 2, sy0 = 2 * (y0 - kPM) - 2;
-    for (int e = t; e < kSH * kSW; e += 256) {
-      const int sy = e / kSW, sx = e - sy * kSW;
+    for (int e = t; e < T::SH * T::SW; e += 256) {
+      const int sy = e / T::SW, sx = e - sy * T::SW;
       srcs[e] = src[(size_t)reflect101(sy0 + sy, sh) * sld + reflect101(sx0 + sx, sw)];
     }
     __syncthreads();
     const int k5[5] = {1, 4, 6, 4, 1};
-    for (int e = t; e < kWH * kWW; e += 256) {
-      const int wy = e / kWW, wx = e - wy * kWW;
+    for (int e = t; e < T::WH * T::WW; e += 256) {
+      const int wy = e / T::WW, wx = e - wy * T::WW;
       const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
-      const int ry = min(max(2 * gy - 2 - sy0, 0), kSH - 5), rx = min(max(2 * gx - 2 - sx0, 0), kSW - 5);
+      const int ry = min(max(2 * gy - 2 - sy0, 0), T::SH - 5), rx = min(max(2 * gx - 2 - sx0, 0), T::SW - 5);
       int acc = 0;
 #pragma unroll
       for (int i = 0; i < 5; i++) {
-        const uint8_t *row = srcs + (ry + i) * kSW + rx;
+        const uint8_t *row = srcs + (ry + i) * T::SW + rx;
         int r = 0;
 #pragma unroll
         for (int j = 0; j < 5; j++) r += k5[j] * row[j];
@@ -166,20 +174,20 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
     }
   }
   __syncthreads();
-  write_level(win, x0, y0, w, h, (uint8_t *)p.img[l], (int16_t *)p.der[l]);
+  write_level<PW, PH>(win, x0, y0, w, h, (uint8_t *)p.img[l], (int16_t *)p.der[l]);
   if (l + 1 >= p.levels) return;
   // level l+1: the 32 x 8 tile + 1 halo, each cell pyrDown of the window at its reflect-101 coordinate
   const int dw = p.w[l + 1], dh = p.h[l + 1], qx0 = x0 / 2, qy0 = y0 / 2;
   if (qy0 >= dh || qx0 >= dw) return;
   const int k5[5] = {1, 4, 6, 4, 1};
-  for (int e = t; e < (kQH + 2) * (kQW + 2); e += 256) {
-    const int ty = e / (kQW + 2), tx = e - ty * (kQW + 2);
+  for (int e = t; e < (T::QH + 2) * (T::QW + 2); e += 256) {
+    const int ty = e / (T::QW + 2), tx = e - ty * (T::QW + 2);
     const int x = reflect101(qx0 + tx - 1, dw), y = reflect101(qy0 + ty - 1, dh);
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
       // level-l row 2y + i - 2 (the window cell holds its reflect-101 value)
-      const uint8_t *row = win + (2 * y + i - 2 - (y0 - kPM)) * kWW - (x0 - kPM);
+      const uint8_t *row = win + (2 * y + i - 2 - (y0 - kPM)) * T::WW - (x0 - kPM);
       int r = 0;
 #pragma unroll
       for (int j = 0; j < 5; j++) r += k5[j] * row[2 * x + j - 2];
@@ -188,12 +196,12 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
     q[e] = (uint8_t)((acc + 128) >> 8);
   }
   __syncthreads();
-  const int tx = t & (kQW - 1), ty = t / kQW, gx = qx0 + tx, gy = qy0 + ty;
-  if (gx < dw && gy < dh) {
+  const int tx = t % T::QW, ty = t / T::QW, gx = qx0 + tx, gy = qy0 + ty;
+  if (ty < T::QH && gx < dw && gy < dh) {
     const size_t o = (size_t)gy * dw + gx;
-    ((uint8_t *)p.img[l + 1])[o] = q[(ty + 1) * (kQW + 2) + tx + 1];
+    ((uint8_t *)p.img[l + 1])[o] = q[(ty + 1) * (T::QW + 2) + tx + 1];
     int16_t dx, dy;
-    scharr_at(q, kQW + 2, tx + 1, ty + 1, dx, dy);
+    scharr_at(q, T::QW + 2, tx + 1, ty + 1, dx, dy);
     *(int *)((int16_t *)p.der[l + 1] + 2 * o) = (int)(((unsigned)(uint16_t)dy << 16) | (uint16_t)dx);
   }
 }
@@ -225,7 +233,11 @@ void launch_pyramids(hipStream_t s, const PyrJob &job) {
         wl = max(wl, job.p[c].w[l]);
         hl = max(hl, job.p[c].h[l]);
       }
-    return ((wl + kPW - 1) / kPW) * ((hl + kPH - 1) / kPH);
+    return std::make_pair(wl, hl);
+  };
+  auto grid = [&](int l, int pw, int ph) {
+    auto [wl, hl] = tiles(l);
+    return ((wl + pw - 1) / pw) * ((hl + ph - 1) / ph);
   };
   if (job.equalize) {
     int w0 = 0, h0 = 0;
@@ -234,9 +246,11 @@ void launch_pyramids(hipStream_t s, const PyrJob &job) {
       if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
     hipLaunchKernelGGL(k_hist_multi, dim3(min(256, (w0 * h0 + 4095) / 4096), 1, job.ncam), dim3(256), 0, s, job);
   }
-  hipLaunchKernelGGL(k_pyr_pair<true>, dim3(tiles(0), 1, job.ncam), dim3(256), 0, s, job, 0);
+  // level 0 (the big image): 64 x 16 tiles, four pixels per thread; levels >= 2 (<= 188 x 120 at 752 x 480):
+  // 32 x 8 tiles, so each workgroup's serial staging and reduction stay short
+  hipLaunchKernelGGL((k_pyr_pair<true, 64, 16>), dim3(grid(0, 64, 16), 1, job.ncam), dim3(256), 0, s, job, 0);
   for (int l = 2; l < maxl; l += 2)
-    hipLaunchKernelGGL(k_pyr_pair<false>, dim3(tiles(l), 1, job.ncam), dim3(256), 0, s, job, l);
+    hipLaunchKernelGGL((k_pyr_pair<false, 32, 8>), dim3(grid(l, 32, 8), 1, job.ncam), dim3(256), 0, s, job, l);
 }
 
 double pyramid_bytes(const PyrJob &job) {
