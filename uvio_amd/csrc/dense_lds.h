@@ -418,42 +418,48 @@ __device__ __forceinline__ dbl4 tile_rank16(const double *A, LA la, const double
   return acc;
 }
 
-// One column step K of the wave-resident panel: the pivot column of the block's own rows through a
-// 16-entry LDS broadcast, the reciprocal by frcp1; compile-time loop bounds keep the panel in registers.
+// One column step K of the wave-resident panel; compile-time loop bounds keep the panel in registers.  The
+// pivot column of the block's own rows (lane p holds row oJ + p) reaches every lane by v_readlane (uniform
+// values, no LDS round trip): step K receives d and w (column K at rows oJ + p, p > K), computes l for this
+// lane, updates the NEXT pivot column first and reads it out of lanes K+1 .. 15 for step K+1 before the bulk
+// of its row update.  The reciprocal's Newton step is folded into l (l = l0 + l0 (1 - d x), l0 = v x,
+// x = v_rcp_f64(d)).  Lanes <= K take l = 0 (their row is left as it is), without a branch.
 // (Two-column steps with a 2x2 pivot block measured slower: the redundant elimination of the second
 // column costs more FP64 issue than the saved broadcast.)
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 template <int SMAX, int K>
-__device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], double *bc, double *Dd, int oJ, int n, int nrows,
-                                            int lane) {
+__device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n, int lane, double d,
+                                            const double (&w)[16]) {
   if constexpr (K < 16) {
     if (oJ + K >= n) return;
-    if (lane < 16) bc[lane] = v[0][K];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const double d = bc[K];
-    if (lane == 0) Dd[oJ + K] = d;
-    const double dinv = frcp1(d);
-    double w[16];
+    const double x = __builtin_amdgcn_rcp(d);
+    const double e = fma(-d, x, 1.0);
+    const double l0 = v[0][K] * x;
+    const double l = (lane > K) ? fma(l0, e, l0) : 0.0;
+    v[0][K] = (lane > K) ? l : v[0][K];
+    double dn = 0.0, wn[16];
+    if constexpr (K + 1 < 16) {
+      v[0][K + 1] = fma(-l, w[K + 1], v[0][K + 1]);
+      dn = readlane_f64(v[0][K + 1], K + 1);
 #pragma unroll
-    for (int p = K + 1; p < 16; p++) w[p] = bc[p];
-    if (lane > K) {
-      const double l = v[0][K] * dinv;
-      v[0][K] = l;
-#pragma unroll
-      for (int p = K + 1; p < 16; p++) v[0][p] = fma(-l, w[p], v[0][p]);
+      for (int p = K + 2; p < 16; p++) wn[p] = readlane_f64(v[0][K + 1], p);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int s = 1; s < SMAX; s++) {
-      if (oJ + 64 * s < nrows) {
-        const double l = v[s][K] * dinv;
-        v[s][K] = l;
+    for (int p = K + 2; p < 16; p++) v[0][p] = fma(-l, w[p], v[0][p]);
 #pragma unroll
-        for (int p = K + 1; p < 16; p++) v[s][p] = fma(-l, w[p], v[s][p]);
-      }
+    for (int s = 1; s < SMAX; s++) {  // rows 64 s + lane: all below the panel's diagonal block
+      const double ls0 = v[s][K] * x;
+      const double ls = fma(ls0, e, ls0);
+      v[s][K] = ls;
+#pragma unroll
+      for (int p = K + 1; p < 16; p++) v[s][p] = fma(-ls, w[p], v[s][p]);
     }
-    __builtin_amdgcn_wave_barrier();  // every lane has read bc before the next step overwrites it
-    panel_steps<SMAX, K + 1>(v, bc, Dd, oJ, n, nrows, lane);
+    if constexpr (K + 1 < 16) panel_steps<SMAX, K + 1>(v, oJ, n, lane, dn, wn);
   }
 }
 
@@ -511,8 +517,14 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
 #pragma unroll
           for (int p = 0; p < 16; p++) v[s][p] = (i < nrows && oJ + p < n && p <= ro) ? A[la(i, oJ + p)] : 0.0;
         }
-        __shared__ double bc[16];
-        panel_steps<SMAX, 0>(v, bc, Dd, oJ, n, nrows, lane);
+        double w0[16];
+#pragma unroll
+        for (int p = 1; p < 16; p++) w0[p] = readlane_f64(v[0][0], p);
+        panel_steps<SMAX, 0>(v, oJ, n, lane, readlane_f64(v[0][0], 0), w0);
+        // the pivots: lane p < 16 still holds d_p on its diagonal (step p leaves its own row as it is)
+#pragma unroll
+        for (int p = 0; p < 16; p++)
+          if (lane == p && oJ + p < n) Dd[oJ + p] = v[0][p];
 #pragma unroll
         for (int s = 0; s < SMAX; s++) {
           const int ro = lane + 64 * s, i = oJ + ro;

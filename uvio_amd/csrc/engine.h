@@ -229,7 +229,12 @@ struct DeviceBufs {
   // feature group runs; its column map in a dedicated device buffer (pinned mirror), the run it belongs to
   hipStream_t aux = nullptr;
   hipEvent_t ev_aux_in = nullptr, ev_aux_out = nullptr;
+  // the prefactor's column maps: kPreSlots pinned / device slots used in turn, each freed by its copy's event
+  // (a slot is reused kPreSlots prefactors later, so the host never waits on the one just enqueued)
+  static constexpr int kPreSlots = 8;
   int *hidx_pre = nullptr, *hidx_pre_h = nullptr;
+  hipEvent_t ev_pre[kPreSlots] = {};
+  int pre_slot = 0;
   std::vector<int> pre_hidx;  // columns of the pending prefactor (empty: none)
   int pre_N = -1;
   long long pre_epoch = -1;  // Engine::p_epoch_ when the prefactor was enqueued

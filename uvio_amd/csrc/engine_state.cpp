@@ -232,6 +232,8 @@ Engine::~Engine() {
   if (d_.stg_h) hipHostFree(d_.stg_h);
   if (d_.hidx_pre_h) hipHostFree(d_.hidx_pre_h);
   if (d_.chain_host) hipHostFree(d_.chain_host);
+  for (auto &e : d_.ev_pre)
+    if (e) hipEventDestroy(e);
   if (d_.ev_aux_in) hipEventDestroy(d_.ev_aux_in);
   if (d_.ev_aux_out) hipEventDestroy(d_.ev_aux_out);
   if (d_.aux) hipStreamDestroy(d_.aux);
@@ -298,8 +300,10 @@ void Engine::alloc_device() {
   dalloc(&d_.partials, (size_t)maxch * d_.max_ncol * d_.max_ncol);
   dalloc(&d_.R, (size_t)2 * d_.max_ncol * d_.ldh);
   dalloc(&d_.hidx, d_.max_ncol + d_.max_rows);
-  dalloc(&d_.hidx_pre, d_.max_ncol);
-  HP_HIP(hipHostMalloc((void **)&d_.hidx_pre_h, sizeof(int) * std::max(d_.max_ncol, 1), hipHostMallocDefault));
+  dalloc(&d_.hidx_pre, (size_t)DeviceBufs::kPreSlots * d_.max_ncol);
+  HP_HIP(hipHostMalloc((void **)&d_.hidx_pre_h, sizeof(int) * DeviceBufs::kPreSlots * std::max(d_.max_ncol, 1),
+                       hipHostMallocDefault));
+  for (auto &e : d_.ev_pre) HP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   int rmax = std::max(d_.max_ncol, kMaxEkfRows);
   dalloc(&d_.ekf.M, (size_t)cap * rmax);
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
@@ -409,7 +413,7 @@ void Engine::dev_sync() {
     d_.fout_pending = 0;
   }
   auto t0 = std::chrono::steady_clock::now();
-  HP_HIP(hipStreamSynchronize(d_.stream));
+  spin_sync(d_.stream);
   timing_.sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   timing_.device_syncs++;
   if (kprof_.on) kprof_.harvest(true);
@@ -604,12 +608,16 @@ void Engine::ekf_update_info(int nch, int n, const std::vector<int> &hidx, doubl
 void Engine::info_prefactor(const std::vector<int> &hidx) {
   const int n = (int)hidx.size();
   if (n < 1 || n > d_.max_ncol) return;
-  HP_HIP(hipEventSynchronize(d_.ev_aux_out));  // the pinned column map is free (normally long since)
-  std::memcpy(d_.hidx_pre_h, hidx.data(), sizeof(int) * n);
+  const int slot = d_.pre_slot;
+  d_.pre_slot = (d_.pre_slot + 1) % DeviceBufs::kPreSlots;
+  int *hh = d_.hidx_pre_h + (size_t)slot * d_.max_ncol, *hd = d_.hidx_pre + (size_t)slot * d_.max_ncol;
+  HP_HIP(hipEventSynchronize(d_.ev_pre[slot]));  // this slot's copy, kPreSlots prefactors ago, has run
+  std::memcpy(hh, hidx.data(), sizeof(int) * n);
   HP_HIP(hipEventRecord(d_.ev_aux_in, d_.stream));
   HP_HIP(hipStreamWaitEvent(d_.aux, d_.ev_aux_in, 0));
-  HP_HIP(hipMemcpyAsync(d_.hidx_pre, d_.hidx_pre_h, sizeof(int) * n, hipMemcpyHostToDevice, d_.aux));
-  launch_ekf_info_pre(d_.aux, d_.P, d_.ldp, N_, n, d_.hidx_pre, d_.ekf);
+  HP_HIP(hipMemcpyAsync(hd, hh, sizeof(int) * n, hipMemcpyHostToDevice, d_.aux));
+  HP_HIP(hipEventRecord(d_.ev_pre[slot], d_.aux));
+  launch_ekf_info_pre(d_.aux, d_.P, d_.ldp, N_, n, hd, d_.ekf);
   HP_HIP(hipEventRecord(d_.ev_aux_out, d_.aux));
   d_.pre_hidx = hidx;
   d_.pre_N = N_;

@@ -169,7 +169,7 @@ Tracker::~Tracker() {
 
 void Tracker::sync() {
   auto t0 = std::chrono::steady_clock::now();
-  HP_HIP(hipStreamSynchronize(s_));
+  spin_sync(s_);
   sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   device_syncs++;
 }
@@ -812,7 +812,10 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     in_flight_ = nullptr;
     f();
     auto t0 = std::chrono::steady_clock::now();
-    HP_HIP(hipEventSynchronize(ev_match_));
+    for (hipError_t e; (e = hipEventQuery(ev_match_)) != hipSuccess;) {  // spin (see spin_sync)
+      if (e != hipErrorNotReady) throw HpError(UVIO_HP_E_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+      __builtin_ia32_pause();
+    }
     sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     device_syncs++;
     return;

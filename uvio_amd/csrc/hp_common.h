@@ -26,4 +26,18 @@ struct HpError : std::runtime_error {
       throw ::uvhp::HpError(UVIO_HP_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
+// Wait for a stream by polling it from this thread instead of hipStreamSynchronize: the calling thread stays
+// on its core (a blocking wait lets the core idle and clock down, and the host work right after the wait -- the
+// feature-database walks, the next batch -- then runs measurably slower).  Every host wait of the library is
+// latency-critical and short (< a few ms).
+inline void spin_sync(hipStream_t s) {
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady)
+      throw HpError(UVIO_HP_E_DEVICE, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    __builtin_ia32_pause();
+  }
+}
+
 }  // namespace uvhp

@@ -579,12 +579,15 @@ __device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int
 }
 
 // P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1), zero upper) and L_P (n x n).
-template <int SMAX, int PACKED>
+// MODE: the storage (compile-time, so LDS accesses are DS instructions rather than FLAT)
+template <int SMAX, int MODE>
 __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
                                                     int n, double *__restrict__ Laug, double *__restrict__ Lout,
                                                     double *gbuf, int mode) {
+  constexpr int PACKED = MODE == 1;
   extern __shared__ double lds[];
-  double *A = (mode == 2) ? gbuf : lds;
+  double *A = (MODE == 2) ? gbuf : lds;
+  (void)mode;
   const int ld = n | 1;
   const size_t asz = PACKED ? packed_lds_doubles(n) : (size_t)n * ld;
   double *Dd = A + asz;
@@ -617,12 +620,14 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
 
 // [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T -> w = U^-1 c.
 // Writes U (n x n, ld n) and w (n).
-template <int SMAX, int PACKED>
+template <int SMAX, int MODE>
 __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
                                                     double *__restrict__ Uout, double *__restrict__ w, double *gbuf,
                                                     int mode) {
+  constexpr int PACKED = MODE == 1;
   extern __shared__ double lds[];
-  double *A = (mode == 2) ? gbuf : lds;
+  double *A = (MODE == 2) ? gbuf : lds;
+  (void)mode;
   const int ld = n | 1;
   const int na = n + 1;
   const size_t asz = PACKED ? packed_lds_doubles(na) : (size_t)na * ld;
@@ -651,20 +656,20 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
 }
 // the instantiation for a factor of `rows` rows (panel rows per lane) and storage mode
 template <class KP>
-static KP pick_info_kernel(const KP (&tab)[4][2], int rows, int mode) {
+static KP pick_info_kernel(const KP (&tab)[4][3], int rows, int mode) {
   const int si = rows <= 64 ? 0 : rows <= 128 ? 1 : rows <= 192 ? 2 : 3;
-  return tab[si][mode == 1 ? 1 : 0];
+  return tab[si][mode];
 }
 typedef void (*CholPFn)(const double *, int, const int *, int, double *, double *, double *, int);
 typedef void (*CholZFn)(const double *, int, double, double *, double *, double *, int);
-static const CholPFn kCholP[4][2] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>},
-                                     {k_info_cholP<2, 0>, k_info_cholP<2, 1>},
-                                     {k_info_cholP<3, 0>, k_info_cholP<3, 1>},
-                                     {k_info_cholP<4, 0>, k_info_cholP<4, 1>}};
-static const CholZFn kCholZ[4][2] = {{k_info_cholZ<1, 0>, k_info_cholZ<1, 1>},
-                                     {k_info_cholZ<2, 0>, k_info_cholZ<2, 1>},
-                                     {k_info_cholZ<3, 0>, k_info_cholZ<3, 1>},
-                                     {k_info_cholZ<4, 0>, k_info_cholZ<4, 1>}};
+static const CholPFn kCholP[4][3] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>, k_info_cholP<1, 2>},
+                                     {k_info_cholP<2, 0>, k_info_cholP<2, 1>, k_info_cholP<2, 2>},
+                                     {k_info_cholP<3, 0>, k_info_cholP<3, 1>, k_info_cholP<3, 2>},
+                                     {k_info_cholP<4, 0>, k_info_cholP<4, 1>, k_info_cholP<4, 2>}};
+static const CholZFn kCholZ[4][3] = {{k_info_cholZ<1, 0>, k_info_cholZ<1, 1>, k_info_cholZ<1, 2>},
+                                     {k_info_cholZ<2, 0>, k_info_cholZ<2, 1>, k_info_cholZ<2, 2>},
+                                     {k_info_cholZ<3, 0>, k_info_cholZ<3, 1>, k_info_cholZ<3, 2>},
+                                     {k_info_cholZ<4, 0>, k_info_cholZ<4, 1>, k_info_cholZ<4, 2>}};
 
 // storage mode and dynamic LDS bytes of an info-form factor of nrows x n (+ the n doubles of D)
 static int info_chol_mode(int nrows, int n, size_t *bytes) {

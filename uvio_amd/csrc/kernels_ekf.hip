@@ -173,14 +173,17 @@ static size_t ekf_ms_lds_bytes(int n, bool with_S) {
 // L^-1 = D^-1/2 L_u^-1 (lower, zeros above, ld r) into Linv_out and y = L^-1 r = D^1/2 (D^-1 L_u^-1 r).
 // chi2_gate: StateHelper::initialize's test (StateHelper.cpp:458-470) on this factor: chi2 = |y|^2 in a
 // fixed order against thr -> *chi2_gate (the P-update gate) and [chi2, accepted] into gate_out[0..1].
-template <int SMAX>
+// LDS: the factor in LDS (a compile-time choice, so every access of the factorization is a DS instruction;
+// a runtime choice makes them all FLAT)
+template <int SMAX, bool LDS>
 __global__ void __launch_bounds__(512) k_ekf_fact(const double *__restrict__ Sup, int r,
                                                   const double *__restrict__ res, int res_stride,
                                                   double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
                                                   int use_lds, int *chi2_gate, double chi2_thr,
                                                   double *__restrict__ gate_out) {
   extern __shared__ double lds[];
-  double *A = use_lds ? lds : Sg;
+  double *A = LDS ? lds : Sg;
+  (void)use_lds;
   const int ld = r | 1;  // odd row stride: conflict-free 64-bit LDS reads down a column
   double *Dd = A + (size_t)(r + 1) * ld, *sd = Dd + r;
   staged_copy(
@@ -364,8 +367,9 @@ void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, co
 static void ensure_ekf_lds_attrs() {
   static bool done = false;
   if (done) return;
-  const void *fns[6] = {(const void *)k_ekf_MS,      (const void *)k_ekf_WP,      (const void *)k_ekf_fact<1>,
-                        (const void *)k_ekf_fact<2>, (const void *)k_ekf_fact<3>, (const void *)k_ekf_fact<4>};
+  const void *fns[6] = {(const void *)k_ekf_MS,            (const void *)k_ekf_WP,
+                        (const void *)k_ekf_fact<1, true>, (const void *)k_ekf_fact<2, true>,
+                        (const void *)k_ekf_fact<3, true>, (const void *)k_ekf_fact<4, true>};
   for (int k = 0; k < 6; k++)
     if (set_dyn_lds(fns[k], kMaxDynLds) < kMaxDynLds)
       throw std::runtime_error("dynamic LDS limit not granted for an EKF kernel (" + std::to_string(k) + ")");
@@ -411,7 +415,14 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   {
     KScope ks(sc.kp, KC_LDL);
     const int rows = r + 1;
-    auto *kf = rows <= 64 ? k_ekf_fact<1> : rows <= 128 ? k_ekf_fact<2> : rows <= 192 ? k_ekf_fact<3> : k_ekf_fact<4>;
+    auto *kf = use_lds ? (rows <= 64    ? k_ekf_fact<1, true>
+                          : rows <= 128 ? k_ekf_fact<2, true>
+                          : rows <= 192 ? k_ekf_fact<3, true>
+                                        : k_ekf_fact<4, true>)
+                       : (rows <= 64    ? k_ekf_fact<1, false>
+                          : rows <= 128 ? k_ekf_fact<2, false>
+                          : rows <= 192 ? k_ekf_fact<3, false>
+                                        : k_ekf_fact<4, false>);
     hipLaunchKernelGGL(kf, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg, use_lds,
                        sc.chi2_gate, sc.chi2_thr, sc.dx + N);
   }
