@@ -604,67 +604,59 @@ __global__ void __launch_bounds__(64) k_subpix(SubpixJob job, float *__restrict_
 }
 
 // ---------------------------------------------------------------- pyramidal LK
-__device__ __forceinline__ int img_px(const uint8_t *g, int w, int h, int x, int y) {
-  return g[(size_t)reflect101(y, h) * w + reflect101(x, w)];
+// The LK fixed-point products in 32 bits: the reference's CV_DESCALE sums are at most 255 * 2^14 (image) and
+// 4080 * 2^14 (Scharr derivative, |d| <= 16 * 255) in magnitude, so int32 holds them exactly.
+__device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
+// a . w over four bilinear taps on the full-rate 24-bit multipliers (v_mad_i32_i24 instead of the quarter-rate
+// v_mul_lo_u32): pixels (<= 255), derivatives (|d| <= 4080) and weights (-1 .. 2^14) are far inside the signed
+// 24-bit range, and every product and sum stays below 2^31.
+__device__ __forceinline__ int dot4_i24(int a0, int a1, int a2, int a3, int w0, int w1, int w2, int w3) {
+  return __mul24(a0, w0) + __mul24(a1, w1) + __mul24(a2, w2) + __mul24(a3, w3);
 }
-__device__ __forceinline__ int der_px(const int16_t *d, int w, int h, int x, int y, int c) {
-  if (x < 0 || y < 0 || x >= w || y >= h) return 0;
-  return d[((size_t)y * w + x) * 2 + c];
+// Exact wave sums of the LK window partials through DPP instead of six ds_bpermute rounds.  Per lane at most
+// 4 window pixels (win <= 16): |diff * dI| <= 8161 * 4080, so a lane's partial is below 2^27 and a 16-lane row
+// sum below 2^31 -- quad_perm xor 1, xor 2, row_half_mirror, row_mirror add in int32 (each lane then holds its
+// row's sum), and the four rows are added in int64 from v_readlane.  The whole wave must be active.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ int descale(long long x, int n) { return (int)((x + (1ll << (n - 1))) >> n); }
-// Exact wave sums of integer partials through DPP instead of six ds_bpermute rounds: every partial and every
-// total here is an integer below 2^53 in magnitude, so the FP64 adds are exact in any order (LK window sums:
-// |partial| < 2^32, |total| < 2^38).  Within a row of 16 lanes: quad_perm xor 1, xor 2, row_half_mirror,
-// row_mirror (each lane then holds its row's sum); across rows: row_bcast15 / row_bcast31 into row 3 and
-// v_readlane of lane 63.  The whole wave must be active.
-template <int CTRL, int ROWMASK = 0xf>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, ROWMASK, 0xf, false);
-  const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
+// Wave sums of int32 lane partials whose 16-lane row sums still fit in int32 (the LK bounds below): the row
+// stages are 32-bit integer adds, the four row sums are read into scalar registers and added as int64.
 template <int N>
-__device__ __forceinline__ void wave_sum_exact(long long (&v)[N]) {
-  double d[N];
+__device__ __forceinline__ void wave_sum_rows_i32(const int (&v)[N], long long (&out)[N]) {
+  int d[N];
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] = (double)v[k];
+  for (int k = 0; k < N; k++) d[k] = v[k];
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0xB1>(d[k]);   // quad_perm [1, 0, 3, 2]
+  for (int k = 0; k < N; k++) d[k] += dpp_i32<0xB1>(d[k]);
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x4E>(d[k]);   // quad_perm [2, 3, 0, 1]
+  for (int k = 0; k < N; k++) d[k] += dpp_i32<0x4E>(d[k]);
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x141>(d[k]);  // row_half_mirror
+  for (int k = 0; k < N; k++) d[k] += dpp_i32<0x141>(d[k]);
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x140>(d[k]);  // row_mirror
+  for (int k = 0; k < N; k++) d[k] += dpp_i32<0x140>(d[k]);
 #pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x142, 0xa>(d[k]);  // row_bcast15 -> rows 1, 3
-#pragma unroll
-  for (int k = 0; k < N; k++) d[k] += dpp_f64<0x143, 0xc>(d[k]);  // row_bcast31 -> rows 2, 3
-#pragma unroll
-  for (int k = 0; k < N; k++) {
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, d[k]);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, 63), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), 63);
-    v[k] = (long long)__builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-  }
+  for (int k = 0; k < N; k++)
+    out[k] = ((long long)__builtin_amdgcn_readlane(d[k], 0) + (long long)__builtin_amdgcn_readlane(d[k], 16)) +
+             ((long long)__builtin_amdgcn_readlane(d[k], 32) + (long long)__builtin_amdgcn_readlane(d[k], 48));
 }
-
 constexpr int kLkMargin = 4, kLkMaxWin = 16, kLkMaxTile = kLkMaxWin + 1 + 2 * kLkMargin;
+static_assert(kLkMaxWin * kLkMaxWin <= 4 * 64, "wave_sum_rows_i32 bound: at most 4 window pixels per lane");
 // one 64-lane workgroup per point; lanes own window pixels lane, lane+64, ... (225 for win 15).
 // (qx, qy) is nextPts[ptidx] of LKTrackerInvoker: it carries the result between levels, and an
 // early exit leaves it at its last written value, exactly as the oracle's p1[pi].
-__device__ __forceinline__ int bilin_img(const uint8_t *g, int w, int h, int X, int Y, int i00, int i01, int i10, int i11) {
-  return descale((long long)img_px(g, w, h, X, Y) * i00 + img_px(g, w, h, X + 1, Y) * i01 + img_px(g, w, h, X, Y + 1) * i10 +
-                     img_px(g, w, h, X + 1, Y + 1) * i11,
-                 14 - 5);
-}
-__device__ __forceinline__ int bilin_der(const int16_t *d, int w, int h, int X, int Y, int c, int i00, int i01, int i10,
-                                         int i11) {
-  return descale((long long)der_px(d, w, h, X, Y, c) * i00 + der_px(d, w, h, X + 1, Y, c) * i01 +
-                     der_px(d, w, h, X, Y + 1, c) * i10 + der_px(d, w, h, X + 1, Y + 1, c) * i11,
-                 14);
-}
-
+#ifdef UVHP_LK_PROF
+// tools/bench_lk.hip: per-point cycle breakdown (level setup, J staging, iterations) of lk_point
+struct LkProf {
+  unsigned long long setup, stage, iter, total;
+  int n_iter, n_stage, n_level, pad;
+};
+__device__ LkProf g_lk_prof[4096];
+#define LKP_T(v) const unsigned long long v = clock64()
+#else
+#define LKP_T(v)
+#endif
 __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
                                          float *__restrict__ p1, uint8_t *__restrict__ status, int pi, int win,
                                          int max_level, int max_iters, float crit_eps, int init_from_p0,
@@ -681,15 +673,93 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
   // an iteration moves the window more than kLkMargin pixels from where it was staged
   __shared__ uint8_t Jt[kLkMaxTile * kLkMaxTile];
   const int S = win + 1 + 2 * kLkMargin;
+  // Every gather below is unconditional, so the loads of all of a lane's pixels are in flight together (a
+  // per-pixel branch makes one load round per pixel): a lane past the window reads the last pixel's
+  // location and carries zero derivatives and template value.  Window pixel (wx, wy) of this lane's slot q
+  // and its offset in the staged J tile are the same on every level.
+  int wx[kPer], wy[kPer], jo[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; q++) {
+    const int e = min(lane + 64 * q, area - 1);
+    wy[q] = e / win;
+    wx[q] = e - wy[q] * win;
+    jo[q] = wy[q] * S + wx[q];
+  }
+  constexpr int kStageN = (kLkMaxTile * kLkMaxTile + 63) / 64;
+  int sx[kStageN], sy[kStageN];
+#pragma unroll
+  for (int k = 0; k < kStageN; k++) {
+    const int e = min(lane + 64 * k, S * S - 1);
+    sy[k] = e / S;
+    sx[k] = e - sy[k] * S;
+  }
   float qx = init_from_p0 ? p0[2 * pi] : p1[2 * pi], qy = init_from_p0 ? p0[2 * pi + 1] : p1[2 * pi + 1];
   uint8_t st = 1;
   int nlev = 0, nit = 0;  // levels with a prev window gathered, iterations (algorithmic bytes, LkSlots::bytes)
+#ifdef UVHP_LK_PROF
+  unsigned long long c_setup = 0, c_stage = 0, c_iter = 0;
+  int n_stage = 0;
+  LKP_T(c_begin);
+#endif
+  const float p0x = p0[2 * pi], p0y = p0[2 * pi + 1];
+  // The template window of level l and its derivatives: the four bilinear taps of each pixel, image at
+  // reflect-101 coordinates, derivatives zero outside the level (both channels in one 32-bit load).  The
+  // template depends only on p0, so level l - 1's taps are gathered as soon as level l's are consumed and
+  // their latency overlaps level l's iterations.  The window corner is clamped into the level's valid range
+  // for the gather only: a level whose window is outside is skipped below and its taps are not used.
+  int gi[kPer][4], gd[kPer][4], gm[kPer];  // gm: bit k set = derivative tap k inside the level
+  auto gather = [&](int l) {
+    const uint8_t *I = prev.img[l];
+    const int *d32 = reinterpret_cast<const int *>(prev.der[l]);
+    const int Iw_ = prev.w[l], Ih_ = prev.h[l];
+    const float sc = (float)(1. / (1 << l));
+    float prx = p0x * sc, pry = p0y * sc;
+    prx -= halfw;
+    pry -= halfw;
+    const int ipx = min(max((int)floorf(prx), -win), Iw_ - 1), ipy = min(max((int)floorf(pry), -win), Ih_ - 1);
+    if (ipx >= 0 && ipx + win < Iw_ && ipy >= 0 && ipy + win < Ih_) {  // window and taps inside: plain loads
+#pragma unroll
+      for (int q = 0; q < kPer; q++) {
+        const size_t o = (size_t)(ipy + wy[q]) * Iw_ + ipx + wx[q];
+        gi[q][0] = I[o];
+        gi[q][1] = I[o + 1];
+        gi[q][2] = I[o + Iw_];
+        gi[q][3] = I[o + Iw_ + 1];
+        gd[q][0] = d32[o];
+        gd[q][1] = d32[o + 1];
+        gd[q][2] = d32[o + Iw_];
+        gd[q][3] = d32[o + Iw_ + 1];
+        gm[q] = 0xf;
+      }
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int X = ipx + wx[q], Y = ipy + wy[q];
+      const int rx0 = reflect101(X, Iw_), rx1 = reflect101(X + 1, Iw_);
+      const size_t ry0 = (size_t)reflect101(Y, Ih_) * Iw_, ry1 = (size_t)reflect101(Y + 1, Ih_) * Iw_;
+      gi[q][0] = I[ry0 + rx0];
+      gi[q][1] = I[ry0 + rx1];
+      gi[q][2] = I[ry1 + rx0];
+      gi[q][3] = I[ry1 + rx1];
+      const int cx0 = min(max(X, 0), Iw_ - 1), cx1 = min(max(X + 1, 0), Iw_ - 1);
+      const size_t cy0 = (size_t)min(max(Y, 0), Ih_ - 1) * Iw_, cy1 = (size_t)min(max(Y + 1, 0), Ih_ - 1) * Iw_;
+      gd[q][0] = d32[cy0 + cx0];
+      gd[q][1] = d32[cy0 + cx1];
+      gd[q][2] = d32[cy1 + cx0];
+      gd[q][3] = d32[cy1 + cx1];
+      // the masks are applied where the taps are consumed: a select right after a load would wait for it here
+      const bool vx0 = X >= 0 && X < Iw_, vx1 = X + 1 >= 0 && X + 1 < Iw_;
+      const bool vy0 = Y >= 0 && Y < Ih_, vy1 = Y + 1 >= 0 && Y + 1 < Ih_;
+      gm[q] = (vx0 && vy0) | (vx1 && vy0) << 1 | (vx0 && vy1) << 2 | (vx1 && vy1) << 3;
+    }
+  };
+  if (maxL >= 0) gather(maxL);
   for (int level = maxL; level >= 0; level--) {
-    const uint8_t *I = prev.img[level], *J = next.img[level];
-    const int16_t *dI = prev.der[level];
+    const uint8_t *J = next.img[level];
     const int Iw_ = prev.w[level], Ih_ = prev.h[level], Jw_ = next.w[level], Jh_ = next.h[level];
     const float sc = (float)(1. / (1 << level));
-    float prx = p0[2 * pi] * sc, pry = p0[2 * pi + 1] * sc;
+    float prx = p0x * sc, pry = p0y * sc;
     if (level == maxL) {
       qx = qx * sc;
       qy = qy * sc;
@@ -699,9 +769,11 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     }
     prx -= halfw;
     pry -= halfw;
+    LKP_T(c_l0);
     const int ipx = (int)floorf(prx), ipy = (int)floorf(pry);
     if (ipx < -win || ipx >= Iw_ || ipy < -win || ipy >= Ih_) {
       if (level == 0) st = 0;
+      if (level > 0) gather(level - 1);
       continue;
     }
     float a = prx - ipx, b = pry - ipy;
@@ -709,32 +781,29 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     int iw01 = (int)rintf(a * (1.f - b) * WSCALE);
     int iw10 = (int)rintf((1.f - a) * b * WSCALE);
     int iw11 = (1 << 14) - iw00 - iw01 - iw10;
-    long long sA11 = 0, sA12 = 0, sA22 = 0;
+    int sA11 = 0, sA12 = 0, sA22 = 0;
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
-      const int e = lane + 64 * q;
-      Iw[q] = dIx[q] = dIy[q] = 0;
-      if (e < area) {
-        const int y = e / win, x = e - y * win, X = ipx + x, Y = ipy + y;
-        const int ival = bilin_img(I, Iw_, Ih_, X, Y, iw00, iw01, iw10, iw11);
-        const int ixv = bilin_der(dI, Iw_, Ih_, X, Y, 0, iw00, iw01, iw10, iw11);
-        const int iyv = bilin_der(dI, Iw_, Ih_, X, Y, 1, iw00, iw01, iw10, iw11);
-        Iw[q] = (int16_t)ival;
-        dIx[q] = (int16_t)ixv;
-        dIy[q] = (int16_t)iyv;
-        sA11 += (long long)ixv * ixv;
-        sA12 += (long long)ixv * iyv;
-        sA22 += (long long)iyv * iyv;
-      }
+      const int ival = descale(dot4_i24(gi[q][0], gi[q][1], gi[q][2], gi[q][3], iw00, iw01, iw10, iw11), 14 - 5);
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (!(gm[q] >> k & 1)) gd[q][k] = 0;
+      auto lo = [](int v) { return (int)(int16_t)(v & 0xffff); };
+      auto hi = [](int v) { return v >> 16; };
+      const int ixv = descale(dot4_i24(lo(gd[q][0]), lo(gd[q][1]), lo(gd[q][2]), lo(gd[q][3]), iw00, iw01, iw10, iw11), 14);
+      const int iyv = descale(dot4_i24(hi(gd[q][0]), hi(gd[q][1]), hi(gd[q][2]), hi(gd[q][3]), iw00, iw01, iw10, iw11), 14);
+      const bool in = lane + 64 * q < area;
+      Iw[q] = in ? (int16_t)ival : 0;
+      dIx[q] = in ? (int16_t)ixv : 0;
+      dIy[q] = in ? (int16_t)iyv : 0;
+      sA11 += dIx[q] * dIx[q];
+      sA12 += dIx[q] * dIy[q];
+      sA22 += dIy[q] * dIy[q];
     }
-    {
-      long long s3[3] = {sA11, sA12, sA22};
-      wave_sum_exact<3>(s3);
-      sA11 = s3[0];
-      sA12 = s3[1];
-      sA22 = s3[2];
-    }
-    const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+    if (level > 0) gather(level - 1);
+    long long s3[3];
+    wave_sum_rows_i32<3>({sA11, sA12, sA22}, s3);
+    const float A11 = (float)s3[0] * FLT_SCALE, A12 = (float)s3[1] * FLT_SCALE, A22 = (float)s3[2] * FLT_SCALE;
     float D = A11 * A22 - A12 * A12;
     const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
     if (minEig < 1e-4f || D < 1.19209290e-07f) {
@@ -743,10 +812,14 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     }
     D = 1.f / D;
     nlev++;
+#ifdef UVHP_LK_PROF
+    c_setup += clock64() - c_l0;
+#endif
     float nx = qx - halfw, ny = qy - halfw;
     float pdx = 0.f, pdy = 0.f;
     int ox = -(1 << 28), oy = -(1 << 28);
     for (int j = 0; j < max_iters; j++) {
+      LKP_T(c_i0);
       const int inx = (int)floorf(nx), iny = (int)floorf(ny);
       if (inx < -win || inx >= Jw_ || iny < -win || iny >= Jh_) {
         if (level == 0) st = 0;
@@ -756,11 +829,22 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
         __syncthreads();
         ox = inx - kLkMargin;
         oy = iny - kLkMargin;
-        for (int e = lane; e < S * S; e += 64) {
-          const int ty = e / S;
-          Jt[e] = (uint8_t)img_px(J, Jw_, Jh_, ox + e - ty * S, oy + ty);
+        uint8_t v[kStageN];
+        if (ox >= 0 && ox + S <= Jw_ && oy >= 0 && oy + S <= Jh_) {
+#pragma unroll
+          for (int k = 0; k < kStageN; k++) v[k] = J[(size_t)(oy + sy[k]) * Jw_ + ox + sx[k]];
+        } else {
+#pragma unroll
+          for (int k = 0; k < kStageN; k++) v[k] = J[(size_t)reflect101(oy + sy[k], Jh_) * Jw_ + reflect101(ox + sx[k], Jw_)];
         }
+#pragma unroll
+        for (int k = 0; k < kStageN; k++)
+          if (lane + 64 * k < S * S) Jt[lane + 64 * k] = v[k];
         __syncthreads();
+#ifdef UVHP_LK_PROF
+        c_stage += clock64() - c_i0;
+        n_stage++;
+#endif
       }
       a = nx - inx;
       b = ny - iny;
@@ -768,33 +852,42 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
       iw01 = (int)rintf(a * (1.f - b) * WSCALE);
       iw10 = (int)rintf((1.f - a) * b * WSCALE);
       iw11 = (1 << 14) - iw00 - iw01 - iw10;
-      long long ib1 = 0, ib2 = 0;
+      int ib1 = 0, ib2 = 0;
       nit++;
+      const uint8_t *t0 = Jt + (iny - oy) * S + (inx - ox);
+      int tp[kPer][4];
 #pragma unroll
       for (int q = 0; q < kPer; q++) {
-        const int e = lane + 64 * q;
-        if (e < area) {
-          const int y = e / win, x = e - y * win;
-          const uint8_t *t = Jt + (iny - oy + y) * S + (inx - ox + x);
-          const int diff = descale((long long)t[0] * iw00 + t[1] * iw01 + t[S] * iw10 + t[S + 1] * iw11, 14 - 5) - Iw[q];
-          ib1 += (long long)diff * dIx[q];
-          ib2 += (long long)diff * dIy[q];
-        }
+        const uint8_t *t = t0 + jo[q];
+        tp[q][0] = t[0];
+        tp[q][1] = t[1];
+        tp[q][2] = t[S];
+        tp[q][3] = t[S + 1];
       }
-      {
-        long long s2[2] = {ib1, ib2};
-        wave_sum_exact<2>(s2);
-        ib1 = s2[0];
-        ib2 = s2[1];
+#pragma unroll
+      for (int q = 0; q < kPer; q++) {  // pixels past the window have dIx = dIy = 0
+        const int diff = descale(dot4_i24(tp[q][0], tp[q][1], tp[q][2], tp[q][3], iw00, iw01, iw10, iw11), 14 - 5) - Iw[q];
+        ib1 += diff * dIx[q];
+        ib2 += diff * dIy[q];
       }
-      const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+      long long s2[2];
+      wave_sum_rows_i32<2>({ib1, ib2}, s2);
+      const float b1 = (float)s2[0] * FLT_SCALE, b2 = (float)s2[1] * FLT_SCALE;
       const float dx = (A12 * b2 - A22 * b1) * D;
       const float dy = (A12 * b1 - A11 * b2) * D;
       nx += dx;
       ny += dy;
       qx = nx + halfw;
       qy = ny + halfw;
-      if ((double)dx * dx + (double)dy * dy <= (double)crit_eps) break;
+#ifdef UVHP_LK_PROF
+      c_iter += clock64() - c_i0;
+#endif
+      // the reference's test is in double; a float estimate (relative error < 2^-21) decides it unless it
+      // lies within 1e-4 of the threshold, where the double test runs
+      const float e2 = dx * dx + dy * dy;
+      bool conv = e2 < crit_eps * 0.9999f;
+      if (!conv && !(e2 > crit_eps * 1.0001f)) conv = (double)dx * dx + (double)dy * dy <= (double)crit_eps;
+      if (conv) break;
       if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
         qx -= dx * 0.5f;
         qy -= dy * 0.5f;
@@ -809,6 +902,9 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     p1[2 * pi + 1] = qy;
     status[pi] = st;
     if (bytes) atomicAdd(bytes, (unsigned long long)(256 * (5 * nlev + nit)));
+#ifdef UVHP_LK_PROF
+    if (pi < 4096) g_lk_prof[pi] = LkProf{c_setup, c_stage, c_iter - c_stage, clock64() - c_begin, nit, n_stage, nlev, 0};
+#endif
   }
 }
 
