@@ -132,7 +132,9 @@ __device__ void singular_values3(const double *A, double *sv) {
     for (int j = 0; j < 3; j++) a[i][j] = A[i] * A[j] + A[3 + i] * A[3 + j] + A[6 + i] * A[6 + j];
   for (int sweep = 0; sweep < 60; sweep++) {
     double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
-    if (off < 1e-300) break;
+    // converged once the off-diagonal is 1e-18 of the diagonal: a further rotation has c == 1 and moves no
+    // diagonal entry by a bit (oracle la.h:singular_values3 stops at the same point)
+    if (off < 1e-300 || off <= 1e-36 * (a[0][0] * a[0][0] + a[1][1] * a[1][1] + a[2][2] * a[2][2])) break;
     for (int p = 0; p < 2; p++)
       for (int q = p + 1; q < 3; q++) {
         if (a[p][q] == 0) continue;
