@@ -508,9 +508,11 @@ void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, in
 // Cholesky factor of a singular Gram does.  The eigenvalues of G P_II + s2 I are >= s2, so the LU solve
 // below is well conditioned.
 
-// full symmetric G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk order).
-// One workgroup row per G row a: thread b >= a reads the partials' (a, b) entries (coalesced along the row,
-// only the written upper triangle is fetched) and writes G[a][b] and G[b][a].
+// the upper triangle of G (ncol x ncol, ld = ncol) from the chunk partials (upper triangles, fixed chunk
+// order).  One workgroup row per G row a: thread b >= a reads the partials' (a, b) entries (coalesced along the
+// row, only the upper triangle is fetched) and writes G[a][b].  The lower triangle is never written: its one
+// consumer (k_gemm_mfma with symA) reads G[b][a] for b < a -- a mirror store here wrote one double per cache
+// line (PMC r03t: 0.20 MB written for an 82 KB G at cfg2).
 __global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ partials, int nch, int ncol,
                                                      double *__restrict__ G, int *zero) {
   const int a = blockIdx.y, b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -529,22 +531,26 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double *__restrict__ 
   }
   for (; c < nch; c++) acc += partials[c * stride + u];
   G[u] = acc;
-  G[(size_t)b * ncol + a] = acc;
 }
 
 // C (m x n) = op(A) op(B); op(X) = X or X^T.  The small dense products of the information form (E = L^T G L,
 // (n+1)^2 with n ~ 100-243) on the matrix cores: one 16 x 16 output tile per wave (v_mfma_f64_16x16x4f64,
 // eight k-slabs loaded ahead of their MFMAs).  tri = 1: B is lower triangular (k >= j0 only), tri = 2:
-// op(A) is upper triangular (k >= i0 only) -- the zero blocks of the triangular factor are skipped.
-constexpr int kGemmWaves = 4;
-__global__ void __launch_bounds__(64 * kGemmWaves) k_gemm_mfma(int ta, int tb, int tri, int m, int n, int k,
+// op(A) is upper triangular (k >= i0 only) -- the zero blocks of the triangular factor are skipped.  symA: A is
+// symmetric with only its upper triangle stored (element (i, k) read at (min, max)).  Like k_info_P the
+// workgroups run on kGemmXcds XCDs only (each reads both operands into its L2).
+constexpr int kGemmWaves = 4, kGemmXcds = 2;
+__global__ void __launch_bounds__(64 * kGemmWaves) k_gemm_mfma(int ta, int tb, int tri, int symA, int m, int n, int k,
                                                               const double *__restrict__ A, int lda,
                                                               const double *__restrict__ B, int ldb,
                                                               double *__restrict__ C, int ldc) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int ntj = (n + 15) / 16;
-  const int tile = blockIdx.x * kGemmWaves + wid, ti = tile / ntj, tj = tile - ti * ntj;
+  const int nwg = ((m + 15) / 16 * ntj + kGemmWaves - 1) / kGemmWaves, per = (nwg + kGemmXcds - 1) / kGemmXcds;
+  const int xcd = blockIdx.x % 8, wg = xcd * per + blockIdx.x / 8;
+  if (xcd >= kGemmXcds || wg >= nwg || wg >= (xcd + 1) * per) return;
+  const int tile = wg * kGemmWaves + wid, ti = tile / ntj, tj = tile - ti * ntj;
   const int i0 = 16 * ti, j0 = 16 * tj;
   if (i0 >= m) return;  // a whole wave (no barriers in this kernel)
   const int ia = min(i0 + r16, m - 1), jb = min(j0 + r16, n - 1);
@@ -552,7 +558,12 @@ __global__ void __launch_bounds__(64 * kGemmWaves) k_gemm_mfma(int ta, int tb, i
   const int kbeg = tri == 1 ? j0 : tri == 2 ? i0 : 0;
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   acc = tile_chain(
-      kbeg, k, kq, [&](int kk) { return iv ? (ta ? A[(size_t)kk * lda + ia] : A[(size_t)ia * lda + kk]) : 0.0; },
+      kbeg, k, kq,
+      [&](int kk) {
+        if (!iv) return 0.0;
+        if (symA) return A[(size_t)min(ia, kk) * lda + max(ia, kk)];
+        return ta ? A[(size_t)kk * lda + ia] : A[(size_t)ia * lda + kk];
+      },
       [&](int kk) { return jv ? (tb ? B[(size_t)jb * ldb + kk] : B[(size_t)kk * ldb + jb]) : 0.0; }, acc);
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -560,10 +571,10 @@ __global__ void __launch_bounds__(64 * kGemmWaves) k_gemm_mfma(int ta, int tb, i
     if (row < m && col < n) C[(size_t)row * ldc + col] = acc[q];
   }
 }
-static void launch_gemm_mfma(hipStream_t s, int ta, int tb, int tri, int m, int n, int k, const double *A, int lda,
-                             const double *B, int ldb, double *C, int ldc) {
-  const int tiles = ((m + 15) / 16) * ((n + 15) / 16);
-  hipLaunchKernelGGL(k_gemm_mfma, dim3((tiles + kGemmWaves - 1) / kGemmWaves), dim3(64 * kGemmWaves), 0, s, ta, tb, tri,
+static void launch_gemm_mfma(hipStream_t s, int ta, int tb, int tri, int symA, int m, int n, int k, const double *A,
+                             int lda, const double *B, int ldb, double *C, int ldc) {
+  const int tiles = ((m + 15) / 16) * ((n + 15) / 16), nwg = (tiles + kGemmWaves - 1) / kGemmWaves;
+  hipLaunchKernelGGL(k_gemm_mfma, dim3(8 * ((nwg + kGemmXcds - 1) / kGemmXcds)), dim3(64 * kGemmWaves), 0, s, ta, tb, tri, symA,
                      m, n, k, A, lda, B, ldb, C, ldc);
 }
 
@@ -692,16 +703,23 @@ static int info_chol_mode(int nrows, int n, size_t *bytes) {
 // negative-diagonal count.   (P+ = P - V (I - s2 Z^-1) V^T, see launch_ekf_info)
 // Grid over the upper 16 x 16 tile pairs (bi <= bj) of P, 4 waves: wave w accumulates both products over the
 // k-slabs w, w + 4, ... on the matrix cores (four slabs' loads issued ahead of their MFMAs), the waves' partial
-// tiles are added in LDS in a fixed order.
+// tiles are added in LDS in a fixed order.  The tile pairs run on kInfoPXcds of the 8 XCDs (blocks labelled
+// blockIdx % 8 >= kInfoPXcds exit at once), each XCD a contiguous range of pairs: every XCD that runs tiles
+// reads nearly all of V and X into its own L2, so eight XCDs fetched them eight times (PMC r03o: 4.2 MB per
+// launch at cfg2 against 1.2 MB of operands).
+constexpr int kInfoPXcds = 2;
 __global__ void __launch_bounds__(256) k_info_P(double *__restrict__ P, int ldp, int N, const double *__restrict__ V,
                                                 const double *__restrict__ X, int n, double s2,
                                                 const double *__restrict__ w, double *__restrict__ dx, int *neg,
                                                 const int *gate, int nb) {
+  const int xcd = blockIdx.x % 8, npair = nb * (nb + 1) / 2, per = (npair + kInfoPXcds - 1) / kInfoPXcds;
+  int b = xcd * per + blockIdx.x / 8;
+  if (xcd >= kInfoPXcds || b >= npair || b >= (xcd + 1) * per) return;
   if (gate && *gate == 0) return;  // no accepted rows: the reference makes no update
   __shared__ double red[2][4][256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
-  int b = blockIdx.x, bi = 0;
+  int bi = 0;
   while (b >= nb - bi) {
     b -= nb - bi;
     bi++;
@@ -796,15 +814,16 @@ void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double
   double *E = T1 + (size_t)na * na;               // (n+1)^2
   double *Uf = E + (size_t)na * na;               // n^2   U   (5 (n+1)^2 in total)
   double *w = sc.y;
-  launch_gemm_mfma(s, 0, 0, 1, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug (Laug lower triangular)
-  launch_gemm_mfma(s, 1, 0, 2, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
+  launch_gemm_mfma(s, 0, 0, 1, 1, na, na, na, Gbuf, na, Laug, na, T1, na);  // G Laug (G upper-stored, Laug lower)
+  launch_gemm_mfma(s, 1, 0, 2, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
   hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2);
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
   const int nb = (N + 15) / 16;
-  hipLaunchKernelGGL(k_info_P, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx,
-                     sc.neg, sc.gate, nb);
+  const int per = (nb * (nb + 1) / 2 + kInfoPXcds - 1) / kInfoPXcds;
+  hipLaunchKernelGGL(k_info_P, dim3(8 * per), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg,
+                     sc.gate, nb);
 }
 
 void launch_ekf_info(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
