@@ -72,8 +72,8 @@ WORKLOADS = {
     "cfg2l": ("euroc_mav", "images",
               dict(init_max_features=800, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
                    dt_slam_delay=1.0),
-              dict(spawn=4, churn=4),
-              "cfg2l EuRoC V1_02-shaped stereo 752x480 images with track loss (scene churn 1/4 per frame), 400 "
+              dict(spawn=4, churn=3),
+              "cfg2l EuRoC V1_02-shaped stereo 752x480 images with track loss (scene churn 1/3 per frame), 400 "
               "tracks, 11 clones, <=200 MSCKF + 50 SLAM"),
     "cfg3": ("tum_vi", "images",
              dict(max_clone_size=20, init_max_features=800, num_pts=400, max_msckf_in_update=400,

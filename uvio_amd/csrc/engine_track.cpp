@@ -259,6 +259,7 @@ void Tracker::alloc_pyr(CamState &c, int w, int h) {
   HP_HIP(hipMalloc(&c.d_raw, (size_t)w * h * (downsample_ ? 4 : 1)));
   if (downsample_) HP_HIP(hipMalloc(&c.d_half, (size_t)w * h));
   HP_HIP(hipMalloc(&c.d_hist, 256 * sizeof(unsigned)));
+  HP_HIP(hipMemset(c.d_hist, 0, 256 * sizeof(unsigned)));  // cleared after use by each frame's pyramid
   HP_HIP(hipMalloc(&c.d_score, (size_t)w * h));
 }
 

@@ -99,6 +99,9 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   __shared__ uint8_t q[(T::QH + 2) * (T::QW + 2)];
   __shared__ uint8_t srcs[EQ ? 1 : T::SH * T::SW];
   const int c = blockIdx.z, t = threadIdx.x;
+  // the levels 2-3 launch runs after level 0's has read the histogram: it clears it for the next frame (the
+  // tracker zeroes it once at allocation), which saves a fill per camera and frame
+  if (!EQ && l == 2 && job.equalize && blockIdx.x == 0) job.hist[c][t] = 0u;
   const DPyr &p = job.p[c];
   if (l >= p.levels) return;
   const int w = p.w[l], h = p.h[l];
@@ -139,22 +142,53 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   // level l over the window (reflect-101 coordinates)
   const uint8_t *src = EQ ? job.src[c] : p.img[l - 1];
   const int sld = EQ ? job.stride[c] : p.w[l - 1];
+  // All of a thread's source bytes are loaded before any is used (a load consumed in the same loop iteration
+  // made one memory round trip per iteration); a window inside the image takes plain loads, one touching an
+  // edge the reflect-101 coordinates.
   if constexpr (EQ) {
-    for (int e = t; e < T::WH * T::WW; e += 256) {
-      const int wy = e / T::WW, wx = e - wy * T::WW;
-      const int gx = reflect101(x0 + wx - kPM, w), gy = reflect101(y0 + wy - kPM, h);
-      win[e] = lut[src[(size_t)gy * sld + gx]];
+    constexpr int NW = T::WH * T::WW, NWP = (NW + 255) / 256;
+    uint8_t v[NWP];
+    const int bx = x0 - kPM, by = y0 - kPM;
+    if (bx >= 0 && bx + T::WW <= w && by >= 0 && by + T::WH <= h) {
+#pragma unroll
+      for (int k = 0; k < NWP; k++) {
+        const int e = min(t + 256 * k, NW - 1), wy = e / T::WW, wx = e - wy * T::WW;
+        v[k] = src[(size_t)(by + wy) * sld + bx + wx];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NWP; k++) {
+        const int e = min(t + 256 * k, NW - 1), wy = e / T::WW, wx = e - wy * T::WW;
+        v[k] = src[(size_t)reflect101(by + wy, h) * sld + reflect101(bx + wx, w)];
+      }
     }
+#pragma unroll
+    for (int k = 0; k < NWP; k++)
+      if (t + 256 * k < NW) win[t + 256 * k] = lut[v[k]];
   } else {
     // level l-1 over every pyrDown tap of the window, at virtual coordinates (each cell the value at its
     // reflect-101 coordinate in level l-1).  Every window cell that is read later (rows / columns up to one
     // past the level's edge: reflected by at most 3) has its taps inside this block; the deeper-reflected
     // margin cells nothing reads are clamped into it
     const int sw = p.w[l - 1], sh = p.h[l - 1], sx0 = 2 * (x0 - kPM) - 2, sy0 = 2 * (y0 - kPM) - 2;
-    for (int e = t; e < T::SH * T::SW; e += 256) {
-      const int sy = e / T::SW, sx = e - sy * T::SW;
-      srcs[e] = src[(size_t)reflect101(sy0 + sy, sh) * sld + reflect101(sx0 + sx, sw)];
+    constexpr int NS = T::SH * T::SW, NSP = (NS + 255) / 256;
+    uint8_t v[NSP];
+    if (sx0 >= 0 && sx0 + T::SW <= sw && sy0 >= 0 && sy0 + T::SH <= sh) {
+#pragma unroll
+      for (int k = 0; k < NSP; k++) {
+        const int e = min(t + 256 * k, NS - 1), sy = e / T::SW, sx = e - sy * T::SW;
+        v[k] = src[(size_t)(sy0 + sy) * sld + sx0 + sx];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NSP; k++) {
+        const int e = min(t + 256 * k, NS - 1), sy = e / T::SW, sx = e - sy * T::SW;
+        v[k] = src[(size_t)reflect101(sy0 + sy, sh) * sld + reflect101(sx0 + sx, sw)];
+      }
     }
+#pragma unroll
+    for (int k = 0; k < NSP; k++)
+      if (t + 256 * k < NS) srcs[t + 256 * k] = v[k];
     __syncthreads();
     const int k5[5] = {1, 4, 6, 4, 1};
     for (int e = t; e < T::WH * T::WW; e += 256) {
@@ -206,17 +240,40 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   }
 }
 
+// Histogram of each camera's input: a packed, 16-byte aligned image is read 16 pixels per load (one load per
+// thread at 752 x 480 with the launch below); otherwise eight byte loads are issued before their counts.
 __global__ void __launch_bounds__(256) k_hist_multi(PyrJob job) {
   __shared__ unsigned hs[256];
   const int c = blockIdx.z;
   const DPyr &p = job.p[c];
-  const int w = p.w[0], h = p.h[0], stride = job.stride[c];
+  const int w = p.w[0], h = p.h[0], stride = job.stride[c], n = w * h;
   const uint8_t *img = job.src[c];
   hs[threadIdx.x] = 0;
   __syncthreads();
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < w * h; e += gridDim.x * blockDim.x) {
-    const int y = e / w, x = e - y * w;
-    atomicAdd(&hs[img[(size_t)y * stride + x]], 1u);
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  if (stride == w && (reinterpret_cast<uintptr_t>(img) & 15) == 0) {
+    for (int e = 16 * tid; e < n; e += 16 * nth) {
+      if (e + 16 <= n) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(img + e);
+        const unsigned wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) atomicAdd(&hs[(wd[k >> 2] >> (8 * (k & 3))) & 0xff], 1u);
+      } else {
+        for (int k = e; k < n; k++) atomicAdd(&hs[img[k]], 1u);
+      }
+    }
+  } else {
+    for (int e0 = tid; e0 < n; e0 += 8 * nth) {
+      int v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int e = min(e0 + k * nth, n - 1), y = e / w, x = e - y * w;
+        v[k] = img[(size_t)y * stride + x];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (e0 + k * nth < n) atomicAdd(&hs[v[k]], 1u);
+    }
   }
   __syncthreads();
   if (hs[threadIdx.x]) atomicAdd(&job.hist[c][threadIdx.x], hs[threadIdx.x]);
@@ -242,8 +299,10 @@ void launch_pyramids(hipStream_t s, const PyrJob &job) {
   if (job.equalize) {
     int w0 = 0, h0 = 0;
     for (int c = 0; c < job.ncam; c++) w0 = max(w0, job.p[c].w[0]), h0 = max(h0, job.p[c].h[0]);
-    for (int c = 0; c < job.ncam; c++)
-      if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
+    // the histograms are zero here: cleared by the previous frame's levels 2-3 launch (below), or at allocation
+    if (maxl <= 2)
+      for (int c = 0; c < job.ncam; c++)
+        if (hipMemsetAsync(job.hist[c], 0, 256 * sizeof(unsigned), s) != hipSuccess) throw std::runtime_error("hipMemsetAsync");
     hipLaunchKernelGGL(k_hist_multi, dim3(min(256, (w0 * h0 + 4095) / 4096), 1, job.ncam), dim3(256), 0, s, job);
   }
   // level 0 (the big image): 64 x 16 tiles, four pixels per thread; levels >= 2 (<= 188 x 120 at 752 x 480):
@@ -315,12 +374,13 @@ __device__ __forceinline__ bool has_arc9(unsigned m) {
   return (r & 0xFFFFu) != 0;
 }
 
-// FAST-9 test + cornerScore<16> of the pixel at p (row stride `ld`); 0 = not a corner
-__device__ int fast_corner_score(const uint8_t *p, int ld, int thr) {
-  const int v = p[0];
-  int ring[16];
+// FAST-9 test + cornerScore<16> of a pixel from its value v and Bresenham ring; 0 = not a corner
+__device__ __forceinline__ void fast_ring(const uint8_t *p, int ld, int &v, int (&ring)[16]) {
+  v = p[0];
 #pragma unroll
   for (int k = 0; k < 16; k++) ring[k] = p[c_fast_off[k][1] * ld + c_fast_off[k][0]];
+}
+__device__ int fast_corner_score(const int v, const int (&ring)[16], int thr) {
   unsigned dk = 0, br = 0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -378,12 +438,25 @@ __global__ void __launch_bounds__(256) k_fast_score(FastJob job, const int *__re
   uint8_t *__restrict__ score = job.score[k];
   const int w = job.w[k], sw = job.sw[k], sh = job.sh[k];
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
-  const int rows = min(kFastBand, sh - i0);
-  for (int e = threadIdx.x; e < rows * sw; e += blockDim.x) {
-    const int i = i0 + e / sw, j = e % sw;
-    int sc = 0;
-    if (i >= 3 && i < sh - 3 && j >= 3 && j < sw - 3) sc = fast_corner_score(img + (size_t)(y0 + i) * w + x0 + j, w, thr);
-    score[(size_t)(y0 + i) * w + x0 + j] = (uint8_t)sc;
+  const int rows = min(kFastBand, sh - i0), np = rows * sw;
+  // two pixels per thread and round: both rings' loads are in flight before either is scored
+  for (int e0 = threadIdx.x; e0 < np; e0 += 2 * blockDim.x) {
+    int v[2], ring[2][16], ii[2], jj[2];
+    bool in[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int e = min(e0 + u * (int)blockDim.x, np - 1);
+      ii[u] = i0 + e / sw;
+      jj[u] = e % sw;
+      in[u] = ii[u] >= 3 && ii[u] < sh - 3 && jj[u] >= 3 && jj[u] < sw - 3;
+      // a pixel of the cell's 3-pixel border reads its own (interior-clamped) ring and is not scored
+      const int ci = min(max(ii[u], 3), sh - 4), cj = min(max(jj[u], 3), sw - 4);
+      if (sh >= 7 && sw >= 7) fast_ring(img + (size_t)(y0 + ci) * w + x0 + cj, w, v[u], ring[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+      if (e0 + u * (int)blockDim.x < np)
+        score[(size_t)(y0 + ii[u]) * w + x0 + jj[u]] = (uint8_t)(in[u] ? fast_corner_score(v[u], ring[u], thr) : 0);
   }
 }
 
@@ -410,9 +483,18 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
   __shared__ int ncand;
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
   if (threadIdx.x == 0) ncand = 0;
-  for (int e = threadIdx.x; e < area; e += blockDim.x) {
-    const int i = e / sw, j = e - i * sw;
-    score[e] = scmap[(size_t)(y0 + i) * w + x0 + j];
+  // eight loads in flight per thread before their LDS stores (a store right behind its load made one memory
+  // round trip per pixel row of the loop)
+  for (int e0 = threadIdx.x; e0 < area; e0 += 8 * blockDim.x) {
+    uint8_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int e = min(e0 + k * (int)blockDim.x, area - 1), i = e / sw, j = e - i * sw;
+      v[k] = scmap[(size_t)(y0 + i) * w + x0 + j];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (e0 + k * (int)blockDim.x < area) score[e0 + k * blockDim.x] = v[k];
   }
   __syncthreads();
   // survivors are appended with one LDS atomic per wavefront (ballot + prefix popcount): a per-thread
@@ -541,10 +623,16 @@ __global__ void __launch_bounds__(64) k_subpix(SubpixJob job, float *__restrict_
     if (ix - ox < 0 || ix - ox > 2 * kSubpixMargin || iy - oy < 0 || iy - oy > 2 * kSubpixMargin) {
       ox = ix - kSubpixMargin;
       oy = iy - kSubpixMargin;
-      for (int e = lane; e < S * S; e += 64) {
-        const int ty = e / S;
-        tile[e] = px_clamped(img, w, h, ox + e - ty * S, oy + ty);
+      constexpr int NT = (kTile * kTile + 63) / 64;  // all of a lane's loads in flight before the LDS stores
+      float v[NT];
+#pragma unroll
+      for (int k = 0; k < NT; k++) {
+        const int e = min(lane + 64 * k, S * S - 1), ty = e / S;
+        v[k] = px_clamped(img, w, h, ox + e - ty * S, oy + ty);
       }
+#pragma unroll
+      for (int k = 0; k < NT; k++)
+        if (lane + 64 * k < S * S) tile[lane + 64 * k] = v[k];
       __syncthreads();
     }
     for (int e = lane; e < bw * bw; e += 64) {
@@ -1090,16 +1178,32 @@ __global__ void __launch_bounds__(256) k_ransac_hyp(RansacSlots job, int max_ite
   double F[27];
   const int nm = fundamental_7pt_d(x0, y0, x1, y1, F);
   if (lane == 0) nmodels[it] = nm;
-  for (int m = 0; m < nm; m++) {
-    int g = 0;
-    for (int i = lane; i < n; i += 64)
-      g += epipolar_inlier(F + 9 * m, p0n[2 * i], p0n[2 * i + 1], p1n[2 * i], p1n[2 * i + 1], t);
+  // the inlier counts of all of the hypothesis' models in one pass over the points (the models' division
+  // chains interleave and each point is loaded once), two points per lane in flight
+  int g[3] = {0, 0, 0};
+  for (int i0 = lane; i0 < n; i0 += 128) {
+    const int i1 = min(i0 + 64, n - 1);
+    const float2 a0 = reinterpret_cast<const float2 *>(p0n)[i0], b0 = reinterpret_cast<const float2 *>(p1n)[i0];
+    const float2 a1 = reinterpret_cast<const float2 *>(p0n)[i1], b1 = reinterpret_cast<const float2 *>(p1n)[i1];
+    const bool second = i0 + 64 < n;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o, 64);
-    if (lane == 0) good[it * 3 + m] = g;
-    if (lane == 0)
-      for (int k = 0; k < 9; k++) Fout[(size_t)it * 27 + 9 * m + k] = F[9 * m + k];
+    for (int m = 0; m < 3; m++)
+      if (m < nm) {
+        g[m] += epipolar_inlier(F + 9 * m, a0.x, a0.y, b0.x, b0.y, t);
+        if (second) g[m] += epipolar_inlier(F + 9 * m, a1.x, a1.y, b1.x, b1.y, t);
+      }
   }
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+    if (m < nm) {
+      int gm = g[m];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) gm += __shfl_xor(gm, o, 64);
+      if (lane == 0) {
+        good[it * 3 + m] = gm;
+        for (int k = 0; k < 9; k++) Fout[(size_t)it * 27 + 9 * m + k] = F[9 * m + k];
+      }
+    }
 }
 
 __device__ int ransac_update_iters_d(double p, double ep, int model_points, int max_iters) {
