@@ -229,6 +229,10 @@ struct DeviceBufs {
   // feature group runs; its column map in a dedicated device buffer (pinned mirror), the run it belongs to
   hipStream_t aux = nullptr;
   hipEvent_t ev_aux_in = nullptr, ev_aux_out = nullptr;
+  // staging uploads run on their own stream (the DMA transfer overlaps the kernels already queued on `stream`,
+  // which waits on ev_copy before its next launch)
+  hipStream_t copy = nullptr;
+  hipEvent_t ev_copy = nullptr;
   // the prefactor's column maps: kPreSlots pinned / device slots used in turn, each freed by its copy's event
   // (a slot is reused kPreSlots prefactors later, so the host never waits on the one just enqueued)
   static constexpr int kPreSlots = 8;

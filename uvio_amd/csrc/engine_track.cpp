@@ -160,11 +160,25 @@ Tracker::~Tracker() {
   }
   if (d_lk_bytes_) (void)hipFree(d_lk_bytes_);
   if (ev_match_) (void)hipEventDestroy(ev_match_);
+  if (ev_up_) (void)hipEventDestroy(ev_up_);
+  if (up_) (void)hipStreamDestroy(up_);
   if (b_) {
     if (b_->dmem) (void)hipFree(b_->dmem);
     if (b_->hmem) (void)hipHostFree(b_->hmem);
     delete b_;
   }
+}
+
+// The tracker's device buffers an upload writes are read only by this frame's later launches: the previous
+// frame's users of them finished before its results were read back.
+void Tracker::upload(void *dst, const void *src, size_t bytes) {
+  if (!up_) {
+    HP_HIP(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking));
+    HP_HIP(hipEventCreateWithFlags(&ev_up_, hipEventDisableTiming));
+  }
+  HP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, up_));
+  HP_HIP(hipEventRecord(ev_up_, up_));
+  HP_HIP(hipStreamWaitEvent(s_, ev_up_, 0));
 }
 
 void Tracker::sync() {
@@ -421,7 +435,7 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
   }
   if (nc == 0) return;
   fj.ncam = nf;
-  HP_HIP(hipMemcpyAsync(b.cells, b.hp(b.cells), 2 * nc * sizeof(int), hipMemcpyHostToDevice, s_));
+  upload(b.cells, b.hp(b.cells), 2 * nc * sizeof(int));
   launch_fast_multi(s_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
   HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, s_));
   sync();
@@ -463,7 +477,7 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     sj.end[sj.ncam] = np;
     sj.ncam++;
   }
-  HP_HIP(hipMemcpyAsync(b.det, h_det, 2 * np * sizeof(float), hipMemcpyHostToDevice, s_));
+  upload(b.det, h_det, 2 * np * sizeof(float));
   launch_subpix_multi(s_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
   const bool do_lk = lk_to && nr == 1;
   if (do_lk) {
@@ -797,7 +811,7 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     ns++;
   }
   if (ns == 0) return;
-  HP_HIP(hipMemcpyAsync(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters), hipMemcpyHostToDevice, s_));
+  upload(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters));
   lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
   {
     KScope ks(kp_, KC_LK);

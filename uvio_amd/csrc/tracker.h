@@ -86,6 +86,11 @@ class Tracker {
   std::unordered_map<int, std::vector<int>> subset_cache_;
   std::function<void()> in_flight_;
   hipEvent_t ev_match_ = nullptr;
+  // host-to-device uploads on their own stream: the DMA transfer overlaps the kernels queued before it (the
+  // pyramid) instead of starting after them; s_ waits on ev_up_ before its next launch
+  hipStream_t up_ = nullptr;
+  hipEvent_t ev_up_ = nullptr;
+  void upload(void *dst, const void *src, size_t bytes);
 
   CamState &cam_state(int cid);
   void alloc_pyr(CamState &c, int w, int h);
