@@ -210,6 +210,7 @@ void Tracker::ensure_cap(int n) {
       b.p1[k] = d.take<float>(2 * cap);
       b.st[k] = d.take<uint8_t>(cap);
       b.mask[k] = d.take<uint8_t>(cap);
+      b.p1n[k] = d.take<float>(2 * cap);  // the tracked points undistorted (RANSAC's input), for the database
     }
     b.cells = d.take<int>(2 * ncell);
     b.fastn = d.take<int>(ncell);
@@ -220,7 +221,6 @@ void Tracker::ensure_cap(int n) {
     const size_t mirror = d.off;
     for (int k = 0; k < kMaxCams; k++) {
       b.p0n[k] = d.take<float>(2 * cap);
-      b.p1n[k] = d.take<float>(2 * cap);
       b.nm[k] = d.take<int>(kRansacIters);
       b.good[k] = d.take<int>(3 * kRansacIters);
       b.F[k] = d.take<double>(27 * kRansacIters);
@@ -368,12 +368,14 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
       }
     }
   }
-  launch_decimate(s_, dec);
-  {
-    KScope ks(kp_, KC_PYR);
-    launch_pyramids(s_, job);
-  }
-  if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
+  pyr_launch_ = [this, dec, job]() {
+    launch_decimate(s_, dec);
+    {
+      KScope ks(kp_, KC_PYR);
+      launch_pyramids(s_, job);
+    }
+    if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
+  };
   if (ncam == 2 && use_stereo_) {
     feed_stereo(t, cam_ids[0], cam_ids[1], db);
   } else if (ncam > 2 && use_stereo_) {
@@ -383,6 +385,7 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
     feed_multi(t, cam_ids, ncam, db);  // mono, or binocular tracking of each camera on its own
   }
   in_flight_ = nullptr;  // not reached (no matching this frame): the caller does that work afterwards
+  ensure_pyr();          // a frame without matching still builds its pyramid for the next one
   // pyr_last / mask_last <- this frame's (every TrackKLT path ends this way)
   for (int k = 0; k < ncam; k++) {
     CamState &c = cs_[cam_ids[k]];
@@ -812,13 +815,14 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
   }
   if (ns == 0) return;
   upload(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters));
+  ensure_pyr();
   lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
   {
     KScope ks(kp_, KC_LK);
     launch_lk(s_, lk, ns, win_, pyr_levels_, kLkIters, kLkEps, true);
   }
   launch_ransac(s_, rs, ns, kRansacIters, kRansacConf);
-  HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.mask[hi] + b.cap), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.p1n[hi] + 2 * b.cap), hipMemcpyDeviceToHost, s_));
   if (in_flight_) {
     // wait for the matching results only, not for the work the callback enqueues behind them
     if (!ev_match_) HP_HIP(hipEventCreateWithFlags(&ev_match_, hipEventDisableTiming));
@@ -836,6 +840,20 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     return;
   }
   sync();
+}
+
+// The database's normalized coordinates of tracked point i of a matching slot: RANSAC's undistortion of the same
+// float LK result (k_undistort runs cam_undistort_f, read back with the results) for the radial-tangential model,
+// whose arithmetic is the same on both sides; the equidistant model's tan may differ by an ulp on the device,
+// so it is undistorted here.
+void Tracker::tracked_undistort(int slot, int i, int cam, const KeyPt &k, float &un, float &vn) const {
+  if (cams_[cam].model == 0) {
+    const float *h = b_->hp(b_->p1n[slot]);
+    un = h[2 * i];
+    vn = h[2 * i + 1];
+  } else {
+    cam_undistort_f(cams_[cam], k.x, k.y, un, vn);
+  }
 }
 
 void Tracker::match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out) {
@@ -880,6 +898,8 @@ void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
       det[k].ids = c.ids_last;
     }
   }
+  for (int k = 0; k < n; k++)
+    if (first[k]) ensure_pyr();  // detection on this frame's images
   detect_mono_multi(det.data(), n);
   std::vector<MatchJob> jobs;
   std::vector<int> who;
@@ -917,17 +937,19 @@ void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
     const int W = pn.w[0], H = pn.h[0];
     std::vector<KeyPt> good;
     std::vector<size_t> gid;
+    std::vector<int> gsrc;
     for (size_t i = 0; i < pts_new.size(); i++) {
       if (pts_new[i].x < 0 || pts_new[i].y < 0 || (int)pts_new[i].x >= W || (int)pts_new[i].y >= H) continue;
       if (mask_px(c.mask_new, W, (int)pts_new[i].x, (int)pts_new[i].y) > 127) continue;
       if (mask_ll[i]) {
         good.push_back(pts_new[i]);
         gid.push_back(det[k].ids[i]);
+        gsrc.push_back((int)i);
       }
     }
     for (size_t i = 0; i < good.size(); i++) {
       float un, vn;
-      cam_undistort_f(cams_[cam], good[i].x, good[i].y, un, vn);
+      tracked_undistort((int)j, gsrc[i], cam, good[i], un, vn);
       db(gid[i], t, cam, good[i].x, good[i].y, un, vn);
     }
     c.pts_last.swap(good);
@@ -941,6 +963,7 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   const DPyr &nl = A.pyr[1 - A.last], &nr = B.pyr[1 - B.last];
   const DPyr &ll = A.pyr[A.last], &lr = B.pyr[B.last];
   if (A.pts_last.empty() && B.pts_last.empty()) {
+    ensure_pyr();  // detection on this frame's images
     std::vector<KeyPt> gl, gr;
     std::vector<size_t> il, ir;
     detect_stereo(cl, cr, nl, nr, A.mask_new, B.mask_new, gl, gr, il, ir);
@@ -952,12 +975,19 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   }
   std::vector<KeyPt> pl_old = A.pts_last, pr_old = B.pts_last;
   std::vector<size_t> il_old = A.ids_last, ir_old = B.ids_last;
-  detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
+  {
+    HostProfScope hs(*hp_, "trk.detect");
+    detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
+  }
   MatchJob jm[2];
   ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two slots
   match_prepare(0, ll, nl, cl, cl, pl_old, jm[0]);
   match_prepare(1, lr, nr, cr, cr, pr_old, jm[1]);
-  match_run(jm, 2);
+  {
+    HostProfScope hs(*hp_, "trk.match");
+    match_run(jm, 2);
+  }
+  HostProfScope hs_post(*hp_, "trk.post");
   const MatchJob &jl = jm[0], &jr = jm[1];
   std::vector<KeyPt> pl_new = pl_old, pr_new = pr_old;
   std::vector<uint8_t> mask_ll, mask_rr;
@@ -973,6 +1003,7 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   const int Wl = nl.w[0], Hl = nl.h[0], Wr = nr.w[0], Hr = nr.h[0];
   std::vector<KeyPt> gl, gr;
   std::vector<size_t> gil, gir;
+  std::vector<int> sl, sr;  // each kept point's index in its matching slot
   // first index of each id among the right points (the reference's linear search returns the first)
   std::unordered_map<size_t, size_t> first_r;
   first_r.reserve(ir_old.size() * 2);
@@ -988,9 +1019,12 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
       gr.push_back(pr_new[ir]);
       gil.push_back(il_old[i]);
       gir.push_back(ir_old[ir]);
+      sl.push_back((int)i);
+      sr.push_back((int)ir);
     } else if (mask_ll[i]) {
       gl.push_back(pl_new[i]);
       gil.push_back(il_old[i]);
+      sl.push_back((int)i);
     }
   }
   std::unordered_set<size_t> in_gir(gir.begin(), gir.end());  // membership in gir, kept in step with it
@@ -1000,17 +1034,18 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
     if (mask_rr[i] && !added) {
       gr.push_back(pr_new[i]);
       gir.push_back(ir_old[i]);
+      sr.push_back((int)i);
       in_gir.insert(ir_old[i]);
     }
   }
   for (size_t i = 0; i < gl.size(); i++) {
     float un, vn;
-    cam_undistort_f(cams_[cl], gl[i].x, gl[i].y, un, vn);
+    tracked_undistort(0, sl[i], cl, gl[i], un, vn);
     db(gil[i], t, cl, gl[i].x, gl[i].y, un, vn);
   }
   for (size_t i = 0; i < gr.size(); i++) {
     float un, vn;
-    cam_undistort_f(cams_[cr], gr[i].x, gr[i].y, un, vn);
+    tracked_undistort(1, sr[i], cr, gr[i], un, vn);
     db(gir[i], t, cr, gr[i].x, gr[i].y, un, vn);
   }
   A.pts_last.swap(gl);

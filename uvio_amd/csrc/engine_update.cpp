@@ -256,7 +256,10 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
     if (cid < 0 || cid >= o_.num_cameras || !imgs[i]) return UVIO_HP_E_ARG;
     camids.push_back(cid);
   }
-  if (!tracker_) tracker_.reset(new Tracker(o_, cams_, d_.stream, &kprof_));
+  if (!tracker_) {
+    tracker_.reset(new Tracker(o_, cams_, d_.stream, &kprof_));
+    tracker_->set_host_prof(&hprof_);
+  }
   // Propagator::propagate_and_clone reads nothing the tracker produces.  When nothing can run between the
   // tracking and the propagation (no zero-velocity check, no UWB range before t), the host computes it
   // while the frame's LK + RANSAC are on the device and enqueues its launches behind them: the same
@@ -305,6 +308,7 @@ bool Engine::propagation_can_precede_tracking(double t) const {
 
 int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, int track_syncs,
                            double track_wait, bool try_init) {
+  HPROF("after_tracking");
   auto rT2 = clk::now();
   timing_ = uvio_hp_timing_t{};
   frame_feats_.clear();

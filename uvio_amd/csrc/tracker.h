@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "hp_common.h"
+#include "hprof.h"
 #include "kernels.h"
 
 namespace uvhp {
@@ -45,6 +46,7 @@ class Tracker {
   size_t currid;
   // TrackBase::set_num_features (TrackBase.h:152): after an initializer succeeds (VioManagerHelper.cpp:124)
   void set_num_features(int n);
+  void set_host_prof(HostProf *p) { hp_ = p; }
   int device_syncs = 0;     // host waits in the last feed
   double sync_wait = 0.0;   // seconds blocked in them
   // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand
@@ -86,11 +88,23 @@ class Tracker {
   std::unordered_map<int, std::vector<int>> subset_cache_;
   std::function<void()> in_flight_;
   hipEvent_t ev_match_ = nullptr;
+  HostProf own_hp_;                // used when the engine does not share its own
+  HostProf *hp_ = &own_hp_;        // the engine's section timer (UVIO_HP_HOST_PROF)
   // host-to-device uploads on their own stream: the DMA transfer overlaps the kernels queued before it (the
   // pyramid) instead of starting after them; s_ waits on ev_up_ before its next launch
   hipStream_t up_ = nullptr;
   hipEvent_t ev_up_ = nullptr;
   void upload(void *dst, const void *src, size_t bytes);
+  // the frame's decimation + pyramid launches, deferred until the new pyramid is first needed: the detection on
+  // the previous frame's pyramid and the upload of the matching inputs go out before it, so the upload's DMA
+  // overlaps the pyramid kernels
+  std::function<void()> pyr_launch_;
+  void ensure_pyr() {
+    if (!pyr_launch_) return;
+    std::function<void()> f = std::move(pyr_launch_);
+    pyr_launch_ = nullptr;
+    f();
+  }
 
   CamState &cam_state(int cid);
   void alloc_pyr(CamState &c, int w, int h);
@@ -127,6 +141,7 @@ class Tracker {
                      MatchJob &j);
   void match_run(MatchJob *jobs, int nj);
   void match_collect(int slot, const MatchJob &j, std::vector<KeyPt> &k1, std::vector<uint8_t> &mask_out);
+  void tracked_undistort(int slot, int i, int cam, const KeyPt &k, float &un, float &vn) const;
 };
 
 }  // namespace uvhp
