@@ -403,16 +403,21 @@ void *Engine::stage_reserve(size_t bytes, void **host) {
   return dev;
 }
 
-// The upload goes out on the copy stream and the main stream waits on its event: enqueued on the main stream
-// the transfer started only after every kernel queued before it (the chain's SLAM tables behind the MSCKF
-// update), and its ~15-20 us from start to completion showed as an idle gap before the next launch.  The ring
-// region is not read by anything queued earlier (it is reused only after a restart, which syncs).
+// With kernels still queued on the main stream the upload goes out on the copy stream and the main stream waits
+// on its event: enqueued on the main stream the transfer started only after every kernel queued before it (the
+// chain's SLAM tables behind the MSCKF update), and its ~15-20 us from start to completion showed as an idle
+// gap before the next launch.  On an idle main stream the copy goes there directly (the cross-stream wait only
+// adds latency then).  The ring region is not read by anything queued earlier (reused only after a restart,
+// which syncs).
 void Engine::stage_flush() {
   if (d_.stg_used == d_.stg_flushed) return;
+  const bool idle = hipStreamQuery(d_.stream) == hipSuccess;
   HP_HIP(hipMemcpyAsync(d_.stg_d + d_.stg_flushed, d_.stg_h + d_.stg_flushed, d_.stg_used - d_.stg_flushed,
-                        hipMemcpyHostToDevice, d_.copy));
-  HP_HIP(hipEventRecord(d_.ev_copy, d_.copy));
-  HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_copy, 0));
+                        hipMemcpyHostToDevice, idle ? d_.stream : d_.copy));
+  if (!idle) {
+    HP_HIP(hipEventRecord(d_.ev_copy, d_.copy));
+    HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_copy, 0));
+  }
   d_.stg_flushed = d_.stg_used;
 }
 

@@ -176,6 +176,10 @@ void Tracker::upload(void *dst, const void *src, size_t bytes) {
     HP_HIP(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking));
     HP_HIP(hipEventCreateWithFlags(&ev_up_, hipEventDisableTiming));
   }
+  if (hipStreamQuery(s_) == hipSuccess) {  // nothing to overlap: the cross-stream wait would only add latency
+    HP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s_));
+    return;
+  }
   HP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, up_));
   HP_HIP(hipEventRecord(ev_up_, up_));
   HP_HIP(hipStreamWaitEvent(s_, ev_up_, 0));
