@@ -804,6 +804,10 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     const double thr = 2.0 / fmax;
     rs.c0[ns] = c0;
     rs.c1[ns] = c1;
+    lk.c0[ns] = c0;
+    lk.c1[ns] = c1;
+    lk.p0n[ns] = b.p0n[sl];
+    lk.p1n[ns] = b.p1n[sl];
     rs.p0[ns] = b.p0[sl];
     rs.p1[ns] = b.p1[sl];
     rs.p0n[ns] = b.p0n[sl];
@@ -820,12 +824,13 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
   if (ns == 0) return;
   upload(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters));
   ensure_pyr();
+  lk.undistort = 1;  // RANSAC's undistortion in the LK epilogue (one launch less on the frame's critical path)
   lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
   {
     KScope ks(kp_, KC_LK);
     launch_lk(s_, lk, ns, win_, pyr_levels_, kLkIters, kLkEps, true);
   }
-  launch_ransac(s_, rs, ns, kRansacIters, kRansacConf);
+  launch_ransac(s_, rs, ns, kRansacIters, kRansacConf, lk.undistort != 0);
   HP_HIP(hipMemcpyAsync(b.hp(b.p1[lo]), b.p1[lo], span(b.p1[lo], b.p1n[hi] + 2 * b.cap), hipMemcpyDeviceToHost, s_));
   if (in_flight_) {
     // wait for the matching results only, not for the work the callback enqueues behind them

@@ -120,13 +120,14 @@ void Engine::feed_imu(double t, const double wm[3], const double am[3]) {
 // FeatureDatabase::update_feature (FeatureDatabase.cpp:59-85)
 void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float un, float vn) {
   auto it = db_.find(id);
-  FeatP f;
+  Feature *f;  // no shared_ptr copy (two atomic reference-count updates per observation)
   if (it != db_.end()) {
-    f = it->second;
+    f = it->second.get();
   } else {
-    f = std::make_shared<Feature>();
-    f->featid = id;
-    db_insert(id, f);
+    FeatP nf = std::make_shared<Feature>();
+    nf->featid = id;
+    f = nf.get();
+    db_insert(id, std::move(nf));
   }
   f->track(cam).m.push_back(FeatMeas{u, v, un, vn, t});
 }

@@ -331,6 +331,11 @@ struct LkSlots {
   // optional: algorithmic bytes of the launch accumulated on the device (SURVEY.md §8(d) LK term:
   // 256 (5 + iterations) per point and pyramid level visited)
   unsigned long long *bytes = nullptr;
+  // optional (undistort != 0): each point's p0 (camera c0) and result p1 (c1) undistorted into p0n / p1n by
+  // its wavefront at the end, RANSAC's inputs (launch_ransac with undistorted = true skips its own pass)
+  CamParams c0[kMaxCams], c1[kMaxCams];
+  float *p0n[kMaxCams] = {}, *p1n[kMaxCams] = {};
+  int undistort = 0;
 };
 void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,
                bool init_from_p0);
@@ -348,6 +353,7 @@ struct RansacSlots {
   float t[kMaxCams];
   int n[kMaxCams];
 };
-void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf);
+void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf,
+                   bool undistorted = false);
 
 }  // namespace uvhp

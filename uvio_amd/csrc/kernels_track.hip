@@ -745,7 +745,7 @@ __device__ LkProf g_lk_prof[4096];
 #else
 #define LKP_T(v)
 #endif
-__device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
+__device__ __forceinline__ float2 lk_point(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
                                          float *__restrict__ p1, uint8_t *__restrict__ status, int pi, int win,
                                          int max_level, int max_iters, float crit_eps, int init_from_p0,
                                          unsigned long long *bytes) {
@@ -994,6 +994,7 @@ __device__ __forceinline__ void lk_point(const DPyr &prev, const DPyr &next, con
     if (pi < 4096) g_lk_prof[pi] = LkProf{c_setup, c_stage, c_iter - c_stage, clock64() - c_begin, nit, n_stage, nlev, 0};
 #endif
   }
+  return make_float2(qx, qy);  // the result every lane holds (wave-uniform)
 }
 
 // point blockIdx.x of slot blockIdx.y (both cameras' temporal tracks in one launch)
@@ -1001,8 +1002,17 @@ __global__ void __launch_bounds__(64) k_lk(LkSlots job, int win, int max_level, 
                                            int init_from_p0) {
   const int slot = blockIdx.y;
   if ((int)blockIdx.x >= job.n[slot]) return;
-  lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], blockIdx.x, win, max_level, max_iters,
-           crit_eps, init_from_p0, job.bytes);
+  const float2 q = lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], blockIdx.x, win,
+                            max_level, max_iters, crit_eps, init_from_p0, job.bytes);
+  if (job.undistort && threadIdx.x < 2) {  // RANSAC's undistortion of this point, the k_undistort formula
+    const int p = blockIdx.x, w = threadIdx.x;
+    const float px = w ? q.x : job.p0[slot][2 * p], py = w ? q.y : job.p0[slot][2 * p + 1];
+    float x, y;
+    cam_undistort_f(w ? job.c1[slot] : job.c0[slot], px, py, x, y);
+    float *out = w ? job.p1n[slot] : job.p0n[slot];
+    out[2 * p] = x;
+    out[2 * p + 1] = y;
+  }
 }
 
 // ---------------------------------------------------------------- undistort + RANSAC
@@ -1319,11 +1329,11 @@ void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_le
                      init_from_p0 ? 1 : 0);
 }
 
-void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf) {
+void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf, bool undistorted) {
   int nmax = 0;
   for (int k = 0; k < nslot; k++) nmax = max(nmax, job.n[k]);
   if (nmax <= 0) return;
-  hipLaunchKernelGGL(k_undistort, dim3((nmax + 127) / 128, 2 * nslot), dim3(128), 0, s, job);
+  if (!undistorted) hipLaunchKernelGGL(k_undistort, dim3((nmax + 127) / 128, 2 * nslot), dim3(128), 0, s, job);
   hipLaunchKernelGGL(k_ransac_hyp, dim3((max_iters + 3) / 4, nslot), dim3(256), 0, s, job, max_iters);
   hipLaunchKernelGGL(k_ransac_select, dim3(1, nslot), dim3(256), 0, s, job, max_iters, conf);
 }
