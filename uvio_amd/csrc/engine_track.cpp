@@ -11,6 +11,41 @@
 
 namespace uvhp {
 
+// Open-addressing id -> value table for the per-frame track bookkeeping (a few hundred ids): one allocation per
+// frame instead of one node per id (std::unordered_map / set cost tens of microseconds per frame here).
+// emplace keeps the first value of an id, as std::unordered_map::emplace does.
+class IdTable {
+ public:
+  explicit IdTable(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 1) cap <<= 1;
+    keys_.assign(cap, kEmpty);
+    vals_.resize(cap);
+    mask_ = cap - 1;
+  }
+  void emplace(size_t id, size_t v) {
+    size_t h = slot(id);
+    while (keys_[h] != kEmpty && keys_[h] != id) h = (h + 1) & mask_;
+    if (keys_[h] == kEmpty) {
+      keys_[h] = id;
+      vals_[h] = v;
+    }
+  }
+  const size_t *find(size_t id) const {
+    for (size_t h = slot(id);; h = (h + 1) & mask_) {
+      if (keys_[h] == id) return &vals_[h];
+      if (keys_[h] == kEmpty) return nullptr;
+    }
+  }
+  bool contains(size_t id) const { return find(id) != nullptr; }
+
+ private:
+  static constexpr size_t kEmpty = ~(size_t)0;
+  size_t slot(size_t id) const { return (size_t)((id * 0x9E3779B97F4A7C15ull) >> 20) & mask_; }
+  std::vector<size_t> keys_, vals_;
+  size_t mask_ = 0;
+};
+
 namespace {
 constexpr int kRansacIters = 1000;      // findFundamentalMat(FM_RANSAC, thr, 0.999) default maxIters
 constexpr double kRansacConf = 0.999;   // TrackKLT.cpp:878
@@ -710,7 +745,8 @@ void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, cons
     std::vector<int> boxes;  // drawn into a clone of the LEFT mask (TrackKLT.cpp:713)
     std::vector<KeyPt> kp;
     std::vector<size_t> kid;
-    const std::unordered_set<size_t> left_ids(ids0.begin(), ids0.end());
+    IdTable left_ids(ids0.size());
+    for (size_t id : ids0) left_ids.emplace(id, 0);
     for (size_t i = 0; i < pts1.size(); i++) {
       const KeyPt &k = pts1[i];
       const int x = (int)k.x, y = (int)k.y, edge = 10;
@@ -719,7 +755,7 @@ void Tracker::detect_stereo(int cl, int cr, const DPyr &p0, const DPyr &p1, cons
       if (xc < 0 || xc >= scw || yc < 0 || yc >= sch) continue;
       const int xg = (int)std::floor(k.x / size_x), yg = (int)std::floor(k.y / size_y);
       if (xg < 0 || xg >= grid_x_ || yg < 0 || yg >= grid_y_) continue;
-      const bool is_stereo = left_ids.count(ids1[i]) != 0;
+      const bool is_stereo = left_ids.contains(ids1[i]);
       if (close.at(xc, yc) > 127 && !is_stereo) continue;
       if (mask_px(mask1, W, x, y) > 127) continue;
       close.at(xc, yc) = 255;
@@ -1014,14 +1050,13 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   std::vector<size_t> gil, gir;
   std::vector<int> sl, sr;  // each kept point's index in its matching slot
   // first index of each id among the right points (the reference's linear search returns the first)
-  std::unordered_map<size_t, size_t> first_r;
-  first_r.reserve(ir_old.size() * 2);
+  IdTable first_r(ir_old.size());
   for (size_t n = 0; n < ir_old.size(); n++) first_r.emplace(ir_old[n], n);
   for (size_t i = 0; i < pl_new.size(); i++) {
     if (pl_new[i].x < 0 || pl_new[i].y < 0 || (int)pl_new[i].x > Wl || (int)pl_new[i].y > Hl) continue;
-    const auto fr = first_r.find(il_old[i]);
-    const bool found = fr != first_r.end();
-    const size_t ir = found ? fr->second : 0;
+    const size_t *fr = first_r.find(il_old[i]);
+    const bool found = fr != nullptr;
+    const size_t ir = found ? *fr : 0;
     if (mask_ll[i] && found && mask_rr[ir]) {
       if (pr_new[ir].x < 0 || pr_new[ir].y < 0 || (int)pr_new[ir].x >= Wr || (int)pr_new[ir].y >= Hr) continue;
       gl.push_back(pl_new[i]);
@@ -1036,15 +1071,16 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
       sl.push_back((int)i);
     }
   }
-  std::unordered_set<size_t> in_gir(gir.begin(), gir.end());  // membership in gir, kept in step with it
+  IdTable in_gir(gir.size() + pr_new.size());  // membership in gir, kept in step with it
+  for (size_t id : gir) in_gir.emplace(id, 0);
   for (size_t i = 0; i < pr_new.size(); i++) {
     if (pr_new[i].x < 0 || pr_new[i].y < 0 || (int)pr_new[i].x >= Wr || (int)pr_new[i].y >= Hr) continue;
-    const bool added = in_gir.count(ir_old[i]) != 0;
+    const bool added = in_gir.contains(ir_old[i]);
     if (mask_rr[i] && !added) {
       gr.push_back(pr_new[i]);
       gir.push_back(ir_old[i]);
       sr.push_back((int)i);
-      in_gir.insert(ir_old[i]);
+      in_gir.emplace(ir_old[i], 0);
     }
   }
   for (size_t i = 0; i < gl.size(); i++) {

@@ -528,12 +528,45 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
     }
   }
   __syncthreads();
-  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order):
-  // kmax rounds of a wavefront min over each wave's strided share of the candidates, then the same
-  // over the waves' winners on wave 0
+  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order)
   const int n = min(ncand, kFastMaxCand);
   unsigned *ckey = (unsigned *)cand_s;
   for (int a = threadIdx.x; a < n; a += blockDim.x) ckey[a] = ((unsigned)(255 - cand_s[a]) << 16) | (unsigned)cand_idx[a];
+  int P = 1;
+  while (P < n) P <<= 1;
+  if (n > 0 && P <= kFastMaxCand) {
+    // a bitonic sort of the keys padded to a power of two (the padding sorts last): log2(P) (log2(P) + 1) / 2
+    // barrier-separated compare-exchange passes instead of kmax sequential min rounds; the keys are unique,
+    // so the first kmax are the selection's exactly
+    for (int a = n + threadIdx.x; a < P; a += blockDim.x) ckey[a] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < P; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned a0 = ckey[i], b0 = ckey[ixj];
+            if ((a0 > b0) == ((i & k) == 0)) {
+              ckey[i] = b0;
+              ckey[ixj] = a0;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int r = threadIdx.x; r < min(n, kmax); r += blockDim.x) {
+      const unsigned key = ckey[r];
+      const int ia = (int)(key & 0xFFFFu);
+      float *o = out + ((size_t)c * kmax + r) * 3;
+      o[0] = (float)(x0 + ia % sw);
+      o[1] = (float)(y0 + ia / sw);
+      o[2] = (float)(255 - (int)(key >> 16));
+    }
+    if (threadIdx.x == 0) out_n[c] = min(n, kmax);
+    return;
+  }
+  // (more candidates than the padded sort fits) kmax rounds of a wavefront min over each wave's strided
+  // share of the candidates, then the same over the waves' winners on wave 0
   __shared__ unsigned wtop[(kFastThreads / 64) * kFastMaxK];
   const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
