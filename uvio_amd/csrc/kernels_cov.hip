@@ -433,34 +433,58 @@ __global__ void __launch_bounds__(64) k_trinv16(const double *__restrict__ L, in
 // W (N x r, ld r) = M L^-T, i.e. W L^T = M, blocked by 16 columns with the matrix cores:
 //   tile = M[:, p] - W[:, <p] L[p, <p]^T   (v_mfma_f64_16x16x4_f64 over the solved columns)
 //   W[:, p] = tile Dinv_p^T                 (4 MFMAs with the diagonal block inverse)
-// One 64-lane workgroup per 16 rows of M; the solved part of its rows stays in LDS, L (L2-resident)
-// is read in batches of 16 columns so the loads of a batch are in flight together.  With hidx, M is
-// read as P[row][hidx[k]] (ldm = ldp), i.e. the columns P[:, I] of the covariance.
+// One 64-lane workgroup per 16 rows of M; the solved part of its rows stays in LDS.  Loads are batched so
+// that few memory round trips sit on the block chain: the column map is staged in LDS once, the next block's
+// M tile is loaded while the current one is solved, and L (L2-resident) is read 64 columns (16 loads per
+// lane) per batch before their 16 MFMAs (one round trip per batch instead of one per 16 columns).  The
+// accumulation order is the plain ascending k order either way.  With hidx, M is read as P[row][hidx[k]]
+// (ldm = ldp), i.e. the columns P[:, I] of the covariance.
 constexpr int kTrsmMaxR = 264;
 __global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, int ldm, const int *__restrict__ hidx, int N,
                                                 int r, const double *__restrict__ L, int ldl,
                                                 const double *__restrict__ Dinv, double *__restrict__ W) {
   __shared__ double Wt[16][kTrsmMaxR + 1];
   __shared__ double Tt[16][17];
+  __shared__ int hs[kTrsmMaxR];
   const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
   const int row0 = blockIdx.x * 16;
-  for (int j0 = 0; j0 < r; j0 += 16) {
-    dbl4 acc;
+  if (hidx)
+    for (int k = l; k < r; k += 64) hs[k] = hidx[k];
+  __syncthreads();
+  auto load_m = [&](int j0, double (&m)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int row = row0 + kq + 4 * q, col = j0 + r16;
-      double v = 0.0;
-      if (row < N && col < r) v = hidx ? M[(size_t)row * ldm + hidx[col]] : M[(size_t)row * ldm + col];
-      acc[q] = v;
+      m[q] = (row < N && col < r) ? (hidx ? M[(size_t)row * ldm + hs[col]] : M[(size_t)row * ldm + col]) : 0.0;
     }
+  };
+  double mnext[4];
+  load_m(0, mnext);
+  for (int j0 = 0; j0 < r; j0 += 16) {
+    dbl4 acc;
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[q] = mnext[q];
+    if (j0 + 16 < r) load_m(j0 + 16, mnext);  // in flight while this block is solved
+    // a column jj >= r of the last block reads row r - 1 of L (finite): its tile column is never stored, and
+    // its contribution to the valid columns goes through Dinv[j][m] with m > j, which is 0 (lower triangular)
     const int jj = j0 + r16;
     const double *Lj = L + (size_t)min(jj, r - 1) * ldl;
-    for (int k0 = 0; k0 < j0; k0 += 16) {  // j0 is a multiple of 16
+    int k0 = 0;
+    for (; k0 + 64 <= j0; k0 += 64) {  // 64 solved columns per batch: 16 L loads per lane in flight
+      double a[16], b[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) b[u] = Lj[k0 + 4 * u + kq];  // unconditional: see below
+#pragma unroll
+      for (int u = 0; u < 16; u++) a[u] = -Wt[r16][k0 + 4 * u + kq];
+#pragma unroll
+      for (int u = 0; u < 16; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+    }
+    for (; k0 < j0; k0 += 16) {  // j0 is a multiple of 16
       double a[4], b[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         a[u] = -Wt[r16][k0 + 4 * u + kq];
-        b[u] = (jj < r) ? Lj[k0 + 4 * u + kq] : 0.0;
+        b[u] = Lj[k0 + 4 * u + kq];
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
