@@ -294,8 +294,14 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
   __syncthreads();
 
   FEAT_TS(1)
-  // ---- geometry (wave 0): triangulation + Levenberg-Marquardt (MSCKF / delayed init only) ----
-  if ((F.mode == 0 || F.mode == 2) && wave == 0) {
+  // ---- geometry: triangulation (waves 0-1) + Levenberg-Marquardt (all 4 waves; MSCKF / delayed init only) ----
+  // Two of three LM trials are rejections (lam *= lam_mult, same Hessian; cfg2: 3.3 rejections and 1.8
+  // acceptances per feature), so each iteration evaluates four trials at once: wave w solves with the damping
+  // the reference would reach after w more rejections (lam multiplied w times, in the reference's order) and
+  // forms its cost; every wave then replays the reference's control flow over the four results in order
+  // (FeatureInitializer.cpp:197-375), so the accepted step, lam, runs and eps are the sequential ones.
+  if (F.mode == 0 || F.mode == 2) {
+    __shared__ double lm_H[9], lm_pf[3], lm_cond, lm_cand[2][4][4];
     const DClone &ca = clones[F.anchor_slot];
     const DCam &ka = cams[F.anchor_cam];
     double R_GtoA[9], p_AinG[3];
@@ -318,119 +324,162 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       un = mm.un;
       vn = mm.vn;
     }
-    // linear triangulation
-    double Ai[6] = {0, 0, 0, 0, 0, 0}, bi[3] = {0, 0, 0};
-    if (act) {
-      double b0[3] = {(double)un, (double)vn, 1.0}, b[3];
-      m3t_vec(R_AtoCi, b0, b);
-      double nb = norm3(b);
-      b[0] /= nb; b[1] /= nb; b[2] /= nb;
-      double Bp[9], A9[9];
-      skew(b, Bp);
-      m3_mul_at(Bp, Bp, A9);
-      Ai[0] = A9[0]; Ai[1] = A9[1]; Ai[2] = A9[2]; Ai[3] = A9[4]; Ai[4] = A9[5]; Ai[5] = A9[8];
-      m3_vec(A9, p_CiinA, bi);
-    }
-    double A[9], bb[3];
-    {
+    if (wave == 0) {
+      // linear triangulation
+      double Ai[6] = {0, 0, 0, 0, 0, 0}, bi[3] = {0, 0, 0};
+      if (act) {
+        double b0[3] = {(double)un, (double)vn, 1.0}, b[3];
+        m3t_vec(R_AtoCi, b0, b);
+        double nb = norm3(b);
+        b[0] /= nb; b[1] /= nb; b[2] /= nb;
+        double Bp[9], A9[9];
+        skew(b, Bp);
+        m3_mul_at(Bp, Bp, A9);
+        Ai[0] = A9[0]; Ai[1] = A9[1]; Ai[2] = A9[2]; Ai[3] = A9[4]; Ai[4] = A9[5]; Ai[5] = A9[8];
+        m3_vec(A9, p_CiinA, bi);
+      }
       double v9[9] = {Ai[0], Ai[1], Ai[2], Ai[3], Ai[4], Ai[5], bi[0], bi[1], bi[2]}, s9[9];
       ordered_sum<9>(red, v9, lane, m, s9);
-      A[0] = s9[0]; A[1] = s9[1]; A[2] = s9[2]; A[3] = s9[1]; A[4] = s9[3]; A[5] = s9[4];
-      A[6] = s9[2]; A[7] = s9[4]; A[8] = s9[5];
-      bb[0] = s9[6];
-      bb[1] = s9[7];
-      bb[2] = s9[8];
+      if (lane == 0)
+        for (int k = 0; k < 9; k++) lm_H[k] = s9[k];
     }
-    double pf[3];
-    colpiv_solve3(A, bb, pf);
-    double sv[3];
-    singular_values3(A, sv);
-    double condA = sv[0] / sv[2];
+    __syncthreads();
+    // the solve (wave 0) and the condition number (wave 1) of A p = b side by side
+    if (wave < 2) {
+      const double A[9] = {lm_H[0], lm_H[1], lm_H[2], lm_H[1], lm_H[3], lm_H[4], lm_H[2], lm_H[4], lm_H[5]};
+      if (wave == 0) {
+        const double bb[3] = {lm_H[6], lm_H[7], lm_H[8]};
+        double p3[3];
+        colpiv_solve3(A, bb, p3);
+        if (lane == 0)
+          for (int k = 0; k < 3; k++) lm_pf[k] = p3[k];
+      } else {
+        double sv[3];
+        singular_values3(A, sv);
+        if (lane == 0) lm_cond = sv[0] / sv[2];
+      }
+    }
+    __syncthreads();
+    double pf[3] = {lm_pf[0], lm_pf[1], lm_pf[2]};
     int st = 0;
-    double npf = norm3(pf);
-    if (fabs(condA) > bp.fi_max_cond || pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || isnan(npf)) st = 1;
-    if (st == 0 && bp.fi_refine) {
+    {
+      const double condA = lm_cond;
+      const double npf = norm3(pf);
+      if (fabs(condA) > bp.fi_max_cond || pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || isnan(npf)) st = 1;
+    }
+    if (st == 0 && bp.fi_refine) {  // block-uniform from here to the end of the LM loop
+      double *wred = red + 72 * wave;  // this wave's ordered_sum<1> slots (wave 0's <9> sums run between barriers)
       double rho = 1 / pf[2], alpha = pf[0] / pf[2], beta = pf[1] / pf[2];
       double lam = bp.fi_init_lamda, eps = 10000;
-      int runs = 0;
-      bool recompute = true;
+      int runs = 0, par = 0;
+      bool recompute = true, done = false;
       double Hs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
       double cost_old;
       {
         double e1 = act ? lm_err(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn) : 0.0;
-        ordered_sum<1>(red, &e1, lane, m, &cost_old);
+        ordered_sum<1>(wred, &e1, lane, m, &cost_old);
       }
-      while (runs < bp.fi_max_runs && lam < bp.fi_max_lamda && eps > bp.fi_min_dx) {
+      __syncthreads();
+      while (!done && runs < bp.fi_max_runs && lam < bp.fi_max_lamda && eps > bp.fi_min_dx) {
         if (recompute) {
-          double h[6] = {0, 0, 0, 0, 0, 0}, gg[3] = {0, 0, 0};
-          if (act) {
-            double H[6], r[2];
-            lm_terms(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn, H, r);
-            // H^T H (upper 6) and H^T r
-            h[0] = H[0] * H[0] + H[3] * H[3];
-            h[1] = H[0] * H[1] + H[3] * H[4];
-            h[2] = H[0] * H[2] + H[3] * H[5];
-            h[3] = H[1] * H[1] + H[4] * H[4];
-            h[4] = H[1] * H[2] + H[4] * H[5];
-            h[5] = H[2] * H[2] + H[5] * H[5];
-            gg[0] = H[0] * r[0] + H[3] * r[1];
-            gg[1] = H[1] * r[0] + H[4] * r[1];
-            gg[2] = H[2] * r[0] + H[5] * r[1];
+          if (wave == 0) {
+            double h[6] = {0, 0, 0, 0, 0, 0}, gg[3] = {0, 0, 0};
+            if (act) {
+              double H[6], r[2];
+              lm_terms(R_AtoCi, p_AinCi, alpha, beta, rho, un, vn, H, r);
+              // H^T H (upper 6) and H^T r
+              h[0] = H[0] * H[0] + H[3] * H[3];
+              h[1] = H[0] * H[1] + H[3] * H[4];
+              h[2] = H[0] * H[2] + H[3] * H[5];
+              h[3] = H[1] * H[1] + H[4] * H[4];
+              h[4] = H[1] * H[2] + H[4] * H[5];
+              h[5] = H[2] * H[2] + H[5] * H[5];
+              gg[0] = H[0] * r[0] + H[3] * r[1];
+              gg[1] = H[1] * r[0] + H[4] * r[1];
+              gg[2] = H[2] * r[0] + H[5] * r[1];
+            }
+            double v9[9] = {h[0], h[1], h[2], h[3], h[4], h[5], gg[0], gg[1], gg[2]}, s9[9];
+            ordered_sum<9>(red, v9, lane, m, s9);
+            if (lane == 0)
+              for (int k = 0; k < 9; k++) lm_H[k] = s9[k];
           }
-          double v9[9] = {h[0], h[1], h[2], h[3], h[4], h[5], gg[0], gg[1], gg[2]}, s9[9];
-          ordered_sum<9>(red, v9, lane, m, s9);
-          for (int k = 0; k < 6; k++) Hs[k] = s9[k];
-          for (int k = 0; k < 3; k++) g[k] = s9[6 + k];
+          __syncthreads();
+          for (int k = 0; k < 6; k++) Hs[k] = lm_H[k];
+          for (int k = 0; k < 3; k++) g[k] = lm_H[6 + k];
         }
+        // trial of this wave: the damping after `wave` further rejections
+        double lw = lam;
+        for (int k = 0; k < wave; k++) lw = lw * bp.fi_lam_mult;
         double Hl3[9] = {Hs[0], Hs[1], Hs[2], Hs[1], Hs[3], Hs[4], Hs[2], Hs[4], Hs[5]};
-        Hl3[0] *= (1.0 + lam);
-        Hl3[4] *= (1.0 + lam);
-        Hl3[8] *= (1.0 + lam);
+        Hl3[0] *= (1.0 + lw);
+        Hl3[4] *= (1.0 + lw);
+        Hl3[8] *= (1.0 + lw);
         double dx[3];
         colpiv_solve3(Hl3, g, dx);
         double cost;
         {
           double e1 = act ? lm_err(R_AtoCi, p_AinCi, alpha + dx[0], beta + dx[1], rho + dx[2], un, vn) : 0.0;
-          ordered_sum<1>(red, &e1, lane, m, &cost);
+          ordered_sum<1>(wred, &e1, lane, m, &cost);
         }
-        if (cost <= cost_old && (cost_old - cost) / cost_old < bp.fi_min_dcost) {
-          alpha += dx[0];
-          beta += dx[1];
-          rho += dx[2];
-          eps = 0;
-          break;
+        if (lane == 0) {
+          double *c = lm_cand[par][wave];
+          c[0] = cost;
+          c[1] = dx[0];
+          c[2] = dx[1];
+          c[3] = dx[2];
         }
-        if (cost <= cost_old) {
-          recompute = true;
-          cost_old = cost;
-          alpha += dx[0];
-          beta += dx[1];
-          rho += dx[2];
-          runs++;
-          lam = lam / bp.fi_lam_mult;
-          eps = sqrt(dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2]);
-        } else {
+        __syncthreads();
+        // the reference's sequence over the four trials (the loop condition is re-checked before each)
+        for (int w = 0; w < 4; w++) {
+          if (w > 0 && !(runs < bp.fi_max_runs && lam < bp.fi_max_lamda && eps > bp.fi_min_dx)) {
+            done = true;
+            break;
+          }
+          const double *c = lm_cand[par][w];
+          const double cw = c[0], d0 = c[1], d1 = c[2], d2 = c[3];
+          if (cw <= cost_old && (cost_old - cw) / cost_old < bp.fi_min_dcost) {
+            alpha += d0;
+            beta += d1;
+            rho += d2;
+            eps = 0;
+            done = true;
+            break;
+          }
+          if (cw <= cost_old) {
+            recompute = true;
+            cost_old = cw;
+            alpha += d0;
+            beta += d1;
+            rho += d2;
+            runs++;
+            lam = lam / bp.fi_lam_mult;
+            eps = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+            break;
+          }
           recompute = false;
           lam = lam * bp.fi_lam_mult;
-          continue;
         }
+        par ^= 1;
       }
       pf[0] = alpha / rho;
       pf[1] = beta / rho;
       pf[2] = 1 / rho;
-      double np = norm3(pf);
-      double vh[3] = {pf[0] / np, pf[1] / np, pf[2] / np};
-      double bl = 0.0;
-      if (act) {
-        double dd = dot3(p_CiinA, vh);
-        double perp[3] = {p_CiinA[0] - dd * vh[0], p_CiinA[1] - dd * vh[1], p_CiinA[2] - dd * vh[2]};
-        bl = norm3(perp);
+      if (wave == 0) {
+        double np = norm3(pf);
+        double vh[3] = {pf[0] / np, pf[1] / np, pf[2] / np};
+        double bl = 0.0;
+        if (act) {
+          double dd = dot3(p_CiinA, vh);
+          double perp[3] = {p_CiinA[0] - dd * vh[0], p_CiinA[1] - dd * vh[1], p_CiinA[2] - dd * vh[2]};
+          bl = norm3(perp);
+        }
+        double base_line_max = wave_max(bl);
+        if (pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || (np / base_line_max) > bp.fi_max_baseline ||
+            isnan(np))
+          st = 2;
       }
-      double base_line_max = wave_max(bl);
-      if (pf[2] < bp.fi_min_dist || pf[2] > bp.fi_max_dist || (np / base_line_max) > bp.fi_max_baseline || isnan(np))
-        st = 2;
     }
-    if (lane == 0) {
+    if (tid == 0) {
       sh.status = st;
       double pG[3];
       m3t_vec(R_GtoA, pf, pG);
