@@ -282,6 +282,11 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     DBatchParams bp = batch_params(b, s2, mult);
     bp.xv = fr_xv;
     bp.tri_in = tri_in;
+    const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: per-feature phase cycle counts
+    if (tsdump) {                                          // 8 k_feature + 4 k_chi2 stamps per feature
+      HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 16 * nf));
+      HP_HIP(hipMemsetAsync(bp.dbg_ts, 0, sizeof(long long) * 16 * nf, d_.stream));
+    }
     {
       KScope ks(&kprof_, KC_FEATURE);
       launch_feature_linearize(d_.stream, bp, it.t_feats, it.t_meas, it.t_vars, fr_cl, fr_cam, d_.P, d_.chi2, d_.H,
@@ -293,6 +298,20 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       KScope ks(&kprof_, KC_CHI2);
       launch_chi2_batch(d_.stream, bp, it.t_feats, d_.P, it.t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout + b.fout_off,
                         max_rows_f, d_.acc, d_.R);
+    }
+    if (tsdump) {  // synchronous copy-back: debug runs only (the chain loses its overlap)
+      std::vector<long long> h(16 * (size_t)nf);
+      HP_HIP(hipStreamSynchronize(d_.stream));
+      HP_HIP(hipMemcpy(h.data(), bp.dbg_ts, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+      HP_HIP(hipFree(bp.dbg_ts));
+      if (FILE *fp = std::fopen(tsdump, "ab")) {
+        for (int i = 0; i < nf; i++) {
+          long long rec[16] = {mode, nf, b.feats[i].nmeas, b.feats[i].nf};
+          for (int k = 0; k < 12; k++) rec[4 + k] = h[16 * (size_t)i + k];
+          std::fwrite(rec, sizeof(long long), 16, fp);
+        }
+        std::fclose(fp);
+      }
     }
     it.m = b.rows;
   };

@@ -57,72 +57,108 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
-// colPivHouseholderQr().solve for 3x3 (A row-major), single right-hand side
-__device__ void colpiv_solve3(const double *Ain, const double *bin, double *x) {
+// colPivHouseholderQr().solve for 3x3 (A row-major), single right-hand side.  Every loop is unrolled and the
+// pivot swap / rank cut / permuted store are selects on compile-time indices, so A, b, cn and perm stay in
+// registers (a runtime column index would put them in scratch memory, on the LM's critical path).
+__device__ __forceinline__ void colpiv_solve3(const double *Ain, const double *bin, double *x) {
   double A[9], b[3];
+#pragma unroll
   for (int i = 0; i < 9; i++) A[i] = Ain[i];
+#pragma unroll
   for (int i = 0; i < 3; i++) b[i] = bin[i];
   int perm[3] = {0, 1, 2};
   double cn[3];
+#pragma unroll
   for (int j = 0; j < 3; j++) cn[j] = A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j];
   int rank = 3;
   double maxpivot = 0;
+  bool stop = false;
+#pragma unroll
   for (int k = 0; k < 3; k++) {
+    if (stop) continue;
     int best = k;
+    double bv = cn[k];
+#pragma unroll
     for (int j = k + 1; j < 3; j++)
-      if (cn[j] > cn[best]) best = j;
-    if (best != k) {
-      for (int i = 0; i < 3; i++) {
-        double t = A[3 * i + k];
-        A[3 * i + k] = A[3 * i + best];
-        A[3 * i + best] = t;
+      if (cn[j] > bv) {
+        best = j;
+        bv = cn[j];
       }
-      double t = cn[k];
-      cn[k] = cn[best];
-      cn[best] = t;
-      int tp = perm[k];
-      perm[k] = perm[best];
-      perm[best] = tp;
-    }
+#pragma unroll
+    for (int c = k + 1; c < 3; c++)
+      if (best == c) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+          double t = A[3 * i + k];
+          A[3 * i + k] = A[3 * i + c];
+          A[3 * i + c] = t;
+        }
+        double t = cn[k];
+        cn[k] = cn[c];
+        cn[c] = t;
+        int tp = perm[k];
+        perm[k] = perm[c];
+        perm[c] = tp;
+      }
     double alpha = 0;
+#pragma unroll
     for (int i = k; i < 3; i++) alpha += A[3 * i + k] * A[3 * i + k];
     alpha = sqrt(alpha);
     if (k == 0) maxpivot = alpha;
     if (alpha <= maxpivot * 1e-15 || alpha == 0) {
       rank = k;
-      break;
+      stop = true;
+      continue;
     }
     if (A[3 * k + k] > 0) alpha = -alpha;
     double v[3] = {0, 0, 0};
+#pragma unroll
     for (int i = k; i < 3; i++) v[i] = A[3 * i + k];
     v[k] -= alpha;
     double vn = 0;
+#pragma unroll
     for (int i = k; i < 3; i++) vn += v[i] * v[i];
     if (vn > 0) {
+#pragma unroll
       for (int j = k; j < 3; j++) {
         double s = 0;
+#pragma unroll
         for (int i = k; i < 3; i++) s += v[i] * A[3 * i + j];
         s = 2 * s / vn;
+#pragma unroll
         for (int i = k; i < 3; i++) A[3 * i + j] -= s * v[i];
       }
       double s = 0;
+#pragma unroll
       for (int i = k; i < 3; i++) s += v[i] * b[i];
       s = 2 * s / vn;
+#pragma unroll
       for (int i = k; i < 3; i++) b[i] -= s * v[i];
     }
+#pragma unroll
     for (int j = k + 1; j < 3; j++) {
       double s = 0;
+#pragma unroll
       for (int i = k + 1; i < 3; i++) s += A[3 * i + j] * A[3 * i + j];
       cn[j] = s;
     }
   }
   double y[3] = {0, 0, 0};
-  for (int i = rank - 1; i >= 0; i--) {
-    double v = b[i];
-    for (int k = i + 1; k < rank; k++) v -= A[3 * i + k] * y[k];
-    y[i] = v / A[3 * i + i];
+#pragma unroll
+  for (int i = 2; i >= 0; i--) {
+    if (i < rank) {
+      double v = b[i];
+#pragma unroll
+      for (int k = i + 1; k < 3; k++)
+        if (k < rank) v -= A[3 * i + k] * y[k];
+      y[i] = v / A[3 * i + i];
+    }
   }
-  for (int i = 0; i < 3; i++) x[perm[i]] = y[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      if (perm[i] == j) x[j] = y[i];
 }
 
 // singular values (descending) of 3x3 A via Jacobi eigenvalues of A^T A
@@ -654,9 +690,9 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       double *row = Hl + (size_t)(2 * tid + i) * ldl;
       double *hf = Hf + (2 * tid + i) * 3;
       // H_f = dz_dpfg * dpfg_dlambda
-      for (int j = 0; j < ncolf; j++)
-        hf[j] = dz_dpfg[3 * i] * dl[j] + dz_dpfg[3 * i + 1] * dl[3 + j] + dz_dpfg[3 * i + 2] * dl[6 + j];
-      for (int j = ncolf; j < 3; j++) hf[j] = 0.0;
+#pragma unroll
+      for (int j = 0; j < 3; j++)  // compile-time columns: dl stays in registers
+        hf[j] = (j < ncolf) ? dz_dpfg[3 * i] * dl[j] + dz_dpfg[3 * i + 1] * dl[3 + j] + dz_dpfg[3 * i + 2] * dl[6 + j] : 0.0;
       // clone block: dz_dpfc * [R_ItoC skew(p_FinIi), -dpfc_dpfg]
       for (int j = 0; j < 3; j++) {
         row[mm.lc_clone + j] =
