@@ -1167,7 +1167,9 @@ __device__ int fundamental_7pt_d(const double *x0, const double *y0, const doubl
   c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
   int nr = solve_cubic_d(c, r);
   if (nr < 1 || nr > 3) return 0;
-  for (int k = 0; k < nr; k++) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {  // compile-time model index: F and r stay in registers
+    if (k >= nr) continue;
     double lambda = r[k], mu = 1.;
     double s = f1[8] * r[k] + f2[8];
     double *Fm = F + 9 * k;
@@ -1178,6 +1180,7 @@ __device__ int fundamental_7pt_d(const double *x0, const double *y0, const doubl
     } else {
       Fm[8] = 0.;
     }
+#pragma unroll
     for (int i = 0; i < 8; i++) Fm[i] = f1[i] * lambda + f2[i] * mu;
   }
   return nr;
