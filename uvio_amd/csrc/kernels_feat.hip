@@ -240,6 +240,65 @@ __device__ __forceinline__ double lm_err(const double *R_AtoCi, const double *p_
   return dn * dn;
 }
 
+// The three reflectors applied to the local Jacobian [Hl | r] (rows x ldl), one column per TPC adjacent threads.
+// The column products keep one summation order whatever TPC is: four partial sums w_q over the rows i = q mod 4
+// (rows past the last multiple of 4 go to w_0, in order), combined as (w_0 + w_1) + (w_2 + w_3); thread `part`
+// of a column accumulates the w_q with q = part mod TPC and the four sums meet through lane shuffles, so the
+// projected rows are the same bits for TPC = 1, 2, 4.  The update then splits the rows over the TPC threads.
+template <int TPC>
+__device__ __forceinline__ void ns_apply(double *Hl, const double *V, int rows, int ldl, int tid, double b1, double b2,
+                                         double b3, double g21, double g31, double g32) {
+  constexpr int NQ = 4 / TPC;
+  const int part = tid & (TPC - 1), lane = tid & 63, base = lane & ~(TPC - 1);
+  const int rows4 = rows & ~3;
+  for (int j = tid / TPC; j < ldl; j += 256 / TPC) {
+    double a1[NQ], a2[NQ], a3[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; k++) a1[k] = a2[k] = a3[k] = 0.0;
+    for (int i = 0; i < rows4; i += 4) {
+#pragma unroll
+      for (int k = 0; k < NQ; k++) {
+        const int r = i + part + TPC * k;
+        const double a = Hl[(size_t)r * ldl + j];
+        a1[k] += V[r * 3] * a;
+        a2[k] += V[r * 3 + 1] * a;
+        a3[k] += V[r * 3 + 2] * a;
+      }
+    }
+    if (part == 0)
+      for (int r = rows4; r < rows; r++) {
+        const double a = Hl[(size_t)r * ldl + j];
+        a1[0] += V[r * 3] * a;
+        a2[0] += V[r * 3 + 1] * a;
+        a3[0] += V[r * 3 + 2] * a;
+      }
+    double w1[4], w2[4], w3[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (TPC == 1) {
+        w1[q] = a1[q];
+        w2[q] = a2[q];
+        w3[q] = a3[q];
+      } else {
+        w1[q] = __shfl(a1[q / TPC], base + q % TPC, 64);
+        w2[q] = __shfl(a2[q / TPC], base + q % TPC, 64);
+        w3[q] = __shfl(a3[q / TPC], base + q % TPC, 64);
+      }
+    }
+    const double s1 = (w1[0] + w1[1]) + (w1[2] + w1[3]);
+    const double s2 = (w2[0] + w2[1]) + (w2[2] + w2[3]);
+    const double s3 = (w3[0] + w3[1]) + (w3[2] + w3[3]);
+    const double u1 = b1 * s1;
+    const double u2 = b2 * (s2 - g21 * u1);
+    const double u3 = b3 * (s3 - g31 * u1 - g32 * u2);
+#pragma unroll 4
+    for (int k = part; k < rows; k += TPC) {
+      double *p = Hl + (size_t)k * ldl + j;
+      *p -= V[k * 3] * u1 + V[k * 3 + 1] * u2 + V[k * 3 + 2] * u3;
+    }
+  }
+}
+
 struct FeatShared {
   double p_FinA[3], p_FinG[3], p_FinA_fej[3], p_FinG_fej[3];
   int status;
@@ -778,36 +837,12 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
     __syncthreads();
     const double b1 = sh.beta[0], b2 = sh.beta[1], b3 = sh.beta[2];
     const double g21 = red[0], g31 = red[1], g32 = red[2];
-    for (int j = tid; j < ldl; j += 256) {
-      double w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0}, w3[4] = {0, 0, 0, 0};
-      int i = 0;
-      for (; i + 4 <= rows; i += 4) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const double a = Hl[(size_t)(i + q) * ldl + j];
-          w1[q] += V[(i + q) * 3] * a;
-          w2[q] += V[(i + q) * 3 + 1] * a;
-          w3[q] += V[(i + q) * 3 + 2] * a;
-        }
-      }
-      for (; i < rows; i++) {
-        const double a = Hl[(size_t)i * ldl + j];
-        w1[0] += V[i * 3] * a;
-        w2[0] += V[i * 3 + 1] * a;
-        w3[0] += V[i * 3 + 2] * a;
-      }
-      const double s1 = (w1[0] + w1[1]) + (w1[2] + w1[3]);
-      const double s2 = (w2[0] + w2[1]) + (w2[2] + w2[3]);
-      const double s3 = (w3[0] + w3[1]) + (w3[2] + w3[3]);
-      const double u1 = b1 * s1;
-      const double u2 = b2 * (s2 - g21 * u1);
-      const double u3 = b3 * (s3 - g31 * u1 - g32 * u2);
-#pragma unroll 4
-      for (int k = 0; k < rows; k++) {
-        double *p = Hl + (size_t)k * ldl + j;
-        *p -= V[k * 3] * u1 + V[k * 3 + 1] * u2 + V[k * 3 + 2] * u3;
-      }
-    }
+    if (ldl <= 64)
+      ns_apply<4>(Hl, V, rows, ldl, tid, b1, b2, b3, g21, g31, g32);
+    else if (ldl <= 128)
+      ns_apply<2>(Hl, V, rows, ldl, tid, b1, b2, b3, g21, g31, g32);
+    else
+      ns_apply<1>(Hl, V, rows, ldl, tid, b1, b2, b3, g21, g31, g32);
     __syncthreads();
     r0 = 3;
   }
