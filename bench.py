@@ -1,13 +1,16 @@
 """Headline benchmark: VIO frames/s of the full per-frame track -> propagate -> update loop.
 
-Workload at N = 1 (BASELINE.json configs[1], SURVEY.md §8 cfg 2): EuRoC V1_02-shaped stereo 752x480 rig from
-configs/euroc_mav (radtan, 2 cameras, 20 Hz, 200 Hz IMU), 11 clones (+1 at update time), up to 200 MSCKF
-features per update and 50 SLAM landmarks.  Input: a synthetic EuRoC-shaped stream (uvio_amd/sim.py: seeded
-smooth trajectory, IMU from analytic derivatives + the config's noise densities) whose camera images are
-ray-cast from a textured room (uvio_amd/render.py) and are resident in HBM before the timed region.  One
-step = one camera frame: the IMU samples since the last frame, then VioManager::feed_measurement_camera
-(TrackKLT on the device: equalizeHist, pyramid, FAST grid detection, cornerSubPix, stereo + temporal
-pyramidal LK, RANSAC) -> propagate + clone -> MSCKF update -> SLAM update / delayed init -> marginalize.
+Workload at N = 1: cfg3 (BASELINE.json configs[2], SURVEY.md §8 cfg 3), the largest single-GPU configuration of
+BASELINE.json: a TUM-VI room1-shaped stereo fisheye 512x512 rig from configs/tum_vi (equidistant, 2 cameras,
+20 Hz, 200 Hz IMU), 20 clones (+1 at update time), 400 tracks per camera, up to 400 MSCKF features per update
+and 50 SLAM landmarks.  Input: a synthetic stream (uvio_amd/sim.py: seeded smooth trajectory, IMU from analytic
+derivatives + the config's noise densities) whose camera images are ray-cast from a textured room
+(uvio_amd/render.py) and are resident in HBM before the timed region.  One step = one camera frame: the IMU
+samples since the last frame, then VioManager::feed_measurement_camera (TrackKLT on the device: equalizeHist,
+pyramid, FAST grid detection, cornerSubPix, stereo + temporal pyramidal LK, RANSAC) -> propagate + clone ->
+MSCKF update -> SLAM update / delayed init -> marginalize.  The same frames are then fed once more as host
+images (uvio_hp_feed_camera, the reference caller's form: the library uploads them) into a second estimator;
+that rate is reported as "host_feed" (PCIe-inclusive, never "value").
 
 Steady state: the warm-up runs at least --warmup frames and then until the clone window is full
 (max_clones + 1 clones at update time) and the SLAM slots are >= 90 % populated (at most --max-warmup
@@ -16,28 +19,32 @@ frames); the line reports the effective warm-up and whether steady state was rea
 Multi-GPU (--gpus N > 1; launched either by torch.distributed.run, or by this script itself, which then
 spawns N worker processes before any GPU call): the north star's feature-sharded update --
 every rank runs the same stream and each MSCKF update's per-feature linearization, chi2 gate and Gram are
-split across the ranks with one RCCL all-reduce; cfg4t (UZH-FPV, 25 clones x 800 features per update) at
-N <= 4 and cfg5t (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value =
+split across the ranks with one RCCL all-reduce; cfg4 (UZH-FPV, 25 clones x 800 features per update) at
+N <= 4 and cfg5 (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value =
 frames of the one stream / wall time).  --replicas instead runs one independent estimator per GPU (weak).
 
 Other workloads (--workload, SURVEY.md §8 cfg 1-5; parity-test cases and stress lines):
   cfg1  EuRoC MH_01-shaped MONO 752x480 images (configs/euroc_mav, max_cameras 1), 11 clones, <= 100 MSCKF
-  cfg3  TUM-VI room1-shaped stereo fisheye 512x512 images (configs/tum_vi), 20 clones, 400 tracks per
-        camera, <= 400 MSCKF + 50 SLAM (LDS-tiled KLT stress)
-  cfg4  UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images (configs/uzhfpv_outdoor_45), 25 clones,
-        800 tracks, <= 800 MSCKF + 50 SLAM
-  cfg5  rpng_sim 4-camera 752x480 images, each camera tracked on its own (configs/rpng_sim_uwb), + 6 UWB
+  cfg2  EuRoC V1_02-shaped stereo 752x480 images (configs/euroc_mav), 11 clones, <= 200 MSCKF + 50 SLAM
+  cfg2l cfg2 with track loss (scene churn), 400 tracks
+  cfg4 / cfg5  the backend stress at BASELINE's feature counts: TrackSIM feed with 800 / 1500 MSCKF features
+        per update, each seen in every clone (26 clones x 2 cameras / 31 clones x 1 of 4 cameras, + 6 UWB
+        anchors and IMU intrinsics + g-sensitivity at cfg5) -- the shapes BASELINE.json's cfg4 / cfg5 name
+  cfg4i UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images (configs/uzhfpv_outdoor_45), 25 clones,
+        800 tracks, <= 800 MSCKF + 50 SLAM (TrackKLT front-end on rendered images)
+  cfg5i rpng_sim 4-camera 752x480 images, each camera tracked on its own (configs/rpng_sim_uwb), + 6 UWB
         anchors at 10 Hz, IMU intrinsics + g-sensitivity calibrated, 30 clones, 1500 tracks
-  cfg4t / cfg5t  the backend stress at BASELINE's feature counts: TrackSIM feed with 800 / 1500 MSCKF features
-        per update, each seen in every clone (26 clones x 2 cameras / 31 clones x 1 of 4 cameras)
+  (cfg4t / cfg5t, the names of cfg4 / cfg5 in rounds 1-3, and cfg4 / cfg5 images of round 3 = cfg4i / cfg5i)
 
 roofline: live HIP-event timing of the kernel classes (uvio_hp_set_kernel_timing) over the timed region;
 achieved = algorithmic FLOPs (FP64 classes) or bytes (tracker classes) of the class's launches (SURVEY.md
 §8(d), formulas in DESIGN.md §6) / their summed event time; "roofline" is the class with the largest device
-time, "rooflines" lists every class.  traffic = HBM bytes per launch from the committed rocprofv3 PMC passes
-of the same workload (profiles/, FETCH_SIZE x 2 + WRITE_SIZE).  cpu_baseline: the oracle/ CPU restatement
-(single-threaded) on a bounded sample of the same stream, rank 0 only.  ate: posyaw-aligned ATE RMSE against
-the stream's ground truth (ov_eval's definition, uvio_amd/evaluation.py).
+time in this run (the EKF-update chain aggregate excluded, its LDL factor is its own class), "rooflines" lists
+every class.  traffic = HBM bytes per launch from the committed rocprofv3 PMC passes of the same workload
+(profiles/, FETCH_SIZE x 2 + WRITE_SIZE); mfma_util = SQ_VALU_MFMA_BUSY_CYCLES of the class's kernels over
+(launch duration x shader clock x 256 CUs), from the same committed passes.  cpu_baseline: the oracle/ CPU
+restatement on a bounded sample of the same stream, rank 0 only.  ate: posyaw-aligned ATE RMSE against the
+stream's ground truth (ov_eval's definition, uvio_amd/evaluation.py).
 """
 import argparse
 import json
@@ -80,41 +87,40 @@ WORKLOADS = {
                   max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
              dict(spawn=4),
              "cfg3 TUM-VI room1-shaped stereo fisheye 512x512 images, 20 clones, 400 tracks/cam, <=400 MSCKF + 50 SLAM"),
-    "cfg4": ("uzhfpv_outdoor_45", "images",
-             dict(max_clone_size=25, init_max_features=800, num_pts=400, max_msckf_in_update=800, max_slam_features=50,
-                  max_slam_in_update=25, dt_slam_delay=1.0),
-             dict(spawn=4),
-             "cfg4 UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images, 25 clones, 800 tracks (400/cam), "
-             "<=800 MSCKF + 50 SLAM"),
-    "cfg5": ("rpng_sim_uwb", "images",
-             dict(max_clone_size=30, init_max_features=1500, num_pts=375, max_msckf_in_update=1500,
-                  max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
-             dict(spawn=4, uwb=True),
-             "cfg5 rpng_sim 4-cam 752x480 images (each camera tracked on its own) + 6 UWB anchors (2 fixed), IMU "
-             "intrinsics, 30 clones, 1500 tracks (375/cam), <=1500 MSCKF + 50 SLAM"),
     # the backend stress at the BASELINE feature counts: every MSCKF update holds 800 / 1500 features seen in
     # every clone (TrackSIM feed); the feature-sharded multi-GPU lines run these
-    "cfg4t": ("uzhfpv_outdoor_45", "tracks",
-              dict(max_clone_size=25, max_msckf_in_update=800, max_slam_features=50, max_slam_in_update=25,
-                   dt_slam_delay=1.0),
-              dict(spawn=800, frac_lost=0.0, frac_long=0.02),
-              "cfg4t UZH-FPV outdoor_45-shaped stereo fisheye 640x480 tracks, 25 clones, 800 MSCKF feats x 52 meas"),
-    "cfg5t": ("rpng_sim_uwb", "tracks",
-              dict(max_clone_size=30, max_msckf_in_update=1500, max_slam_features=50, max_slam_in_update=25,
-                   dt_slam_delay=1.0),
-              dict(spawn=1500, frac_lost=0.0, frac_long=0.02, uwb=True),
-              "cfg5t rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
+    "cfg4": ("uzhfpv_outdoor_45", "tracks",
+             dict(max_clone_size=25, max_msckf_in_update=800, max_slam_features=50, max_slam_in_update=25,
+                  dt_slam_delay=1.0),
+             dict(spawn=800, frac_lost=0.0, frac_long=0.02),
+             "cfg4 UZH-FPV outdoor_45-shaped stereo fisheye 640x480 tracks, 25 clones, 800 MSCKF feats x 52 meas"),
+    "cfg5": ("rpng_sim_uwb", "tracks",
+             dict(max_clone_size=30, max_msckf_in_update=1500, max_slam_features=50, max_slam_in_update=25,
+                  dt_slam_delay=1.0),
+             dict(spawn=1500, frac_lost=0.0, frac_long=0.02, uwb=True),
+             "cfg5 rpng_sim 4-cam 752x480 tracks + 6 UWB anchors (2 fixed), IMU intrinsics, 30 clones, 1500 MSCKF feats"),
+    "cfg4i": ("uzhfpv_outdoor_45", "images",
+              dict(max_clone_size=25, init_max_features=800, num_pts=400, max_msckf_in_update=800, max_slam_features=50,
+                   max_slam_in_update=25, dt_slam_delay=1.0),
+              dict(spawn=4),
+              "cfg4i UZH-FPV outdoor_45-shaped stereo fisheye 640x480 images, 25 clones, 800 tracks (400/cam), "
+              "<=800 MSCKF + 50 SLAM"),
+    "cfg5i": ("rpng_sim_uwb", "images",
+              dict(max_clone_size=30, init_max_features=1500, num_pts=375, max_msckf_in_update=1500,
+                   max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
+              dict(spawn=4, uwb=True),
+              "cfg5i rpng_sim 4-cam 752x480 images (each camera tracked on its own) + 6 UWB anchors (2 fixed), IMU "
+              "intrinsics, 30 clones, 1500 tracks (375/cam), <=1500 MSCKF + 50 SLAM"),
 }
 
-# oracle frames in the cpu_baseline sample (~10-30 s of single-core CPU work per workload)
+# names of rounds 1-3 (the TrackSIM stress lines were cfg4t / cfg5t)
+ALIASES = {"cfg4t": "cfg4", "cfg5t": "cfg5"}
+# oracle frames in the cpu_baseline sample (~10-30 s of CPU work per workload)
 CPU_CV_THREADS = 4  # num_opencv_threads of every reference config
-CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg2l": 60, "cfg3": 60, "cfg4": 20, "cfg5": 10, "cfg4t": 3, "cfg5t": 2}
-# The roofline's kernel class per workload: the class with the most device time in the 300-frame rocprof
-# statistics of that workload (profiles/r03o_*: cfg2 k_feature 138 us/frame against the LDL factors' 129).  Fixed
-# here so that a short run (the driver's --steps 20) reports the same class as the long one; a run in which the
-# class did not launch falls back to the largest class of that run.
-HEADLINE_CLASS = {"cfg1": "feature", "cfg2": "feature", "cfg2l": "lk", "cfg3": "lk", "cfg4": "chi2", "cfg5": "feature",
-                  "cfg4t": "chi2", "cfg5t": "feature"}
+CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg2l": 60, "cfg3": 60, "cfg4i": 20, "cfg5i": 10, "cfg4": 3, "cfg5": 2}
+# shader clock for cycle counts (MI355X peak engine clock, MI355X_MICROARCH.md) and the CU count
+SCLK_HZ = 2.4e9
+N_CU = 256
 
 
 def workload_options(U, name):
@@ -224,9 +230,10 @@ class Driver:
                 return t
 
 
-# committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, tools/pmc_summary.py), newest first.  cfg4 / cfg5 were
-# TrackSIM workloads before r03b (now cfg4t / cfg5t): their older summaries do not describe the image workloads
-PMC_MIN_TAG = {"cfg4": "r03b", "cfg5": "r03b"}
+# committed rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE / FP64 MFMA, tools/pmc_summary.py), newest first.  The
+# workload names cfg4 / cfg5 changed meaning in r04 (TrackSIM stress, before: images), so only r04+ passes count
+# for them and for their image variants
+PMC_MIN_TAG = {"cfg4": "r04", "cfg5": "r04", "cfg4i": "r04", "cfg5i": "r04"}
 
 
 def pmc_files(workload):
@@ -243,8 +250,9 @@ CLASS_GROUP_KERNELS = {"feature": ["k_feature"], "chi2": ["k_chi2"], "gram": ["k
 
 
 def pmc_class_traffic(workload, name, kernels):
-    """(HBM bytes per launch group of the kernel class, source file) from the newest PMC summary holding it:
-    the members' summed bytes over the number of groups (CLASS_GROUP_KERNELS)."""
+    """(HBM bytes per launch group of the kernel class, MFMA busy cycles per launch group or None, source file)
+    from the newest PMC summary holding it: the members' summed counters over the number of groups
+    (CLASS_GROUP_KERNELS)."""
     for path in pmc_files(workload):
         try:
             with open(os.path.join(ROOT, path)) as f:
@@ -256,8 +264,11 @@ def pmc_class_traffic(workload, name, kernels):
         if not hit or groups == 0:
             continue
         tot = sum(k[n]["traffic"] * k[n]["launches"] for n in hit)
-        return tot / groups, path
-    return None, None
+        busy = None
+        if any("mfma_busy_cycles" in k[n] for n in hit):
+            busy = sum(k[n].get("mfma_busy_cycles", 0.0) * k[n]["launches"] for n in hit) / groups
+        return tot / groups, busy, path
+    return None, None, None
 
 
 def max_over_ranks(x, device="cuda"):
@@ -327,11 +338,17 @@ def roofline_entry(name, st, wl):
         per = st["bytes"] / n
         achieved = per / avg / 1e9 if avg > 0 else 0.0
         peak, unit = HBM_PEAK_GBS, "GB/s"
-    traffic, src = pmc_class_traffic(wl, name, st["kernels"])
-    return {"kernel": name, "kernels": st["kernels"], "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": achieved / peak, "traffic": traffic, "traffic_source": src, "launches": st["launches"],
-            "avg_launch_us": avg * 1e6, ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per,
-            "device_s": secs}
+    traffic, busy, src = pmc_class_traffic(wl, name, st["kernels"])
+    e = {"kernel": name, "kernels": st["kernels"], "bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
+         "frac": achieved / peak, "traffic": traffic, "traffic_source": src, "launches": st["launches"],
+         "avg_launch_us": avg * 1e6, ("flops_per_launch" if bound == "mfma" else "bytes_per_launch"): per,
+         "device_s": secs}
+    if bound == "mfma":
+        # matrix-core busy cycles (summed over the CUs) per launch group over the chip's cycles in this run's average
+        # launch time: the whole-chip MFMA utilisation of the class
+        e["mfma_busy_cycles_per_launch"] = busy
+        e["mfma_util"] = busy / (avg * SCLK_HZ * N_CU) if (busy is not None and avg > 0) else None
+    return e
 
 
 def main():
@@ -342,8 +359,10 @@ def main():
     ap.add_argument("--max-warmup", type=int, default=200, help="warm-up cap while waiting for steady state")
     ap.add_argument("--cpu-frames", type=int, default=None,
                     help="timed oracle frames for cpu_baseline (0 = skip; default: ~10-30 s of CPU work per workload)")
-    ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS), default="auto",
-                    help="auto: cfg2 at 1 GPU, feature-sharded cfg4t at 2-4 GPUs, cfg5t beyond")
+    ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS) + sorted(ALIASES), default="auto",
+                    help="auto: cfg3 at 1 GPU, feature-sharded cfg4 at 2-4 GPUs, cfg5 beyond")
+    ap.add_argument("--no-host-feed", action="store_true",
+                    help="skip the second timed pass that feeds the frames as host images (uvio_hp_feed_camera)")
     ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
     ap.add_argument("--shard", action="store_true", help="feature sharding also at N = 1 (RCCL world of 1)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
@@ -362,9 +381,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     shard = (world > 1 and not args.replicas) or args.shard
-    wl = args.workload
+    wl = ALIASES.get(args.workload, args.workload)
     if wl == "auto":
-        wl = "cfg2" if world == 1 else ("cfg4t" if world <= 4 else "cfg5t")
+        wl = "cfg3" if world == 1 else ("cfg4" if world <= 4 else "cfg5")
     if args.cpu_frames is None:
         args.cpu_frames = CPU_FRAMES[wl]
     if args.ktime_period is None:
@@ -461,6 +480,11 @@ def main():
     ks1 = mgr.kernel_stats(flush=True)
     acc_ate = ate_fn(est_p, gt_p, est_q, gt_q, align="posyaw")
     raw = ate_fn(est_p, gt_p, align="none")
+    ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras)) if images else None
+    host_feed = None
+    if frames is not None and world == 1 and not args.no_host_feed:
+        mgr.close()
+        host_feed = host_feed_pass(U, opts, sim, frames, warm, args.steps, barrier, x_ref=[r[2] for r in rec])
 
     if rank == 0:
         # replicas: world streams were processed; sharded: one stream, split
@@ -471,13 +495,10 @@ def main():
             ks[k] = dict(a, launches=a["launches"] - b["launches"], seconds=a["seconds"] - b["seconds"],
                          flops=a["flops"] - b["flops"], bytes=a["bytes"] - b["bytes"])
         rl = {k: roofline_entry(k, v, wl) for k, v in ks.items() if v["launches"] > 0}
-        # the workload's headline class; otherwise the dominant class of this run by device time (the EKF-update
-        # chain contains the LDL class)
+        # the dominant kernel class of this run by device time (the EKF-update chain aggregate is excluded: it
+        # contains the LDL class and several latency-bound kernels)
         cand = {k: v for k, v in rl.items() if k != "ekf_update"}
-        dom = HEADLINE_CLASS.get(wl)
-        if dom not in cand:
-            dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
-        ntr = sum(len(mgr.get_tracks(c)[0]) for c in range(opts.num_cameras)) if images else None
+        dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
         cpu = None
         if args.cpu_frames > 0:
             # the oracle needs only the clone window filled; fewer warm-up frames bound its run time
@@ -520,6 +541,7 @@ def main():
                     "frames": args.steps},
             "roofline": rl.get(dom),
             "rooflines": rl,
+            "host_feed": host_feed,
             "cpu_baseline": cpu,
         }
         result_out.write(json.dumps(out) + "\n")
@@ -527,6 +549,32 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def host_feed_pass(U, opts, sim, frames, warm, steps, barrier, x_ref):
+    """The same frames once more, fed as host u8 images through uvio_hp_feed_camera (the reference caller's
+    form, SURVEY.md §8b: the library uploads each image) into a fresh estimator: the PCIe-inclusive frame rate.
+    The host copies of the images are made before the timed region; the estimate must equal the device-feed
+    run's (same inputs, same library)."""
+    host = {i: [im.cpu().numpy() for im in v] for i, v in frames.cache.items()}
+    mgr = U.VioManager(opts, device=0)
+    drv = Driver(sim, mgr, host, device_imgs=False)
+    for _ in range(warm):
+        drv.step()
+    xs = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        drv.step()
+        xs.append(mgr.get_imu_state()[1])
+    barrier()
+    t1 = time.perf_counter()
+    mgr.close()
+    same = all(np.array_equal(a, b) for a, b in zip(xs, x_ref))
+    img_bytes = sum(im.nbytes for im in host[next(iter(host))])
+    return {"value": steps / (t1 - t0), "unit": "frames/s", "ms_per_step": 1e3 * (t1 - t0) / steps,
+            "bytes_uploaded_per_frame": img_bytes, "estimate_equal_to_device_feed": same,
+            "note": "uvio_hp_feed_camera with pageable host images, same frames and warm-up as value's run"}
 
 
 def cpu_baseline(opts, wl, warmup, frames, dev_frames):

@@ -161,6 +161,10 @@ typedef struct {
    * §4): seconds of its single wait for the device plus the host replay of the results.  The chain books this
    * time in slam_delayed (the last stage); msckf_update / slam_update hold the host enqueue times of theirs */
   double chain_wait;
+  /* upload staging ring this frame: restarts of the ring (each waits for the device), and 1 when
+   * the update chain's state blob had to be copied out of the ring's previous epoch (engine_chain.cpp) */
+  int stage_restarts;
+  int chain_blob_old_epoch;
 } uvio_hp_timing_t;
 
 /* Live device timing of the kernel classes the benchmark prices against a roofline (HIP events on the

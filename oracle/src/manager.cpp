@@ -157,7 +157,10 @@ bool Manager::try_to_initialize() {
   db.cleanup_measurements(state.timestamp);
   tracker.num_features = (int)std::floor((double)o.num_pts / (double)o.num_cameras);
   if (norm(state.imu->vel()) > o.zupt_max_velocity) has_moved_since_zupt = true;
-  return true;
+  // VioManagerHelper.cpp:164, 187: success is recorded, yet the call returns false; the next camera frame
+  // returns true through thread_init_success (:91-93)
+  thread_init_success = true;
+  return false;
 }
 
 int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_point rT1, bool try_init) {
@@ -166,12 +169,19 @@ int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_
   timing.tracking = secs(rT1, rT2);
   fdbg.feats.clear();
   // VioManager.cpp:308-317 (camera frames only; a simulated frame needs an initialized filter, :236-240)
+  // UVioManager.cpp:152 / VioManager.cpp:294: the zero-velocity check comes first and reads is_initialized_vio
+  // as it was before this frame's initialization check
+  const bool was_initialized = is_initialized;
   if (!is_initialized) {
-    if (!try_init || !try_to_initialize()) return UVIO_HP_E_STATE;
+    if (!try_init) return UVIO_HP_E_STATE;
+    if (!thread_init_success) {
+      try_to_initialize();
+      return UVIO_HP_E_STATE;
+    }
     is_initialized = true;
   }
   // UVioManager.cpp:147-162 / VioManager.cpp:291-307: zero-velocity update; on success the frame ends here
-  if (zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) {
+  if (was_initialized && zupt && (!o.zupt_only_at_beginning || !has_moved_since_zupt)) {
     if (state.timestamp != t) {
       int z = zupt->try_update(state, db, t);
       if (z < 0) return z;

@@ -37,6 +37,7 @@ struct Manager {
   TrackKLT tracker;
   size_t currid;
   bool is_initialized = false;
+  bool thread_init_success = false;  // VioManager.h:226
   double startup_time = -1;
   double distance = 0;
   double timelastupdate = -1;

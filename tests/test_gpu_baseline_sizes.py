@@ -4,10 +4,10 @@ frames update with the full window:
 
   cfg1  EuRoC MH_01-shaped MONO images, 11 clones, <= 100 MSCKF + 50 SLAM
   cfg3  TUM-VI fisheye stereo images, 20 clones, 400 tracks / camera, <= 400 MSCKF
-  cfg4  UZH-FPV stereo fisheye 640x480 images, 25 clones, 800 tracks (the bench line's TrackKLT stream)
-  cfg4t UZH-FPV stereo fisheye tracks, 25 clones, 800 MSCKF features x 52 measurements
-  cfg5  rpng_sim 4 cameras (752x480 images, each tracked on its own) + 6 UWB anchors, 30 clones
-  cfg5t rpng_sim 4 cameras + 6 UWB anchors, IMU intrinsics + Tg, 30 clones, 1500 MSCKF features (tracks)
+  cfg4i UZH-FPV stereo fisheye 640x480 images, 25 clones, 800 tracks (the bench line's TrackKLT stream)
+  cfg4  UZH-FPV stereo fisheye tracks, 25 clones, 800 MSCKF features x 52 measurements
+  cfg5i rpng_sim 4 cameras (752x480 images, each tracked on its own) + 6 UWB anchors, 30 clones
+  cfg5  rpng_sim 4 cameras + 6 UWB anchors, IMU intrinsics + Tg, 30 clones, 1500 MSCKF features (tracks)
   iros  config/iros_2023_uvio as shipped (mono, downsample_cameras, ANCHORED_MSCKF_INVERSE_DEPTH MSCKF,
         GLOBAL_3D SLAM, 4 UWB anchors of which 2 fixed, initialized through try_to_initialize_uwb_anchors)
 
@@ -97,9 +97,9 @@ def test_lockstep_cfg4_images_baseline_size():
     import uvio_amd as U
     from uvio_amd.render import SceneRenderer
     B = _bench()
-    opts = B.workload_options(U, "cfg4")
+    opts = B.workload_options(U, "cfg4i")
     n = 30
-    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg4")
+    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg4i")
     steps = _lockstep(opts, sim, n, renderer=SceneRenderer(opts, device="cuda"))
     rows, full = _stats(steps, opts.max_clone_size)
     assert steps[-1][0]["P"].shape[0] >= 15 + 1 + 16 + 6 * 25  # 25 clones after the marginalization
@@ -109,9 +109,9 @@ def test_lockstep_cfg4_images_baseline_size():
 def test_lockstep_cfg4_baseline_size():
     import uvio_amd as U
     B = _bench()
-    opts = B.workload_options(U, "cfg4t")
+    opts = B.workload_options(U, "cfg4")
     n = 30
-    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg4t")
+    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg4")
     steps = _lockstep(opts, sim, n)
     rows, full = _stats(steps, opts.max_clone_size)
     assert max(r[2] for r in rows) == 800  # direct-to-staging tables, chunked build, tiled T GEMM, MFMA Gram
@@ -122,9 +122,9 @@ def test_lockstep_cfg4_baseline_size():
 def test_lockstep_cfg5_baseline_size():
     import uvio_amd as U
     B = _bench()
-    opts = B.workload_options(U, "cfg5t")
+    opts = B.workload_options(U, "cfg5")
     n = 35
-    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg5t")
+    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg5")
     steps = _lockstep(opts, sim, n)
     rows, full = _stats(steps, opts.max_clone_size)
     assert max(r[2] for r in rows) == 1500
@@ -136,9 +136,9 @@ def test_lockstep_cfg5_images_baseline_size():
     import uvio_amd as U
     from uvio_amd.render import SceneRenderer
     B = _bench()
-    opts = B.workload_options(U, "cfg5")
+    opts = B.workload_options(U, "cfg5i")
     n = 34
-    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg5")
+    sim = B.make_stream(opts, n + 2, seed=5, workload="cfg5i")
     steps = _lockstep(opts, sim, n, renderer=SceneRenderer(opts, device="cuda"))
     rows, full = _stats(steps, opts.max_clone_size)
     assert steps[-1][0]["P"].shape[0] >= 15 + 24 + 1 + 56 + 6 * 30 + 20

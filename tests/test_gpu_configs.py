@@ -128,6 +128,11 @@ def test_upload_staging_recycling_is_invisible():
         g.close()
         runs.append(snaps)
     assert max(a["timing"]["n_msckf"] for a in runs[0]) >= 256  # the direct-staging path ran
+    # the small ring restarted, also between the update chain's blob and its first launch, whose copy of the blob
+    # out of the previous epoch must precede the new epoch's upload (engine_chain.cpp, stage_flush(on_main))
+    assert sum(a["timing"]["stage_restarts"] for a in runs[1]) > 0
+    assert sum(a["timing"]["chain_blob_old_epoch"] for a in runs[1]) > 0
+    assert sum(a["timing"]["stage_restarts"] for a in runs[0]) == 0
     for a, b in zip(*runs):
         assert np.array_equal(a["x"], b["x"]) and np.array_equal(a["P"], b["P"])
 

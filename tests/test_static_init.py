@@ -106,7 +106,8 @@ def test_static_initializer_branches_match_numpy():
 def test_oracle_starts_from_rest_on_images():
     """iros_2023_uvio (ZUPT on, so no jerk is awaited): a platform at rest, mono downsampled images.  The
     filter stays uninitialized until the initializer's IMU window spans init_window_time, then initializes
-    on its own at the first such frame (the disparity test sees a still platform), and estimates gravity."""
+    on its own at the first such frame (the disparity test sees a still platform) and reports it on the next
+    frame, and estimates gravity."""
     import uvio_amd as U
     from oracle import oracle as O
     from uvio_amd.render import SceneRenderer
@@ -126,17 +127,22 @@ def test_oracle_starts_from_rest_on_images():
     assert not flags[0] and flags[-1], flags
     k = flags.index(True)
     assert all(flags[k:])
+    # the initializer succeeds on frame k - 1, which ends there (try_to_initialize returns false after success,
+    # VioManagerHelper.cpp:164,187): the state is set at the initializer's time, no clone yet; frame k finds
+    # thread_init_success (:91-93), propagates and clones
+    assert states[k - 1][3]["n_clones"] == 0 and states[k][3]["n_clones"] == 1
+    assert states[k - 1][2][0] < states[k - 1][0] and states[k][2][0] == states[k][0]
     # the first frame at which (a) the initializer's IMU window (trimmed at t - w - 0.1 + dt) spans the
     # window and (b) the disparity test has tracks with two observations in the older half: TrackKLT writes
     # no observation for the first image (it only detects), so the tracks' observations start at frame 1
     lag = 1.0 / sim.imu_rate + 1e-9
     w = opts.init_window_time
-    for i, (t, ok, _, _) in enumerate(states[:k + 1]):
+    for i, (t, ok, _, _) in enumerate(states[:k]):
         m = (sim.imu_t >= sim.t0 - 0.4) & (sim.imu_t <= t + lag)
         m &= sim.imu_t >= t - w - 0.10 + opts.calib_camimu_dt
         e = _numpy_static(opts, sim.imu_t[m], sim.wm[m], sim.am[m], False)
         two_old = sim.cam_t[2] < t - 0.5 * w
-        assert (e is not None and two_old) == (i == k), (i, k)
+        assert (e is not None and two_old) == (i == k - 1), (i, k)
     # after initialization the filter runs: the state is at the frame time, gravity matches the truth
     t, _, (ts, x), timing = states[-1]
     assert ts == t and timing["n_clones"] >= 1

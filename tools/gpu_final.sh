@@ -1,5 +1,5 @@
 # Round profile set on one MI355X: GPU tests, bench lines cfg2..cfg5 with CPU baselines, kernel-trace statistics
-# of the default bench (per-frame summary).  PMC passes: tools/gpu_pmc.sh.   usage: bash tools/gpu_final.sh TAG
+# of the cfg3 (default) and cfg2 benches (per-frame summaries).  PMC passes: tools/gpu_pmc.sh.   usage: bash tools/gpu_final.sh TAG
 set -e
 TAG=${1:-rXX}
 R=$GRAFT_REPO_ROOT
@@ -7,13 +7,15 @@ O=$R/gpurun_out/$TAG
 cd $R && mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg2_bench.json 2> $O/cfg2.err
-for wl in cfg2l cfg3 cfg4 cfg5 cfg4t cfg5t; do
+timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg3_bench.json 2> $O/cfg3.err
+for wl in cfg2 cfg2l cfg4i cfg5i cfg4 cfg5; do
   timeout -k 10 400 python -u bench.py --workload $wl > $O/${TAG}_${wl}_bench.json 2> $O/$wl.err
 done
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg2_bench_driver_form.json 2> $O/cfg2_driver.err
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg3_bench_driver_form.json 2> $O/cfg3_driver.err
 export TMPDIR=/tmp
-(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof2 -o run -- python3 $R/bench.py --cpu-frames 0 > $O/prof2.log 2>&1)
-python tools/prof_summary.py $O/prof2/run_kernel_trace.csv > $O/${TAG}_cfg2_per_frame.txt
-cp $O/prof2/run_kernel_stats.csv $O/${TAG}_cfg2_kernel_stats.csv
-rm -f $O/prof2/run_kernel_trace.csv
+for wl in cfg3 cfg2; do
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run -- python3 $R/bench.py --workload $wl --cpu-frames 0 --no-host-feed > $O/prof_$wl.log 2>&1)
+  python tools/prof_summary.py $O/prof_$wl/run_kernel_trace.csv > $O/${TAG}_${wl}_per_frame.txt
+  cp $O/prof_$wl/run_kernel_stats.csv $O/${TAG}_${wl}_kernel_stats.csv
+  rm -f $O/prof_$wl/run_kernel_trace.csv
+done

@@ -72,7 +72,7 @@ class Timing(C.Structure):
                 ("msckf_rows", C.c_int), ("msckf_cols", C.c_int), ("k_feat_launches", C.c_int),
                 ("k_feat_s", C.c_double), ("k_feat_flops", C.c_double), ("device_syncs", C.c_int),
                 ("sync_wait", C.c_double), ("zupt", C.c_int), ("n_anchor_change", C.c_int),
-                ("chain_wait", C.c_double)]
+                ("chain_wait", C.c_double), ("stage_restarts", C.c_int), ("chain_blob_old_epoch", C.c_int)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -350,6 +350,9 @@ class Engine {
   size_t currid_;
   // ---- manager ----
   bool is_initialized_ = false;
+  // VioManager::thread_init_success (VioManager.h:226): the initializer succeeded on an earlier frame; the
+  // manager reports initialized only on the next camera frame (VioManagerHelper.cpp:91-93, 187)
+  bool init_success_ = false;
   double startup_time_ = -1, distance_ = 0, timelastupdate_ = -1;
   bool anchors_initialized_ = false;
   std::map<double, std::unordered_map<size_t, double>> past_uwb_;
@@ -444,7 +447,7 @@ class Engine {
   T *stage(const T *src, size_t n) {
     return (T *)stage_bytes(src, sizeof(T) * n);
   }
-  void stage_flush();
+  void stage_flush(bool on_main = false);
   // wait for the device (counted in the frame's timing: device_syncs, sync_wait)
   void dev_sync();
   bool propagation_can_precede_tracking(double t) const;

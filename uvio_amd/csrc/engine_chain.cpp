@@ -235,9 +235,11 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     HPROF("chain.stage");
     if (d_.stg_epoch != blob_epoch) {
       // the ring restarted after the blob was staged: it is on the device (the restart flushed it and waited);
-      // copied out before anything staged since then is flushed over it
+      // copied out before anything staged since then is flushed over it -- the flush goes on the same stream,
+      // behind the copy (on the copy stream it could overwrite the blob's old bytes before the copy reads them)
       HP_HIP(hipMemcpyAsync(frame, blob_staged, blob.size(), hipMemcpyDeviceToDevice, d_.stream));
-      stage_flush();
+      stage_flush(true);
+      timing_.chain_blob_old_epoch = 1;
     } else {
       stage_flush();
       HP_HIP(hipMemcpyAsync(frame, blob_staged, blob.size(), hipMemcpyDeviceToDevice, d_.stream));

@@ -5,11 +5,12 @@
 // Host-only and run once per camera frame until it succeeds: a few hundred IMU samples and one pass
 // over the feature database, nothing the device would speed up.  The reference runs it on a detached
 // thread when use_multi_threading_subs is set; here it runs inline (the reference's single-threaded
-// branch, VioManagerHelper.cpp:182-183), so no camera times queue up while it runs and the frame that
-// initializes goes straight on to the propagation and update (VioManager.cpp:310-320).
+// branch, VioManagerHelper.cpp:182-183), so no camera times queue up while it runs.  As in the reference,
+// a successful attempt returns false: the frame that initialized ends there (UVioManager.cpp:168-175) and
+// the next camera frame, finding thread_init_success, propagates and updates (VioManagerHelper.cpp:91-93).
 // The dynamic initializer (DynamicInitializer.cpp, a Ceres MLE) is outside the hot path (SURVEY.md §8
-// f3 names the static one): where the reference would call it (init_dyn_use and a moving platform) the
-// attempt reports "not initialized".
+// f3 names the static one): where the reference would call it (init_dyn_use and a moving platform,
+// InertialInitializer.cpp:135-139) the frame fails with UVIO_HP_E_CONFIG and says so.
 #include <cmath>
 
 #include "engine.h"
@@ -157,7 +158,14 @@ bool Engine::try_to_initialize() {
   }
   const bool wait_for_jerk = !o_.try_zupt;  // VioManagerHelper.cpp:106
   const bool has_jerk = !moving_10 && moving_21, is_still = !moving_10 && !moving_21;
-  if (!(((has_jerk && wait_for_jerk) || (is_still && !wait_for_jerk)) && o_.init_imu_thresh > 0.0)) return false;
+  if (!(((has_jerk && wait_for_jerk) || (is_still && !wait_for_jerk)) && o_.init_imu_thresh > 0.0)) {
+    if (o_.init_dyn_use && !is_still)
+      throw HpError(UVIO_HP_E_CONFIG,
+                    "try_to_initialize: the platform is moving and init_dyn_use is set, so the reference would run "
+                    "its dynamic initializer (InertialInitializer.cpp:135-139), which is not built; start from rest "
+                    "or call initialize_with_gt");
+    return false;
+  }
   double t_init = 0;
   std::vector<double> cov;
   bool ok;
@@ -174,13 +182,15 @@ bool Engine::try_to_initialize() {
   if (tracker_) tracker_->set_num_features((int)std::floor((double)o_.num_pts / (double)o_.num_cameras));
   const double *v = imu_->val + 7;
   if (std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) > o_.zupt_max_velocity) has_moved_since_zupt_ = true;
-  is_initialized_ = true;
+  // thread_init_success = true, but try_to_initialize returns false (VioManagerHelper.cpp:164, 187): the
+  // frame that initialized ends here (UVioManager.cpp:168-175); the next camera frame reports success
+  init_success_ = true;
   {
     std::lock_guard<std::mutex> lk(imu_mtx_);
     init_imu_.clear();
     init_imu_.shrink_to_fit();
   }
-  return true;
+  return false;
 }
 
 }  // namespace uvhp

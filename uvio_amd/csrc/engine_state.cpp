@@ -381,6 +381,7 @@ void *Engine::stage_bytes(const void *src, size_t bytes) {
     dev_sync();
     d_.stg_used = d_.stg_flushed = 0;
     d_.stg_epoch++;
+    timing_.stage_restarts++;
   }
   if (bytes) std::memcpy(d_.stg_h + d_.stg_used, src, bytes);
   void *dev = d_.stg_d + d_.stg_used;
@@ -396,6 +397,7 @@ void *Engine::stage_reserve(size_t bytes, void **host) {
     dev_sync();
     d_.stg_used = d_.stg_flushed = 0;
     d_.stg_epoch++;
+    timing_.stage_restarts++;
   }
   *host = d_.stg_h + d_.stg_used;
   void *dev = d_.stg_d + d_.stg_used;
@@ -408,10 +410,12 @@ void *Engine::stage_reserve(size_t bytes, void **host) {
 // chain's SLAM tables behind the MSCKF update), and its ~15-20 us from start to completion showed as an idle
 // gap before the next launch.  On an idle main stream the copy goes there directly (the cross-stream wait only
 // adds latency then).  The ring region is not read by anything queued earlier (reused only after a restart,
-// which syncs).
-void Engine::stage_flush() {
+// which syncs).  The one exception is a copy queued on the main stream after a restart that still reads the
+// previous epoch's bytes (the chain's blob, engine_chain.cpp): its caller passes on_main, so the upload of the
+// new epoch, which may overwrite those bytes, is ordered behind the copy.
+void Engine::stage_flush(bool on_main) {
   if (d_.stg_used == d_.stg_flushed) return;
-  const bool idle = hipStreamQuery(d_.stream) == hipSuccess;
+  const bool idle = on_main || hipStreamQuery(d_.stream) == hipSuccess;
   HP_HIP(hipMemcpyAsync(d_.stg_d + d_.stg_flushed, d_.stg_h + d_.stg_flushed, d_.stg_used - d_.stg_flushed,
                         hipMemcpyHostToDevice, idle ? d_.stream : d_.copy));
   if (!idle) {

@@ -90,7 +90,7 @@ void Engine::feed_imu(double t, const double wm[3], const double am[3]) {
   // InertialInitializer::feed_imu (InertialInitializer.cpp:49-71): its age test reads the new message's
   // time, so the buffer is emptied only by a message older than oldest (never, in time order); the
   // window is trimmed in InertialInitializer::initialize
-  if (!is_initialized_) {
+  if (!is_initialized_ && !init_success_) {
     init_imu_.push_back(s);
     if (oldest != -1 && t < oldest) init_imu_.clear();
   }
@@ -318,9 +318,20 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
   timing_.sync_wait = track_wait;
   // VioManager.cpp:308-317: a camera frame before initialization tries the initializer (the simulated
   // feed requires an initialized filter, VioManager.cpp:236-240)
-  if (!is_initialized_ && !(try_init && try_to_initialize())) return UVIO_HP_E_STATE;
+  // The initializer runs single-threaded (use_multi_threading_subs off): on success it sets the state and
+  // returns false, so that frame ends uninitialized and the next camera frame finds thread_init_success
+  // (VioManagerHelper.cpp:91-93, 187).  The zero-velocity check of that next frame is skipped: it precedes
+  // the initialization check and reads is_initialized_vio (VioManager.cpp:294, UVioManager.cpp:152).
+  const bool was_initialized = is_initialized_;
+  if (!is_initialized_) {
+    if (!try_init || !init_success_) {
+      if (try_init) try_to_initialize();
+      return UVIO_HP_E_STATE;
+    }
+    is_initialized_ = true;
+  }
   // zero-velocity update (UVioManager.cpp:147-162, VioManager.cpp:291-307): on success the frame ends here
-  if (o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
+  if (was_initialized && o_.try_zupt && (!o_.zupt_only_at_beginning || !has_moved_since_zupt_)) {
     if (timestamp_ != t) did_zupt_update_ = zupt_try_update(t) == 1;
     if (did_zupt_update_) {
       // Propagator / UpdaterZeroVelocity::clean_old_imu_measurements(t + dt - 0.10)
