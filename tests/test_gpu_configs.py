@@ -132,7 +132,7 @@ def test_upload_staging_recycling_is_invisible():
     # out of the previous epoch must precede the new epoch's upload (engine_chain.cpp, stage_flush(on_main))
     assert sum(a["timing"]["stage_restarts"] for a in runs[1]) > 0
     assert sum(a["timing"]["chain_blob_old_epoch"] for a in runs[1]) > 0
-    assert sum(a["timing"]["stage_restarts"] for a in runs[0]) == 0
+    assert sum(a["timing"]["stage_restarts"] for a in runs[1]) > sum(a["timing"]["stage_restarts"] for a in runs[0])
     for a, b in zip(*runs):
         assert np.array_equal(a["x"], b["x"]) and np.array_equal(a["P"], b["P"])
 

@@ -198,10 +198,11 @@ int main() {
     assert tot == 64 and bad == 0
 
 
-def _lockstep_oracles(opts, n_frames, eps, steer, seed=5, **simkw):
+def _lockstep_oracles(opts, n_frames, eps, steer, seed=5, perturb=None, **simkw):
     """Two oracles in lock-step, the second adopting the first's state with every mean entry perturbed by up
     to eps relative (a stand-in for the device's rounding-level differences); with steer, the second gets the
-    first's per-feature results of each frame (the harness of tests/test_gpu_parity.py run_lockstep)."""
+    first's per-feature results of each frame (the harness of tests/test_gpu_parity.py run_lockstep).
+    perturb(nf, x, meta) -> x: a further change of the adopted mean before frame nf."""
     from oracle import oracle as O
     from test_gpu_parity import Steps, _snap
     from uvio_amd.sim import SimStream
@@ -211,8 +212,11 @@ def _lockstep_oracles(opts, n_frames, eps, steer, seed=5, **simkw):
     steps = Steps()
 
     def before(nf, t):
-        x = a.get_state_vector()[0]
-        b.set_state(x * (1 + eps * rng.uniform(-1, 1, x.shape)), a.get_fej_vector(), a.get_cov())
+        x, meta = a.get_state_vector()
+        x = x * (1 + eps * rng.uniform(-1, 1, x.shape))
+        if perturb is not None:
+            x = perturb(nf, x, meta)
+        b.set_state(x, a.get_fej_vector(), a.get_cov())
 
     def before_feed(m):
         if steer and m is b:
@@ -254,3 +258,46 @@ def test_rounding_tie_steering_explains_disagreements(euroc_yaml):
     assert len(found) >= 5 and len(found) >= 0.8 * len(ev)
     assert all(e["margin"] < 10 * STEER_MARGIN and e["after"] <= 1e-9 for e in found)
     assert p1 < 1e-7 and xP1 < 1e-11            # ... and steering removes their effect on the state
+
+
+K_IMU, K_QUAT, K_POSE = 0, 2, 3  # oracle/src/state.h Kind
+
+
+def _newest_clone_position(meta):
+    """value offset of the newest clone's position in the state vector (clones are the PoseJPL variables after
+    the cameras' extrinsics, State.cpp:28-166; quaternion first, then position)"""
+    off, last = 0, None
+    for kind, _, size in meta:
+        if kind == K_POSE:
+            last = off
+        off += size + (1 if kind in (K_IMU, K_QUAT, K_POSE) else 0)
+    return last + 4
+
+
+def test_rounding_tie_steering_refuses_a_real_error(euroc_yaml):
+    """Negative control of the lock-step witness: the second oracle's newest clone position is moved by 1e-7 m on
+    a few frames (a real error, far above rounding, yet small).  The features that see that clone disagree by
+    more than the strict bounds, no single near-tie float cast explains them (found False, or no candidate within
+    the margin), and _check_steer -- the lock-step tests' gate -- fails."""
+    import uvio_amd as U
+    from test_gpu_parity import STEER_MARGIN, _check_steer
+    opts = U.load_options(euroc_yaml, max_msckf_in_update=100, max_slam_features=20, max_slam_in_update=10,
+                          dt_slam_delay=0.3)
+    hit = []
+
+    def perturb(nf, x, meta):
+        if nf in (18, 22, 26):
+            x = x.copy()
+            x[_newest_clone_position(meta)] += 1e-7
+            hit.append(nf)
+        return x
+
+    steps = _lockstep_oracles(opts, 30, 0.0, steer=True, perturb=perturb, spawn=80, frac_long=0.3)
+    assert hit == [18, 22, 26]
+    ev = steps.steer
+    refused = [e for e in ev if not e["found"] or e["margin"] >= STEER_MARGIN]
+    for e in ev:
+        print(e)
+    assert len(refused) >= 3, ev
+    with pytest.raises(AssertionError):
+        _check_steer(ev, record=False)
