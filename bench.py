@@ -123,18 +123,37 @@ SCLK_HZ = 2.4e9
 N_CU = 256
 
 
-def workload_options(U, name):
+def _kv(items):
+    out = {}
+    for it in items:
+        k, v = it.split("=", 1)
+        try:
+            out[k] = json.loads(v)
+        except ValueError:
+            out[k] = v
+    return out
+
+
+def workload_options(U, name, extra=None):
+    """the workload's options; extra: further overrides (ablations), "anchors_fix" = 0/1 sets every UWB anchor's
+    fix flag (uwb_anchors.yaml "fix")"""
     cfg, _, ov, _, _ = WORKLOADS[name]
-    return U.load_options(os.path.join(CONFIGS, cfg, "estimator_config.yaml"), record_timing=1, **ov)
+    ov = dict(ov, **(extra or {}))
+    fix = ov.pop("anchors_fix", None)
+    opts = U.load_options(os.path.join(CONFIGS, cfg, "estimator_config.yaml"), record_timing=1, **ov)
+    if fix is not None:
+        for i in range(opts.n_anchors):
+            opts.anchors[i].fix = int(fix)
+    return opts
 
 
 def cfg2_options(U):
     return workload_options(U, "cfg2")
 
 
-def make_stream(opts, n_frames, seed, workload="cfg2"):
+def make_stream(opts, n_frames, seed, workload="cfg2", extra=None):
     from uvio_amd.sim import SimStream
-    kw = dict(WORKLOADS[workload][3])
+    kw = dict(WORKLOADS[workload][3], **(extra or {}))
     anchors = None
     if kw.pop("uwb", False):
         anchors = [opts.anchors[i] for i in range(opts.n_anchors)]
@@ -361,6 +380,10 @@ def main():
                     help="timed oracle frames for cpu_baseline (0 = skip; default: ~10-30 s of CPU work per workload)")
     ap.add_argument("--workload", choices=["auto"] + sorted(WORKLOADS) + sorted(ALIASES), default="auto",
                     help="auto: cfg3 at 1 GPU, feature-sharded cfg4 at 2-4 GPUs, cfg5 beyond")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="override an estimator option of the workload (ablations; the line records it)")
+    ap.add_argument("--sim", action="append", default=[], metavar="KEY=VALUE",
+                    help="override a SimStream argument of the workload (ablations; the line records it)")
     ap.add_argument("--no-host-feed", action="store_true",
                     help="skip the second timed pass that feeds the frames as host images (uvio_hp_feed_camera)")
     ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
@@ -403,11 +426,12 @@ def main():
     from uvio_amd.evaluation import ate as ate_fn
 
     images = WORKLOADS[wl][1] == "images"
-    opts = workload_options(U, wl)
+    opt_set, sim_set = _kv(args.set), _kv(args.sim)
+    opts = workload_options(U, wl, opt_set)
     max_warm = max(args.warmup, args.max_warmup)
     n_frames = max_warm + args.steps + 2
     # replicas: one stream per rank; sharded: every rank runs the same stream and splits its MSCKF updates
-    sim = make_stream(opts, n_frames + 2, seed=5 if shard else 5 + rank, workload=wl)
+    sim = make_stream(opts, n_frames + 2, seed=5 if shard else 5 + rank, workload=wl, extra=sim_set)
     dev = torch.device("cuda", local)
     frames = Frames(sim, dev) if images else None
     if frames is not None:
@@ -503,7 +527,7 @@ def main():
         if args.cpu_frames > 0:
             # the oracle needs only the clone window filled; fewer warm-up frames bound its run time
             cpu_warm = warm if images else min(warm, int(opts.max_clone_size) + 3)
-            cpu = cpu_baseline(opts, wl, cpu_warm, args.cpu_frames, frames)
+            cpu = cpu_baseline(opts, wl, cpu_warm, args.cpu_frames, frames, sim_set)
         out = {
             "metric": "VIO frames/sec (track+propagate+update) at clones x feats",
             "value": value,
@@ -534,7 +558,8 @@ def main():
                        "state_dim": acc["cov_dim"], "host_waits_per_frame": acc["syncs"] / args.steps,
                        "host_wait_ms_per_frame": 1e3 * acc["sync_wait"] / args.steps,
                        "stage_ms": {k: round(1e3 * v / args.steps, 4) for k, v in stage_s.items()},
-                       "parallelism": ("feature-shard%d" % world) if shard else ("replicas%d" % world)},
+                       "parallelism": ("feature-shard%d" % world) if shard else ("replicas%d" % world),
+                       "overrides": {"options": opt_set, "sim": sim_set} if (opt_set or sim_set) else None},
             "ate_rmse_m": acc_ate["pos_m"],
             "ate": {"align": "posyaw (ov_eval AlignTrajectory.cpp:84-106)", "pos_rmse_m": acc_ate["pos_m"],
                     "ori_rmse_deg": acc_ate["ori_deg"], "unaligned_pos_rmse_m": raw["pos_m"],
@@ -577,14 +602,14 @@ def host_feed_pass(U, opts, sim, frames, warm, steps, barrier, x_ref):
             "note": "uvio_hp_feed_camera with pageable host images, same frames and warm-up as value's run"}
 
 
-def cpu_baseline(opts, wl, warmup, frames, dev_frames):
+def cpu_baseline(opts, wl, warmup, frames, dev_frames, sim_set=None):
     """oracle/ (the CPU restatement) on the same stream (rank 0's), one thread, bounded sample."""
     from oracle import oracle as O
     # the reference's configs run OpenCV on num_opencv_threads = 4 (config/*/estimator_config.yaml:87-89): the
     # oracle's restated parallel OpenCV calls (LK per point, pyrDown / Scharr per row) use as many; the estimator
     # itself is single-threaded in the reference
     threads = O.set_threads(CPU_CV_THREADS)
-    sim = make_stream(opts, warmup + frames + 2, seed=5, workload=wl)
+    sim = make_stream(opts, warmup + frames + 2, seed=5, workload=wl, extra=sim_set)
     host = None
     if dev_frames is not None:
         host = {}
