@@ -4,15 +4,10 @@
 #include <cstring>
 #include <string>
 
-#include "manager.h"
+#include "handle.h"
 
 using namespace orc;
 
-struct orc_handle {
-  Manager m;
-  std::string err;
-  explicit orc_handle(const uvio_hp_options_t &o) : m(o) {}
-};
 
 extern "C" {
 

@@ -830,13 +830,8 @@ UpdaterUWB::UpdaterUWB(const uvio_hp_options_t &o) : sigma_range(o.uwb_sigma_ran
   fill_chi2(chi_squared_table);
 }
 
-// UpdaterUWB.cpp:53-90 + UVioUpdaterHelper.cpp:147-241
-int UpdaterUWB::update_single(State &s, double timestamp, size_t anchor_id, double range) {
-  (void)timestamp;
-  auto ait = s.anchors.find(anchor_id);
-  if (ait == s.anchors.end()) return 0;
-  VarP anchor = ait->second;
-  std::vector<Ref> x_order;
+// UVioUpdaterHelper::get_uwb_jacobian_single (UVioUpdaterHelper.cpp:147-241): residual and H_x of one range
+void uwb_jacobian_single(State &s, const VarP &anchor, double range, Mat &res, Mat &H_x, std::vector<Ref> &x_order) {
   int total_hx = 0;
   Ref clone_I = imu_pose_ref(s);
   x_order.push_back(clone_I);
@@ -859,22 +854,35 @@ int UpdaterUWB::update_single(State &s, double timestamp, size_t anchor_id, doub
   double const_bias = anchor->val[3], dist_bias = anchor->val[4];
   Mat d = p_AinG - (R_GtoI.T() * (-p_IinU) + p_IinG);
   double dn = norm(d);
-  Mat res(1, 1);
+  res = Mat(1, 1);
   res[0] = range - ((1 + dist_bias) * dn + const_bias);
   Mat H_n = (1.0 / dn) * d.T();
   Mat H_z_I(3, 6);
   H_z_I.set_block(0, 0, R_GtoI.T() * skew_x(-p_IinU));
   H_z_I.set_block(0, 3, -Mat::Identity(3));
-  Mat H_x(1, total_hx);
+  H_x = Mat(1, total_hx);
   H_x.set_block(0, id_I, (1 + dist_bias) * (H_n * H_z_I));
   if (id_cal >= 0) H_x.set_block(0, id_cal, (1 + dist_bias) * (H_n * R_GtoI.T()));
   if (id_anc >= 0) {
     Mat Ha(1, 5);
-    Ha.set_block(0, 0, (1 + dist_bias) * (H_n * R_GtoI.T()));  // reference quirk, kept
+    // reference quirk, kept (UVioUpdaterHelper.cpp:236): the anchor-position block repeats the calibration
+    // block's R_GtoI^T; d(range)/d(p_AinG) is (1 + dist_bias) H_n (tests/test_fd_goldens.py measures the gap)
+    Ha.set_block(0, 0, (1 + dist_bias) * (H_n * R_GtoI.T()));
     Ha[3] = 1;
     Ha[4] = dn;
     H_x.set_block(0, id_anc, Ha);
   }
+}
+
+// UpdaterUWB.cpp:53-90
+int UpdaterUWB::update_single(State &s, double timestamp, size_t anchor_id, double range) {
+  (void)timestamp;
+  auto ait = s.anchors.find(anchor_id);
+  if (ait == s.anchors.end()) return 0;
+  VarP anchor = ait->second;
+  std::vector<Ref> x_order;
+  Mat res, H_x;
+  uwb_jacobian_single(s, anchor, range, res, H_x, x_order);
   double R = sigma_range * sigma_range;
   Mat P_marg = StateHelper::get_marginal_covariance(s, x_order);
   Mat S = H_x * P_marg * H_x.T();

@@ -93,6 +93,8 @@ struct UpdaterSLAM {
   int perform_anchor_change(State &s, VarP landmark, double new_anchor_timestamp, size_t new_cam_id);
 };
 
+void uwb_jacobian_single(State &s, const VarP &anchor, double range, Mat &res, Mat &H_x, std::vector<Ref> &x_order);
+
 struct UpdaterUWB {
   double sigma_range, chi2_mult;
   std::map<int, double> chi_squared_table;
