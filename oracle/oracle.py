@@ -73,6 +73,13 @@ def load():
         lib.orc_lk.argtypes = [u8, u8, i32, i32, i32, i32, i32, C.c_float, f32, f32, u8, i32]
         lib.orc_ransac_mask.argtypes = [f32, f32, f32, f32, i32, C.c_double, C.c_double, i32, u8]
         lib.orc_fundamental_7pt.argtypes = [f64, f64, f64, f64, f64]
+        ip = C.POINTER(C.c_int)
+        lib.orc_probe_boxplus.argtypes = [C.c_void_p, f64, i32]
+        lib.orc_probe_predict.argtypes = [C.c_void_p, f64, f64, f64, f64, i32, ip, ip, ip, i32, ip]
+        lib.orc_probe_uwb.argtypes = [C.c_void_p, C.c_uint64, f64, f64, i32, ip, ip, ip, i32, ip]
+        lib.orc_probe_feature_jacobian.argtypes = [C.c_void_p, i32, i32, ip, f64, f32, f32, f64, f64, i32, C.c_double,
+                                                   f64, f64, f64, i32, ip, ip, ip, i32, ip]
+        lib.orc_probe_triangulate.argtypes = [C.c_void_p, i32, ip, f64, f32, f32, i32, f64, ip, f64]
         _lib = lib
     return _lib
 
@@ -96,6 +103,84 @@ class OracleManager(VioManager):
         if rc != 0:
             raise RuntimeError("orc_%s failed (%d)" % (name, rc))
         return [{"featid": int(f[0]), "used": bool(kept[i]), "to_delete": bool(dele[i])} for i, f in enumerate(features)]
+
+    # ---- probes of single restated routines (oracle/src/probe.cpp; tests/test_fd_goldens.py) ----
+    @staticmethod
+    def _dp(a):
+        return a.ctypes.data_as(C.POINTER(C.c_double))
+
+    @staticmethod
+    def _ip(a):
+        return a.ctypes.data_as(C.POINTER(C.c_int))
+
+    def _check_probe(self, rc, what):
+        if rc != 0:
+            raise RuntimeError("orc_probe_%s failed (%d)" % (what, rc))
+
+    def probe_boxplus(self, dx):
+        """x <- x boxplus dx on every variable (Type::update), dx indexed by covariance id"""
+        dx = np.ascontiguousarray(dx, dtype=np.float64)
+        self._check_probe(self._lib.orc_probe_boxplus(self._h, self._dp(dx), dx.size), "boxplus")
+
+    def probe_predict(self, dm, dp):
+        """Propagator::predict_and_compute on one IMU interval: (F, Qd, [(cov id, size)] of the phi order); the
+        IMU mean is replaced by the prediction.  dm / dp: (t, wm[3], am[3])"""
+        dm = np.ascontiguousarray(dm, dtype=np.float64)
+        dp = np.ascontiguousarray(dp, dtype=np.float64)
+        cap = 64 * 64
+        F, Q = np.zeros(cap), np.zeros(cap)
+        ids, sz = np.zeros(16, np.int32), np.zeros(16, np.int32)
+        n, nv = C.c_int(), C.c_int()
+        self._check_probe(self._lib.orc_probe_predict(self._h, self._dp(dm), self._dp(dp), self._dp(F), self._dp(Q), cap,
+                                                      C.byref(n), self._ip(ids), self._ip(sz), 16, C.byref(nv)), "predict")
+        k = n.value
+        return F[:k * k].reshape(k, k), Q[:k * k].reshape(k, k), list(zip(ids[:nv.value], sz[:nv.value]))
+
+    def probe_uwb(self, anchor_id):
+        """(predicted range, H_x, [(cov id, size)]) of UVioUpdaterHelper::get_uwb_jacobian_single"""
+        H = np.zeros(64)
+        ids, sz = np.zeros(8, np.int32), np.zeros(8, np.int32)
+        pred, nc, nv = C.c_double(), C.c_int(), C.c_int()
+        self._check_probe(self._lib.orc_probe_uwb(self._h, C.c_uint64(int(anchor_id)), C.byref(pred), self._dp(H), 64,
+                                                  C.byref(nc), self._ip(ids), self._ip(sz), 8, C.byref(nv)), "uwb")
+        return pred.value, H[:nc.value].copy(), list(zip(ids[:nv.value], sz[:nv.value]))
+
+    def probe_feature_jacobian(self, rep, cams, times, uv, uvn, lam, uvn0=(0.0, 0.0), anchor_cam=-1, anchor_time=-1.0):
+        """(res, H_f, H_x, [(cov id, size)]) of UpdaterHelper::get_feature_jacobian_full for a landmark with value
+        lam in representation rep"""
+        m = len(cams)
+        cams = np.ascontiguousarray(cams, dtype=np.int32)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        uv = np.ascontiguousarray(uv, dtype=np.float32).reshape(-1)
+        uvn = np.ascontiguousarray(uvn, dtype=np.float32).reshape(-1)
+        lam = np.ascontiguousarray(lam, dtype=np.float64)
+        u0 = np.ascontiguousarray(uvn0, dtype=np.float64)
+        cap = 512
+        res, Hf, Hx = np.zeros(2 * m), np.zeros(2 * m * 3), np.zeros(2 * m * cap)
+        ids, sz = np.zeros(128, np.int32), np.zeros(128, np.int32)
+        nc, nv = C.c_int(), C.c_int()
+        fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+        self._check_probe(self._lib.orc_probe_feature_jacobian(
+            self._h, rep, m, self._ip(cams), self._dp(times), fp(uv), fp(uvn), self._dp(lam), self._dp(u0), anchor_cam,
+            C.c_double(anchor_time), self._dp(res), self._dp(Hf), self._dp(Hx), cap, C.byref(nc), self._ip(ids),
+            self._ip(sz), 128, C.byref(nv)), "feature_jacobian")
+        dim = 1 if rep == 5 else 3
+        return (res, Hf[:2 * m * dim].reshape(2 * m, dim), Hx[:2 * m * nc.value].reshape(2 * m, nc.value),
+                list(zip(ids[:nv.value], sz[:nv.value])))
+
+    def probe_triangulate(self, cams, times, uv, uvn, refine=True):
+        """FeatureInitializer::single_triangulation (+ single_gaussnewton): (ok, p_FinG, p_FinA, anchor cam, time)"""
+        m = len(cams)
+        cams = np.ascontiguousarray(cams, dtype=np.int32)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        uv = np.ascontiguousarray(uv, dtype=np.float32).reshape(-1)
+        uvn = np.ascontiguousarray(uvn, dtype=np.float32).reshape(-1)
+        out = np.zeros(6)
+        ac, at = C.c_int(), C.c_double()
+        fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))  # noqa: E731
+        ok = self._lib.orc_probe_triangulate(self._h, m, self._ip(cams), self._dp(times), fp(uv), fp(uvn),
+                                             1 if refine else 0, self._dp(out), C.byref(ac), C.byref(at))
+        return bool(ok), out[:3].copy(), out[3:].copy(), ac.value, at.value
 
     def feed_measurement_imu_batch(self, t, wm, am):
         for i in range(len(t)):
