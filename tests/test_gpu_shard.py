@@ -1,12 +1,17 @@
-"""Feature-sharded MSCKF update on the GPU.
+"""Feature-sharded MSCKF update on the GPU (UpdaterMSCKF.cpp:118-286).
 
 * world 1 over a real RCCL communicator (ncclCommInitRank with one rank, ncclAllReduce on the library's
-  stream): the sharded update path in lock-step against the oracle, same bounds as test_gpu_parity.py.
-* world 2 on one MI355X (two processes, host all-reduce over gloo, since RCCL needs one GPU per rank):
-  both replicas hold bit-identical states after every frame, each rank linearized only its chunk, and
-  the run agrees with an unsharded run of the same stream (same update sets; final state within 1e-6
-  relative: the Gram sums in a different association, and the filter carries the rounding forward).
+  stream): the sharded update path in lock-step against the oracle, same bounds as test_gpu_parity.py, on a
+  EuRoC stream and at the BASELINE sizes it exists for (bench.py cfg4: 800 MSCKF features x 52 measurements,
+  cfg5: 1500 features, IMU intrinsics, UWB), where the tiled T GEMM (m >= 4096), the MFMA Gram (m >= 8192),
+  the chunked batch build (>= 256 features) and the n > 135 information-form factors run.
+* world 2 and 4 on one MI355X at cfg4 / cfg5 (one fresh process per rank, host all-reduce over gloo, since
+  RCCL needs one GPU per rank): EVERY rank runs its own oracle in lock-step at the strict bounds (its MSCKF
+  per-feature results are its shard of the oracle's), the replicas' states and covariances are bit-identical
+  after every frame, and the shards are disjoint and together make up the oracle's update.
+* world 2 on the EuRoC stream: the sharded run agrees with an unsharded run of the same stream.
 """
+import hashlib
 import os
 import socket
 
@@ -14,7 +19,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from test_gpu_parity import _check_lockstep, _rel, _snap, run_lockstep
+from test_gpu_parity import _check_lockstep, _features_updated, _rel, _snap, _steer_cap, run_lockstep
 
 pytestmark = pytest.mark.gpu
 
@@ -114,3 +119,122 @@ def test_sharded_world2_gloo_one_gpu():
     for (x, _, nm, rows, _), (xr, tr) in zip(f0, ref):
         assert nm == tr["n_msckf"]
     assert _rel(f0[-1][0], ref[-1][0]) < 1e-6
+
+
+# ---- BASELINE sizes (bench.py cfg4 / cfg5 TrackSIM streams) ----
+BIG = {"cfg4": 30, "cfg5": 35}
+
+
+def _bench():
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def _big(wl):
+    import uvio_amd as U
+    B = _bench()
+    opts = B.workload_options(U, wl)
+    n = BIG[wl]
+    return opts, B.make_stream(opts, n + 2, seed=5, workload=wl), n
+
+
+def _assert_big(steps, wl):
+    assert max(a["timing"]["n_msckf"] for a, _ in steps) == {"cfg4": 800, "cfg5": 1500}[wl]
+    assert max(a["timing"]["msckf_rows"] for a, _ in steps) >= 8192
+
+
+@pytest.mark.parametrize("wl", ["cfg4", "cfg5"])
+def test_sharded_world1_rccl_lockstep_baseline_size(wl):
+    import uvio_amd as U
+    from uvio_amd.manager import shard_unique_id
+    opts, s, n = _big(wl)
+    g = U.VioManager(opts)
+    g.enable_feature_sharding(0, 1, backend="rccl", unique_id=shard_unique_id(), min_features=1)
+    steps = run_lockstep(opts, s, n, mgr=g)
+    g.close()
+    _assert_big(steps, wl)
+    _check_lockstep(steps)
+
+
+def _digest(a):
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _rank_lockstep(rank, world, port, q, wl):
+    """one rank of a feature-sharded run over gloo, in lock-step with its own oracle"""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"rank": rank, "err": None}
+    try:
+        import uvio_amd as U
+        opts, s, n = _big(wl)
+        g = U.VioManager(opts, device=0)
+        g.enable_feature_sharding(rank, world, backend="host", min_features=1)
+        steps = run_lockstep(opts, s, n, mgr=g)
+        g.close()
+        out["frames"] = [(_digest(a["x"]), _digest(a["P"]), a["timing"]["n_msckf"], a["timing"]["msckf_rows"],
+                          sorted(int(i) for i in a["feats"][0]), sorted(int(i) for i in b["feats"][0]))
+                         for a, b in steps]
+        out["steer"] = list(steps.steer)
+        out["n_features"] = _features_updated(steps)
+        try:
+            out["worst"] = _check_lockstep(steps, max_events=None, sharded=True)
+        except AssertionError as e:
+            out["err"] = repr(e)[:4000]
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        out["err"] = "exception: " + repr(e)[:4000]
+    q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wl,world", [("cfg4", 2), ("cfg4", 4), ("cfg5", 2), ("cfg5", 4)])
+def test_sharded_gloo_lockstep_baseline_size(wl, world):
+    from conftest import record_steer
+    from test_gpu_parity import STEER_MARGIN
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_lockstep, args=(r, world, port, q, wl)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=280) for _ in range(world)], key=lambda o: o["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for o in outs:
+        assert o["err"] is None, (o["rank"], o["err"])
+    n = BIG[wl]
+    f0 = outs[0]["frames"]
+    assert all(len(o["frames"]) == n for o in outs)
+    assert max(fr[2] for fr in f0) == {"cfg4": 800, "cfg5": 1500}[wl]
+    assert max(fr[3] for fr in f0) >= 8192
+    per_rank = [0] * world
+    for k in range(n):
+        frs = [o["frames"][k] for o in outs]
+        # replicas: bit-identical state and covariance, same update set and accepted rows
+        assert len({(fr[0], fr[1], fr[2], fr[3]) for fr in frs}) == 1, ("replicas diverged", k)
+        # the shards: disjoint, and together the oracle's MSCKF update (every rank's oracle saw the same one)
+        union = []
+        for r, fr in enumerate(frs):
+            union += fr[4]
+            per_rank[r] += len(fr[4])
+        assert len(union) == len(set(union)), ("shards overlap", k)
+        assert sorted(union) == frs[0][5] and all(fr[5] == frs[0][5] for fr in frs), ("shards != update", k)
+    assert min(per_rank) > 0, per_rank
+    # the oracles' rounding-tie steering: every event one near tie, at most 1 % of the features updated
+    ev = [e for o in outs for e in o["steer"]]
+    nf = sum(o["n_features"] for o in outs)
+    cap = _steer_cap(nf)
+    record_steer(ev, nf, cap)
+    assert all(e["found"] and e["margin"] < STEER_MARGIN for e in ev), ev
+    assert len(ev) <= cap, (len(ev), cap)
+    print("worst per rank", [o["worst"] for o in outs])
