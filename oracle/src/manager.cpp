@@ -116,7 +116,7 @@ int Manager::do_uwb_propagate_update(const UwbMsg &m) {
     }
   if (!valid) return 0;
   if (!prop.propagate_uwb(state, m.t)) return 0;
-  if (state.timestamp != m.t) return 0;
+  if (state.timestamp != (prop.experiment_uwb_dt ? m.t - state.calib_dt->val[0] : m.t)) return 0;
   for (auto &r : m.ranges) {
     if (state.anchors.find(r.first) != state.anchors.end()) {
       int rc = uwb.update_single(state, m.t, r.first, r.second);
@@ -201,7 +201,9 @@ int Manager::after_tracking(double t, const std::vector<int> &camids, clk::time_
   }
   if (!past_uwb.empty()) {
     for (auto it = past_uwb.begin(); it != past_uwb.lower_bound(t); it++) {
-      if (it->first < t && it->first > state.timestamp) {
+      // (experiment, see Propagator::propagate_uwb: compare on the camera clock)
+      const double tu = prop.experiment_uwb_dt ? it->first - state.calib_dt->val[0] : it->first;
+      if (tu < t && tu > state.timestamp) {
         int rc = do_uwb_propagate_update(it->second);
         if (rc < 0) return rc;
       }

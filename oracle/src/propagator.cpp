@@ -1,12 +1,17 @@
 // ORACLE — test infrastructure only (see la.h header).
 #include "propagator.h"
 
+#include <cstdlib>
+
 #include <cstdio>
 
 namespace orc {
 
 Propagator::Propagator(const uvio_hp_options_t &o)
-    : sigma_w(o.sigma_w), sigma_a(o.sigma_a), sigma_wb(o.sigma_wb), sigma_ab(o.sigma_ab), gravity(V3(0, 0, o.gravity_mag)) {}
+    : sigma_w(o.sigma_w), sigma_a(o.sigma_a), sigma_wb(o.sigma_wb), sigma_ab(o.sigma_ab), gravity(V3(0, 0, o.gravity_mag)) {
+  const char *e = std::getenv("ORC_EXPERIMENT_UWB_DT");
+  experiment_uwb_dt = e && e[0] == '1';
+}
 
 // Propagator.h:65-91
 void Propagator::feed_imu(const ImuData &m, double oldest_time) {
@@ -146,7 +151,7 @@ bool Propagator::propagate_and_clone(State &s, double timestamp, int *status) {
 // UVioPropagator.cpp:27-115 (quirks kept: time1 ignores the cam-imu offset and
 // last_prop_time_offset is not updated)
 bool Propagator::propagate_uwb(State &s, double timestamp) {
-  if (s.timestamp >= timestamp) return false;
+  if (s.timestamp >= (experiment_uwb_dt ? timestamp - s.calib_dt->val[0] : timestamp)) return false;
   double time0 = s.timestamp + last_prop_time_offset;
   double time1 = timestamp;
   std::vector<ImuData> prop = select_imu_readings(imu_data, time0, time1);
@@ -155,6 +160,14 @@ bool Propagator::propagate_uwb(State &s, double timestamp) {
   std::vector<Ref> order = phi_order(s);
   if (!StateHelper::EKFPropagation(s, order, order, Phi, Qd)) return false;
   s.timestamp = timestamp;
+  // EXPERIMENT ONLY, off by default (the cfg5 ATE study): keep the state on the camera clock as
+  // propagate_and_clone does (the IMU is now at timestamp = camera time + dt), instead of the reference's
+  // IMU-clock timestamp that the next propagation then offsets by dt once more
+  if (experiment_uwb_dt) {
+    s.timestamp = timestamp - s.calib_dt->val[0];
+    last_prop_time_offset = s.calib_dt->val[0];
+    have_last_prop_time_offset = true;
+  }
   return true;
 }
 

@@ -20,6 +20,8 @@ struct Propagator {
   Mat gravity;  // (0,0,g)
   std::vector<ImuData> imu_data;
   bool have_last_prop_time_offset = false;
+  // ORC_EXPERIMENT_UWB_DT=1: not the reference (see propagate_uwb); the cfg5 ATE study only
+  bool experiment_uwb_dt = false;
   double last_prop_time_offset = 0.0;
 
   explicit Propagator(const uvio_hp_options_t &o);
