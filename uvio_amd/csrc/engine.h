@@ -353,6 +353,9 @@ class Engine {
   // VioManager::thread_init_success (VioManager.h:226): the initializer succeeded on an earlier frame; the
   // manager reports initialized only on the next camera frame (VioManagerHelper.cpp:91-93, 187)
   bool init_success_ = false;
+  // inside feed_camera (the update chain then runs the tracker's next detection ahead, Tracker::predetect);
+  // UVIO_HP_NO_PREDETECT=1 turns that off (A/B runs)
+  bool camera_frame_ = false, predetect_on_ = true;
   double startup_time_ = -1, distance_ = 0, timelastupdate_ = -1;
   bool anchors_initialized_ = false;
   std::map<double, std::unordered_map<size_t, double>> past_uwb_;

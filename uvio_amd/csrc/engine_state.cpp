@@ -348,6 +348,7 @@ void Engine::alloc_device() {
   d_.stg_cap = d_.pin_bytes + 2 * 64 * 64 * sizeof(double) + 64 * 1024;
   // test hook: a smaller ring recycles every few batches (tests/test_gpu_configs.py staging test)
   if (const char *e = std::getenv("UVIO_HP_STAGE_BYTES")) d_.stg_cap = std::min(d_.stg_cap, (size_t)std::atoll(e));
+  if (const char *e = std::getenv("UVIO_HP_NO_PREDETECT")) predetect_on_ = e[0] != '1';
   HP_HIP(hipHostMalloc(&d_.stg_h, d_.stg_cap, hipHostMallocDefault));
   HP_HIP(hipMalloc(&d_.stg_d, d_.stg_cap));
 }

@@ -121,7 +121,7 @@ size_t span(const void *a, const void *b_end) { return (size_t)((const char *)b_
 }  // namespace
 
 Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t s, KProf *kp)
-    : cams_(cams), s_(s), kp_(kp) {
+    : cams_(cams), s_(s), kp_(kp), cur_(s) {
   downsample_ = o.downsample_cameras != 0;
   // TrackKLT construction in VioManager.cpp:98-107: num_pts per camera = init_max_features / ncam
   num_features_ = (int)std::floor((double)o.init_max_features / (double)o.num_cameras);
@@ -161,6 +161,7 @@ Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t 
 
 void Tracker::set_num_features(int n) {
   if (n <= 0) throw HpError(UVIO_HP_E_CONFIG, "tracker: num features must be positive");
+  discard_predetect();  // made with the previous count
   num_features_ = n;
   int gx = grid_x_, gy = grid_y_;
   if (num_features_ < gx * gy) {
@@ -197,6 +198,11 @@ Tracker::~Tracker() {
   if (ev_match_) (void)hipEventDestroy(ev_match_);
   if (ev_up_) (void)hipEventDestroy(ev_up_);
   if (up_) (void)hipStreamDestroy(up_);
+  if (ev_pyr_) (void)hipEventDestroy(ev_pyr_);
+  if (sd_) {
+    (void)hipStreamSynchronize(sd_);
+    (void)hipStreamDestroy(sd_);
+  }
   if (b_) {
     if (b_->dmem) (void)hipFree(b_->dmem);
     if (b_->hmem) (void)hipHostFree(b_->hmem);
@@ -207,6 +213,10 @@ Tracker::~Tracker() {
 // The tracker's device buffers an upload writes are read only by this frame's later launches: the previous
 // frame's users of them finished before its results were read back.
 void Tracker::upload(void *dst, const void *src, size_t bytes) {
+  if (cur_ != s_) {  // predetect: its own stream, nothing queued on it to overlap
+    HP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cur_));
+    return;
+  }
   if (!up_) {
     HP_HIP(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking));
     HP_HIP(hipEventCreateWithFlags(&ev_up_, hipEventDisableTiming));
@@ -222,15 +232,23 @@ void Tracker::upload(void *dst, const void *src, size_t bytes) {
 
 void Tracker::sync() {
   auto t0 = std::chrono::steady_clock::now();
-  spin_sync(s_);
-  sync_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  device_syncs++;
+  spin_sync(cur_);
+  const double w = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (pre_mode_) {
+    pre_wait += w;
+    pre_syncs++;
+  } else {
+    sync_wait += w;
+    device_syncs++;
+  }
 }
 
 void Tracker::ensure_cap(int n) {
   Bufs &b = *b_;
   if (n <= b.cap) return;
   if (b.dmem) {
+    if (sd_) spin_sync(sd_);
+    if (cur_ != s_) spin_sync(s_);  // predetect: the frame's updates hold no tracker buffer, but wait anyway
     sync();
     HP_HIP(hipFree(b.dmem));
     HP_HIP(hipHostFree(b.hmem));
@@ -346,6 +364,7 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
   in_flight_ = std::move(in_flight);
   device_syncs = 0;
   sync_wait = 0.0;
+  if (pre_.valid && pre_.cams != std::vector<int>(cam_ids, cam_ids + ncam)) discard_predetect();
   if (histogram_method_ == 2)
     throw HpError(UVIO_HP_E_CONFIG, "histogram_method 2 (CLAHE) is not implemented by the KLT front-end");
   if (ncam > kMaxCams) throw HpError(UVIO_HP_E_ARG, "too many cameras in one feed");
@@ -413,6 +432,8 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
       KScope ks(kp_, KC_PYR);
       launch_pyramids(s_, job);
     }
+    if (!ev_pyr_) HP_HIP(hipEventCreateWithFlags(&ev_pyr_, hipEventDisableTiming));
+    HP_HIP(hipEventRecord(ev_pyr_, s_));
     if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
   };
   if (ncam == 2 && use_stereo_) {
@@ -432,7 +453,10 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
     c.have_last = true;
     c.mask_last.swap(c.mask_new);
   }
+  last_cams_.assign(cam_ids, cam_ids + ncam);
+  pre_.valid = false;  // consumed by this feed (or not made for it)
 }
+
 
 // ---------------------------------------------------------------- detection
 // Grider_GRID::perform_griding + cornerSubPix for the requests of several cameras at once: the FAST
@@ -478,8 +502,8 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
   if (nc == 0) return;
   fj.ncam = nf;
   upload(b.cells, b.hp(b.cells), 2 * nc * sizeof(int));
-  launch_fast_multi(s_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
-  HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, s_));
+  launch_fast_multi(cur_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
+  HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, cur_));
   sync();
   const int *h_fastn = b.hp(b.fastn);
   const float *h_fast = b.hp(b.fast);
@@ -520,7 +544,7 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     sj.ncam++;
   }
   upload(b.det, h_det, 2 * np * sizeof(float));
-  launch_subpix_multi(s_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
+  launch_subpix_multi(cur_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
   const bool do_lk = lk_to && nr == 1;
   if (do_lk) {
     LkSlots lk{};
@@ -530,14 +554,15 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     lk.p1[0] = b.det1;
     lk.st[0] = b.detst;
     lk.n[0] = np;
-    lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
+    // the kernel-class timing brackets the library stream only: a predetect's LK is not timed (nor counted)
+    lk.bytes = (kp_ && kp_->on && !pre_mode_) ? d_lk_bytes_ : nullptr;
     {
-      KScope ks(kp_, KC_LK);
-      launch_lk(s_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
+      KScope ks(pre_mode_ ? nullptr : kp_, KC_LK);
+      launch_lk(cur_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
     }
-    HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + np), hipMemcpyDeviceToHost, s_));
+    HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + np), hipMemcpyDeviceToHost, cur_));
   } else {
-    HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * np * sizeof(float), hipMemcpyDeviceToHost, s_));
+    HP_HIP(hipMemcpyAsync(h_det, b.det, 2 * np * sizeof(float), hipMemcpyDeviceToHost, cur_));
   }
   sync();
   int at = 0;
@@ -945,7 +970,15 @@ void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
   }
   for (int k = 0; k < n; k++)
     if (first[k]) ensure_pyr();  // detection on this frame's images
-  detect_mono_multi(det.data(), n);
+  if (pre_.valid) {  // run ahead by predetect (every camera had tracks, so none is first)
+    for (int k = 0; k < n; k++) {
+      det[k].pts.swap(pre_.pts[k]);
+      det[k].ids.swap(pre_.ids[k]);
+    }
+    pre_.valid = false;
+  } else {
+    detect_mono_multi(det.data(), n);
+  }
   std::vector<MatchJob> jobs;
   std::vector<int> who;
   size_t most = 0;
@@ -1018,9 +1051,19 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
     B.ids_last = ir;
     return;
   }
-  std::vector<KeyPt> pl_old = A.pts_last, pr_old = B.pts_last;
-  std::vector<size_t> il_old = A.ids_last, ir_old = B.ids_last;
-  {
+  std::vector<KeyPt> pl_old, pr_old;
+  std::vector<size_t> il_old, ir_old;
+  if (pre_.valid) {  // run ahead by predetect
+    pl_old.swap(pre_.pts[0]);
+    pr_old.swap(pre_.pts[1]);
+    il_old.swap(pre_.ids[0]);
+    ir_old.swap(pre_.ids[1]);
+    pre_.valid = false;
+  } else {
+    pl_old = A.pts_last;
+    pr_old = B.pts_last;
+    il_old = A.ids_last;
+    ir_old = B.ids_last;
     HostProfScope hs(*hp_, "trk.detect");
     detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
   }
@@ -1097,6 +1140,65 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   B.pts_last.swap(gr);
   A.ids_last.swap(gil);
   B.ids_last.swap(gir);
+}
+
+// The next feed's perform_detection_* on the last pyramids / points / masks (see tracker.h), on the detection
+// stream.  Only when every camera of the last feed has tracks: a camera without tracks detects on the NEW
+// frame's pyramid (TrackKLT.cpp:104-110, 215-222), which does not exist yet.
+void Tracker::predetect() {
+  pre_syncs = 0;
+  pre_wait = 0.0;
+  if (pre_.valid || last_cams_.empty()) return;
+  const int n = (int)last_cams_.size();
+  const bool stereo = n == 2 && use_stereo_;
+  if (stereo) {
+    if (cs_[last_cams_[0]].pts_last.empty() && cs_[last_cams_[1]].pts_last.empty()) return;
+  } else {
+    for (int c : last_cams_)
+      if (cs_[c].pts_last.empty()) return;
+  }
+  if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+  if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
+  pre_.currid0 = currid;
+  pre_.cams = last_cams_;
+  pre_.pts.assign(n, {});
+  pre_.ids.assign(n, {});
+  cur_ = sd_;
+  pre_mode_ = true;
+  try {
+    if (stereo) {
+      CamState &A = cs_[last_cams_[0]], &B = cs_[last_cams_[1]];
+      pre_.pts[0] = A.pts_last;
+      pre_.pts[1] = B.pts_last;
+      pre_.ids[0] = A.ids_last;
+      pre_.ids[1] = B.ids_last;
+      detect_stereo(last_cams_[0], last_cams_[1], A.pyr[A.last], B.pyr[B.last], A.mask_last, B.mask_last, pre_.pts[0],
+                    pre_.pts[1], pre_.ids[0], pre_.ids[1]);
+    } else {
+      std::vector<MonoDet> det(n);
+      for (int k = 0; k < n; k++) {
+        CamState &c = cs_[last_cams_[k]];
+        det[k].cam = last_cams_[k];
+        det[k].p = &c.pyr[c.last];
+        det[k].mask = &c.mask_last;
+        det[k].pts = c.pts_last;
+        det[k].ids = c.ids_last;
+      }
+      detect_mono_multi(det.data(), n);
+      for (int k = 0; k < n; k++) {
+        pre_.pts[k].swap(det[k].pts);
+        pre_.ids[k].swap(det[k].ids);
+      }
+    }
+  } catch (...) {
+    cur_ = s_;
+    pre_mode_ = false;
+    currid = pre_.currid0;
+    throw;
+  }
+  cur_ = s_;
+  pre_mode_ = false;
+  pre_.valid = true;
 }
 
 // ---------------------------------------------------------------- inspection

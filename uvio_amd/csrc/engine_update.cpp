@@ -295,6 +295,11 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
   }
   if (early_exc) std::rethrow_exception(early_exc);
   if (early && early_rc) return early_rc;
+  struct FrameFlag {
+    bool &f;
+    explicit FrameFlag(bool &x) : f(x) { f = true; }
+    ~FrameFlag() { f = false; }
+  } in_camera_frame(camera_frame_);
   return after_tracking(t, camids, rT1, tracker_->device_syncs, tracker_->sync_wait, true);
 }
 

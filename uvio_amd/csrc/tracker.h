@@ -51,6 +51,15 @@ class Tracker {
   double sync_wait = 0.0;   // seconds blocked in them
   // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand
   unsigned long long lk_bytes();
+  // The next feed's detection, run ahead.  TrackKLT::perform_detection_{monocular,stereo} reads only the
+  // previous frame's pyramid, points, ids and mask (TrackKLT.cpp:130, 249: img_pyramid_last, pts_last,
+  // ids_last, img_mask_last), so it can run as soon as a feed has ended -- on its own stream, while the device
+  // works on that frame's updates (Engine::update_frame calls it before its wait).  The next feed uses the
+  // result when it has the same cameras; otherwise, or after set_num_features, the result is discarded and
+  // currid restored, so ids and points are always those of the serial order.
+  void predetect();
+  int pre_syncs = 0;        // host waits / seconds of the last predetect
+  double pre_wait = 0.0;
 
  private:
   struct CamState {
@@ -110,6 +119,23 @@ class Tracker {
   void alloc_pyr(CamState &c, int w, int h);
   void ensure_cap(int n);
   void sync();
+  // detection stream state: the detection functions launch on cur_ (s_, or sd_ while predetect runs)
+  hipStream_t sd_ = nullptr, cur_ = nullptr;
+  hipEvent_t ev_pyr_ = nullptr;  // after the last pyramid launch on s_ (predetect reads that pyramid)
+  bool pre_mode_ = false;
+  struct PreDet {
+    bool valid = false;
+    std::vector<int> cams;
+    size_t currid0 = 0;
+    std::vector<std::vector<KeyPt>> pts;
+    std::vector<std::vector<size_t>> ids;
+  };
+  PreDet pre_;
+  std::vector<int> last_cams_;
+  void discard_predetect() {
+    if (pre_.valid) currid = pre_.currid0;
+    pre_.valid = false;
+  }
   const std::vector<int> &subsets(int count);
 
   // one Grider_GRID request: camera, pyramid, user mask, min-distance boxes, cells to fill -> corners
