@@ -2,6 +2,7 @@
 
 * ``uvio_amd/libuvio_hp.so`` — the product: host orchestration (C++) + gfx950 HIP kernels, C ABI
   declared in ``include/uvio_hp.h``.  Compiled with hipcc --offload-arch=gfx950 only.
+* ``uvio_amd/uvio_run_asl`` — the ROS-free serial runner over ASL dataset folders (a C-ABI caller).
 * ``oracle/build/liboracle.so`` — the CPU restatement used as the parity checker (test infrastructure).
 
 Usage: ``python -m uvio_amd.build`` (or ``__graft_entry__.build()``).
@@ -76,6 +77,22 @@ def build_product(force=False, verbose=False):
     return LIB
 
 
+RUNNER = os.path.join(ROOT, "uvio_amd", "uvio_run_asl")
+
+
+def build_runner(force=False):
+    """uvio_amd/uvio_run_asl: the ROS-free serial runner over ASL dataset folders (csrc/run_asl.cpp), a plain
+    C++ caller of the C ABI (g++, libuvio_hp.so found next to it, zlib for the PNGs)"""
+    src = os.path.join(CSRC, "run_asl.cpp")
+    deps = [src, os.path.join(ROOT, "include", "uvio_hp.h"), LIB]
+    if not force and not _newer(RUNNER, deps):
+        return RUNNER
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), src, "-o", RUNNER,
+           "-L", os.path.dirname(LIB), "-luvio_hp", "-Wl,-rpath,$ORIGIN", "-lz"]
+    subprocess.check_call(cmd)
+    return RUNNER
+
+
 def build_oracle():
     odir = os.path.join(ROOT, "oracle")
     subprocess.check_call(["make", "-s", "-C", odir])
@@ -84,8 +101,9 @@ def build_oracle():
 
 def build_all(force=False, verbose=False):
     lib = build_product(force=force, verbose=verbose)
+    run = build_runner(force=force)
     orc = build_oracle()
-    return lib, orc
+    return lib, run, orc
 
 
 if __name__ == "__main__":
