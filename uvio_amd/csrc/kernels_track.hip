@@ -17,6 +17,13 @@
 
 namespace uvhp {
 
+// The dispatcher deals workgroups round robin to the 8 XCDs, each with its own L2: workgroup w of nwg is
+// given the index that puts a contiguous range of indices on each XCD (a bijection on [0, nwg))
+__device__ __forceinline__ int xcd_contiguous(int w, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = w % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + w / 8;
+}
+
 __device__ __forceinline__ int reflect101(int p, int n) {
   if (n == 1) return 0;
   while (p < 0 || p >= n) p = (p < 0) ? -p : 2 * n - 2 - p;
@@ -98,15 +105,18 @@ __global__ void __launch_bounds__(256) k_pyr_pair(PyrJob job, int l) {
   __shared__ uint8_t win[T::WH * T::WW];
   __shared__ uint8_t q[(T::QH + 2) * (T::QW + 2)];
   __shared__ uint8_t srcs[EQ ? 1 : T::SH * T::SW];
-  const int c = blockIdx.z, t = threadIdx.x;
+  // tiles of one camera in raster order, a contiguous range of them per XCD (neighbouring tiles share their
+  // margin rows / columns through that XCD's L2)
+  const int idx = xcd_contiguous(blockIdx.x + blockIdx.z * gridDim.x, gridDim.x * gridDim.z);
+  const int c = idx / gridDim.x, tile = idx - c * gridDim.x, t = threadIdx.x;
   // the levels 2-3 launch runs after level 0's has read the histogram: it clears it for the next frame (the
   // tracker zeroes it once at allocation), which saves a fill per camera and frame
-  if (!EQ && l == 2 && job.equalize && blockIdx.x == 0) job.hist[c][t] = 0u;
+  if (!EQ && l == 2 && job.equalize && tile == 0) job.hist[c][t] = 0u;
   const DPyr &p = job.p[c];
   if (l >= p.levels) return;
   const int w = p.w[l], h = p.h[l];
   const int ntx = (w + PW - 1) / PW;
-  const int x0 = (blockIdx.x % ntx) * PW, y0 = (blockIdx.x / ntx) * PH;
+  const int x0 = (tile % ntx) * PW, y0 = (tile / ntx) * PH;
   if (y0 >= h) return;
   if constexpr (EQ) {
     // LUT of EqualizeHistLut_Invoker from an inclusive LDS scan of the counts (blockDim == 256)
@@ -632,7 +642,7 @@ __global__ void __launch_bounds__(64) k_subpix(SubpixJob job, float *__restrict_
   __shared__ double sums[5];
   __shared__ float cur[2];
   __shared__ int done;
-  const int p = blockIdx.x, lane = threadIdx.x;
+  const int p = xcd_contiguous(blockIdx.x, gridDim.x), lane = threadIdx.x;  // neighbouring corners on one XCD
   int cam = 0;
   while (cam < job.ncam - 1 && p >= job.end[cam]) cam++;
   if (p >= job.end[cam]) return;
@@ -1030,15 +1040,18 @@ __device__ __forceinline__ float2 lk_point(const DPyr &prev, const DPyr &next, c
   return make_float2(qx, qy);  // the result every lane holds (wave-uniform)
 }
 
-// point blockIdx.x of slot blockIdx.y (both cameras' temporal tracks in one launch)
+// one point of one slot per workgroup (both cameras' temporal tracks in one launch).  Consecutive points (the
+// tracker's order: grid cells, so image neighbours) go to one XCD, whose L2 then serves their overlapping
+// windows and pyramid rows once instead of once per XCD
 __global__ void __launch_bounds__(64) k_lk(LkSlots job, int win, int max_level, int max_iters, float crit_eps,
                                            int init_from_p0) {
-  const int slot = blockIdx.y;
-  if ((int)blockIdx.x >= job.n[slot]) return;
-  const float2 q = lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], blockIdx.x, win,
+  const int idx = xcd_contiguous(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int slot = idx / gridDim.x, p = idx - slot * gridDim.x;
+  if (p >= job.n[slot]) return;
+  const float2 q = lk_point(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], p, win,
                             max_level, max_iters, crit_eps, init_from_p0, job.bytes);
   if (job.undistort && threadIdx.x < 2) {  // RANSAC's undistortion of this point, the k_undistort formula
-    const int p = blockIdx.x, w = threadIdx.x;
+    const int w = threadIdx.x;
     const float px = w ? q.x : job.p0[slot][2 * p], py = w ? q.y : job.p0[slot][2 * p + 1];
     float x, y;
     cam_undistort_f(w ? job.c1[slot] : job.c0[slot], px, py, x, y);
