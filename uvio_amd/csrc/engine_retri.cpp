@@ -91,11 +91,17 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
         o.featid = ids[i];
         o.u = pts[i].x;
         o.v = pts[i].y;
-        cam_undistort_f(cams_[cam], o.u, o.v, o.un, o.vn);
         o.cam = cam;
         frame_obs_.push_back(o);
       }
     }
+    // undistort_cv with the camera models as of now (independent per point: on the pool)
+    pool_.parallel_for(frame_obs_.size(), 128, [&](size_t b, size_t e) {
+      for (size_t k = b; k < e; k++) {
+        DRetriObs &o = frame_obs_[k];
+        cam_undistort_f(cams_[o.cam], o.u, o.v, o.un, o.vn);
+      }
+    });
   } else if (o_.do_calib_camera_intrinsics) {
     // undistort_cv with the camera models as of now: this frame's updates may have moved the intrinsics
     // since the feed undistorted the same pixels for the database (StateHelper.cpp:190-195)

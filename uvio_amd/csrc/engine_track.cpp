@@ -1025,11 +1025,15 @@ void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
         gsrc.push_back((int)i);
       }
     }
-    for (size_t i = 0; i < good.size(); i++) {
-      float un, vn;
-      tracked_undistort((int)j, gsrc[i], cam, good[i], un, vn);
-      db(gid[i], t, cam, good[i].x, good[i].y, un, vn);
-    }
+    std::vector<float> nu(2 * good.size());
+    auto undist = [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) tracked_undistort((int)j, gsrc[i], cam, good[i], nu[2 * i], nu[2 * i + 1]);
+    };
+    if (pool_)
+      pool_->parallel_for(good.size(), 128, undist);
+    else
+      undist(0, good.size());
+    for (size_t i = 0; i < good.size(); i++) db(gid[i], t, cam, good[i].x, good[i].y, nu[2 * i], nu[2 * i + 1]);
     c.pts_last.swap(good);
     c.ids_last.swap(gid);
   }
@@ -1126,16 +1130,22 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
       in_gir.emplace(ir_old[i], 0);
     }
   }
-  for (size_t i = 0; i < gl.size(); i++) {
-    float un, vn;
-    tracked_undistort(0, sl[i], cl, gl[i], un, vn);
-    db(gil[i], t, cl, gl[i].x, gl[i].y, un, vn);
-  }
-  for (size_t i = 0; i < gr.size(); i++) {
-    float un, vn;
-    tracked_undistort(1, sr[i], cr, gr[i], un, vn);
-    db(gir[i], t, cr, gr[i].x, gr[i].y, un, vn);
-  }
+  // the undistortions are independent per point (on the pool); the database inserts keep their order
+  std::vector<float> uvl(2 * gl.size()), uvr(2 * gr.size());
+  auto undist = [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; i++) {
+      if (i < gl.size())
+        tracked_undistort(0, sl[i], cl, gl[i], uvl[2 * i], uvl[2 * i + 1]);
+      else
+        tracked_undistort(1, sr[i - gl.size()], cr, gr[i - gl.size()], uvr[2 * (i - gl.size())], uvr[2 * (i - gl.size()) + 1]);
+    }
+  };
+  if (pool_)
+    pool_->parallel_for(gl.size() + gr.size(), 128, undist);
+  else
+    undist(0, gl.size() + gr.size());
+  for (size_t i = 0; i < gl.size(); i++) db(gil[i], t, cl, gl[i].x, gl[i].y, uvl[2 * i], uvl[2 * i + 1]);
+  for (size_t i = 0; i < gr.size(); i++) db(gir[i], t, cr, gr[i].x, gr[i].y, uvr[2 * i], uvr[2 * i + 1]);
   A.pts_last.swap(gl);
   B.pts_last.swap(gr);
   A.ids_last.swap(gil);
