@@ -507,12 +507,10 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     if (fo > 0) HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * fo, hipMemcpyDeviceToHost, d_.stream));
     d_.fout_pending = 0;
     // the next frame's detection (Tracker::predetect) while the device runs this chain: it reads only this
-    // frame's tracker results, on the tracker's detection stream
+    // frame's tracker results; on the tracker's detection stream and worker thread, joined by the next feed
     if (camera_frame_ && predetect_on_ && tracker_) {
       HPROF("chain.predetect");
-      tracker_->predetect();
-      timing_.device_syncs += tracker_->pre_syncs;
-      timing_.sync_wait += tracker_->pre_wait;
+      tracker_->predetect_async();
     }
     dev_sync();
   }

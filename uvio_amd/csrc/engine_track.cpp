@@ -161,6 +161,7 @@ Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t 
 
 void Tracker::set_num_features(int n) {
   if (n <= 0) throw HpError(UVIO_HP_E_CONFIG, "tracker: num features must be positive");
+  predetect_join();
   discard_predetect();  // made with the previous count
   num_features_ = n;
   int gx = grid_x_, gy = grid_y_;
@@ -179,6 +180,7 @@ void Tracker::set_num_features(int n) {
 }
 
 unsigned long long Tracker::lk_bytes() {
+  predetect_join();
   unsigned long long v = 0;
   HP_HIP(hipMemcpyAsync(&v, d_lk_bytes_, sizeof(v), hipMemcpyDeviceToHost, s_));
   HP_HIP(hipStreamSynchronize(s_));
@@ -186,6 +188,15 @@ unsigned long long Tracker::lk_bytes() {
 }
 
 Tracker::~Tracker() {
+  if (worker_.joinable()) {
+    {
+      std::unique_lock<std::mutex> lk(wm_);
+      wcv_.wait(lk, [&] { return !w_task_ && !w_busy_; });
+      w_quit_ = true;
+    }
+    wcv_.notify_all();
+    worker_.join();
+  }
   for (auto &kv : cs_) {
     for (int k = 0; k < 2; k++)
       if (kv.second.pyr_mem[k]) (void)hipFree(kv.second.pyr_mem[k]);
@@ -361,6 +372,7 @@ const std::vector<int> &Tracker::subsets(int count) {
 void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
                    const uint8_t *const *masks, bool device_imgs, const DbSink &db,
                    std::function<void()> in_flight) {
+  predetect_join();
   in_flight_ = std::move(in_flight);
   device_syncs = 0;
   sync_wait = 0.0;
@@ -1161,11 +1173,12 @@ void Tracker::predetect() {
   if (pre_.valid || last_cams_.empty()) return;
   const int n = (int)last_cams_.size();
   const bool stereo = n == 2 && use_stereo_;
+  // cs_.at: the engine's thread may read the map (last_tracks) while this runs on the worker
   if (stereo) {
-    if (cs_[last_cams_[0]].pts_last.empty() && cs_[last_cams_[1]].pts_last.empty()) return;
+    if (cs_.at(last_cams_[0]).pts_last.empty() && cs_.at(last_cams_[1]).pts_last.empty()) return;
   } else {
     for (int c : last_cams_)
-      if (cs_[c].pts_last.empty()) return;
+      if (cs_.at(c).pts_last.empty()) return;
   }
   if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
   if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
@@ -1177,7 +1190,7 @@ void Tracker::predetect() {
   pre_mode_ = true;
   try {
     if (stereo) {
-      CamState &A = cs_[last_cams_[0]], &B = cs_[last_cams_[1]];
+      CamState &A = cs_.at(last_cams_[0]), &B = cs_.at(last_cams_[1]);
       pre_.pts[0] = A.pts_last;
       pre_.pts[1] = B.pts_last;
       pre_.ids[0] = A.ids_last;
@@ -1187,7 +1200,7 @@ void Tracker::predetect() {
     } else {
       std::vector<MonoDet> det(n);
       for (int k = 0; k < n; k++) {
-        CamState &c = cs_[last_cams_[k]];
+        CamState &c = cs_.at(last_cams_[k]);
         det[k].cam = last_cams_[k];
         det[k].p = &c.pyr[c.last];
         det[k].mask = &c.mask_last;
@@ -1211,6 +1224,47 @@ void Tracker::predetect() {
   pre_.valid = true;
 }
 
+void Tracker::worker_loop() {
+  std::unique_lock<std::mutex> lk(wm_);
+  for (;;) {
+    wcv_.wait(lk, [&] { return w_task_ || w_quit_; });
+    if (w_quit_) return;
+    w_task_ = false;
+    w_busy_ = true;
+    lk.unlock();
+    try {
+      predetect();
+    } catch (...) {
+      w_err_ = std::current_exception();
+    }
+    lk.lock();
+    w_busy_ = false;
+    wcv_.notify_all();
+  }
+}
+
+void Tracker::predetect_async() {
+  predetect_join();
+  if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });
+  {
+    std::lock_guard<std::mutex> lk(wm_);
+    w_task_ = true;
+  }
+  wcv_.notify_all();
+}
+
+void Tracker::predetect_join() {
+  if (!worker_.joinable()) return;
+  std::exception_ptr e;
+  {
+    std::unique_lock<std::mutex> lk(wm_);
+    wcv_.wait(lk, [&] { return !w_task_ && !w_busy_; });
+    e = w_err_;
+    w_err_ = nullptr;
+  }
+  if (e) std::rethrow_exception(e);
+}
+
 // ---------------------------------------------------------------- inspection
 void Tracker::last_tracks(int cam, std::vector<KeyPt> &pts, std::vector<size_t> &ids) const {
   pts.clear();
@@ -1222,6 +1276,7 @@ void Tracker::last_tracks(int cam, std::vector<KeyPt> &pts, std::vector<size_t> 
 }
 
 bool Tracker::last_pyramid(int cam, int level, int *w, int *h, std::vector<uint8_t> *img, std::vector<int16_t> *der) {
+  predetect_join();  // its sync() must see the tracker's own stream selection
   auto it = cs_.find(cam);
   if (it == cs_.end() || !it->second.have_last) return false;
   const DPyr &p = it->second.pyr[it->second.last];

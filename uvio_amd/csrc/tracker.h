@@ -6,7 +6,11 @@
 // bookkeeping), so the feature ids and their order in the database are the reference's.
 // Pyramids stay in HBM: two slots per camera (last, new), swapped every frame.
 #pragma once
+#include <condition_variable>
+#include <exception>
 #include <functional>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -60,7 +64,11 @@ class Tracker {
   // result when it has the same cameras; otherwise, or after set_num_features, the result is discarded and
   // currid restored, so ids and points are always those of the serial order.
   void predetect();
-  int pre_syncs = 0;        // host waits / seconds of the last predetect
+  // predetect on the tracker's worker thread: returns at once; the next feed (or anything that needs the
+  // tracker's detection state) joins it first, rethrowing its error
+  void predetect_async();
+  void predetect_join();
+  int pre_syncs = 0;        // host waits / seconds of the last predetect (on its own thread: off the frame)
   double pre_wait = 0.0;
 
  private:
@@ -135,6 +143,13 @@ class Tracker {
   };
   PreDet pre_;
   std::vector<int> last_cams_;
+  // the predetect worker: one persistent thread, one task at a time
+  std::thread worker_;
+  std::mutex wm_;
+  std::condition_variable wcv_;
+  bool w_task_ = false, w_busy_ = false, w_quit_ = false;
+  std::exception_ptr w_err_;
+  void worker_loop();
   void discard_predetect() {
     if (pre_.valid) currid = pre_.currid0;
     pre_.valid = false;
