@@ -17,11 +17,14 @@ Steady state: the warm-up runs at least --warmup frames and then until the clone
 frames); the line reports the effective warm-up and whether steady state was reached.
 
 Multi-GPU (--gpus N > 1; launched either by torch.distributed.run, or by this script itself, which then
-spawns N worker processes before any GPU call): the north star's feature-sharded update --
-every rank runs the same stream and each MSCKF update's per-feature linearization, chi2 gate and Gram are
-split across the ranks with one RCCL all-reduce; cfg4 (UZH-FPV, 25 clones x 800 features per update) at
-N <= 4 and cfg5 (rpng_sim 4 cameras + UWB, 30 clones x 1500 features) at N > 4, scaling "strong" (value =
-frames of the one stream / wall time).  --replicas instead runs one independent estimator per GPU (weak).
+spawns N worker processes before any GPU call): value = one independent cfg3 estimator per GPU (the N = 1
+workload on every rank, seed 5 + rank; scaling "weak", value = all ranks' frames / the slowest rank's time), so
+the per-N values of one command compare like with like.  In the same job the line's "feature_sharded" object
+measures the north star's feature-sharded update: every rank runs the same BASELINE stream --
+cfg4 (UZH-FPV, 25 clones x 800 features per update) at N <= 4, cfg5 (rpng_sim 4 cameras + UWB, 30 clones x 1500
+features) at N > 4 -- and each MSCKF update's per-feature linearization, chi2 gate and Gram are split across the
+ranks with one RCCL all-reduce (scaling "strong"), next to rank 0's unsharded time on the same stream.  --shard
+makes the sharded run the value instead.
 
 Other workloads (--workload, SURVEY.md §8 cfg 1-5; parity-test cases and stress lines):
   cfg1  EuRoC MH_01-shaped MONO 752x480 images (configs/euroc_mav, max_cameras 1), 11 clones, <= 100 MSCKF
@@ -386,8 +389,12 @@ def main():
                     help="override a SimStream argument of the workload (ablations; the line records it)")
     ap.add_argument("--no-host-feed", action="store_true",
                     help="skip the second timed pass that feeds the frames as host images (uvio_hp_feed_camera)")
-    ap.add_argument("--replicas", action="store_true", help="N > 1: independent replicas instead of feature sharding")
-    ap.add_argument("--shard", action="store_true", help="feature sharding also at N = 1 (RCCL world of 1)")
+    ap.add_argument("--replicas", action="store_true", help="(the N > 1 default) one independent estimator per GPU")
+    ap.add_argument("--shard", action="store_true",
+                    help="value = the feature-sharded run of --workload (every rank one stream, MSCKF updates split; "
+                         "also at N = 1 as an RCCL world of 1)")
+    ap.add_argument("--sharded-steps", type=int, default=100,
+                    help="N > 1: timed frames of the feature-sharded companion run (0 = skip)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
     ap.add_argument("--ktime-period", type=int, default=None,
                     help="kernel-class event timing on every k-th frame of the timed region (0 = off; default: every "
@@ -403,10 +410,13 @@ def main():
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    shard = (world > 1 and not args.replicas) or args.shard
+    # N > 1: value = one independent cfg3 estimator per GPU (weak scaling: the same per-rank work as the N = 1
+    # line); the north star's feature-sharded update (cfg4 at N <= 4, cfg5 beyond) is measured in the same job as
+    # the line's "feature_sharded" object, with its 1-GPU time on the same stream
+    shard = args.shard
     wl = ALIASES.get(args.workload, args.workload)
     if wl == "auto":
-        wl = "cfg3" if world == 1 else ("cfg4" if world <= 4 else "cfg5")
+        wl = ("cfg4" if world <= 4 else "cfg5") if (shard and world > 1) else "cfg3"
     if args.cpu_frames is None:
         args.cpu_frames = CPU_FRAMES[wl]
     if args.ktime_period is None:
@@ -509,6 +519,11 @@ def main():
     if frames is not None and world == 1 and not args.no_host_feed:
         mgr.close()
         host_feed = host_feed_pass(U, opts, sim, frames, warm, args.steps, barrier, x_ref=[r[2] for r in rec])
+    sharded = None
+    if world > 1 and not shard and args.sharded_steps > 0:
+        mgr.close()
+        frames = None
+        sharded = sharded_companion(U, args, world, rank, dev, barrier)
 
     if rank == 0:
         # replicas: world streams were processed; sharded: one stream, split
@@ -567,6 +582,7 @@ def main():
             "roofline": rl.get(dom),
             "rooflines": rl,
             "host_feed": host_feed,
+            "feature_sharded": sharded,
             "cpu_baseline": cpu,
         }
         result_out.write(json.dumps(out) + "\n")
@@ -574,6 +590,55 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def sharded_companion(U, args, world, rank, dev, barrier):
+    """The feature-sharded MSCKF update at this world size: every rank runs the same BASELINE
+    stream (cfg4 at N <= 4, cfg5 beyond) and splits each update's features (one RCCL all-reduce per update);
+    then rank 0 alone runs the same stream unsharded on its GPU (the other ranks wait), for the speedup."""
+    import torch
+    import torch.distributed as dist
+    from uvio_amd.manager import shard_unique_id
+    wl = "cfg4" if world <= 4 else "cfg5"
+    opts = workload_options(U, wl)
+    warm = int(opts.max_clone_size) + 4
+    steps = args.sharded_steps
+    sim = make_stream(opts, warm + steps + 4, seed=5, workload=wl)
+
+    def run(mgr, sync):
+        drv = Driver(sim, mgr, None)
+        for _ in range(warm):
+            drv.step()
+        sync()
+        t0 = time.perf_counter()
+        n_msckf = 0
+        for _ in range(steps):
+            drv.step()
+            n_msckf += mgr.get_timing_raw().n_msckf
+        sync()
+        return time.perf_counter() - t0, n_msckf / steps, mgr.get_imu_state()[1]
+
+    uid = [shard_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    mgr = U.VioManager(opts, device=dev.index)
+    mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
+    el, nm, x_sh = run(mgr, barrier)
+    el = max_over_ranks(el)
+    mgr.close()
+    out = None
+    if rank == 0:
+        m1 = U.VioManager(opts, device=dev.index)
+        el1, _, x_1 = run(m1, lambda: torch.cuda.synchronize())
+        m1.close()
+        out = {"workload": WORKLOADS[wl][4], "scaling": "strong", "n_gpus": world, "steps": steps, "warmup": warm,
+               "value": steps / el, "unit": "frames/s", "ms_per_step": 1e3 * el / steps,
+               "single_gpu_value": steps / el1, "speedup": el1 / el, "mean_msckf_feats": nm,
+               "final_imu_state_max_abs_diff_vs_single": float(np.max(np.abs(x_sh - x_1))),
+               "note": "every rank runs the same stream; each MSCKF update's feature linearization, chi2 gate and "
+                       "Gram are split over the ranks with one RCCL all-reduce (SURVEY.md §8e); single_gpu_value: "
+                       "rank 0 alone, unsharded, same stream, same job"}
+    dist.barrier()
+    return out
 
 
 def host_feed_pass(U, opts, sim, frames, warm, steps, barrier, x_ref):
