@@ -299,6 +299,8 @@ def max_over_ranks(x, device="cuda"):
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return x
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -309,6 +311,8 @@ def all_ranks_true(flag, device="cuda"):
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return flag
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
@@ -387,6 +391,9 @@ def main():
                     help="override an estimator option of the workload (ablations; the line records it)")
     ap.add_argument("--sim", action="append", default=[], metavar="KEY=VALUE",
                     help="override a SimStream argument of the workload (ablations; the line records it)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 on fewer GPUs (tests only): ranks share the visible GPUs, torch.distributed over gloo "
+                         "and the sharded update's all-reduce through the host callback instead of RCCL")
     ap.add_argument("--no-host-feed", action="store_true",
                     help="skip the second timed pass that feeds the frames as host images (uvio_hp_feed_camera)")
     ap.add_argument("--replicas", action="store_true", help="(the N > 1 default) one independent estimator per GPU")
@@ -430,8 +437,13 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import uvio_amd as U
     from uvio_amd.evaluation import ate as ate_fn
 
@@ -452,7 +464,10 @@ def main():
         uid = [shard_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
-        mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
+        if args.rehearse:
+            mgr.enable_feature_sharding(rank, world, backend="host", min_features=args.shard_min)
+        else:
+            mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
     drv = Driver(sim, mgr, frames)
 
     # warm-up: at least --warmup frames, then until the clone window is full and the SLAM slots are populated
@@ -618,10 +633,13 @@ def sharded_companion(U, args, world, rank, dev, barrier):
         sync()
         return time.perf_counter() - t0, n_msckf / steps, mgr.get_imu_state()[1]
 
-    uid = [shard_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
     mgr = U.VioManager(opts, device=dev.index)
-    mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
+    if args.rehearse:
+        mgr.enable_feature_sharding(rank, world, backend="host", min_features=args.shard_min)
+    else:
+        uid = [shard_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        mgr.enable_feature_sharding(rank, world, backend="rccl", unique_id=uid[0], min_features=args.shard_min)
     el, nm, x_sh = run(mgr, barrier)
     el = max_over_ranks(el)
     mgr.close()
