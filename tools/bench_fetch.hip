@@ -29,8 +29,9 @@ __global__ void k_read(const T *__restrict__ a, size_t n, unsigned long long *si
   unsigned long long acc = 0;
   for (; i < n; i += stride) {
     const T v = a[i];
-    const unsigned char *b = reinterpret_cast<const unsigned char *>(&v);
-    acc += b[0] + b[sizeof(T) - 1];
+    unsigned long long w = 0;
+    __builtin_memcpy(&w, &v, sizeof(T) < 8 ? sizeof(T) : 8);
+    acc = acc * 31 + w;
   }
   if (acc == 0x1234567ull) sink[0] = acc;  // keeps the loads
 }
@@ -71,14 +72,17 @@ int main() {
   CK(hipMemset(buf, 1, bytes));
   const int grid = 256 * 16, block = 256;
   printf("kernel,bytes\n");
-#define RD(T)                                                                                          \
+#define RD(T, NAME)                                                                                    \
   hipLaunchKernelGGL(k_read<T>, dim3(grid), dim3(block), 0, 0, (const T *)buf, bytes / sizeof(T), sink); \
-  printf("k_read<%s>,%zu\n", #T, bytes);
-#define WR(T)                                                                             \
+  printf("k_read<%s>,%zu\n", NAME, bytes);
+#define WR(T, NAME)                                                                       \
   hipLaunchKernelGGL(k_write<T>, dim3(grid), dim3(block), 0, 0, (T *)buf, bytes / sizeof(T)); \
-  printf("k_write<%s>,%zu\n", #T, bytes);
-  RD(uint8_t) RD(uint16_t) RD(uint32_t) RD(uint64_t) RD(uint4)
-  WR(uint8_t) WR(uint16_t) WR(uint32_t) WR(uint64_t) WR(uint4)
+  printf("k_write<%s>,%zu\n", NAME, bytes);
+  // names as the trace demangles them
+  RD(uint8_t, "unsigned char") RD(uint16_t, "unsigned short") RD(uint32_t, "unsigned int")
+  RD(uint64_t, "unsigned long") RD(uint4, "HIP_vector_type<unsigned int, 4u>")
+  WR(uint8_t, "unsigned char") WR(uint16_t, "unsigned short") WR(uint32_t, "unsigned int")
+  WR(uint64_t, "unsigned long") WR(uint4, "HIP_vector_type<unsigned int, 4u>")
   // LK-like gathers over a 8192 x 4096 image (32 MiB of pixels, 128 MiB of derivatives)
   const int w = 8192, h = 4096;
   uint8_t *img = (uint8_t *)buf;

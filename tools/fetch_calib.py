@@ -26,10 +26,8 @@ F, W = load(sys.argv[2], "FETCH_SIZE"), load(sys.argv[3], "WRITE_SIZE")
 
 
 def find(d, k):
-    base = k.split("<")[0]
-    arg = k[len(base):]
     for name, v in d.items():
-        if name.startswith(base) and (not arg or arg.strip("<>") in name):
+        if name == k or name.startswith(k + "("):
             return v
     return None
 
