@@ -232,14 +232,33 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
       o.cam = cam_of[k];
       o.pad = 0;
     }
-    const int nw = pool_.threads();
+    // bucket the observations by owning worker once (a counting sort that keeps observation order inside a
+    // bucket), then each worker appends its bucket with the feature objects prefetched a few entries ahead
+    // -- the appends are cache-miss bound (feature, its track array, the measurement storage)
+    const uint32_t nw = (uint32_t)pool_.threads();
+    std::vector<uint32_t> start(nw + 1, 0), order(nobs);
+    std::vector<uint16_t> owner(nobs);
+    for (size_t k = 0; k < nobs; k++) {
+      const uint64_t h = (uint64_t)((uintptr_t)fp[k] >> 6) * 0x9E3779B97F4A7C15ull;
+      owner[k] = (uint16_t)(((h >> 32) * nw) >> 32);
+      start[owner[k] + 1]++;
+    }
+    for (uint32_t w = 0; w < nw; w++) start[w + 1] += start[w];
+    {
+      std::vector<uint32_t> pos(start.begin(), start.end() - 1);
+      for (size_t k = 0; k < nobs; k++) order[pos[owner[k]]++] = (uint32_t)k;
+    }
     pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
-      for (size_t w = b; w < e; w++)
-        for (size_t k = 0; k < nobs; k++) {
-          if (((uintptr_t)fp[k] >> 6) % (uintptr_t)nw != w) continue;
+      for (size_t w = b; w < e; w++) {
+        const uint32_t i0 = start[w], i1 = start[w + 1];
+        for (uint32_t i = i0; i < i1; i++) {
+          if (i + 16 < i1) __builtin_prefetch(fp[order[i + 16]], 1);
+          if (i + 8 < i1) __builtin_prefetch(fp[order[i + 8]]->tracks.data(), 1);
+          const size_t k = order[i];
           fp[k]->track((size_t)cam_of[k]).m.push_back(
               FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
         }
+      }
     });
   }
   return after_tracking(t, camids, rT1);
@@ -425,6 +444,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     HPROF("select.flags");
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
+        // software pipeline over the dependent misses: map node -> feature -> track array
+        if (i + 12 < e) __builtin_prefetch(all[i + 12].first->get());
+        if (i + 6 < e) __builtin_prefetch((*all[i + 6].first)->tracks.data());
         const Feature &f = **all[i].first;
         if (f.to_delete) continue;
         bool newer = false, has = false;
@@ -579,6 +601,8 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     std::vector<uint8_t> empty(all.size(), 0);
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
+        if (i + 12 < e) __builtin_prefetch(all[i + 12], 1);
+        if (i + 6 < e) __builtin_prefetch(all[i + 6]->tracks.data(), 1);
         all[i]->clean_older_measurements(mt);
         empty[i] = all[i]->count() < 1;
       }
