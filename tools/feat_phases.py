@@ -43,3 +43,6 @@ for mode in sorted(set(a[:, 0])):
         if len(c):
             dc = np.diff(c, axis=1)
             print("      chi2: stage+S %.0f  ldl %.0f  chi2 %.0f  cyc (n=%d)" % tuple(list(np.mean(dc, axis=0)) + [len(c)]))
+            k = int(np.argmax(c[:, 3] - c[:, 0]))
+            print("      chi2 slowest feature (meas %d): stage+S %.0f  ldl %.0f  chi2 %.0f  cyc" % (
+                sel[sel[:, 15] > 0][k, 2], *dc[k]))

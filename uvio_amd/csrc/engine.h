@@ -126,6 +126,7 @@ struct CamTrack {
 struct Feature {
   size_t featid = 0;
   bool to_delete = false;
+  bool held = false;     // read by this frame's update chain: trimmed after the chain, not during it
   size_t dense_idx = 0;  // slot in Engine::dense_
   // Per camera, in the iteration order of the reference's unordered_map<size_t, vector<...>> members:
   // with libstdc++ and at most UVIO_HP_MAX_CAMS small integer keys every key sits in its own bucket and
@@ -364,6 +365,10 @@ class Engine {
   ShardComm shard_;
   WorkPool pool_;
   std::vector<FeatP> pending_delete_;  // features handed to an updater this frame (cleanup candidates)
+  // host work that update_frame runs while the device executes the chain (set by the caller, cleared by the run)
+  std::function<void()> chain_overlap_;
+  // FeatureDatabase::cleanup_measurements(t) over the database's features, skipping the held ones if asked
+  void cleanup_measurements(double t, bool skip_held);
   HostProf hprof_;                     // UVIO_HP_HOST_PROF section timer (debug)
   FILE *timing_csv_ = nullptr;         // record_timing_information (VioManager.cpp:105-122)
   KProf kprof_;                        // live per-class kernel timing (uvio_hp_set_kernel_timing)

@@ -512,6 +512,12 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       HPROF("chain.predetect");
       tracker_->predetect_async();
     }
+    if (chain_overlap_) {
+      HPROF("chain.overlap");
+      auto f = std::move(chain_overlap_);
+      chain_overlap_ = nullptr;
+      f();
+    }
     dev_sync();
   }
   auto tm3 = clk::now();

@@ -96,6 +96,7 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
       }
     }
     // undistort_cv with the camera models as of now (independent per point: on the pool)
+    HPROF("retri.undist");
     pool_.parallel_for(frame_obs_.size(), 128, [&](size_t b, size_t e) {
       for (size_t k = b; k < e; k++) {
         DRetriObs &o = frame_obs_[k];

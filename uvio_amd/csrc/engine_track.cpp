@@ -1152,10 +1152,14 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
         tracked_undistort(1, sr[i - gl.size()], cr, gr[i - gl.size()], uvr[2 * (i - gl.size())], uvr[2 * (i - gl.size()) + 1]);
     }
   };
-  if (pool_)
-    pool_->parallel_for(gl.size() + gr.size(), 128, undist);
-  else
-    undist(0, gl.size() + gr.size());
+  {
+    HostProfScope hs(*hp_, "trk.post.undist");
+    if (pool_)
+      pool_->parallel_for(gl.size() + gr.size(), 128, undist);
+    else
+      undist(0, gl.size() + gr.size());
+  }
+  HostProfScope hs_db(*hp_, "trk.post.db");
   for (size_t i = 0; i < gl.size(); i++) db(gil[i], t, cl, gl[i].x, gl[i].y, uvl[2 * i], uvl[2 * i + 1]);
   for (size_t i = 0; i < gr.size(); i++) db(gir[i], t, cr, gr[i].x, gr[i].y, uvr[2 * i], uvr[2 * i + 1]);
   A.pts_last.swap(gl);

@@ -546,10 +546,31 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   timing_.n_slam_delayed = (int)slam_delayed.size();
   int rc = 0;
   auto rT4 = clk::now(), rT5 = rT4, rT6 = rT4;
+  // FeatureDatabase::cleanup_measurements(margtimestep) of every feature the updaters do not read runs while
+  // the device executes the chain: one feature's trimming is independent of the others', nothing between
+  // the updates and the cleanup reads the trimmed (older than the marginalized clone) measurements of an
+  // unread feature, and erasing a node keeps the other nodes' iteration order.  The held features (every
+  // one handed to an updater, pending_delete_) are trimmed at the reference's point, after the chain.
+  const bool do_clean = (int)clones_.size() > o_.max_clone_size;
+  const double mt_clean = do_clean ? margtimestep() : 0.0;
+  bool cleaned_early = false;
+  std::vector<FeatP> held;
   if (!shard_.enabled && !no_chain_) {
+    if (do_clean) {
+      held = pending_delete_;
+      for (auto &f : held) f->held = true;
+      chain_overlap_ = [this, mt_clean, &cleaned_early]() {
+        cleanup_measurements(mt_clean, true);
+        cleaned_early = true;
+      };
+    }
     // the three updaters as one device chain with one host wait (engine_chain.cpp)
     rc = update_frame(up, slam_upd, slam_delayed);
-    if (rc) return rc;
+    chain_overlap_ = nullptr;
+    if (rc) {
+      for (auto &f : held) f->held = false;
+      return rc;
+    }
     rT6 = clk::now();
     timing_.msckf_update = chain_times_[0];
     timing_.slam_update = chain_times_[1];
@@ -592,24 +613,20 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     rc = slam_change_anchors();
   }
   if (rc) return rc;
-  if ((int)clones_.size() > o_.max_clone_size) {
+  if (do_clean) {
     HPROF("marg.cleanmeas");
-    // FeatureDatabase::cleanup_measurements(margtimestep): per-feature trimming on the pool, then the
-    // emptied features are erased (erasing by key keeps the others' iteration order)
-    double mt = margtimestep();
-    const std::vector<Feature *> all(dense_);  // (a copy: the erasures below reorder dense_)
-    std::vector<uint8_t> empty(all.size(), 0);
-    pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
-      for (size_t i = b; i < e; i++) {
-        if (i + 12 < e) __builtin_prefetch(all[i + 12], 1);
-        if (i + 6 < e) __builtin_prefetch(all[i + 6]->tracks.data(), 1);
-        all[i]->clean_older_measurements(mt);
-        empty[i] = all[i]->count() < 1;
+    if (!cleaned_early) {
+      cleanup_measurements(mt_clean, false);
+    } else {
+      for (auto &f : held) {  // the chain's features still in the database
+        auto it = db_.find(f->featid);
+        if (it == db_.end() || it->second != f) continue;
+        f->clean_older_measurements(mt_clean);
+        if (f->count() < 1) db_erase(it);
       }
-    });
-    for (size_t i = 0; i < all.size(); i++)
-      if (empty[i]) db_erase(db_.find(all[i]->featid));
+    }
   }
+  for (auto &f : held) f->held = false;
   marginalize_old_clone();
   if (o_.record_timing >= 2) dev_sync();
   auto rT7 = clk::now();
@@ -624,6 +641,24 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   }
   timelastupdate_ = t;
   return 0;
+}
+
+// FeatureDatabase::cleanup_measurements (FeatureDatabase.cpp:226-243): per-feature trimming on the pool, then
+// the emptied features are erased (erasing by key keeps the others' iteration order)
+void Engine::cleanup_measurements(double t, bool skip_held) {
+  const std::vector<Feature *> all(dense_);  // (a copy: the erasures below reorder dense_)
+  std::vector<uint8_t> empty(all.size(), 0);
+  pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; i++) {
+      if (i + 12 < e) __builtin_prefetch(all[i + 12], 1);
+      if (i + 6 < e) __builtin_prefetch(all[i + 6]->tracks.data(), 1);
+      if (skip_held && all[i]->held) continue;
+      all[i]->clean_older_measurements(t);
+      empty[i] = all[i]->count() < 1;
+    }
+  });
+  for (size_t i = 0; i < all.size(); i++)
+    if (empty[i]) db_erase(db_.find(all[i]->featid));
 }
 
 // StateHelper::marginalize_slam (StateHelper.cpp:631-645)
