@@ -8,6 +8,7 @@ GPU: the runner's trajectory (ov_eval format, ground-truth initialized) equals, 
 same messages fed through the Python binding in the same order (host images, uvio_hp_feed_camera)."""
 import json
 import os
+import re
 import struct
 import subprocess
 import zlib
@@ -58,9 +59,23 @@ def asl(tmp_path_factory):
     from uvio_amd.sim import SimStream
     opts = U.load_options(EUROC, init_max_features=200, max_msckf_in_update=100, max_slam_features=20,
                           max_slam_in_update=10, dt_slam_delay=0.3)
+    # the runner reads a config folder: a copy of the EuRoC one with the same values as the binding's options
+    base = tmp_path_factory.mktemp("asl")
+    cfg = base / "config"
+    cfg.mkdir()
+    src = os.path.dirname(EUROC)
+    for name in os.listdir(src):
+        with open(os.path.join(src, name)) as f:
+            text = f.read()
+        if name == "estimator_config.yaml":
+            for key, val in (("init_max_features", 200), ("max_msckf_in_update", 100), ("max_slam", 20),
+                             ("max_slam_in_update", 10), ("dt_slam_delay", 0.3)):
+                text, n = re.subn(r"(?m)^%s:.*$" % key, "%s: %s" % (key, val), text)
+                assert n == 1, key
+        with open(cfg / name, "w") as f:
+            f.write(text)
     sim = SimStream(opts, duration=N_FRAMES / opts.track_frequency + 1.2, seed=5, spawn=4)
     r = SceneRenderer(opts, device="cpu")
-    base = tmp_path_factory.mktemp("asl")
     mav = base / "mav0"
     imgs = {}
     (mav / "imu0").mkdir(parents=True)
@@ -92,15 +107,17 @@ def asl(tmp_path_factory):
             q = g[1:5]
             row = np.r_[g[5:8], q[3], q[:3], g[8:11], g[11:14], g[14:17]]
             f.write("%d,%s\n" % (_ns(t), ",".join(repr(float(v)) for v in row)))
-    return str(base), str(gt), opts, sim, imgs
+    return str(base), str(gt), opts, sim, imgs, str(cfg / "estimator_config.yaml")
 
 
 def test_runner_dry_run_parses_and_decodes(asl):
     from uvio_amd import build
     build.build_runner()
-    folder, gt, opts, sim, imgs = asl
-    out = subprocess.check_output([RUNNER, EUROC, folder, "--gt", gt, "--dry-run"], timeout=120)
+    folder, gt, opts, sim, imgs, cfg = asl
+    out = subprocess.check_output([RUNNER, cfg, folder, "--gt", gt, "--dry-run"], timeout=120)
     s = json.loads(out.decode().strip().splitlines()[-1])
+    for k, v in s["options"].items():  # the config copy carries the binding's options
+        assert v == getattr(opts, k), k
     n_imu = int(np.sum(sim.imu_t >= sim.t0 - 0.4))
     last_cam = max(1e-9 * _ns(sim.cam_t[i]) for (k, i) in imgs)
     assert s["dry_run"] and s["gt_states"] == len(sim.imu_t)
@@ -113,7 +130,7 @@ def test_runner_dry_run_parses_and_decodes(asl):
 def test_runner_rejects_a_bad_png(asl, tmp_path):
     from uvio_amd import build
     build.build_runner()
-    folder, gt, opts, sim, imgs = asl
+    folder, gt, opts, sim, imgs, cfg = asl
     bad = tmp_path / "x"
     os.makedirs(bad / "mav0" / "imu0")
     for k in range(2):
@@ -132,9 +149,9 @@ def test_runner_rejects_a_bad_png(asl, tmp_path):
 def test_runner_matches_the_binding(asl, tmp_path):
     """the C++ runner and the Python binding, same folder, same order: identical trajectories"""
     import uvio_amd as U
-    folder, gt, opts, sim, imgs = asl
+    folder, gt, opts, sim, imgs, cfg = asl
     traj = tmp_path / "traj.txt"
-    subprocess.check_call([RUNNER, EUROC, folder, "--gt", gt, "--out", str(traj)], timeout=300)
+    subprocess.check_call([RUNNER, cfg, folder, "--gt", gt, "--out", str(traj)], timeout=300)
     est = np.loadtxt(traj, ndmin=2)
     assert len(est) >= N_FRAMES - 3
     # the binding: IMU rows and camera pairs in time order (IMU first at equal times), GT init at the first pair

@@ -300,7 +300,11 @@ int main(int argc, char **argv) {
   if (out) std::fclose(out);
   if (h) uvio_hp_destroy(h);
   std::printf("{\"imu\": %zu, \"frames\": %zu, \"skipped_unsynced\": %zu, \"uwb\": %zu, \"images\": %zu, "
-              "\"pixel_sum\": %llu, \"gt_states\": %zu, \"dry_run\": %s}\n",
-              n_imu, n_frames, n_skipped, n_uwb, n_img, (unsigned long long)pix_sum, gt.size(), dry ? "true" : "false");
+              "\"pixel_sum\": %llu, \"gt_states\": %zu, \"dry_run\": %s, \"options\": {\"init_max_features\": %d, "
+              "\"max_msckf_in_update\": %d, \"max_slam_features\": %d, \"max_slam_in_update\": %d, "
+              "\"dt_slam_delay\": %.17g}}\n",
+              n_imu, n_frames, n_skipped, n_uwb, n_img, (unsigned long long)pix_sum, gt.size(), dry ? "true" : "false",
+              opts.init_max_features, opts.max_msckf_in_update, opts.max_slam_features, opts.max_slam_in_update,
+              opts.dt_slam_delay);
   return 0;
 }
