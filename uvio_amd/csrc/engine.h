@@ -419,6 +419,9 @@ class Engine {
   void cov_propagate(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                      const std::vector<double> &Q, const std::vector<int> *rows = nullptr);
   VarP clone_imu_pose(const double *dnc, bool do_dt, const double *staged = nullptr);
+  VarP add_clone_var();
+  bool cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
+                           const std::vector<double> &Q, bool do_dt, const double *ddnc);
   void marginalize(const VarP &v);
   void check_neg_diag(const char *who);
   void info_prefactor(const std::vector<int> &hidx);

@@ -652,6 +652,13 @@ int Engine::propagate_and_clone(double timestamp) {
   double dnc[6] = {lw[0], lw[1], lw[2], imu_->val[7], imu_->val[8], imu_->val[9]};
   const bool do_dt = o_.do_calib_camera_timeoffset != 0;
   const double *ddnc = do_dt ? stage(dnc, 6) : nullptr;
+  // propagation and clone in one launch unless the clone is refused below (a clone at this time exists)
+  if (clones_.find(timestamp) == clones_.end() && cov_propagate_clone(imu_->id, n, ids, Phi, Qd, do_dt, ddnc)) {
+    timestamp_ = timestamp;
+    last_prop_time_offset_ = t_off_new;
+    clones_[timestamp_] = add_clone_var();
+    return 0;
+  }
   cov_propagate(imu_->id, n, ids, Phi, Qd);
   timestamp_ = timestamp;
   last_prop_time_offset_ = t_off_new;

@@ -510,6 +510,23 @@ void Engine::check_neg_diag(const char *who) {
   if (*d_.neg_host > 0) throw HpError(UVIO_HP_E_NUMERIC, std::string(who) + ": negative covariance diagonal");
 }
 
+// cov_propagate of the IMU block (contiguous rows s0 ..) followed by clone_imu_pose, as ONE launch when the
+// propagation is small (launch_prop_clone); false when it did nothing (the caller takes the two-step path)
+bool Engine::cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
+                                 const std::vector<double> &Q, bool do_dt, const double *ddnc) {
+  const int q = (int)iold.size();
+  if (p > 64 || q > 256 || N_ + 6 > d_.ldp || N_ * p > 4096 || std::getenv("UVIO_HP_NO_PROP_FUSE")) return false;
+  const double *dPhi = stage(Phi.data(), (size_t)p * q);
+  const double *dQ = stage(Q.data(), (size_t)p * p);
+  const int *diold = stage(iold.data(), (size_t)q);
+  stage_flush();
+  if (!launch_prop_clone(d_.stream, d_.P, d_.ldp, N_, s0, p, diold, q, dPhi, dQ, d_.T, imu_->id,
+                         do_dt ? calib_dt_->id : 0, do_dt ? ddnc : d_.dnc, do_dt ? 1 : 0))
+    throw HpError(UVIO_HP_E_CAPACITY, "fused propagation refused after the size check");
+  ++p_epoch_;
+  return true;
+}
+
 // StateHelper::clone(imu->pose()) + augment_clone (StateHelper.cpp:341-391, 579-616)
 VarP Engine::clone_imu_pose(const double *dnc, bool do_dt, const double *staged) {
   if (N_ + 6 > d_.ldp) throw HpError(UVIO_HP_E_CAPACITY, "covariance capacity exceeded");
@@ -523,6 +540,11 @@ VarP Engine::clone_imu_pose(const double *dnc, bool do_dt, const double *staged)
   }
   launch_clone(d_.stream, d_.P, d_.ldp, N_, imu_->id, do_dt ? calib_dt_->id : 0, ddnc, do_dt ? 1 : 0);
   ++p_epoch_;
+  return add_clone_var();
+}
+
+// the clone's host variable (its covariance rows / columns N_ .. N_+5 are written on the device)
+VarP Engine::add_clone_var() {
   VarP pose = mk(V_POSE, 6, 7);
   for (int k = 0; k < 7; k++) pose->val[k] = imu_->val[k], pose->fej[k] = imu_->fej[k];
   pose->id = N_;

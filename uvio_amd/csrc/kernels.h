@@ -106,6 +106,10 @@ void launch_cov_propagate(hipStream_t s, double *P, int ld, int N, int s0, int p
                           const double *Phi, const double *Q, double *T, const int *rows = nullptr);
 // StateHelper::clone of imu->pose() + augment_clone time-offset term (StateHelper.cpp:341-391,579-616)
 void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt);
+// launch_cov_propagate (contiguous block) + launch_clone in one launch; false (nothing launched) when too large
+bool launch_prop_clone(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
+                       const double *Phi, const double *Q, double *T, int src0, int dt_id, const double *dnc_dev,
+                       int do_dt);
 // StateHelper::marginalize (StateHelper.cpp:271-339): Pout <- P without rows/cols [m0, m0+ms)
 void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, int N, int m0, int ms);
 // Pout (Nn x Nn) <- P[src, src]: several variables marginalized at once (src: the kept indices, device)

@@ -97,6 +97,74 @@ __global__ void k_clone(double *__restrict__ P, int ld, int N, int src0, int dt_
   }
 }
 
+// EKFPropagation of the contiguous block s0 .. s0+p-1 and the IMU-pose clone in ONE workgroup launch: the three
+// phases above (T, the block write, the clone) with a workgroup barrier between them instead of a kernel
+// boundary, each element computed by the same expression as in k_prop_T / k_prop_write / k_clone (so the
+// result is bit-identical).  For the small propagations (N p <= kPropCloneMaxNp): one CU does them in about
+// the time of the first launch alone and the frame loses two launches.
+constexpr int kPropCloneThreads = 1024, kPropCloneMaxNp = 4096;
+__global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__restrict__ P, int ld, int N, int s0, int p,
+                                                                  const int *__restrict__ iold, int q,
+                                                                  const double *__restrict__ Phi,
+                                                                  const double *__restrict__ Q, double *__restrict__ T,
+                                                                  int src0, int dt_id, const double *__restrict__ dnc,
+                                                                  int do_dt) {
+  for (int idx = threadIdx.x; idx < N * p; idx += blockDim.x) {
+    const int i = idx / p, a = idx % p;
+    const double *Pi = P + (size_t)i * ld;
+    double acc = 0.0;
+    for (int b = 0; b < q; b++) acc += Pi[iold[b]] * Phi[a * q + b];
+    T[(size_t)i * p + a] = acc;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < N * p; idx += blockDim.x) {
+    const int i = idx / p, a = idx % p, col = s0 + a;
+    if (i >= s0 && i < s0 + p) {
+      const int x = i - s0;
+      double acc = (x <= a) ? Q[x * p + a] : Q[a * p + x];
+      for (int c = 0; c < q; c++) acc += Phi[x * q + c] * T[(size_t)iold[c] * p + a];
+      P[(size_t)i * ld + col] = acc;
+    } else {
+      const double v = T[(size_t)i * p + a];
+      P[(size_t)i * ld + col] = v;
+      P[(size_t)col * ld + i] = v;
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < (N + 6) * 6; idx += blockDim.x) {
+    const int i = idx / 6, b = idx % 6;
+    const double db = do_dt ? dnc[b] : 0.0;
+    if (i < N) {
+      double col = P[(size_t)i * ld + src0 + b];
+      double row = P[(size_t)(src0 + b) * ld + i];
+      if (do_dt) {
+        col += P[(size_t)i * ld + dt_id] * db;
+        row += db * P[(size_t)dt_id * ld + i];
+      }
+      P[(size_t)i * ld + N + b] = col;
+      P[(size_t)(N + b) * ld + i] = row;
+    } else {
+      const int a = i - N;
+      double v = P[(size_t)(src0 + a) * ld + src0 + b];
+      if (do_dt) {
+        const double da = dnc[a];
+        v += P[(size_t)(src0 + a) * ld + dt_id] * db;
+        v += da * (P[(size_t)dt_id * ld + src0 + b] + P[(size_t)dt_id * ld + dt_id] * db);
+      }
+      P[(size_t)i * ld + N + b] = v;
+    }
+  }
+}
+
+bool launch_prop_clone(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
+                       const double *Phi, const double *Q, double *T, int src0, int dt_id, const double *dnc_dev,
+                       int do_dt) {
+  if (N * p > kPropCloneMaxNp) return false;
+  hipLaunchKernelGGL(k_prop_clone, dim3(1), dim3(kPropCloneThreads), 0, s, P, ld, N, s0, p, iold, q, Phi, Q, T, src0,
+                     dt_id, dnc_dev, do_dt);
+  return true;
+}
+
 void launch_clone(hipStream_t s, double *P, int ld, int N, int src0, int dt_id, const double *dnc_dev, int do_dt) {
   int n = (N + 6) * 6, bs = 256, gs = (n + bs - 1) / bs;
   hipLaunchKernelGGL(k_clone, dim3(gs), dim3(bs), 0, s, P, ld, N, src0, dt_id, dnc_dev, do_dt);
