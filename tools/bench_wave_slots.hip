@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(512) k_slots(const double *Ain, int r, int inv
   }
   __syncthreads();
   const long long t0 = clock64();
-  ldl_wave_inv<SMAX, SqLayout, BC>(A, SqLayout{ld}, r, r + 1, D, inv != 0, prof);
+  ldl_wave_inv<SMAX, SqLayout, BC>(A, SqLayout{ld}, r, r + 1, D, inv != 0, nullptr, prof);
   if (threadIdx.x == 0) tot[0] = clock64() - t0;
   __syncthreads();
   for (int e = threadIdx.x; e < (r + 1) * ld + r + 1; e += blockDim.x) Aout[e] = lds[e];

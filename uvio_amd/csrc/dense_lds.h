@@ -528,28 +528,28 @@ __device__ __forceinline__ double quad_bcast(double v) {
   const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), ctrl, 0xf, 0xf, false);
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-// steps k = K .. 14 of the quad-parallel unit-lower 16x16 inverse; Lb: the block's corner (square storage)
-template <int K>
-__device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *Lb, int ld, int bn, int q) {
+// steps k = K .. 14 of the quad-parallel unit-lower 16x16 inverse of the block at (o, o) of A (layout la)
+template <int K, class LA>
+__device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *A, LA la, int o, int bn, int q) {
   if constexpr (K < 15) {
     const double xk = quad_bcast<(K & 3)>(x[K >> 2]);
 #pragma unroll
     for (int m = 0; m < 4; m++) {
       const int i = q + 4 * m;
-      if (i > K && i < bn) x[m] = fma(-Lb[(size_t)i * ld + K], xk, x[m]);
+      if (i > K && i < bn) x[m] = fma(-A[la(o + i, o + K)], xk, x[m]);
     }
-    quad_inv_steps<K + 1>(x, Lb, ld, bn, q);
+    quad_inv_steps<K + 1>(x, A, la, o, bn, q);
   }
 }
 
 template <int SMAX, class LA, bool BC = false>
 __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows, double *Dd, bool with_inv,
-                                             long long *prof = nullptr) {
+                                             double *Xd = nullptr, long long *prof = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int nb = (n + 15) / 16, nbr = (nrows + 15) / 16;
   if (!LA::square) with_inv = false;
-  const int nslot = with_inv ? nb + 2 : nb;
+  const int nslot = with_inv ? nb + 2 : (Xd ? nb + 1 : nb);
   __shared__ int colcnt;  // column-update tiles finished so far (helpers -> wave 0)
   if (threadIdx.x == 0) colcnt = 0;
   __syncthreads();
@@ -627,7 +627,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         }
       }
       // then: [X_PP] [X_IK, K < I = J-2] [rank-16 tiles (I, C), C >= J+1]
-      const bool do_xd = with_inv && P >= 0 && P < nb;
+      const bool do_xd = (with_inv || Xd) && P >= 0 && P < nb;
       const int I2 = J - 2;
       const int nxo = (with_inv && I2 >= 1 && I2 < nb) ? I2 : 0;
       int ntr = 0;
@@ -636,25 +636,29 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
       const int ntask = (do_xd ? 1 : 0) + nxo + ntr;
       for (int t = wid - 1; t < ntask; t += nh) {
         int u = t;
+        if (do_xd && u == 0) {
+          // X_PP = L_PP^-1 (unit lower), right-looking, no divisions: lane 4c + q keeps column c's entries
+          // of rows q + 4m; step k broadcasts X[k][c] inside the quad (DPP) and the rows below update.  To the
+          // upper triangle of A (with_inv) and / or as a row-major 16 x 16 block to Xd + 256 P (rows past n:
+          // identity)
+          const int oP = 16 * P, bn = min(16, n - oP);
+          const int c = lane >> 2, q = lane & 3;
+          double x[4];
+#pragma unroll
+          for (int m = 0; m < 4; m++) x[m] = (q + 4 * m == c) ? 1.0 : 0.0;
+          quad_inv_steps<0>(x, A, la, oP, bn, q);
+#pragma unroll
+          for (int m = 0; m < 4; m++) {
+            const int i = q + 4 * m;
+            if constexpr (LA::square)
+              if (with_inv && i > c && i < bn && c < bn) A[(size_t)(oP + c) * la.ld + oP + i] = x[m];
+            if (Xd) Xd[(size_t)256 * P + 16 * i + c] = x[m];
+          }
+          continue;
+        }
+        u -= do_xd ? 1 : 0;
         if constexpr (LA::square) {
           const int ld = la.ld;
-          if (do_xd && u == 0) {
-            // X_PP = L_PP^-1 (unit lower), right-looking, no divisions: lane 4c + q keeps column c's entries
-            // of rows q + 4m; step k broadcasts X[k][c] inside the quad (DPP) and the rows below update
-            const int oP = 16 * P, bn = min(16, n - oP);
-            const int c = lane >> 2, q = lane & 3;
-            double x[4];
-#pragma unroll
-            for (int m = 0; m < 4; m++) x[m] = (q + 4 * m == c) ? 1.0 : 0.0;
-            quad_inv_steps<0>(x, A + (size_t)oP * ld + oP, ld, bn, q);
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-              const int i = q + 4 * m;
-              if (i > c && i < bn && c < bn) A[(size_t)(oP + c) * ld + oP + i] = x[m];
-            }
-            continue;
-          }
-          u -= do_xd ? 1 : 0;
           if (u < nxo) {
             // X_IK = -X_II sum_{K' = K .. I-1} L_IK' X_K'K
             const int I = I2, K = u, oI = 16 * I, oK = 16 * K, ri = oI + r16;

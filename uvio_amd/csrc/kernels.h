@@ -164,8 +164,9 @@ struct EkfScratch {
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.
+// form_dinv: k_trinv16 forms Dinv from L first (false: Dinv was written by the factorization that made L)
 void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, int N, int r, const double *L, int ldl,
-                    double *Dinv, double *W);
+                    double *Dinv, double *W, bool form_dinv = true);
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
                        const int *hidx, const double *res, int res_stride, double sigma2, EkfScratch &sc);
 // information-form update for a compressed batch (m > n): G = [H r]^T [H r] from k_gram partials;

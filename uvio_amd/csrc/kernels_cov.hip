@@ -582,9 +582,9 @@ __global__ void __launch_bounds__(64) k_trsm_lt(const double *__restrict__ M, in
 }
 
 void launch_trsm_lt(hipStream_t s, const double *M, int ldm, const int *hidx, int N, int r, const double *L, int ldl,
-                    double *Dinv, double *W) {
+                    double *Dinv, double *W, bool form_dinv) {
   if (r > kTrsmMaxR) throw std::runtime_error("triangular solve wider than the kernel's LDS row");
-  hipLaunchKernelGGL(k_trinv16, dim3((r + 15) / 16), dim3(64), 0, s, L, ldl, r, Dinv);
+  if (form_dinv) hipLaunchKernelGGL(k_trinv16, dim3((r + 15) / 16), dim3(64), 0, s, L, ldl, r, Dinv);
   hipLaunchKernelGGL(k_trsm_lt, dim3((N + 15) / 16), dim3(64), 0, s, M, ldm, hidx, N, r, L, ldl, Dinv, W);
 }
 
@@ -674,11 +674,19 @@ static void launch_gemm_mfma(hipStream_t s, int ta, int tb, int tri, int symA, i
 // factors each 16-column panel, the other waves do the rank-16 updates).  Storage mode: 0 = square in
 // LDS, 1 = packed lower triangle in LDS (n up to ~195), 2 = square in the global scratch gbuf.
 // L_c = L_u D^1/2; an extra right-hand-side row b leaves as L_c^-1 b = D^1/2 (D^-1 L_u^-1 b).
+// Dinv: the inverses of L_c's 16 x 16 diagonal blocks for k_trsm_lt (k_trinv16's layout: block b row-major at
+// Dinv + 256 b, rows past n identity), D^-1/2 times the unit-lower block inverses the factorization forms
+// on its helper waves -- the solve that follows needs no k_trinv16 launch.
 template <int SMAX, class LA>
-__device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int n, int nrows) {
-  ldl_wave_inv<SMAX>(A, la, n, nrows, Dd, false);
+__device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int n, int nrows, double *Dinv) {
+  ldl_wave_inv<SMAX>(A, la, n, nrows, Dd, false, Dinv);
   for (int k = threadIdx.x; k < n; k += blockDim.x) Dd[k] = sqrt(Dd[k]);  // sqrt(d)
   __syncthreads();
+  const int nb = (n + 15) / 16;
+  for (int e = threadIdx.x; e < 256 * nb; e += blockDim.x) {
+    const int row = 16 * (e >> 8) + ((e >> 4) & 15);
+    if (row < n) Dinv[e] = Dinv[e] / Dd[row];
+  }
 }
 
 // P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1), zero upper) and L_P (n x n).
@@ -686,7 +694,7 @@ __device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int
 template <int SMAX, int MODE>
 __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
                                                     int n, double *__restrict__ Laug, double *__restrict__ Lout,
-                                                    double *gbuf, int mode) {
+                                                    double *gbuf, int mode, double *__restrict__ Dinv) {
   constexpr int PACKED = MODE == 1;
   extern __shared__ double lds[];
   double *A = (MODE == 2) ? gbuf : lds;
@@ -707,9 +715,9 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
       });
   __syncthreads();
   if constexpr (PACKED)
-    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n);
+    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n, Dinv);
   else
-    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n);
+    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n, Dinv);
   const int na = n + 1;
   for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
     const int a = e / na, b = e - a * na;
@@ -726,7 +734,7 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
 template <int SMAX, int MODE>
 __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
                                                     double *__restrict__ Uout, double *__restrict__ w, double *gbuf,
-                                                    int mode) {
+                                                    int mode, double *__restrict__ Dinv) {
   constexpr int PACKED = MODE == 1;
   extern __shared__ double lds[];
   double *A = (MODE == 2) ? gbuf : lds;
@@ -748,9 +756,9 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
       });
   __syncthreads();
   if constexpr (PACKED)
-    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n + 1);
+    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n + 1, Dinv);
   else
-    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n + 1);
+    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n + 1, Dinv);
   for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[idx(n, j)] * Dd[j];
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
     const int a = e / n, b = e - a * n;
@@ -763,8 +771,8 @@ static KP pick_info_kernel(const KP (&tab)[4][3], int rows, int mode) {
   const int si = rows <= 64 ? 0 : rows <= 128 ? 1 : rows <= 192 ? 2 : 3;
   return tab[si][mode];
 }
-typedef void (*CholPFn)(const double *, int, const int *, int, double *, double *, double *, int);
-typedef void (*CholZFn)(const double *, int, double, double *, double *, double *, int);
+typedef void (*CholPFn)(const double *, int, const int *, int, double *, double *, double *, int, double *);
+typedef void (*CholZFn)(const double *, int, double, double *, double *, double *, int, double *);
 static const CholPFn kCholP[4][3] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>, k_info_cholP<1, 2>},
                                      {k_info_cholP<2, 0>, k_info_cholP<2, 1>, k_info_cholP<2, 2>},
                                      {k_info_cholP<3, 0>, k_info_cholP<3, 1>, k_info_cholP<3, 2>},
@@ -892,8 +900,8 @@ void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, 
   size_t b1 = 0;
   const int m1 = info_chol_mode(n, n, &b1);
   hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(512), b1, s, P, ldp, hidx, n, Laug, Lf, sc.M,
-                     m1);
-  launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M);  // V = P[:,I] L^-T
+                     m1, sc.Dinv);
+  launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M, false);  // V = P[:,I] L^-T
 }
 
 void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double *partials, int nch, int n,
@@ -910,8 +918,9 @@ void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double
   launch_gemm_mfma(s, 1, 0, 2, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
-  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2);
-  launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W);  // X = V U^-T
+  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2,
+                     sc.Dinv);
+  launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W, false);  // X = V U^-T
   const int nb = (N + 15) / 16;
   const int per = (nb * (nb + 1) / 2 + kInfoPXcds - 1) / kInfoPXcds;
   hipLaunchKernelGGL(k_info_P, dim3(8 * per), dim3(256), 0, s, P, ldp, N, sc.M, sc.W, n, sigma2, w, sc.dx, sc.neg,
