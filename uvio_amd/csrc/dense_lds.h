@@ -132,9 +132,8 @@ __device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
 // through the callables (k = 4 s + kq); the loads of eight k-slabs are issued before their MFMAs, so a
 // chunk costs one memory round trip.  (32-slab chunks measured slower in k_ekf_MS / k_ekf_WP: 24.4 / 10.3
 // against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
-template <class LA, class LB>
+template <class LA, class LB, int U = 8>
 __device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
-  constexpr int U = 8;
   for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
     double a[U], b[U];
 #pragma unroll
@@ -463,62 +462,6 @@ __device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n
   }
 }
 
-// Lane P of every 16-lane row to the whole row: one v_mov_b64_dpp row_newbcast (gfx90a+ DPP64)
-template <int P>
-__device__ __forceinline__ double row_bcast(double v) {
-  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + P, 0xf, 0xf, false);
-}
-__device__ __forceinline__ double row_bcast_i(double v, int p) {  // p: a constant after unrolling
-  switch (p) {
-#define UVHP_RB(P) \
-  case P:          \
-    return row_bcast<P>(v);
-    UVHP_RB(0) UVHP_RB(1) UVHP_RB(2) UVHP_RB(3) UVHP_RB(4) UVHP_RB(5) UVHP_RB(6) UVHP_RB(7)
-    UVHP_RB(8) UVHP_RB(9) UVHP_RB(10) UVHP_RB(11) UVHP_RB(12) UVHP_RB(13) UVHP_RB(14) UVHP_RB(15)
-#undef UVHP_RB
-  }
-  return 0.0;
-}
-// The same column steps with the diagonal block's 16 rows replicated in all four 16-lane rows of slot 0 (lane
-// 16 r + p holds row oJ + p), so the pivot column reaches every lane by row_bcast -- one VALU move per value
-// instead of two v_readlane into SGPRs -- and slots 1.. hold the rows below the block (row oJ + 16 +
-// 64 (s - 1) + lane; a slot whose rows all lie past nrows is skipped).  Same operations in the same order as
-// panel_steps, so the factor is bit-identical.
-template <int S, int K>
-__device__ __forceinline__ void panel_steps_bc(double (&v)[S][16], int oJ, int n, int nrows, int p16, double d) {
-  if constexpr (K < 16) {
-    if (oJ + K >= n) return;
-    const double x = __builtin_amdgcn_rcp(d);
-    const double e = fma(-d, x, 1.0);
-    const double c = v[0][K];
-    const double l0 = c * x;
-    const double l = (p16 > K) ? fma(l0, e, l0) : 0.0;
-    v[0][K] = (p16 > K) ? l : c;
-    double w[16], dn = 0.0;
-    if constexpr (K + 1 < 16) {
-      w[K + 1] = row_bcast<K + 1>(c);
-      v[0][K + 1] = fma(-l, w[K + 1], v[0][K + 1]);
-      dn = row_bcast<K + 1>(v[0][K + 1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int p = K + 2; p < 16; p++) {
-      w[p] = row_bcast_i(c, p);
-      v[0][p] = fma(-l, w[p], v[0][p]);
-    }
-#pragma unroll
-    for (int s = 1; s < S; s++) {
-      if (oJ + 16 + 64 * (s - 1) >= nrows) break;
-      const double ls0 = v[s][K] * x;
-      const double ls = fma(ls0, e, ls0);
-      v[s][K] = ls;
-#pragma unroll
-      for (int p = K + 1; p < 16; p++) v[s][p] = fma(-ls, w[p], v[s][p]);
-    }
-    if constexpr (K + 1 < 16) panel_steps_bc<S, K + 1>(v, oJ, n, nrows, p16, dn);
-  }
-}
-
 // X[k][c] from lane 4c + (k & 3) of the quad (DPP quad_perm broadcast of both halves)
 template <int KK>
 __device__ __forceinline__ double quad_bcast(double v) {
@@ -542,7 +485,7 @@ __device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *A, 
   }
 }
 
-template <int SMAX, class LA, bool BC = false>
+template <int SMAX, class LA>
 __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows, double *Dd, bool with_inv,
                                              double *Xd = nullptr, long long *prof = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -566,30 +509,6 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
             __builtin_amdgcn_s_sleep(1);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        if constexpr (BC) {
-          // slot 0: the block's 16 rows in every 16-lane row; slots 1 .. SMAX: the rows below
-          constexpr int S = SMAX + 1;
-          const int p16 = lane & 15;
-          double v[S][16];
-#pragma unroll
-          for (int s = 0; s < S; s++) {
-            const int ro = s == 0 ? p16 : 16 + 64 * (s - 1) + lane, i = oJ + ro;
-#pragma unroll
-            for (int p = 0; p < 16; p++) v[s][p] = (i < nrows && oJ + p < n && p <= ro) ? A[la(i, oJ + p)] : 0.0;
-          }
-          panel_steps_bc<S, 0>(v, oJ, n, nrows, p16, row_bcast<0>(v[0][0]));
-#pragma unroll
-          for (int p = 0; p < 16; p++)
-            if (lane == p && oJ + p < n) Dd[oJ + p] = v[0][p];
-#pragma unroll
-          for (int s = 0; s < S; s++) {
-            const int ro = s == 0 ? lane : 16 + 64 * (s - 1) + lane, i = oJ + ro;
-            if (s == 0 && lane >= 16) continue;
-#pragma unroll
-            for (int p = 0; p < 16; p++)
-              if (i < nrows && oJ + p < n && p < ro) A[la(i, oJ + p)] = v[s][p];
-          }
-        } else {
         double v[SMAX][16];
 #pragma unroll
         for (int s = 0; s < SMAX; s++) {
@@ -611,7 +530,6 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
 #pragma unroll
           for (int p = 0; p < 16; p++)
             if (i < nrows && oJ + p < n && p < ro) A[la(i, oJ + p)] = v[s][p];
-        }
         }
       }
     } else {

@@ -8,6 +8,7 @@
 // UpdaterUWB (UpdaterUWB.cpp), FeatureDatabase (FeatureDatabase.cpp).
 #pragma once
 #include <chrono>
+#include <atomic>
 #include <functional>
 #include <map>
 #include <memory>
@@ -122,6 +123,9 @@ struct CamTrack {
   size_t cam;
   MeasList m;
 };
+// capacity a new track reserves: one measurement per clone of the window and a few spare (a capacity hint
+// only, set from max_clone_size by the engine): the per-frame appends then do not reallocate as they grow
+inline std::atomic<int> g_track_reserve{0};
 
 struct Feature {
   size_t featid = 0;
@@ -139,7 +143,9 @@ struct Feature {
   CamTrack &track(size_t cam) {
     for (auto &c : tracks)
       if (c.cam == cam) return c;
+    if (tracks.capacity() == 0) tracks.reserve(2);
     tracks.insert(tracks.begin(), CamTrack{cam, {}});
+    if (const int r = g_track_reserve.load(std::memory_order_relaxed)) tracks.front().m.v.reserve((size_t)r);
     return tracks.front();
   }
   const CamTrack *find(size_t cam) const {

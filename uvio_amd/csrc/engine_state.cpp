@@ -91,6 +91,7 @@ static VarP mk(VKind k, int size, int vlen) { return std::make_shared<Var>(k, si
 // State::State (State.cpp:28-166) + UVioManager ctor (UVioManager.cpp:26-58)
 Engine::Engine(const uvio_hp_options_t &o, int device) : o_(o), device_(device) {
   if (o_.num_cameras < 1 || o_.num_cameras > UVIO_HP_MAX_CAMS) throw HpError(UVIO_HP_E_ARG, "num_cameras out of range");
+  g_track_reserve.store(std::max(8, o_.max_clone_size + 4), std::memory_order_relaxed);
   // configurations the reference accepts but this build does not implement fail here, loudly
   if (!o_.use_klt) throw HpError(UVIO_HP_E_CONFIG, "use_klt: false (TrackDescriptor / ORB) is not implemented");
   if (o_.use_aruco) throw HpError(UVIO_HP_E_CONFIG, "use_aruco: true (TrackAruco) is not implemented");

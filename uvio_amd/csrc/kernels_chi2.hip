@@ -244,18 +244,12 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
       const int tj = t - ti * (ti + 1) / 2;
       const int arow = 16 * ti + r16, bcol = 16 * tj + r16;
       const double *ta = Ts + (size_t)min(arow, R - 1) * ldx, *hb = Hs + (size_t)min(bcol, R - 1) * ldx;
+      // 16 k-slabs (64 columns) of loads in flight per round trip: from global memory (rows too long for LDS)
+      // the tile costs ceil(n / 64) memory round trips instead of one per 16 columns; ascending k either way
       dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int k0 = 0; k0 < n; k0 += 16) {
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int k = k0 + 4 * u + kq;
-          a[u] = (arow < R && k < n) ? ta[k] : 0.0;
-          b[u] = (bcol < R && k < n) ? hb[k] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
-      }
+      auto la = [&](int k) { return (arow < R && k < n) ? ta[k] : 0.0; };
+      auto lb = [&](int k) { return (bcol < R && k < n) ? hb[k] : 0.0; };
+      acc = tile_chain<decltype(la), decltype(lb), 16>(0, n, kq, la, lb, acc);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int i = 16 * ti + kq + 4 * q, j = 16 * tj + r16;
@@ -266,12 +260,15 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
   for (int j = tid; j < R; j += blockDim.x) S[R * ldS + j] = Hg[(size_t)j * ldh + n];
   __syncthreads();
   CHI2_TS(1)
-  ldl_blk16(S, ldS, R, R + 1, Lp);
+  // LDL^T with the serial chain on one wave (dense_lds.h ldl_wave): the residual row leaves as
+  // y = D^-1 L_u^-1 r, so chi2 = r^T S^-1 r = sum_k d_k y_k^2
+  double *Dd = Lp;
+  ldl_wave(S, SqLayout{ldS}, R, R + 1, Dd, false);
   CHI2_TS(2)
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {
-    double z = S[R * ldS + k];
-    c2 += z * z / S[k * ldS + k];
+    const double y = S[R * ldS + k];
+    c2 += Dd[k] * (y * y);
   }
   red[tid] = c2;
   __syncthreads();
@@ -321,6 +318,8 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   } else
     hipLaunchKernelGGL(k_gemm_HPg, dim3(8 * ((((n + 15) / 16) * ((m + 15) / 16) + 1) / 2)), dim3(64),
                        sizeof(int) * (size_t)n, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
+  if (max_rows_f + 1 > kWaveMaxRows)
+    throw std::runtime_error("feature with " + std::to_string(max_rows_f) + " rows: wider than the chi2 factorization panel");
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);

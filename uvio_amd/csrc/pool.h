@@ -4,8 +4,14 @@
 // bound at the 20k-40k features of configs 4-5; everything order-dependent (database inserts, erasures,
 // the selected lists) stays sequential in the caller, so results do not depend on the thread count.
 // Threads: UVIO_HP_THREADS, default min(8, hardware threads).
+//
+// A frame issues a dozen parallel loops a few tens of microseconds apart, so a worker that finishes one
+// spins for a while (kSpinUs) on the job generation before it sleeps on the condition variable, and the
+// caller never waits for a worker that has not joined the job: it closes the job when its own share of
+// chunks runs out and waits only for the workers that took part (a late sleeper wakes to a closed job).
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <exception>
@@ -27,7 +33,7 @@ class WorkPool {
   ~WorkPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+      stop_.store(true);
     }
     cv_.notify_all();
     for (auto &t : th_) t.join();
@@ -42,63 +48,83 @@ class WorkPool {
       fn(0, n);
       return;
     }
+    Job job;
+    job.fn = &fn;
+    job.n = n;
+    job.chunk = chunk;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = &fn;
-      n_ = n;
-      chunk_ = chunk;
-      next_.store(0);
-      active_ = (int)th_.size();
-      err_ = nullptr;
-      gen_++;
+      job_ = &job;
+      gen_.fetch_add(1, std::memory_order_release);
+      if (sleeping_ > 0) cv_.notify_all();
     }
-    cv_.notify_all();
-    run_chunks();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return active_ == 0; });
-    job_ = nullptr;
-    if (err_) std::rethrow_exception(err_);
+    run(job);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = nullptr;  // closed: no worker joins from here on
+    }
+    while (job.refs.load(std::memory_order_acquire) != 0) relax();
+    if (job.err) std::rethrow_exception(job.err);
   }
 
  private:
-  void run_chunks() {
+  struct Job {
+    const std::function<void(size_t, size_t)> *fn = nullptr;
+    size_t n = 0, chunk = 1;
+    std::atomic<size_t> next{0};
+    std::atomic<int> refs{0};  // workers inside run()
+    std::mutex err_mu;
+    std::exception_ptr err;
+  };
+  static constexpr int kSpinUs = 200;
+  static void relax() { __builtin_ia32_pause(); }
+  static void run(Job &job) {
     for (;;) {
-      size_t b = next_.fetch_add(chunk_);
-      if (b >= n_) break;
+      const size_t b = job.next.fetch_add(job.chunk);
+      if (b >= job.n) break;
       try {
-        (*job_)(b, std::min(n_, b + chunk_));
+        (*job.fn)(b, std::min(job.n, b + job.chunk));
       } catch (...) {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (!err_) err_ = std::current_exception();
+        std::lock_guard<std::mutex> lk(job.err_mu);
+        if (!job.err) job.err = std::current_exception();
       }
     }
   }
   void worker() {
-    uint64_t seen = 0;
+    uint64_t seen = gen_.load(std::memory_order_acquire);
     for (;;) {
+      // spin for a new job, then sleep
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
+        relax();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
+      }
+      Job *j = nullptr;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
+        if (gen_.load(std::memory_order_relaxed) == seen && !stop_.load()) {
+          sleeping_++;
+          cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_relaxed) != seen; });
+          sleeping_--;
+        }
+        if (stop_.load()) return;
+        seen = gen_.load(std::memory_order_relaxed);
+        j = job_;
+        if (j) j->refs.fetch_add(1, std::memory_order_relaxed);
       }
-      run_chunks();
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (--active_ == 0) done_cv_.notify_one();
+      if (j) {
+        run(*j);
+        j->refs.fetch_sub(1, std::memory_order_release);
       }
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t, size_t)> *job_ = nullptr;
-  size_t n_ = 0, chunk_ = 1;
-  std::atomic<size_t> next_{0};
-  int active_ = 0;
-  std::exception_ptr err_;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::condition_variable cv_;
+  Job *job_ = nullptr;           // the open job (guarded by mu_)
+  std::atomic<uint64_t> gen_{0};  // incremented (under mu_) per job
+  int sleeping_ = 0;             // workers waiting on cv_ (guarded by mu_)
+  std::atomic<bool> stop_{false};
 };
 
 }  // namespace uvhp
