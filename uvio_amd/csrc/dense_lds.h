@@ -485,10 +485,18 @@ __device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *A, 
   }
 }
 
-template <int SMAX, class LA>
+// W > 1 (with SMAX = 1): W panel waves share each 16-column panel.  Every one of them holds the block's own
+// 16 rows in lanes 0 .. 15 (the same arithmetic, so the same values: the pivot column reaches each wave by its
+// own v_readlane) and 48 further rows in lanes 16 .. 63 (wave w: rows 16 + 48 w ..), so a panel of up to
+// 16 + 48 W rows costs one SMAX = 1 column step per column instead of an SMAX = ceil(rows / 64) step; waves
+// W .. are the helpers.  Every value is computed exactly as with W = 1.
+template <int SMAX, class LA, int W = 1>
 __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows, double *Dd, bool with_inv,
                                              double *Xd = nullptr, long long *prof = nullptr) {
+  static_assert(W == 1 || SMAX == 1, "several panel waves hold one slot each");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // this lane's panel row of slot s, relative to the panel's first row
+  auto prow = [&](int s) { return W == 1 ? lane + 64 * s : (lane < 16 ? lane : 16 + 48 * wid + lane - 16); };
   const int r16 = lane & 15, kq = lane >> 4;
   const int nb = (n + 15) / 16, nbr = (nrows + 15) / 16;
   if (!LA::square) with_inv = false;
@@ -501,8 +509,8 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
     const int P = J - 1;
     if (P >= 0 && J < nb) coltarget += nbr - J;
     const long long tslot = prof ? (long long)clock64() : 0;
-    if (wid == 0) {
-      if (J < nb) {
+    if (wid < W) {
+      if (J < nb && (wid == 0 || 16 + 48 * wid < nrows - 16 * J)) {
         const int oJ = 16 * J;
         if (P >= 0) {
           while (__hip_atomic_load(&colcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < coltarget)
@@ -512,7 +520,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         double v[SMAX][16];
 #pragma unroll
         for (int s = 0; s < SMAX; s++) {
-          const int ro = lane + 64 * s, i = oJ + ro;
+          const int ro = prow(s), i = oJ + ro;
 #pragma unroll
           for (int p = 0; p < 16; p++) v[s][p] = (i < nrows && oJ + p < n && p <= ro) ? A[la(i, oJ + p)] : 0.0;
         }
@@ -523,20 +531,21 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         // the pivots: lane p < 16 still holds d_p on its diagonal (step p leaves its own row as it is)
 #pragma unroll
         for (int p = 0; p < 16; p++)
-          if (lane == p && oJ + p < n) Dd[oJ + p] = v[0][p];
+          if (wid == 0 && lane == p && oJ + p < n) Dd[oJ + p] = v[0][p];
 #pragma unroll
         for (int s = 0; s < SMAX; s++) {
-          const int ro = lane + 64 * s, i = oJ + ro;
+          const int ro = prow(s), i = oJ + ro;
+          if (W > 1 && wid > 0 && lane < 16) continue;  // the block's own rows: wave 0 stores them
 #pragma unroll
           for (int p = 0; p < 16; p++)
             if (i < nrows && oJ + p < n && p < ro) A[la(i, oJ + p)] = v[s][p];
         }
       }
     } else {
-      const int nh = nw - 1;
-      // the rank-16 update of block column J by block P (wave 0 waits for it), one tile per helper
+      const int nh = nw - W, hw = wid - W;
+      // the rank-16 update of block column J by block P (the panel waves wait for it), one tile per helper
       if (P >= 0 && J < nb) {
-        for (int I = J + wid - 1; I < nbr; I += nh) {
+        for (int I = J + hw; I < nbr; I += nh) {
           dbl4 acc = tile_load_lower(A, la, 16 * I, 16 * J, nrows, n, kq, r16);
           acc = tile_rank16(A, la, Dd, 16 * I, 16 * J, 16 * P, nrows, n, kq, r16, acc);
           tile_store_lower(A, la, 16 * I, 16 * J, nrows, n, kq, r16, acc);
@@ -552,7 +561,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
       if (P >= 0 && P < nb)
         for (int C = J + 1; C < nb; C++) ntr += nbr - C;
       const int ntask = (do_xd ? 1 : 0) + nxo + ntr;
-      for (int t = wid - 1; t < ntask; t += nh) {
+      for (int t = hw; t < ntask; t += nh) {
         int u = t;
         if (do_xd && u == 0) {
           // X_PP = L_PP^-1 (unit lower), right-looking, no divisions: lane 4c + q keeps column c's entries
@@ -635,7 +644,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         tile_store_lower(A, la, 16 * I, 16 * C, nrows, n, kq, r16, acc);
       }
     }
-    if (prof && lane == 0 && wid < 2 && J < 32) prof[32 * wid + J] = (long long)clock64() - tslot;  // debug timing
+    if (prof && lane == 0 && (wid == 0 || wid == W) && J < 32) prof[wid ? 32 + J : J] = (long long)clock64() - tslot;
     __syncthreads();
   }
 }
