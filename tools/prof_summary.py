@@ -9,7 +9,8 @@ ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'
 last_torch = max([i for i, e in enumerate(ev) if 'at::' in e[2]] + [-1])
 seg = ev[last_torch + 1:]
 if nframes <= 0:  # image workloads: one equalizeHist launch per frame; TrackSIM workloads: one propagation per frame
-    nframes = max(sum(1 for e in seg if 'k_hist_multi' in e[2]), sum(1 for e in seg if 'k_clone' in e[2]), 1)
+    nframes = max(sum(1 for e in seg if 'k_hist_multi' in e[2]),
+                  sum(1 for e in seg if 'k_clone' in e[2] or 'k_prop_clone' in e[2]), 1)
 t0, t1 = seg[0][0], seg[-1][1]
 busy, cur = 0, t0
 for s, e, n, g in seg:

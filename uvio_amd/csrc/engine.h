@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <unordered_map>
 #include <algorithm>
 #include <cstdlib>
@@ -62,6 +63,8 @@ struct MeasList {
   size_t b = 0;         // first live entry
   bool sorted = true;   // live entries in non-decreasing time (every in-order stream); the time searches
                         // (contains / drop_through) fall back to the reference's linear scans otherwise
+  double tf = 0, tl = 0;  // times of the first and the last live entry (valid when not empty): the selection
+                          // scans over every feature decide from these without touching the storage
   using iterator = std::vector<FeatMeas>::iterator;
   using const_iterator = std::vector<FeatMeas>::const_iterator;
   size_t size() const { return v.size() - b; }
@@ -75,13 +78,20 @@ struct MeasList {
   iterator end() { return v.end(); }
   const_iterator begin() const { return v.begin() + (std::ptrdiff_t)b; }
   const_iterator end() const { return v.end(); }
+  double last_t() const { return tl; }
   void push_back(const FeatMeas &x) {
-    if (v.size() > b && x.t < v.back().t) sorted = false;
+    if (v.size() == b)
+      tf = x.t;
+    else if (x.t < tl)
+      sorted = false;
     v.push_back(x);
+    tl = x.t;
   }
   // a live entry at time t (FeatureDatabase::features_containing's std::find, FeatureDatabase.cpp:169-208)
   bool contains(double t) const {
     if (sorted) {
+      if (empty() || t < tf || t > tl) return false;
+      if (t == tf || t == tl) return true;
       auto it = std::lower_bound(begin(), end(), t, [](const FeatMeas &x, double tt) { return x.t < tt; });
       return it != end() && it->t == t;
     }
@@ -101,14 +111,23 @@ struct MeasList {
       if (!(v[i].t <= t)) v[w++] = v[i];
     v.resize(w);
     if (v.size() == b) clear();
+    recache();
+  }
+  void recache() {
+    if (v.size() > b) tf = v[b].t, tl = v.back().t;
   }
   void clear() {
     v.clear();
     b = 0;
     sorted = true;
   }
-  iterator erase(iterator first, iterator last) { return v.erase(first, last); }
+  iterator erase(iterator first, iterator last) {  // (callers may have rewritten entries through iterators)
+    auto r = v.erase(first, last);
+    recache();
+    return r;
+  }
   void drop_front(size_t k) {  // remove the k oldest live entries
+    if (k == 0) return;
     b += k;
     if (b == v.size()) {
       clear();
@@ -116,12 +135,33 @@ struct MeasList {
       v.erase(v.begin(), v.begin() + (std::ptrdiff_t)b);
       b = 0;
     }
+    recache();
   }
   void keep_if_valid(const std::vector<double> &valid);  // keep the entries whose time is in `valid` (sorted)
 };
 struct CamTrack {
   size_t cam;
   MeasList m;
+};
+// A feature's per-camera tracks, stored in the feature object (no separate allocation: a scan over every
+// feature of the database touches one object per feature), in the reference's iteration order (below)
+struct TrackSet {
+  CamTrack t[UVIO_HP_MAX_CAMS];
+  int n = 0;
+  CamTrack *begin() { return t; }
+  CamTrack *end() { return t + n; }
+  const CamTrack *begin() const { return t; }
+  const CamTrack *end() const { return t + n; }
+  size_t size() const { return (size_t)n; }
+  bool empty() const { return n == 0; }
+  CamTrack &front() { return t[0]; }
+  CamTrack &insert_front(size_t cam) {
+    if (n >= UVIO_HP_MAX_CAMS) throw std::runtime_error("feature observed by more than UVIO_HP_MAX_CAMS cameras");
+    for (int i = n; i > 0; i--) t[i] = std::move(t[i - 1]);
+    t[0] = CamTrack{cam, {}};
+    n++;
+    return t[0];
+  }
 };
 // capacity a new track reserves: one measurement per clone of the window and a few spare (a capacity hint
 // only, set from max_clone_size by the engine): the per-frame appends then do not reallocate as they grow
@@ -136,17 +176,16 @@ struct Feature {
   // with libstdc++ and at most UVIO_HP_MAX_CAMS small integer keys every key sits in its own bucket and
   // a new key is linked at the list front, so iteration runs in reverse first-insertion order
   // (tests/test_oracle.py pins this) -- a camera's first measurement inserts its track at the front.
-  std::vector<CamTrack> tracks;
+  TrackSet tracks;
   int anchor_cam_id = -1;
   double anchor_clone_timestamp = -1;
   double p_FinA[3] = {0, 0, 0}, p_FinG[3] = {0, 0, 0};
   CamTrack &track(size_t cam) {
     for (auto &c : tracks)
       if (c.cam == cam) return c;
-    if (tracks.capacity() == 0) tracks.reserve(2);
-    tracks.insert(tracks.begin(), CamTrack{cam, {}});
-    if (const int r = g_track_reserve.load(std::memory_order_relaxed)) tracks.front().m.v.reserve((size_t)r);
-    return tracks.front();
+    CamTrack &c = tracks.insert_front(cam);
+    if (const int r = g_track_reserve.load(std::memory_order_relaxed)) c.m.v.reserve((size_t)r);
+    return c;
   }
   const CamTrack *find(size_t cam) const {
     for (auto &c : tracks)

@@ -75,6 +75,7 @@ void MeasList::keep_if_valid(const std::vector<double> &valid) {
     if (std::binary_search(valid.begin(), valid.end(), v[i].t)) v[w++] = v[i];
   v.resize(w);
   if (v.size() == b) clear();
+  recache();
 }
 // Feature::clean_old_measurements (Feature.cpp:37-60): keep the measurements at the given (sorted) times
 void Feature::clean_old_measurements(const std::vector<double> &valid) {
@@ -516,7 +517,8 @@ void Engine::check_neg_diag(const char *who) {
 bool Engine::cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                                  const std::vector<double> &Q, bool do_dt, const double *ddnc) {
   const int q = (int)iold.size();
-  if (p > 64 || q > 256 || N_ + 6 > d_.ldp || N_ * p > 4096 || std::getenv("UVIO_HP_NO_PROP_FUSE")) return false;
+  if (p > 64 || q > 256 || N_ + 6 > d_.ldp || (long long)N_ * p * q > 120000 || std::getenv("UVIO_HP_NO_PROP_FUSE"))
+    return false;  // (the bound is launch_prop_clone's kPropCloneMaxWork)
   const double *dPhi = stage(Phi.data(), (size_t)p * q);
   const double *dQ = stage(Q.data(), (size_t)p * p);
   const int *diold = stage(iold.data(), (size_t)q);

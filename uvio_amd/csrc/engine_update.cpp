@@ -253,7 +253,8 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
         const uint32_t i0 = start[w], i1 = start[w + 1];
         for (uint32_t i = i0; i < i1; i++) {
           if (i + 16 < i1) __builtin_prefetch(fp[order[i + 16]], 1);
-          if (i + 8 < i1) __builtin_prefetch(fp[order[i + 8]]->tracks.data(), 1);
+          if (i + 8 < i1)
+            for (const CamTrack &c : fp[order[i + 8]]->tracks) __builtin_prefetch(c.m.v.data() + c.m.v.size(), 1);
           const size_t k = order[i];
           fp[k]->track((size_t)cam_of[k]).m.push_back(
               FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
@@ -445,13 +446,12 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
         // software pipeline over the dependent misses: map node -> feature -> track array
-        if (i + 12 < e) __builtin_prefetch(all[i + 12].first->get());
-        if (i + 6 < e) __builtin_prefetch((*all[i + 6].first)->tracks.data());
+        if (i + 8 < e) __builtin_prefetch(all[i + 8].first->get());
         const Feature &f = **all[i].first;
         if (f.to_delete) continue;
         bool newer = false, has = false;
         for (auto &p : f.tracks) {
-          newer = (!p.m.empty() && p.m.back().t >= ts);
+          newer = (!p.m.empty() && p.m.last_t() >= ts);
           if (newer) break;
         }
         if (do_marg)
@@ -650,8 +650,7 @@ void Engine::cleanup_measurements(double t, bool skip_held) {
   std::vector<uint8_t> empty(all.size(), 0);
   pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
     for (size_t i = b; i < e; i++) {
-      if (i + 12 < e) __builtin_prefetch(all[i + 12], 1);
-      if (i + 6 < e) __builtin_prefetch(all[i + 6]->tracks.data(), 1);
+      if (i + 8 < e) __builtin_prefetch(all[i + 8], 1);
       if (skip_held && all[i]->held) continue;
       all[i]->clean_older_measurements(t);
       empty[i] = all[i]->count() < 1;

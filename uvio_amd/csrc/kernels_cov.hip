@@ -100,9 +100,10 @@ __global__ void k_clone(double *__restrict__ P, int ld, int N, int src0, int dt_
 // EKFPropagation of the contiguous block s0 .. s0+p-1 and the IMU-pose clone in ONE workgroup launch: the three
 // phases above (T, the block write, the clone) with a workgroup barrier between them instead of a kernel
 // boundary, each element computed by the same expression as in k_prop_T / k_prop_write / k_clone (so the
-// result is bit-identical).  For the small propagations (N p <= kPropCloneMaxNp): one CU does them in about
-// the time of the first launch alone and the frame loses two launches.
-constexpr int kPropCloneThreads = 1024, kPropCloneMaxNp = 4096;
+// result is bit-identical).  For the small propagations (N p q <= kPropCloneMaxWork multiply-adds in the T
+// phase, e.g. N = 314, p = q = 15 at cfg3): one CU does them in about the time of the first launch alone and
+// the frame loses two launches.
+constexpr int kPropCloneThreads = 1024, kPropCloneMaxWork = 120000;
 __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__restrict__ P, int ld, int N, int s0, int p,
                                                                   const int *__restrict__ iold, int q,
                                                                   const double *__restrict__ Phi,
@@ -159,7 +160,7 @@ __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__rest
 bool launch_prop_clone(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
                        const double *Phi, const double *Q, double *T, int src0, int dt_id, const double *dnc_dev,
                        int do_dt) {
-  if (N * p > kPropCloneMaxNp) return false;
+  if ((long long)N * p * q > kPropCloneMaxWork) return false;
   hipLaunchKernelGGL(k_prop_clone, dim3(1), dim3(kPropCloneThreads), 0, s, P, ld, N, s0, p, iold, q, Phi, Q, T, src0,
                      dt_id, dnc_dev, do_dt);
   return true;
