@@ -662,5 +662,11 @@ __device__ __forceinline__ void ldl_wave(double *A, LA la, int n, int nrows, dou
     ldl_wave_inv<4>(A, la, n, nrows, Dd, with_inv);
 }
 constexpr int kWaveMaxRows = 256;  // ldl_wave's panel capacity (4 rows per lane)
+// The single-workgroup factor kernels (k_ekf_fact, k_info_cholP / Z): 16 waves, W = panel_waves(rows) of them
+// share each panel (ldl_wave_inv<1, LA, W>), the rest are helpers.  On MI355X (tools/bench_wave_slots.hip,
+// profiles/r04j_ldl_panel_waves.txt) r = 100 with the inverse: 102k -> 89k cycles, r = 135: 126k -> 97k.
+constexpr int kFactThreads = 1024;
+__host__ __device__ constexpr int panel_waves(int rows) { return rows <= 64 ? 1 : (rows - 16 + 47) / 48; }
+static_assert(panel_waves(kWaveMaxRows) <= 5, "panel waves of the largest factor");
 
 }  // namespace uvhp

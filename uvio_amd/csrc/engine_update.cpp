@@ -428,26 +428,31 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
 
   std::vector<FeatP> feats_lost, feats_marg, feats_slam;
   auto t_sel = clk::now();
-  // FeatureDatabase::features_not_containing_newer(t, false, true)
-  // (and features_containing(margtimestep)): per-feature flags on the pool, lists built in db_ order
-  std::unordered_set<const Feature *> in_marg;
+  // FeatureDatabase::features_not_containing_newer(t, false, true) and features_containing(margtimestep), then
+  // VioManager.cpp:377-392's filter of the lost list (a track in one of this frame's cameras, not in the marg
+  // list): per-feature flags on the pool, lists built in db_ order
   {
     const bool do_marg = (int)clones_.size() > o_.max_clone_size || (int)clones_.size() > 5;
     const double mt = do_marg ? margtimestep() : 0.0, ts = timestamp_;
     // pointers to the map's values (no shared_ptr copies: a reference-count round trip per feature
     // costs more than the scan at cfg4's database sizes); nothing inserts into db_ during the scan
-    std::vector<std::pair<const FeatP *, uint8_t>> all;  // feature, bit 0 lost, bit 1 marg
+    std::vector<const FeatP *> all;  // the map's values in db_ order
+    std::vector<const Feature *> fs;  // the features themselves (the scan reads no map node)
     all.reserve(db_.size());
+    fs.reserve(db_.size());
     {
       HPROF("select.walk");
-      for (auto &kv : db_) all.emplace_back(&kv.second, 0);
+      for (auto &kv : db_) {
+        all.push_back(&kv.second);
+        fs.push_back(kv.second.get());
+      }
     }
     HPROF("select.flags");
+    std::vector<uint8_t> flag(all.size(), 0);  // bit 0 lost, bit 1 marg
     pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) {
-        // software pipeline over the dependent misses: map node -> feature -> track array
-        if (i + 8 < e) __builtin_prefetch(all[i + 8].first->get());
-        const Feature &f = **all[i].first;
+        if (i + 8 < e) __builtin_prefetch(fs[i + 8]);
+        const Feature &f = *fs[i];
         if (f.to_delete) continue;
         bool newer = false, has = false;
         for (auto &p : f.tracks) {
@@ -459,29 +464,23 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
             has = p.m.contains(mt);  // binary search on an in-order track
             if (has) break;
           }
-        all[i].second = (uint8_t)((newer ? 0 : 1) | (has ? 2 : 0));
+        bool lost = !newer && !has;
+        if (lost) {
+          bool found = false;
+          for (auto &p : f.tracks)
+            if (std::find(camids.begin(), camids.end(), (int)p.cam) != camids.end()) {
+              found = true;
+              break;
+            }
+          lost = found;
+        }
+        flag[i] = (uint8_t)((lost ? 1 : 0) | (has ? 2 : 0));
       }
     });
-    for (auto &a : all) {
-      if (a.second & 1) feats_lost.push_back(*a.first);
-      if (a.second & 2) {
-        feats_marg.push_back(*a.first);
-        in_marg.insert(a.first->get());
-      }
+    for (size_t i = 0; i < all.size(); i++) {
+      if (flag[i] & 1) feats_lost.push_back(*all[i]);
+      if (flag[i] & 2) feats_marg.push_back(*all[i]);
     }
-  }
-  {
-    std::vector<FeatP> keep;
-    for (auto &f : feats_lost) {
-      bool found = false;
-      for (auto &p : f->tracks)
-        if (std::find(camids.begin(), camids.end(), (int)p.cam) != camids.end()) {
-          found = true;
-          break;
-        }
-      if (found && !in_marg.count(f.get())) keep.push_back(f);
-    }
-    feats_lost = keep;
   }
   std::vector<FeatP> feats_maxtracks;
   {

@@ -678,9 +678,9 @@ static void launch_gemm_mfma(hipStream_t s, int ta, int tb, int tri, int symA, i
 // Dinv: the inverses of L_c's 16 x 16 diagonal blocks for k_trsm_lt (k_trinv16's layout: block b row-major at
 // Dinv + 256 b, rows past n identity), D^-1/2 times the unit-lower block inverses the factorization forms
 // on its helper waves -- the solve that follows needs no k_trinv16 launch.
-template <int SMAX, class LA>
+template <int W, class LA>
 __device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int n, int nrows, double *Dinv) {
-  ldl_wave_inv<SMAX>(A, la, n, nrows, Dd, false, Dinv);
+  ldl_wave_inv<1, LA, W>(A, la, n, nrows, Dd, false, Dinv);
   for (int k = threadIdx.x; k < n; k += blockDim.x) Dd[k] = sqrt(Dd[k]);  // sqrt(d)
   __syncthreads();
   const int nb = (n + 15) / 16;
@@ -692,8 +692,8 @@ __device__ __forceinline__ void info_chol_body(double *A, LA la, double *Dd, int
 
 // P_II = P[hidx, hidx] = L_P L_P^T.  Writes Laug = diag(L_P, 1) ((n+1) x (n+1), zero upper) and L_P (n x n).
 // MODE: the storage (compile-time, so LDS accesses are DS instructions rather than FLAT)
-template <int SMAX, int MODE>
-__global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
+template <int W, int MODE>
+__global__ void __launch_bounds__(kFactThreads) k_info_cholP(const double *__restrict__ P, int ldp, const int *__restrict__ hidx,
                                                     int n, double *__restrict__ Laug, double *__restrict__ Lout,
                                                     double *gbuf, int mode, double *__restrict__ Dinv) {
   constexpr int PACKED = MODE == 1;
@@ -716,9 +716,9 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
       });
   __syncthreads();
   if constexpr (PACKED)
-    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n, Dinv);
+    info_chol_body<W>(A, PkLayout{}, Dd, n, n, Dinv);
   else
-    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n, Dinv);
+    info_chol_body<W>(A, SqLayout{ld}, Dd, n, n, Dinv);
   const int na = n + 1;
   for (int e = threadIdx.x; e < na * na; e += blockDim.x) {
     const int a = e / na, b = e - a * na;
@@ -732,8 +732,8 @@ __global__ void __launch_bounds__(512) k_info_cholP(const double *__restrict__ P
 
 // [E c; c^T .] = Laug^T G Laug;  Z = E + s2 I = U U^T with the augmented row c^T -> w = U^-1 c.
 // Writes U (n x n, ld n) and w (n).
-template <int SMAX, int MODE>
-__global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E, int n, double s2,
+template <int W, int MODE>
+__global__ void __launch_bounds__(kFactThreads) k_info_cholZ(const double *__restrict__ E, int n, double s2,
                                                     double *__restrict__ Uout, double *__restrict__ w, double *gbuf,
                                                     int mode, double *__restrict__ Dinv) {
   constexpr int PACKED = MODE == 1;
@@ -757,9 +757,9 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
       });
   __syncthreads();
   if constexpr (PACKED)
-    info_chol_body<SMAX>(A, PkLayout{}, Dd, n, n + 1, Dinv);
+    info_chol_body<W>(A, PkLayout{}, Dd, n, n + 1, Dinv);
   else
-    info_chol_body<SMAX>(A, SqLayout{ld}, Dd, n, n + 1, Dinv);
+    info_chol_body<W>(A, SqLayout{ld}, Dd, n, n + 1, Dinv);
   for (int j = threadIdx.x; j < n; j += blockDim.x) w[j] = A[idx(n, j)] * Dd[j];
   for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
     const int a = e / n, b = e - a * n;
@@ -768,20 +768,21 @@ __global__ void __launch_bounds__(512) k_info_cholZ(const double *__restrict__ E
 }
 // the instantiation for a factor of `rows` rows (panel rows per lane) and storage mode
 template <class KP>
-static KP pick_info_kernel(const KP (&tab)[4][3], int rows, int mode) {
-  const int si = rows <= 64 ? 0 : rows <= 128 ? 1 : rows <= 192 ? 2 : 3;
-  return tab[si][mode];
+static KP pick_info_kernel(const KP (&tab)[5][3], int rows, int mode) {
+  return tab[panel_waves(rows) - 1][mode];
 }
 typedef void (*CholPFn)(const double *, int, const int *, int, double *, double *, double *, int, double *);
 typedef void (*CholZFn)(const double *, int, double, double *, double *, double *, int, double *);
-static const CholPFn kCholP[4][3] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>, k_info_cholP<1, 2>},
+static const CholPFn kCholP[5][3] = {{k_info_cholP<1, 0>, k_info_cholP<1, 1>, k_info_cholP<1, 2>},
                                      {k_info_cholP<2, 0>, k_info_cholP<2, 1>, k_info_cholP<2, 2>},
                                      {k_info_cholP<3, 0>, k_info_cholP<3, 1>, k_info_cholP<3, 2>},
-                                     {k_info_cholP<4, 0>, k_info_cholP<4, 1>, k_info_cholP<4, 2>}};
-static const CholZFn kCholZ[4][3] = {{k_info_cholZ<1, 0>, k_info_cholZ<1, 1>, k_info_cholZ<1, 2>},
+                                     {k_info_cholP<4, 0>, k_info_cholP<4, 1>, k_info_cholP<4, 2>},
+                                     {k_info_cholP<5, 0>, k_info_cholP<5, 1>, k_info_cholP<5, 2>}};
+static const CholZFn kCholZ[5][3] = {{k_info_cholZ<1, 0>, k_info_cholZ<1, 1>, k_info_cholZ<1, 2>},
                                      {k_info_cholZ<2, 0>, k_info_cholZ<2, 1>, k_info_cholZ<2, 2>},
                                      {k_info_cholZ<3, 0>, k_info_cholZ<3, 1>, k_info_cholZ<3, 2>},
-                                     {k_info_cholZ<4, 0>, k_info_cholZ<4, 1>, k_info_cholZ<4, 2>}};
+                                     {k_info_cholZ<4, 0>, k_info_cholZ<4, 1>, k_info_cholZ<4, 2>},
+                                     {k_info_cholZ<5, 0>, k_info_cholZ<5, 1>, k_info_cholZ<5, 2>}};
 
 // storage mode and dynamic LDS bytes of an info-form factor of nrows x n (+ the n doubles of D)
 static int info_chol_mode(int nrows, int n, size_t *bytes) {
@@ -900,7 +901,7 @@ void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, 
   if (n + 1 > kWaveMaxRows) throw std::runtime_error("information-form update wider than the factorization panel");
   size_t b1 = 0;
   const int m1 = info_chol_mode(n, n, &b1);
-  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(512), b1, s, P, ldp, hidx, n, Laug, Lf, sc.M,
+  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(kFactThreads), b1, s, P, ldp, hidx, n, Laug, Lf, sc.M,
                      m1, sc.Dinv);
   launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M, false);  // V = P[:,I] L^-T
 }
@@ -919,7 +920,7 @@ void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double
   launch_gemm_mfma(s, 1, 0, 2, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
-  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(512), b2, s, E, n, sigma2, Uf, w, sc.W, m2,
+  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(kFactThreads), b2, s, E, n, sigma2, Uf, w, sc.W, m2,
                      sc.Dinv);
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W, false);  // X = V U^-T
   const int nb = (N + 15) / 16;
@@ -1014,7 +1015,7 @@ static void ensure_lds_attrs() {
   if (done) return;
   if (set_dyn_lds((const void *)k_gram_reduce_chol, 150 * 1024) < 150 * 1024)
     throw std::runtime_error("dynamic LDS limit not granted for k_gram_reduce_chol");
-  for (int a = 0; a < 4; a++)
+  for (int a = 0; a < 5; a++)
     for (int b = 0; b < 2; b++)
       if (set_dyn_lds((const void *)kCholP[a][b], kMaxDynLds) < kMaxDynLds ||
           set_dyn_lds((const void *)kCholZ[a][b], kMaxDynLds) < kMaxDynLds)

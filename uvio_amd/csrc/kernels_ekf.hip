@@ -175,8 +175,9 @@ static size_t ekf_ms_lds_bytes(int n, bool with_S) {
 // fixed order against thr -> *chi2_gate (the P-update gate) and [chi2, accepted] into gate_out[0..1].
 // LDS: the factor in LDS (a compile-time choice, so every access of the factorization is a DS instruction;
 // a runtime choice makes them all FLAT)
-template <int SMAX, bool LDS>
-__global__ void __launch_bounds__(512) k_ekf_fact(const double *__restrict__ Sup, int r,
+// W: the panel waves of ldl_wave_inv (panel rows 16 + 48 W); one workgroup of kFactThreads.
+template <int W, bool LDS>
+__global__ void __launch_bounds__(kFactThreads) k_ekf_fact(const double *__restrict__ Sup, int r,
                                                   const double *__restrict__ res, int res_stride,
                                                   double *__restrict__ Linv_out, double *__restrict__ y_out, double *Sg,
                                                   int use_lds, int *chi2_gate, double chi2_thr,
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(512) k_ekf_fact(const double *__restrict__ Sup
         }
       });
   __syncthreads();
-  ldl_wave_inv<SMAX>(A, SqLayout{ld}, r, r + 1, Dd, true);
+  ldl_wave_inv<1, SqLayout, W>(A, SqLayout{ld}, r, r + 1, Dd, true);
   for (int k = threadIdx.x; k < r; k += blockDim.x) {
     const double q = sqrt(Dd[k]);
     sd[k] = q;
@@ -367,10 +368,11 @@ void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, co
 static void ensure_ekf_lds_attrs() {
   static bool done = false;
   if (done) return;
-  const void *fns[6] = {(const void *)k_ekf_MS,            (const void *)k_ekf_WP,
+  const void *fns[7] = {(const void *)k_ekf_MS,            (const void *)k_ekf_WP,
                         (const void *)k_ekf_fact<1, true>, (const void *)k_ekf_fact<2, true>,
-                        (const void *)k_ekf_fact<3, true>, (const void *)k_ekf_fact<4, true>};
-  for (int k = 0; k < 6; k++)
+                        (const void *)k_ekf_fact<3, true>, (const void *)k_ekf_fact<4, true>,
+                        (const void *)k_ekf_fact<5, true>};
+  for (int k = 0; k < 7; k++)
     if (set_dyn_lds(fns[k], kMaxDynLds) < kMaxDynLds)
       throw std::runtime_error("dynamic LDS limit not granted for an EKF kernel (" + std::to_string(k) + ")");
   done = true;
@@ -414,17 +416,13 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   double *Sg = sc.S + 3 * (size_t)r * r;  // (r+1)(r|1) + 2r <= 2 r^2 doubles once r >= 40 (else LDS)
   {
     KScope ks(sc.kp, KC_LDL);
-    const int rows = r + 1;
-    auto *kf = use_lds ? (rows <= 64    ? k_ekf_fact<1, true>
-                          : rows <= 128 ? k_ekf_fact<2, true>
-                          : rows <= 192 ? k_ekf_fact<3, true>
-                                        : k_ekf_fact<4, true>)
-                       : (rows <= 64    ? k_ekf_fact<1, false>
-                          : rows <= 128 ? k_ekf_fact<2, false>
-                          : rows <= 192 ? k_ekf_fact<3, false>
-                                        : k_ekf_fact<4, false>);
-    hipLaunchKernelGGL(kf, dim3(1), dim3(512), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg, use_lds,
-                       sc.chi2_gate, sc.chi2_thr, sc.dx + N);
+    const int w = panel_waves(r + 1);
+    auto *kf = use_lds ? (w == 1 ? k_ekf_fact<1, true> : w == 2 ? k_ekf_fact<2, true> : w == 3 ? k_ekf_fact<3, true>
+                          : w == 4 ? k_ekf_fact<4, true> : k_ekf_fact<5, true>)
+                       : (w == 1 ? k_ekf_fact<1, false> : w == 2 ? k_ekf_fact<2, false> : w == 3 ? k_ekf_fact<3, false>
+                          : w == 4 ? k_ekf_fact<4, false> : k_ekf_fact<5, false>);
+    hipLaunchKernelGGL(kf, dim3(1), dim3(kFactThreads), use_lds ? bytes : 0, s, Sup, r, res, res_stride, Linv, sc.y, Sg,
+                       use_lds, sc.chi2_gate, sc.chi2_thr, sc.dx + N);
   }
   // LDL^T of the r x r innovation covariance with the residual as an extra row: r^3/3 + r^2 FLOPs; the
   // lower triangle and the residual read, the factor written
