@@ -517,8 +517,8 @@ void Engine::check_neg_diag(const char *who) {
 bool Engine::cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                                  const std::vector<double> &Q, bool do_dt, const double *ddnc) {
   const int q = (int)iold.size();
-  if (p > 64 || q > 256 || N_ + 6 > d_.ldp || (long long)N_ * p * q > 120000 || std::getenv("UVIO_HP_NO_PROP_FUSE"))
-    return false;  // (the bound is launch_prop_clone's kPropCloneMaxWork)
+  if (p > 48 || q > 48 || N_ + 6 > d_.ldp || N_ * p > 8 * 1024 || std::getenv("UVIO_HP_NO_PROP_FUSE"))
+    return false;  // (launch_prop_clone's bounds)
   const double *dPhi = stage(Phi.data(), (size_t)p * q);
   const double *dQ = stage(Q.data(), (size_t)p * p);
   const int *diold = stage(iold.data(), (size_t)q);

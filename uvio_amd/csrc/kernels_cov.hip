@@ -100,30 +100,56 @@ __global__ void k_clone(double *__restrict__ P, int ld, int N, int src0, int dt_
 // EKFPropagation of the contiguous block s0 .. s0+p-1 and the IMU-pose clone in ONE workgroup launch: the three
 // phases above (T, the block write, the clone) with a workgroup barrier between them instead of a kernel
 // boundary, each element computed by the same expression as in k_prop_T / k_prop_write / k_clone (so the
-// result is bit-identical).  For the small propagations (N p q <= kPropCloneMaxWork multiply-adds in the T
-// phase, e.g. N = 314, p = q = 15 at cfg3): one CU does them in about the time of the first launch alone and
+// result is bit-identical).  For the propagations of up to 8 T elements per thread and p, q <= 48 (cfg2-4):
 // the frame loses two launches.
-constexpr int kPropCloneThreads = 1024, kPropCloneMaxWork = 120000;
+constexpr int kPropCloneThreads = 1024, kPropCloneMaxEl = 8, kPropCloneMaxPQ = 48;
 __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__restrict__ P, int ld, int N, int s0, int p,
                                                                   const int *__restrict__ iold, int q,
                                                                   const double *__restrict__ Phi,
                                                                   const double *__restrict__ Q, double *__restrict__ T,
                                                                   int src0, int dt_id, const double *__restrict__ dnc,
                                                                   int do_dt) {
-  for (int idx = threadIdx.x; idx < N * p; idx += blockDim.x) {
-    const int i = idx / p, a = idx % p;
-    const double *Pi = P + (size_t)i * ld;
-    double acc = 0.0;
-    for (int b = 0; b < q; b++) acc += Pi[iold[b]] * Phi[a * q + b];
-    T[(size_t)i * p + a] = acc;
+  // Phi, Q and the column map in LDS: every P load below depends on nothing but an LDS read
+  __shared__ double sPhi[kPropCloneMaxPQ * kPropCloneMaxPQ], sQ[kPropCloneMaxPQ * kPropCloneMaxPQ];
+  __shared__ int siold[kPropCloneMaxPQ];
+  for (int e = threadIdx.x; e < p * q; e += blockDim.x) sPhi[e] = Phi[e];
+  for (int e = threadIdx.x; e < p * p; e += blockDim.x) sQ[e] = Q[e];
+  for (int e = threadIdx.x; e < q; e += blockDim.x) siold[e] = iold[e];
+  __syncthreads();
+  // T: a thread's (up to kPropCloneMaxEl) elements advance together, so their P loads of one b are in flight at
+  // once; each element's sum runs over b in ascending order, as in k_prop_T
+  {
+    double acc[kPropCloneMaxEl];
+    const double *Pi[kPropCloneMaxEl];
+    int ai[kPropCloneMaxEl];
+#pragma unroll
+    for (int e = 0; e < kPropCloneMaxEl; e++) {
+      const int idx = min((int)threadIdx.x + e * (int)blockDim.x, N * p - 1);
+      Pi[e] = P + (size_t)(idx / p) * ld;
+      ai[e] = idx % p;
+      acc[e] = 0.0;
+    }
+    for (int b = 0; b < q; b++) {
+      const int c = siold[b];
+      double v[kPropCloneMaxEl];
+#pragma unroll
+      for (int e = 0; e < kPropCloneMaxEl; e++) v[e] = Pi[e][c];
+#pragma unroll
+      for (int e = 0; e < kPropCloneMaxEl; e++) acc[e] += v[e] * sPhi[ai[e] * q + b];
+    }
+#pragma unroll
+    for (int e = 0; e < kPropCloneMaxEl; e++) {
+      const int idx = threadIdx.x + e * blockDim.x;
+      if (idx < N * p) T[idx] = acc[e];
+    }
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < N * p; idx += blockDim.x) {
     const int i = idx / p, a = idx % p, col = s0 + a;
     if (i >= s0 && i < s0 + p) {
       const int x = i - s0;
-      double acc = (x <= a) ? Q[x * p + a] : Q[a * p + x];
-      for (int c = 0; c < q; c++) acc += Phi[x * q + c] * T[(size_t)iold[c] * p + a];
+      double acc = (x <= a) ? sQ[x * p + a] : sQ[a * p + x];
+      for (int c = 0; c < q; c++) acc += sPhi[x * q + c] * T[(size_t)siold[c] * p + a];
       P[(size_t)i * ld + col] = acc;
     } else {
       const double v = T[(size_t)i * p + a];
@@ -160,7 +186,7 @@ __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__rest
 bool launch_prop_clone(hipStream_t s, double *P, int ld, int N, int s0, int p, const int *iold, int q,
                        const double *Phi, const double *Q, double *T, int src0, int dt_id, const double *dnc_dev,
                        int do_dt) {
-  if ((long long)N * p * q > kPropCloneMaxWork) return false;
+  if (N * p > kPropCloneMaxEl * kPropCloneThreads || p > kPropCloneMaxPQ || q > kPropCloneMaxPQ) return false;
   hipLaunchKernelGGL(k_prop_clone, dim3(1), dim3(kPropCloneThreads), 0, s, P, ld, N, s0, p, iold, q, Phi, Q, T, src0,
                      dt_id, dnc_dev, do_dt);
   return true;
