@@ -246,6 +246,8 @@ struct DeviceBufs {
   double *chi2 = nullptr;
   double *H = nullptr;       // H_all (max_rows x ldh)
   double *Tall = nullptr;    // H_all P_can (max_rows x ldh), chi2 gate
+  double *chi2S = nullptr;   // per-feature S of the large chi2 gates (launch_chi2_batch grows it)
+  size_t chi2S_cap = 0;      // doubles
   double *partials = nullptr;
   double *R = nullptr;       // compressed (ncol x ncol, + global Cholesky scratch)
   int *hidx = nullptr;

@@ -299,7 +299,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       for (auto &F : b.feats) max_rows_f = std::max(max_rows_f, (mode == 0) ? 2 * F.nmeas - 3 : 2 * F.nmeas);
       KScope ks(&kprof_, KC_CHI2);
       launch_chi2_batch(d_.stream, bp, it.t_feats, d_.P, it.t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout + b.fout_off,
-                        max_rows_f, d_.acc, d_.R);
+                        max_rows_f, d_.acc, d_.R, &d_.chi2S, &d_.chi2S_cap);
     }
     if (tsdump) {  // synchronous copy-back: debug runs only (the chain loses its overlap)
       std::vector<long long> h(16 * (size_t)nf);

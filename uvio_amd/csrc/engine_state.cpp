@@ -226,7 +226,7 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame};
+                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame, d_.chi2S};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);

@@ -993,7 +993,7 @@ int Engine::run_batch(Batch &b, int mode, double sigma_pix_sq, double chi2_mult,
     // d_.R (the information-form Gram buffer, 2 max_ncol ldh doubles) holds the gathered P_can until the
     // T GEMM has read it; the Gram reduce writes it only later on the same stream
     launch_chi2_batch(d_.stream, bp, t_feats, d_.P, t_hidx, d_.H, b.rows, d_.Tall, d_.chi2, d_.fout,
-                      max_rows_f, d_.acc, d_.R);
+                      max_rows_f, d_.acc, d_.R, &d_.chi2S, &d_.chi2S_cap);
   }
   if (b.evtimed) HP_HIP(hipEventRecord(d_.ev1, d_.stream));
   d_.fout_pending = nf;  // copied with the next readback (read_dx) or before the next wait (dev_sync)

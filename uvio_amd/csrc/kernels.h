@@ -123,9 +123,12 @@ void launch_feature_linearize(hipStream_t s, const DBatchParams &bp, const DFeat
                               const double *chi2_table, double *H_all, DFeatOut *out, int max_meas, int max_nf);
 // batched chi2 gate (kernels_chi2.hip): T = H_all P[hidx, hidx], per-feature S / LDL^T / chi2;
 // rejected MSCKF / SLAM features get zero rows.  T_all: like H_all.
+// sbuf / sbuf_cap: the engine's buffer for the per-feature S of features too large for k_chi2's LDS staging
+// (formed by k_chi2_S over many CUs, grown here on demand); nullptr: k_chi2 forms S from global memory itself
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
                        double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
-                       int *acc_count, double *pcan = nullptr);  // pcan: n^2 scratch for the gathered P_can
+                       int *acc_count, double *pcan = nullptr,  // pcan: n^2 scratch for the gathered P_can
+                       double **sbuf = nullptr, size_t *sbuf_cap = nullptr);
 size_t feature_lds_bytes(int max_meas, int max_nf);
 
 // Compression: G = A^T A over rows of A = H_all (m x (n+1), ld = ldh), partials then Cholesky ->

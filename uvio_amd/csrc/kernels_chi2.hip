@@ -182,9 +182,51 @@ size_t chi2_lds_bytes(int max_rows_f, int n) {
 // feature's H_all rows from c0 = (mode >= 2 ? 3 : 0) on (delayed init tests the update rows against
 // chi2(dof = all rows), StateHelper.cpp:463-468).
 constexpr int kChi2Threads = 512;
+
+// The lower triangle of S = T Hhat^T + s2 I of every feature whose H and T rows do not fit k_chi2's LDS: one wave
+// per 16x16 tile (k-ascending MFMA chain, the expression k_chi2 uses), kChiSWaves tiles per workgroup, so the
+// rows are pulled by many CUs at once instead of one.  S_f lands at Sbuf + f * stride in k_chi2's LDS layout
+// (row stride R|1).  Workgroup blockIdx serves feature f = 8 (k / groups) + blockIdx % 8 with k = blockIdx / 8:
+// all of a feature's tiles run on the XCD that k_chi2's workgroup f runs on (blockIdx % 8 labels the XCD), so
+// that workgroup reads S out of its own L2.
+constexpr int kChiSWaves = 4;
+__global__ void __launch_bounds__(64 * kChiSWaves) k_chi2_S(DBatchParams bp, const DFeat *__restrict__ feats,
+                                                            const double *__restrict__ H_all,
+                                                            const double *__restrict__ T_all,
+                                                            const DFeatOut *__restrict__ out, double *__restrict__ Sbuf,
+                                                            size_t stride, int groups) {
+  const int k = blockIdx.x / 8, f = 8 * (k / groups) + blockIdx.x % 8, g = k % groups;
+  if (f >= bp.nfeat) return;
+  const DFeatOut o = out[f];
+  if (o.status != 0 || o.rows <= 0) return;
+  const DFeat F = feats[f];
+  const int n = bp.n_canon, ldh = bp.ldh, c0 = (F.mode >= 2) ? 3 : 0, R = o.rows - c0;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kq = lane >> 4;
+  const int nt = (R + 15) / 16, t = g * kChiSWaves + (threadIdx.x >> 6);
+  if (R <= 0 || t >= nt * (nt + 1) / 2) return;
+  int ti = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+  while (ti * (ti + 1) / 2 > t) ti--;
+  while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+  const int tj = t - ti * (ti + 1) / 2;
+  const int arow = 16 * ti + r16, bcol = 16 * tj + r16;
+  const double *ta = T_all + (size_t)(F.row_off + c0 + min(arow, R - 1)) * ldh;
+  const double *hb = H_all + (size_t)(F.row_off + c0 + min(bcol, R - 1)) * ldh;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  auto la = [&](int kk) { return (arow < R && kk < n) ? ta[kk] : 0.0; };
+  auto lb = [&](int kk) { return (bcol < R && kk < n) ? hb[kk] : 0.0; };
+  acc = tile_chain<decltype(la), decltype(lb), 16>(0, n, kq, la, lb, acc);
+  double *S = Sbuf + (size_t)f * stride;
+  const int ldS = R | 1;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int i = 16 * ti + kq + 4 * q, j = 16 * tj + r16;
+    if (i < R && j <= i) S[(size_t)i * ldS + j] = acc[q] + (i == j ? bp.sigma_pix_sq : 0.0);
+  }
+}
 __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
                                               double *__restrict__ T_all, const double *__restrict__ chi2_table,
-                                              DFeatOut *__restrict__ out, int use_lds, int *acc_count) {
+                                              DFeatOut *__restrict__ out, int use_lds, int *acc_count,
+                                              const double *__restrict__ Sg, size_t sg_stride) {
   extern __shared__ double lds[];
   __shared__ double red[kChi2Threads];
   __shared__ int st;
@@ -214,7 +256,12 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
   double *S = lds;
   const int ldS = R | 1;
   double *Lp = lds + (size_t)(R + 1) * ldS;
-  if (use_lds) {
+  if (Sg) {
+    // S formed by k_chi2_S: the lower triangle rows in this layout already
+    const double *Sf = Sg + (size_t)f * sg_stride;
+    staged_copy(
+        R * ldS, [&](int e) { return (e % ldS <= e / ldS) ? Sf[e] : 0.0; }, [&](int e, double v) { S[e] = v; });
+  } else if (use_lds) {
     const int ldl = n | 1;  // odd row stride: the MFMA operand reads below hit distinct banks
     double *Hl = Lp + (size_t)(R + 1) * 4;
     double *Tl = Hl + (size_t)R * ldl;
@@ -234,7 +281,7 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
     __syncthreads();
   }
   // lower triangle of S = T Hhat^T + s2 I on the matrix cores (16x16 tiles, K = n), then the residual row
-  {
+  if (!Sg) {
     const int lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6, r16 = lane & 15, kq = lane >> 4;
     const int nt = (R + 15) / 16, ntiles = nt * (nt + 1) / 2;
     for (int t = wid; t < ntiles; t += nw) {
@@ -306,7 +353,7 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
 
 void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats, const double *P, const int *hidx,
                        double *H_all, int m, double *T_all, const double *chi2_table, DFeatOut *out, int max_rows_f,
-                       int *acc_count, double *pcan) {
+                       int *acc_count, double *pcan, double **sbuf, size_t *sbuf_cap) {
   if (bp.nfeat <= 0 || m <= 0) return;
   const int n = bp.n_canon;
   if (m >= 4096) {  // enough 64 x 64 tiles to fill the 256 CUs
@@ -327,8 +374,32 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
   if (bytes > 64 * 1024 && (int)bytes > granted)
     throw std::runtime_error("k_chi2 needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
+  // features too large for the LDS staging: S over many CUs first (k_chi2_S), k_chi2 reads it
+  double *Sg = nullptr;
+  size_t stride = 0;
+  if (!use_lds && sbuf && sbuf_cap) {
+    stride = (size_t)max_rows_f * (max_rows_f | 1);
+    const size_t need = stride * (size_t)bp.nfeat;
+    if (need > *sbuf_cap) {
+      auto ok = [](hipError_t e, const char *what) {
+        if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+      };
+      if (*sbuf) {
+        ok(hipStreamSynchronize(s), "chi2 S buffer: stream sync");  // the old buffer may still be read
+        ok(hipFree(*sbuf), "chi2 S buffer: free");
+      }
+      *sbuf = nullptr;
+      *sbuf_cap = 0;
+      ok(hipMalloc(sbuf, need * 3 / 2 * sizeof(double)), "chi2 S buffer: alloc");
+      *sbuf_cap = need * 3 / 2;
+    }
+    Sg = *sbuf;
+    const int nt = (max_rows_f + 15) / 16, groups = (nt * (nt + 1) / 2 + kChiSWaves - 1) / kChiSWaves;
+    hipLaunchKernelGGL(k_chi2_S, dim3(8 * ((bp.nfeat + 7) / 8) * groups), dim3(64 * kChiSWaves), 0, s, bp, feats, H_all,
+                       T_all, out, Sg, stride, groups);
+  }
   hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(kChi2Threads), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
-                     acc_count);
+                     acc_count, Sg, stride);
 }
 
 }  // namespace uvhp
