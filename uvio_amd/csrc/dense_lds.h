@@ -129,10 +129,11 @@ __device__ __forceinline__ dbl4 mfma4(double a, double b, dbl4 c) {
 }
 
 // Accumulate one 16x16 tile over k in [0, kend): acc += sum_k A(r16, k) B(k, r16) with the operands fetched
-// through the callables (k = 4 s + kq); the loads of eight k-slabs are issued before their MFMAs, so a
-// chunk costs one memory round trip.  (32-slab chunks measured slower in k_ekf_MS / k_ekf_WP: 24.4 / 10.3
-// against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
-template <class LA, class LB, int U = 8>
+// through the callables (k = 4 s + kq); the loads of U k-slabs are issued before their MFMAs, so a chunk of
+// 4U columns costs one memory round trip.  U = 8 by default; 16 for the products whose operands come from
+// global memory behind a long latency (the chi2 S tiles, k_ekf_MS).  (32-slab chunks measured slower in
+// k_ekf_MS / k_ekf_WP in round 2: 24.4 / 10.3 against 19-22 / 8.9 us at cfg2, profiles/r02e_cfg2_per_frame.txt.)
+template <int U = 8, class LA, class LB>
 __device__ __forceinline__ dbl4 tile_chain(int kbeg, int kend, int kq, LA la, LB lb, dbl4 acc) {
   for (int k0 = kbeg; k0 < kend; k0 += 4 * U) {
     double a[U], b[U];

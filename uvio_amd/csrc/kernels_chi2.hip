@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(64 * kChiSWaves) k_chi2_S(DBatchParams bp, con
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   auto la = [&](int kk) { return (arow < R && kk < n) ? ta[kk] : 0.0; };
   auto lb = [&](int kk) { return (bcol < R && kk < n) ? hb[kk] : 0.0; };
-  acc = tile_chain<decltype(la), decltype(lb), 16>(0, n, kq, la, lb, acc);
+  acc = tile_chain<16>(0, n, kq, la, lb, acc);
   double *S = Sbuf + (size_t)f * stride;
   const int ldS = R | 1;
 #pragma unroll
@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
       dbl4 acc = {0.0, 0.0, 0.0, 0.0};
       auto la = [&](int k) { return (arow < R && k < n) ? ta[k] : 0.0; };
       auto lb = [&](int k) { return (bcol < R && k < n) ? hb[k] : 0.0; };
-      acc = tile_chain<decltype(la), decltype(lb), 16>(0, n, kq, la, lb, acc);
+      acc = tile_chain<16>(0, n, kq, la, lb, acc);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int i = 16 * ti + kq + 4 * q, j = 16 * tj + r16;

@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
       const double *Hr = H + (size_t)min(jr, r - 1) * ldh;
       const bool jv = jr < r;
       dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = tile_chain(
+      acc = tile_chain<16>(
           0, n, kq, [&](int k) { return Ps[r16 * lds + k]; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
     const double *Ha = H + (size_t)min(ar, r - 1) * ldh, *Tb = Tall + (size_t)min(br, r - 1) * ldt;
     const bool av = ar < r, bv = br < r;
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = tile_chain(
+    acc = tile_chain<16>(
         0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return bv ? Tb[k] : 0.0; }, acc);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
       const double *Prow = P + (size_t)hs[min(row, n - 1)] * ldp;
       const bool rv = row < n;
       dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = tile_chain(
+      acc = tile_chain<16>(
           0, n, kq, [&](int l) { return rv ? Prow[hs[l]] : 0.0; }, [&](int l) { return jv ? Hb[l] : 0.0; }, acc);
 #pragma unroll
       for (int q = 0; q < 4; q++) Ts[(16 * kt + kq + 4 * q) * 17 + r16] = acc[q];
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
     const double *Ha = H + (size_t)min(ar, r - 1) * ldh;
     const bool av = ar < r;
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = tile_chain(
+    acc = tile_chain<16>(
         0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return Ts[k * 17 + r16]; }, acc);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
