@@ -95,30 +95,32 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
         frame_obs_.push_back(o);
       }
     }
-    // undistort_cv with the camera models as of now (independent per point: on the pool)
-    HPROF("retri.undist");
-    pool_.parallel_for(frame_obs_.size(), 128, [&](size_t b, size_t e) {
-      for (size_t k = b; k < e; k++) {
-        DRetriObs &o = frame_obs_[k];
-        cam_undistort_f(cams_[o.cam], o.u, o.v, o.un, o.vn);
-      }
-    });
-  } else if (o_.do_calib_camera_intrinsics) {
-    // undistort_cv with the camera models as of now: this frame's updates may have moved the intrinsics
-    // since the feed undistorted the same pixels for the database (StateHelper.cpp:190-195)
-    pool_.parallel_for(frame_obs_.size(), 2048, [&](size_t b, size_t e) {
-      for (size_t k = b; k < e; k++) {
-        DRetriObs &o = frame_obs_[k];
-        cam_undistort_f(cams_[o.cam], o.u, o.v, o.un, o.vn);
-      }
-    });
   }
   const int nobs = (int)frame_obs_.size();
-  retri_alloc(nobs);
   {
     HPROF("retri.wait_copy");
     if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // last frame's upload read h_obs
-    if (nobs) std::memcpy(rt_.h_obs, frame_obs_.data(), sizeof(DRetriObs) * nobs);
+    rt_.copy_pending = false;
+  }
+  retri_alloc(nobs);
+  // the observations go straight into the pinned upload buffer, on the pool: undistort_cv with the camera
+  // models as of now for the tracker's points, and for the simulated feed's when this frame's updates may have
+  // moved the intrinsics since the feed undistorted the same pixels (StateHelper.cpp:190-195)
+  {
+    HPROF("retri.undist");
+    DRetriObs *h = rt_.h_obs;
+    const bool undist = tracker_ || o_.do_calib_camera_intrinsics;
+    pool_.parallel_for(frame_obs_.size(), undist ? 512 : 8192, [&](size_t b, size_t e) {
+      if (!undist) {
+        std::memcpy(h + b, frame_obs_.data() + b, sizeof(DRetriObs) * (e - b));
+        return;
+      }
+      for (size_t k = b; k < e; k++) {
+        DRetriObs o = frame_obs_[k];
+        cam_undistort_f(cams_[o.cam], o.u, o.v, o.un, o.vn);
+        h[k] = o;
+      }
+    });
   }
   RetriJob job{};
   job.nobs = nobs;
