@@ -293,9 +293,14 @@ struct DeviceBufs {
   // delayed-initialization chain (Engine::slam_delayed_init): per candidate one region of chain_stride doubles
   // [dx (N) | chi2, accepted | init residual (3) | accepted, negative diagonals], chain_k candidates per chain,
   // mirrored in pinned memory
-  double *chain = nullptr, *chain_host = nullptr;
+  // The frame chain's per-update regions sit right in front of dxneg (region r at dxneg - (r + 1) stride), and
+  // chain_host mirrors [regions | dx block | fout] in pinned memory, so the chain's regions and every batch's
+  // per-feature results come back in ONE copy (chain_results_copy)
+  double *chain = nullptr, *chain_host = nullptr;  // the allocations: [chain_k regions][dx block][fout]
   int chain_k = 0;
   size_t chain_stride = 0;
+  double *region_dev(int r) const { return dxneg - (size_t)(r + 1) * chain_stride; }
+  const double *region_host(int r) const { return (const double *)neg_host - (size_t)(r + 1) * chain_stride; }
   int fout_cap = 0;            // per-feature result slots in fout / fout_host (one frame chain's batches)
   char *frame = nullptr;       // the frame chain's device state: clone / camera tables, pose values, mirror
   size_t frame_bytes = 0;
@@ -416,6 +421,7 @@ class Engine {
   std::function<void()> chain_overlap_;
   // FeatureDatabase::cleanup_measurements(t) over the database's features, skipping the held ones if asked
   void cleanup_measurements(double t, bool skip_held);
+  void chain_results_copy(int nreg, int fo);
   HostProf hprof_;                     // UVIO_HP_HOST_PROF section timer (debug)
   FILE *timing_csv_ = nullptr;         // record_timing_information (VioManager.cpp:105-122)
   KProf kprof_;                        // live per-class kernel timing (uvio_hp_set_kernel_timing)

@@ -257,7 +257,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     if (nreg >= d_.chain_k) throw HpError(UVIO_HP_E_CAPACITY, "update chain: too many updates in one frame");
     return nreg++;
   };
-  auto region = [&](int r) { return d_.chain + (size_t)r * st; };
+  auto region = [&](int r) { return d_.region_dev(r); };
   // a batch's feature kernel (+ the chi2 group); results at d_.fout + b.fout_off
   auto enqueue_batch = [&](ChainItem &it, int mode, double s2, double mult, bool chi2, const DFeatOut *tri_in) {
     Batch &b = it.b;
@@ -502,9 +502,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
   const auto tw = clk::now();
   {
     HPROF("chain.wait");
-    if (nreg > 0)
-      HP_HIP(hipMemcpyAsync(d_.chain_host, d_.chain, sizeof(double) * st * nreg, hipMemcpyDeviceToHost, d_.stream));
-    if (fo > 0) HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * fo, hipMemcpyDeviceToHost, d_.stream));
+    chain_results_copy(nreg, fo);
     d_.fout_pending = 0;
     // the next frame's detection (Tracker::predetect) while the device runs this chain: it reads only this
     // frame's tracker results; on the tracker's detection stream and worker thread, joined by the next feed
@@ -543,7 +541,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       timing_.msckf_rows = acc_rows;
       timing_.msckf_cols = it.b.n_canon;
       if (it.region >= 0) {
-        const double *base = d_.chain_host + (size_t)it.region * st;
+        const double *base = d_.region_host(it.region);
         neg_check(base, N_);
         if (acc > 0) apply_dx(base);
       }
@@ -559,7 +557,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
         if (outs[i].status == 0) acc++;
       }
       if (it.region >= 0) {
-        const double *base = d_.chain_host + (size_t)it.region * st;
+        const double *base = d_.region_host(it.region);
         neg_check(base, N_);
         if (acc > 0) apply_dx(base);
       }
@@ -584,7 +582,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
         f->anchor_cam_id = it.b.feats[j].anchor_cam;
         f->anchor_clone_timestamp = f->find((size_t)f->anchor_cam_id)->m.back().t;
         for (int k = 0; k < 3; k++) f->p_FinA[k] = touts[j].p_FinA[k], f->p_FinG[k] = touts[j].p_FinG[k];
-        const double *base = d_.chain_host + (size_t)(it.region + j) * st;
+        const double *base = d_.region_host(it.region + j);
         if (base[Ni + 9] > 0.5) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
         const bool accepted = base[Ni + 8] > 0.5;
         last_upd_.push_back(FeatDebug{f->featid, {f->p_FinG[0], f->p_FinG[1], f->p_FinG[2]}, accepted ? 0 : 3,

@@ -226,7 +226,7 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.dxneg, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame, d_.chi2S};
+                  d_.ekf.Dinv, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame, d_.chi2S};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
@@ -319,16 +319,20 @@ void Engine::alloc_device() {
   d_.dx_bytes = sizeof(double) * (cap + 16);
   // one frame chain holds the MSCKF batch, the SLAM chunks and the delayed initialization's two passes
   d_.fout_cap = maxf + 3 * std::max(o_.max_slam_features, 0) + 64;
-  HP_HIP(hipMalloc((void **)&d_.dxneg, d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap));
+  d_.chain_k = std::max(o_.max_slam_features, 1) + std::max(o_.max_slam_features, 1) / std::max(o_.max_slam_in_update, 1) + 4;
+  d_.chain_stride = (size_t)cap + 16;
+  // [chain regions (reversed) | dx block (neg, dx) | fout] on the device and mirrored in pinned memory
+  const size_t reg_bytes = sizeof(double) * d_.chain_k * d_.chain_stride;
+  const size_t res_bytes = reg_bytes + d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap;
+  HP_HIP(hipMalloc((void **)&d_.chain, res_bytes));
+  HP_HIP(hipMemset(d_.chain, 0, res_bytes));
+  d_.dxneg = (double *)((char *)d_.chain + reg_bytes);
   d_.fout = (DFeatOut *)((char *)d_.dxneg + d_.dx_bytes);
   dalloc(&d_.acc, 4);
   dalloc(&d_.shard, (size_t)d_.max_ncol * d_.max_ncol + 2);
   d_.ekf.neg = (int *)d_.dxneg;
   d_.ekf.dx = d_.dxneg + 1;
-  d_.chain_k = std::max(o_.max_slam_features, 1) + std::max(o_.max_slam_features, 1) / std::max(o_.max_slam_in_update, 1) + 4;
-  d_.chain_stride = (size_t)cap + 16;
-  dalloc(&d_.chain, (size_t)d_.chain_k * d_.chain_stride);
-  HP_HIP(hipHostMalloc((void **)&d_.chain_host, sizeof(double) * d_.chain_k * d_.chain_stride, hipHostMallocDefault));
+  HP_HIP(hipHostMalloc((void **)&d_.chain_host, res_bytes + sizeof(double) * 16 + 64, hipHostMallocDefault));
   // chi2 table: boost::math::quantile(chi_squared(dof), 0.95) for dof 1..999 (UpdaterMSCKF.cpp:52-55)
   for (int i = 1; i < 1000; i++) chi2_table_[i] = chi2_quantile95(i);
   HP_HIP(hipMemcpy(d_.chi2, chi2_table_.data(), 1000 * sizeof(double), hipMemcpyHostToDevice));
@@ -337,8 +341,7 @@ void Engine::alloc_device() {
                  sizeof(DClone) * (C + 4) + sizeof(DCam) * UVIO_HP_MAX_CAMS + sizeof(int) * (d_.max_ncol + d_.max_rows) +
                  sizeof(double) * (cap + 16) + sizeof(DFeatOut) * d_.fout_cap + sizeof(double) * 16 + 4096;
   HP_HIP(hipHostMalloc(&d_.pin, d_.pin_bytes, hipHostMallocDefault));
-  char *pb = (char *)d_.pin + d_.pin_bytes -
-             (d_.dx_bytes + sizeof(DFeatOut) * d_.fout_cap + sizeof(double) * 16 + 64);
+  char *pb = (char *)d_.chain_host + reg_bytes;
   d_.neg_host = (int *)pb;  // same layout as dxneg
   d_.dx_host = (double *)(pb + sizeof(double));
   d_.fout_host = (DFeatOut *)(pb + d_.dx_bytes);
@@ -475,6 +478,16 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
     o.flops = kprof_.flops[k];
     o.bytes = kprof_.bytes[k];
   }
+}
+
+// regions 0 .. nreg-1 of the frame chain, the dx block and the first fo per-feature results: one contiguous span
+// of the results block (DeviceBufs::region_dev), one copy
+void Engine::chain_results_copy(int nreg, int fo) {
+  if (nreg <= 0 && fo <= 0) return;
+  const char *d0 = (const char *)d_.region_dev(std::max(nreg, 0) - 1);
+  const char *d1 = (const char *)(d_.fout + std::max(fo, 0));
+  char *h0 = (char *)d_.region_host(std::max(nreg, 0) - 1);
+  HP_HIP(hipMemcpyAsync(h0, d0, (size_t)(d1 - d0), hipMemcpyDeviceToHost, d_.stream));
 }
 
 void Engine::read_dx(const char *who) {

@@ -1382,7 +1382,7 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
                                  d_.fout + j, F.nmeas, F.nf);
       }
       EkfScratch sc = d_.ekf;
-      sc.dx = d_.chain + (size_t)j * st;
+      sc.dx = d_.region_dev(j);
       double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
       // initialize_invertible with rows 0..2 (H_Linv from the feature's H_finit); its residual column lands in
       // the candidate's region behind the chi2 gate's [chi2, accepted]
@@ -1403,8 +1403,7 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
                          sc.dx + Ni + 8);
     }
     ++p_epoch_;
-    HP_HIP(hipMemcpyAsync(d_.chain_host, d_.chain, sizeof(double) * st * K, hipMemcpyDeviceToHost, d_.stream));
-    HP_HIP(hipMemcpyAsync(d_.fout_host, d_.fout, sizeof(DFeatOut) * K, hipMemcpyDeviceToHost, d_.stream));
+    chain_results_copy(K, K);
     d_.fout_pending = 0;
   }
   dev_sync();
@@ -1417,7 +1416,7 @@ int Engine::slam_delayed_chain(std::vector<FeatP> &fv, const std::vector<size_t>
     const DFeat &F = b.feats[j];
     const DFeatOut &o1 = d_.fout_host[j];
     const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
-    const double *base = d_.chain_host + (size_t)j * st;
+    const double *base = d_.region_host(j);
     if (base[Ni + 9] > 0.5) throw HpError(UVIO_HP_E_NUMERIC, "EKFUpdate: negative covariance diagonal");
     const bool accepted = base[Ni + 8] > 0.5;
     f->to_delete = true;
