@@ -252,9 +252,19 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
       for (size_t w = b; w < e; w++) {
         const uint32_t i0 = start[w], i1 = start[w + 1];
         for (uint32_t i = i0; i < i1; i++) {
-          if (i + 16 < i1) __builtin_prefetch(fp[order[i + 16]], 1);
-          if (i + 8 < i1)
-            for (const CamTrack &c : fp[order[i + 8]]->tracks) __builtin_prefetch(c.m.v.data() + c.m.v.size(), 1);
+          // two-stage software prefetch: the feature object's first three lines (its tracks) 32 ahead, then
+          // the append slot of the observation's camera track 16 ahead
+          if (i + 32 < i1) {
+            const char *p = (const char *)fp[order[i + 32]];
+            __builtin_prefetch(p, 1);
+            __builtin_prefetch(p + 64, 1);
+            __builtin_prefetch(p + 128, 1);
+          }
+          if (i + 16 < i1) {
+            const size_t k2 = order[i + 16];
+            for (const CamTrack &c : fp[k2]->tracks)
+              if ((int)c.cam == cam_of[k2]) __builtin_prefetch(c.m.v.data() + c.m.v.size(), 1);
+          }
           const size_t k = order[i];
           fp[k]->track((size_t)cam_of[k]).m.push_back(
               FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
@@ -530,7 +540,15 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   std::vector<FeatP> up = feats_lost;
   up.insert(up.end(), feats_marg.begin(), feats_marg.end());
   up.insert(up.end(), feats_maxtracks.begin(), feats_maxtracks.end());
-  std::sort(up.begin(), up.end(), [](const FeatP &a, const FeatP &b) { return a->count() < b->count(); });
+  // VioManager.cpp:518 std::sort by measurement count (compare_feat), on the counts computed once: std::sort's
+  // permutation depends only on the comparison outcomes, which are the same
+  {
+    std::vector<std::pair<int, FeatP>> keyed(up.size());
+    for (size_t i = 0; i < up.size(); i++) keyed[i] = {up[i]->count(), std::move(up[i])};
+    std::sort(keyed.begin(), keyed.end(),
+              [](const std::pair<int, FeatP> &a, const std::pair<int, FeatP> &b) { return a.first < b.first; });
+    for (size_t i = 0; i < up.size(); i++) up[i] = std::move(keyed[i].second);
+  }
   if ((int)up.size() > o_.max_msckf_in_update) up.erase(up.begin(), up.end() - o_.max_msckf_in_update);
   // every feature the updaters may flag to_delete (the MSCKF list, SLAM updates, delayed inits); a
   // frame that returns early keeps its entries for the next frame's cleanup
