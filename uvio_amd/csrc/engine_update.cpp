@@ -572,6 +572,15 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   const double mt_clean = do_clean ? margtimestep() : 0.0;
   bool cleaned_early = false;
   std::vector<FeatP> held;
+  // on every exit (a returned error or an exception included): no overlap job left behind, no feature held
+  struct HeldGuard {
+    Engine &e;
+    std::vector<FeatP> &h;
+    ~HeldGuard() {
+      e.chain_overlap_ = nullptr;
+      for (auto &f : h) f->held = false;
+    }
+  } held_guard{*this, held};
   if (!shard_.enabled && !no_chain_) {
     if (do_clean) {
       held = pending_delete_;
@@ -584,10 +593,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     // the three updaters as one device chain with one host wait (engine_chain.cpp)
     rc = update_frame(up, slam_upd, slam_delayed);
     chain_overlap_ = nullptr;
-    if (rc) {
-      for (auto &f : held) f->held = false;
-      return rc;
-    }
+    if (rc) return rc;
     rT6 = clk::now();
     timing_.msckf_update = chain_times_[0];
     timing_.slam_update = chain_times_[1];
@@ -643,7 +649,6 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       }
     }
   }
-  for (auto &f : held) f->held = false;
   marginalize_old_clone();
   if (o_.record_timing >= 2) dev_sync();
   auto rT7 = clk::now();
