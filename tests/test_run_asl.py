@@ -110,6 +110,18 @@ def asl(tmp_path_factory):
     return str(base), str(gt), opts, sim, imgs, str(cfg / "estimator_config.yaml")
 
 
+def _timing_config(cfg, path):
+    """a copy of the runner's config that also writes the reference's timing CSV (VioManager.cpp:105-122)"""
+    d = os.path.dirname(cfg)
+    with open(cfg) as f:
+        text = f.read()
+    text += "\nrecord_timing_information: true\nrecord_timing_filepath: \"%s\"\n" % path
+    out = os.path.join(d, "estimator_config_timing.yaml")
+    with open(out, "w") as f:
+        f.write(text)
+    return out
+
+
 def test_runner_dry_run_parses_and_decodes(asl):
     from uvio_amd import build
     build.build_runner()
@@ -151,8 +163,16 @@ def test_runner_matches_the_binding(asl, tmp_path):
     import uvio_amd as U
     folder, gt, opts, sim, imgs, cfg = asl
     traj = tmp_path / "traj.txt"
-    subprocess.check_call([RUNNER, cfg, folder, "--gt", gt, "--out", str(traj)], timeout=300)
+    tcsv = tmp_path / "timing.csv"
+    subprocess.check_call([RUNNER, _timing_config(cfg, str(tcsv)), folder, "--gt", gt, "--out", str(traj)], timeout=300)
     est = np.loadtxt(traj, ndmin=2)
+    # the timing CSV in the reference's schema: one row per updated frame once the clone window holds 5 clones
+    with open(tcsv) as f:
+        lines = f.read().strip().splitlines()
+    assert lines[0].startswith("# timestamp (sec),tracking,propagation,msckf update,slam update,slam delayed,")
+    rows = np.array([[float(v) for v in l.split(",")] for l in lines[1:]])
+    assert rows.shape[1] == 8 and len(rows) >= len(est) - 6 and np.all(rows[:, 1:] >= 0)
+    assert np.all(np.diff(rows[:, 0]) > 0)
     assert len(est) >= N_FRAMES - 3
     # the binding: IMU rows and camera pairs in time order (IMU first at equal times), GT init at the first pair
     imu = np.loadtxt(os.path.join(folder, "mav0", "imu0", "data.csv"), delimiter=",", ndmin=2)
