@@ -530,7 +530,7 @@ void Engine::check_neg_diag(const char *who) {
 bool Engine::cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                                  const std::vector<double> &Q, bool do_dt, const double *ddnc) {
   const int q = (int)iold.size();
-  if (p > 48 || q > 48 || N_ + 6 > d_.ldp || N_ * p > 8 * 1024 || std::getenv("UVIO_HP_NO_PROP_FUSE"))
+  if (p > 32 || q > 32 || N_ + 6 > d_.ldp || N_ * p > 8 * 1024 || std::getenv("UVIO_HP_NO_PROP_FUSE"))
     return false;  // (launch_prop_clone's bounds)
   const double *dPhi = stage(Phi.data(), (size_t)p * q);
   const double *dQ = stage(Q.data(), (size_t)p * p);

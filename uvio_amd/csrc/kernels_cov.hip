@@ -100,47 +100,41 @@ __global__ void k_clone(double *__restrict__ P, int ld, int N, int src0, int dt_
 // EKFPropagation of the contiguous block s0 .. s0+p-1 and the IMU-pose clone in ONE workgroup launch: the three
 // phases above (T, the block write, the clone) with a workgroup barrier between them instead of a kernel
 // boundary, each element computed by the same expression as in k_prop_T / k_prop_write / k_clone (so the
-// result is bit-identical).  For the propagations of up to 8 T elements per thread and p, q <= 48 (cfg2-4):
-// the frame loses two launches.
-constexpr int kPropCloneThreads = 1024, kPropCloneMaxEl = 8, kPropCloneMaxPQ = 48;
+// result is bit-identical).  For the propagations of N p <= 8192 and p, q <= 32
+// (cfg2-4): the frame loses two launches.
+constexpr int kPropCloneThreads = 512, kPropCloneMaxEl = 16, kPropCloneMaxPQ = 32;
 __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__restrict__ P, int ld, int N, int s0, int p,
                                                                   const int *__restrict__ iold, int q,
                                                                   const double *__restrict__ Phi,
                                                                   const double *__restrict__ Q, double *__restrict__ T,
                                                                   int src0, int dt_id, const double *__restrict__ dnc,
                                                                   int do_dt) {
-  // Phi, Q and the column map in LDS: every P load below depends on nothing but an LDS read
-  __shared__ double sPhi[kPropCloneMaxPQ * kPropCloneMaxPQ], sQ[kPropCloneMaxPQ * kPropCloneMaxPQ];
+  // Phi, Q and the column map in LDS; T rows of the block (rows iold[c]) also kept in LDS for the block write
+  __shared__ double sPhi[kPropCloneMaxPQ * kPropCloneMaxPQ], sQ[kPropCloneMaxPQ * kPropCloneMaxPQ],
+      sT[kPropCloneMaxPQ * kPropCloneMaxPQ];
   __shared__ int siold[kPropCloneMaxPQ];
   for (int e = threadIdx.x; e < p * q; e += blockDim.x) sPhi[e] = Phi[e];
   for (int e = threadIdx.x; e < p * p; e += blockDim.x) sQ[e] = Q[e];
   for (int e = threadIdx.x; e < q; e += blockDim.x) siold[e] = iold[e];
   __syncthreads();
-  // T: a thread's (up to kPropCloneMaxEl) elements advance together, so their P loads of one b are in flight at
-  // once; each element's sum runs over b in ascending order, as in k_prop_T
-  {
-    double acc[kPropCloneMaxEl];
-    const double *Pi[kPropCloneMaxEl];
-    int ai[kPropCloneMaxEl];
+  // T, one covariance row per thread: the row's q inputs loaded at once (one memory round trip), then its p
+  // outputs from registers and LDS; each output's sum runs over b in ascending order, as in k_prop_T
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const double *Pi = P + (size_t)i * ld;
+    double pv[kPropCloneMaxPQ];
+    int ci = -1;  // this row's position in the column map (a row of the propagated block)
 #pragma unroll
-    for (int e = 0; e < kPropCloneMaxEl; e++) {
-      const int idx = min((int)threadIdx.x + e * (int)blockDim.x, N * p - 1);
-      Pi[e] = P + (size_t)(idx / p) * ld;
-      ai[e] = idx % p;
-      acc[e] = 0.0;
+    for (int b = 0; b < kPropCloneMaxPQ; b++) {
+      pv[b] = (b < q) ? Pi[siold[b]] : 0.0;
+      if (b < q && siold[b] == i) ci = b;
     }
-    for (int b = 0; b < q; b++) {
-      const int c = siold[b];
-      double v[kPropCloneMaxEl];
+    for (int a = 0; a < p; a++) {
+      double acc = 0.0;
 #pragma unroll
-      for (int e = 0; e < kPropCloneMaxEl; e++) v[e] = Pi[e][c];
-#pragma unroll
-      for (int e = 0; e < kPropCloneMaxEl; e++) acc[e] += v[e] * sPhi[ai[e] * q + b];
-    }
-#pragma unroll
-    for (int e = 0; e < kPropCloneMaxEl; e++) {
-      const int idx = threadIdx.x + e * blockDim.x;
-      if (idx < N * p) T[idx] = acc[e];
+      for (int b = 0; b < kPropCloneMaxPQ; b++)
+        if (b < q) acc += pv[b] * sPhi[a * q + b];
+      T[(size_t)i * p + a] = acc;
+      if (ci >= 0) sT[ci * p + a] = acc;
     }
   }
   __syncthreads();
@@ -149,7 +143,7 @@ __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__rest
     if (i >= s0 && i < s0 + p) {
       const int x = i - s0;
       double acc = (x <= a) ? sQ[x * p + a] : sQ[a * p + x];
-      for (int c = 0; c < q; c++) acc += sPhi[x * q + c] * T[(size_t)siold[c] * p + a];
+      for (int c = 0; c < q; c++) acc += sPhi[x * q + c] * sT[c * p + a];
       P[(size_t)i * ld + col] = acc;
     } else {
       const double v = T[(size_t)i * p + a];
