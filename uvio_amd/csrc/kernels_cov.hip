@@ -118,7 +118,8 @@ __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__rest
   for (int e = threadIdx.x; e < q; e += blockDim.x) siold[e] = iold[e];
   __syncthreads();
   // T, one covariance row per thread: the row's q inputs loaded at once (one memory round trip), then its p
-  // outputs from registers and LDS; each output's sum runs over b in ascending order, as in k_prop_T
+  // outputs eight at a time (independent sums side by side); each output's sum runs over b in ascending order,
+  // as in k_prop_T
   for (int i = threadIdx.x; i < N; i += blockDim.x) {
     const double *Pi = P + (size_t)i * ld;
     double pv[kPropCloneMaxPQ];
@@ -128,51 +129,88 @@ __global__ void __launch_bounds__(kPropCloneThreads) k_prop_clone(double *__rest
       pv[b] = (b < q) ? Pi[siold[b]] : 0.0;
       if (b < q && siold[b] == i) ci = b;
     }
-    for (int a = 0; a < p; a++) {
-      double acc = 0.0;
+    for (int a0 = 0; a0 < p; a0 += 8) {
+      double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int b = 0; b < kPropCloneMaxPQ; b++)
-        if (b < q) acc += pv[b] * sPhi[a * q + b];
-      T[(size_t)i * p + a] = acc;
-      if (ci >= 0) sT[ci * p + a] = acc;
+      for (int b = 0; b < kPropCloneMaxPQ; b++) {
+        if (b < q) {
+#pragma unroll
+          for (int u = 0; u < 8; u++) acc[u] += pv[b] * sPhi[min(a0 + u, p - 1) * q + b];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (a0 + u < p) {
+          T[(size_t)i * p + a0 + u] = acc[u];
+          if (ci >= 0) sT[ci * p + a0 + u] = acc[u];
+        }
+      }
     }
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < N * p; idx += blockDim.x) {
-    const int i = idx / p, a = idx % p, col = s0 + a;
-    if (i >= s0 && i < s0 + p) {
-      const int x = i - s0;
-      double acc = (x <= a) ? sQ[x * p + a] : sQ[a * p + x];
-      for (int c = 0; c < q; c++) acc += sPhi[x * q + c] * sT[c * p + a];
-      P[(size_t)i * ld + col] = acc;
-    } else {
-      const double v = T[(size_t)i * p + a];
-      P[(size_t)i * ld + col] = v;
-      P[(size_t)col * ld + i] = v;
+  // the block rows / columns, eight elements per thread and round: every load of a round before its stores
+  constexpr int U = 8;
+  for (int base = threadIdx.x; base < N * p; base += U * blockDim.x) {
+    double tv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int idx = base + u * blockDim.x;
+      tv[u] = (idx < N * p) ? T[idx] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int idx = base + u * blockDim.x;
+      if (idx >= N * p) continue;
+      const int i = idx / p, a = idx % p, col = s0 + a;
+      if (i >= s0 && i < s0 + p) {
+        const int x = i - s0;
+        double acc = (x <= a) ? sQ[x * p + a] : sQ[a * p + x];
+        for (int c = 0; c < q; c++) acc += sPhi[x * q + c] * sT[c * p + a];
+        P[(size_t)i * ld + col] = acc;
+      } else {
+        P[(size_t)i * ld + col] = tv[u];
+        P[(size_t)col * ld + i] = tv[u];
+      }
     }
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < (N + 6) * 6; idx += blockDim.x) {
-    const int i = idx / 6, b = idx % 6;
-    const double db = do_dt ? dnc[b] : 0.0;
-    if (i < N) {
-      double col = P[(size_t)i * ld + src0 + b];
-      double row = P[(size_t)(src0 + b) * ld + i];
-      if (do_dt) {
-        col += P[(size_t)i * ld + dt_id] * db;
-        row += db * P[(size_t)dt_id * ld + i];
+  // the clone's rows / columns N .. N+5 (reads never touch them): a round's values first, then its stores
+  for (int base = threadIdx.x; base < (N + 6) * 6; base += U * blockDim.x) {
+    double vc[U], vr[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int idx = base + u * blockDim.x;
+      vc[u] = vr[u] = 0.0;
+      if (idx >= (N + 6) * 6) continue;
+      const int i = idx / 6, b = idx % 6;
+      const double db = do_dt ? dnc[b] : 0.0;
+      if (i < N) {
+        double col = P[(size_t)i * ld + src0 + b];
+        double row = P[(size_t)(src0 + b) * ld + i];
+        if (do_dt) {
+          col += P[(size_t)i * ld + dt_id] * db;
+          row += db * P[(size_t)dt_id * ld + i];
+        }
+        vc[u] = col;
+        vr[u] = row;
+      } else {
+        const int a = i - N;
+        double v = P[(size_t)(src0 + a) * ld + src0 + b];
+        if (do_dt) {
+          const double da = dnc[a];
+          v += P[(size_t)(src0 + a) * ld + dt_id] * db;
+          v += da * (P[(size_t)dt_id * ld + src0 + b] + P[(size_t)dt_id * ld + dt_id] * db);
+        }
+        vc[u] = v;
       }
-      P[(size_t)i * ld + N + b] = col;
-      P[(size_t)(N + b) * ld + i] = row;
-    } else {
-      const int a = i - N;
-      double v = P[(size_t)(src0 + a) * ld + src0 + b];
-      if (do_dt) {
-        const double da = dnc[a];
-        v += P[(size_t)(src0 + a) * ld + dt_id] * db;
-        v += da * (P[(size_t)dt_id * ld + src0 + b] + P[(size_t)dt_id * ld + dt_id] * db);
-      }
-      P[(size_t)i * ld + N + b] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int idx = base + u * blockDim.x;
+      if (idx >= (N + 6) * 6) continue;
+      const int i = idx / 6, b = idx % 6;
+      P[(size_t)i * ld + N + b] = vc[u];
+      if (i < N) P[(size_t)(N + b) * ld + i] = vr[u];
     }
   }
 }
