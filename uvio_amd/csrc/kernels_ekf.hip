@@ -38,23 +38,8 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
   const int r16 = lane & 15, kq = lane >> 4;
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // the update's negative-diagonal count
   if ((int)blockIdx.x < nbM) {
-    // M rows i0 .. i0+15: Ps[i][k] = P[i0 + i][hidx[k]] staged once, each wave takes column tiles of M.  The
-    // wave's first tile's H operand (its first kMPf k-slabs) is loaded before the staging, so its memory round
-    // trip overlaps the gather's two (column map, then P); same MFMA sequence, ascending k, as tile_chain
-    constexpr int kMPf = 48;  // 192 columns
+    // M rows i0 .. i0+15: Ps[i][k] = P[i0 + i][hidx[k]] staged once, each wave takes column tiles of M
     const int i0 = blockIdx.x * 16, lds = n | 1;
-    const int nct = (r + 15) / 16;
-    double hpf[kMPf];
-    {
-      const int jr = 16 * wid + r16;
-      const double *Hr = H + (size_t)min(jr, r - 1) * ldh;
-      const bool jv = wid < nct && jr < r;
-#pragma unroll
-      for (int u = 0; u < kMPf; u++) {
-        const int k = 4 * u + kq;
-        hpf[u] = (jv && k < n) ? Hr[k] : 0.0;
-      }
-    }
     double *Ps = sh;
     staged_copy(
         16 * n,
@@ -67,23 +52,14 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
           Ps[i * lds + k] = v;
         });
     __syncthreads();
+    const int nct = (r + 15) / 16;
     for (int t = wid; t < nct; t += kMSThreads / 64) {
       const int j0 = 16 * t, jr = j0 + r16;
       const double *Hr = H + (size_t)min(jr, r - 1) * ldh;
       const bool jv = jr < r;
       dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      int kdone = 0;
-      if (t == wid) {  // the prefetched slabs first
-        kdone = min(n, 4 * kMPf);
-#pragma unroll
-        for (int u = 0; u < kMPf; u++)
-          if (4 * u < kdone) {
-            const double a = (4 * u + kq < n) ? Ps[r16 * lds + 4 * u + kq] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, hpf[u], acc, 0, 0, 0);
-          }
-      }
       acc = tile_chain<16>(
-          kdone, n, kq, [&](int k) { return Ps[r16 * lds + k]; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
+          0, n, kq, [&](int k) { return Ps[r16 * lds + k]; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int row = i0 + kq + 4 * q, col = j0 + r16;
