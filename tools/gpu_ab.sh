@@ -1,19 +1,18 @@
-# A/B of the current library against another build (UVIO_HP_LIB) on one box, alternating runs so box
-# drift hits both arms alike.  usage: bash tools/gpu_ab.sh OTHER_LIB OUTDIR REPEATS workload...
-set -e
-R=$GRAFT_REPO_ROOT
-B=$1; O=$R/gpurun_out/$2; N=$3; shift 3
+# Same-box A/B of the current library against build/abprev/libuvio_hp_prev.so: alternating cfg3 / cfg2 bench runs.
+# usage: bash tools/gpu_ab.sh TAG [PAIRS]
+TAG=${1:-ab}; PAIRS=${2:-3}; R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/$TAG
 cd $R && mkdir -p $O
-for wl in "$@"; do
-  for i in $(seq 1 $N); do
-    # ABBA: the arm that runs first alternates, so an order effect hits both arms alike
-    if [ $((i % 2)) = 1 ]; then
-      timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
-      UVIO_HP_AB_OLD=1 UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
-    else
-      UVIO_HP_AB_OLD=1 UVIO_HP_LIB=$R/$B timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
-      timeout -k 10 300 python -u bench.py --workload $wl --cpu-frames 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
-    fi
+for i in $(seq 1 $PAIRS); do
+  for wl in cfg3 cfg2; do
+    timeout -k 10 200 python -u bench.py --workload $wl --steps 300 --cpu-frames 0 --no-host-feed > $O/new_${wl}_$i.json 2> /dev/null || exit 1
+    UVIO_HP_LIB=$R/build/abprev/libuvio_hp_prev.so UVIO_HP_AB_OLD=1 timeout -k 10 200 python -u bench.py --workload $wl --steps 300 --cpu-frames 0 --no-host-feed > $O/old_${wl}_$i.json 2> /dev/null || exit 1
   done
 done
-python tools/ab_summary.py $O > $O/summary.txt
+python - "$O" <<'PY'
+import json, glob, sys, statistics
+o = sys.argv[1]
+for wl in ("cfg3", "cfg2"):
+    for arm in ("new", "old"):
+        v = [json.loads(open(f).read().strip().splitlines()[-1])["value"] for f in sorted(glob.glob("%s/%s_%s_*.json" % (o, arm, wl)))]
+        print("%s %s: %s  median %.1f" % (wl, arm, " ".join("%.1f" % x for x in v), statistics.median(v)))
+PY
