@@ -13,6 +13,7 @@
 // chi2 = sum_k z_k^2 / d_k = r^T S^-1 r.  Rejected MSCKF / SLAM features get their rows zeroed so the
 // batch Gram (compression) and the direct EKF see only accepted rows.
 #include "dense_lds.h"
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -377,7 +378,8 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   // features too large for the LDS staging: S over many CUs first (k_chi2_S), k_chi2 reads it
   double *Sg = nullptr;
   size_t stride = 0;
-  if (!use_lds && sbuf && sbuf_cap) {
+  static const bool no_s = std::getenv("UVIO_HP_NO_CHI2_S") != nullptr;  // A/B switch: k_chi2 forms S itself
+  if (!use_lds && sbuf && sbuf_cap && !no_s) {
     stride = (size_t)max_rows_f * (max_rows_f | 1);
     const size_t need = stride * (size_t)bp.nfeat;
     if (need > *sbuf_cap) {

@@ -3,7 +3,8 @@
 // tracked feature, VioManager.cpp:366-596).  Those loops are independent per element and memory-latency
 // bound at the 20k-40k features of configs 4-5; everything order-dependent (database inserts, erasures,
 // the selected lists) stays sequential in the caller, so results do not depend on the thread count.
-// Threads: UVIO_HP_THREADS, default min(8, hardware threads).
+// Threads: UVIO_HP_THREADS, default min(16, hardware threads) (the box's CPU share per GPU; cfg4 186 vs 175
+// frames/s against 8 threads in the same-box A/B profiles/r04o_env_ab.txt).
 //
 // A frame issues a dozen parallel loops a few tens of microseconds apart, so a worker that finishes one
 // spins for a while (kSpinUs) on the job generation before it sleeps on the condition variable, and the
@@ -26,7 +27,7 @@ class WorkPool {
  public:
   WorkPool() {
     int n = (int)std::thread::hardware_concurrency();
-    n = n > 0 ? std::min(n, 8) : 1;
+    n = n > 0 ? std::min(n, 16) : 1;
     if (const char *e = std::getenv("UVIO_HP_THREADS")) n = std::max(1, std::atoi(e));
     for (int i = 1; i < n; i++) th_.emplace_back([this] { worker(); });
   }
