@@ -366,6 +366,12 @@ int uvio_hp_msckf_compressed_update(double *P, int N, const int *H_index, int n,
  * Computed as the Cholesky factor of the Gram matrix: intended for full-column-rank A (the manager's
  * update does not factor the Gram, see uvio_hp_msckf_compressed_update). */
 int uvio_hp_compress(const double *A, int m, int n, double *R_out);
+/* CamBase::undistort_f (ov_core/src/cam/CamBase.h:89; CamRadtan.h:99 cv::undistortPoints, CamEqui.h:108
+ * cv::fisheye::undistortPoints): n pixel points uv (2n floats) -> normalized uvn (2n floats) for model 0
+ * (radtan) or 1 (equidistant), cam = fx fy cx cy d0 d1 d2 d3.  Computed on the device; the equidistant
+ * points whose float could depend on the last bit of tan are recomputed on the host (ambiguous[i] = 1,
+ * may be null), so uvn equals the host libm result for every point. */
+int uvio_hp_undistort(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *ambiguous);
 
 #ifdef __cplusplus
 }

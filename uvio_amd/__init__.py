@@ -5,6 +5,6 @@ The estimator runs in ``libuvio_hp.so`` (host C++ orchestration + gfx950 HIP ker
 only binds it: ``VioManager`` mirrors ov_msckf::VioManager / uvio::UVioManager.
 """
 from . import _native  # noqa: F401
-from .manager import VioManager, apply_overrides, compress, ekf_update, load_options  # noqa: F401
+from .manager import VioManager, apply_overrides, compress, ekf_update, load_options, undistort  # noqa: F401
 
-__all__ = ["VioManager", "load_options", "apply_overrides", "ekf_update", "compress"]
+__all__ = ["VioManager", "load_options", "apply_overrides", "ekf_update", "compress", "undistort"]

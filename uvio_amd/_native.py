@@ -137,6 +137,7 @@ SIGNATURES = [
     ("ekf_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("msckf_compressed_update", _I, [_P(_D), _I, _P(_I), _I, _P(_D), _I, _P(_D), _D, _P(_D)]),
     ("compress", _I, [_P(_D), _I, _I, _P(_D)]),
+    ("undistort", _I, [_I, _P(_D), _I, _P(C.c_float), _P(C.c_float), _P(C.c_uint8)]),
     ("set_state", _I, [C.c_void_p, _P(_D), _P(_D), _I, _P(_D), _I, _I]),
     ("propagate_and_clone", _I, [C.c_void_p, _D]),
     ("msckf_update", _I, [C.c_void_p, _I, _P(C.c_uint64), _P(_I), _P(FeatMeas), _P(FeatResult)]),

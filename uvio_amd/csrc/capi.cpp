@@ -360,4 +360,14 @@ int uvio_hp_compress(const double *A, int m, int n, double *R_out) {
   }
 }
 
+int uvio_hp_undistort(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *ambiguous) {
+  try {
+    return Engine::undistort_standalone(model, cam, n, uv, uvn, ambiguous);
+  } catch (const HpError &ex) {
+    return ex.code;
+  } catch (...) {
+    return UVIO_HP_E_DEVICE;
+  }
+}
+
 }  // extern "C"

@@ -355,6 +355,7 @@ class Engine {
   static int ekf_update_standalone(double *P, int N, const int *H_index, int n, const double *H, int r, const double *res,
                                    double sigma2, double *dx_out, bool compress = false);
   static int compress_standalone(const double *A, int m, int n, double *R_out);
+  static int undistort_standalone(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *amb);
 
  private:
   uvio_hp_options_t o_;

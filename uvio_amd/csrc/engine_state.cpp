@@ -894,4 +894,40 @@ int Engine::compress_standalone(const double *A, int m, int n, double *R_out) {
   return 0;
 }
 
+
+// CamBase::undistort_f (ov_core/src/cam/CamBase.h:89, CamRadtan.h:99 / CamEqui.h:108) over n points on the
+// device; the points whose float result could depend on the equidistant model's tan (cam_undistort_f's flag)
+// are recomputed here with the host's libm, so uvn is the host's result for every point.
+int Engine::undistort_standalone(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *amb) {
+  if ((model != 0 && model != 1) || !cam || n < 0 || (n > 0 && (!uv || !uvn))) return UVIO_HP_E_ARG;
+  if (n == 0) return 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return UVIO_HP_E_DEVICE;
+  CamParams c{};
+  c.model = model;
+  for (int k = 0; k < 8; k++) c.v[k] = cam[k];
+  hipStream_t s;
+  HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  float *d_uv, *d_uvn;
+  uint8_t *d_amb;
+  HP_HIP(hipMalloc(&d_uv, sizeof(float) * 2 * (size_t)n));
+  HP_HIP(hipMalloc(&d_uvn, sizeof(float) * 2 * (size_t)n));
+  HP_HIP(hipMalloc(&d_amb, (size_t)n));
+  std::vector<uint8_t> h_amb(n);
+  HP_HIP(hipMemcpyAsync(d_uv, uv, sizeof(float) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
+  launch_undistort_points(s, c, n, d_uv, d_uvn, d_amb);
+  HP_HIP(hipMemcpyAsync(uvn, d_uvn, sizeof(float) * 2 * (size_t)n, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipMemcpyAsync(h_amb.data(), d_amb, (size_t)n, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipStreamSynchronize(s));
+  hipFree(d_uv);
+  hipFree(d_uvn);
+  hipFree(d_amb);
+  hipStreamDestroy(s);
+  for (int i = 0; i < n; i++) {
+    if (h_amb[i]) cam_undistort_f(c, uv[2 * i], uv[2 * i + 1], uvn[2 * i], uvn[2 * i + 1]);
+    if (amb) amb[i] = h_amb[i];
+  }
+  return 0;
+}
+
 }  // namespace uvhp

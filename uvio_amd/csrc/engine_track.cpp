@@ -91,9 +91,9 @@ struct Tracker::Bufs {
   char *dmem = nullptr, *hmem = nullptr;
   size_t mirror = 0;  // bytes [0, mirror) of the device block are mirrored in pinned host memory
   // device (host mirror: hp(x)); the matching inputs [p0 | sub] x kMaxCams slots and outputs
-  // [p1 | st | mask] x kMaxCams are contiguous so each direction is one copy per frame
+  // [p1 | st | mask | amb | p1n] x kMaxCams are contiguous so each direction is one copy per frame
   float *p0[kMaxCams], *p1[kMaxCams], *p0n[kMaxCams], *p1n[kMaxCams];
-  uint8_t *st[kMaxCams], *mask[kMaxCams];
+  uint8_t *st[kMaxCams], *mask[kMaxCams], *amb[kMaxCams];
   int *sub[kMaxCams], *nm[kMaxCams], *good[kMaxCams];
   double *F[kMaxCams];
   int *cells, *fastn;
@@ -278,6 +278,7 @@ void Tracker::ensure_cap(int n) {
       b.p1[k] = d.take<float>(2 * cap);
       b.st[k] = d.take<uint8_t>(cap);
       b.mask[k] = d.take<uint8_t>(cap);
+      b.amb[k] = d.take<uint8_t>(cap);    // p1n's ambiguity flags (cam_undistort_f)
       b.p1n[k] = d.take<float>(2 * cap);  // the tracked points undistorted (RANSAC's input), for the database
     }
     b.cells = d.take<int>(2 * ncell);
@@ -881,6 +882,7 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     lk.c1[ns] = c1;
     lk.p0n[ns] = b.p0n[sl];
     lk.p1n[ns] = b.p1n[sl];
+    lk.p1amb[ns] = b.amb[sl];
     rs.p0[ns] = b.p0[sl];
     rs.p1[ns] = b.p1[sl];
     rs.p0n[ns] = b.p0n[sl];
@@ -925,11 +927,12 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
 }
 
 // The database's normalized coordinates of tracked point i of a matching slot: RANSAC's undistortion of the same
-// float LK result (k_undistort runs cam_undistort_f, read back with the results) for the radial-tangential model,
-// whose arithmetic is the same on both sides; the equidistant model's tan may differ by an ulp on the device,
-// so it is undistorted here.
+// float LK result (LK's epilogue runs cam_undistort_f, read back with the results).  The radial-tangential
+// model's arithmetic is the same on both sides; the equidistant model's tan may differ by an ulp on the device,
+// which changes the float result only near a float rounding boundary: those points (flagged by the device,
+// a few in 10^5) are undistorted here with the host's libm, so the database holds the host's floats.
 void Tracker::tracked_undistort(int slot, int i, int cam, const KeyPt &k, float &un, float &vn) const {
-  if (cams_[cam].model == 0) {
+  if (cams_[cam].model == 0 || !b_->hp(b_->amb[slot])[i]) {
     const float *h = b_->hp(b_->p1n[slot]);
     un = h[2 * i];
     vn = h[2 * i + 1];
@@ -1041,10 +1044,7 @@ void Tracker::feed_multi(double t, const int *cams, int n, const DbSink &db) {
     auto undist = [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) tracked_undistort((int)j, gsrc[i], cam, good[i], nu[2 * i], nu[2 * i + 1]);
     };
-    if (pool_)
-      pool_->parallel_for(good.size(), 128, undist);
-    else
-      undist(0, good.size());
+    undist(0, good.size());  // reads of the device's results (a host undistortion is rare, see tracked_undistort)
     for (size_t i = 0; i < good.size(); i++) db(gid[i], t, cam, good[i].x, good[i].y, nu[2 * i], nu[2 * i + 1]);
     c.pts_last.swap(good);
     c.ids_last.swap(gid);
@@ -1142,7 +1142,7 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
       in_gir.emplace(ir_old[i], 0);
     }
   }
-  // the undistortions are independent per point (on the pool); the database inserts keep their order
+  // the device's undistortions (a host one is rare, see tracked_undistort); the database inserts keep their order
   std::vector<float> uvl(2 * gl.size()), uvr(2 * gr.size());
   auto undist = [&](size_t b, size_t e) {
     for (size_t i = b; i < e; i++) {
@@ -1154,10 +1154,7 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
   };
   {
     HostProfScope hs(*hp_, "trk.post.undist");
-    if (pool_)
-      pool_->parallel_for(gl.size() + gr.size(), 128, undist);
-    else
-      undist(0, gl.size() + gr.size());
+    undist(0, gl.size() + gr.size());
   }
   HostProfScope hs_db(*hp_, "trk.post.db");
   for (size_t i = 0; i < gl.size(); i++) db(gil[i], t, cl, gl[i].x, gl[i].y, uvl[2 * i], uvl[2 * i + 1]);

@@ -290,7 +290,6 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
   if (!tracker_) {
     tracker_.reset(new Tracker(o_, cams_, d_.stream, &kprof_));
     tracker_->set_host_prof(&hprof_);
-    tracker_->set_pool(&pool_);
   }
   // Propagator::propagate_and_clone reads nothing the tracker produces.  When nothing can run between the
   // tracking and the propagation (no zero-velocity check, no UWB range before t), the host computes it

@@ -225,8 +225,18 @@ HPD void cam_distort_jac(const CamParams &c, double x, double y, double *dzn, do
   }
 }
 
-// undistort_cv: cv::undistortPoints (radtan, 5 iterations) / cv::fisheye::undistortPoints
-HPD void cam_undistort_f(const CamParams &c, float u, float vv, float &xo, float &yo) {
+// True when the float rounding of v is not decided by v's leading 40 bits: a result that differs from v by a
+// few ulps (the equidistant model's tan, whose last bit differs between libm and the device) could round to
+// the other float.  Away from such a boundary (all but <= 2^-15 of the float spacing) the float is the same.
+HPD bool float_round_ambiguous(double v) {
+  const double e = fabs(v) * 0x1p-40;
+  return (float)(v - e) != (float)(v + e);
+}
+
+// undistort_cv: cv::undistortPoints (radtan, 5 iterations) / cv::fisheye::undistortPoints.  Returns true when
+// the result depends on tan's last bits (equidistant only: every other step is an IEEE operation in the same
+// order on host and device), i.e. when a caller that needs the host's libm result must recompute it there.
+HPD bool cam_undistort_f(const CamParams &c, float u, float vv, float &xo, float &yo) {
   const double *v = c.v;
   double px = u, py = vv;
   if (c.model == 0) {
@@ -248,6 +258,7 @@ HPD void cam_undistort_f(const CamParams &c, float u, float vv, float &xo, float
     }
     xo = (float)x;
     yo = (float)y;
+    return false;
   } else {
     double pwx = (px - v[2]) / v[0], pwy = (py - v[3]) / v[1];
     double scale = 1.0;
@@ -264,8 +275,10 @@ HPD void cam_undistort_f(const CamParams &c, float u, float vv, float &xo, float
       }
       scale = tan(theta) / theta_d;
     }
-    xo = (float)(pwx * scale);
-    yo = (float)(pwy * scale);
+    const double xs = pwx * scale, ys = pwy * scale;
+    xo = (float)xs;
+    yo = (float)ys;
+    return theta_d > 1e-8 && (float_round_ambiguous(xs) || float_round_ambiguous(ys));
   }
 }
 

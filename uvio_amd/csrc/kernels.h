@@ -343,8 +343,13 @@ struct LkSlots {
   // its wavefront at the end, RANSAC's inputs (launch_ransac with undistorted = true skips its own pass)
   CamParams c0[kMaxCams], c1[kMaxCams];
   float *p0n[kMaxCams] = {}, *p1n[kMaxCams] = {};
+  // optional: p1n's cam_undistort_f ambiguity flag per point (1: the host recomputes it with its libm tan)
+  uint8_t *p1amb[kMaxCams] = {};
   int undistort = 0;
 };
+// CamBase::undistort_f of n points (uv, 2n floats) into uvn on the device, with cam_undistort_f's ambiguity
+// flag per point in amb (may be null)
+void launch_undistort_points(hipStream_t s, const CamParams &cam, int n, const float *uv, float *uvn, uint8_t *amb);
 void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_level, int max_iters, float eps,
                bool init_from_p0);
 // per slot: undistort p0 (camera c0) and p1 (c1), then findFundamentalMat(FM_RANSAC, thr) over the

@@ -17,6 +17,7 @@
 //
 // MFMA operand layout (f64 16x16x4): A (16x4) lane l holds A[l & 15][l >> 4]; B (4x16) lane l holds
 // B[l >> 4][l & 15]; C/D register q of lane l is D[(l >> 4) + 4 q][l & 15].
+#include <cstdlib>
 #include <algorithm>
 #include <stdexcept>
 
@@ -399,10 +400,19 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
   if (lds > (size_t)kMaxDynLds) throw std::runtime_error("EKF update with too many columns for k_ekf_MS");
   const int nbM = (N + 15) / 16, nt = (r + 15) / 16;
   const int wpb = kMSThreads / 64;
-  const int nbS = sc.Tall ? (nt * (nt + 1) / 2 + wpb - 1) / wpb : nt;  // tile pairs, a wave each / column blocks
+  const double *Tall = sc.Tall;
+  const int nbS = Tall ? (nt * (nt + 1) / 2 + wpb - 1) / wpb : nt;  // tile pairs, a wave each / column blocks
   double *Sup = sc.S + 2 * (size_t)r * r;
+  static const bool split = std::getenv("UVIO_HP_MS_SPLIT") != nullptr;  // diagnostic: M, then S, as two launches
+  if (split) {
+    hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+                       nbM, sc.neg, Tall, sc.ldt);
+    hipLaunchKernelGGL(k_ekf_MS, dim3(nbS), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+                       0, (int *)nullptr, Tall, sc.ldt);
+    return;
+  }
   hipLaunchKernelGGL(k_ekf_MS, dim3(nbM + nbS), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
-                     nbM, sc.neg, sc.Tall, sc.ldt);
+                     nbM, sc.neg, Tall, sc.ldt);
 }
 
 void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,

@@ -1054,11 +1054,28 @@ __global__ void __launch_bounds__(64) k_lk(LkSlots job, int win, int max_level, 
     const int w = threadIdx.x;
     const float px = w ? q.x : job.p0[slot][2 * p], py = w ? q.y : job.p0[slot][2 * p + 1];
     float x, y;
-    cam_undistort_f(w ? job.c1[slot] : job.c0[slot], px, py, x, y);
+    const bool amb = cam_undistort_f(w ? job.c1[slot] : job.c0[slot], px, py, x, y);
     float *out = w ? job.p1n[slot] : job.p0n[slot];
     out[2 * p] = x;
     out[2 * p + 1] = y;
+    if (w && job.p1amb[slot]) job.p1amb[slot][p] = amb ? 1 : 0;
   }
+}
+
+__global__ void __launch_bounds__(256) k_undistort_points(CamParams cam, int n, const float *__restrict__ uv,
+                                                          float *__restrict__ uvn, uint8_t *__restrict__ amb) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  float x, y;
+  const bool a = cam_undistort_f(cam, uv[2 * p], uv[2 * p + 1], x, y);
+  uvn[2 * p] = x;
+  uvn[2 * p + 1] = y;
+  if (amb) amb[p] = a ? 1 : 0;
+}
+
+void launch_undistort_points(hipStream_t s, const CamParams &cam, int n, const float *uv, float *uvn, uint8_t *amb) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_undistort_points, dim3((n + 255) / 256), dim3(256), 0, s, cam, n, uv, uvn, amb);
 }
 
 // ---------------------------------------------------------------- undistort + RANSAC

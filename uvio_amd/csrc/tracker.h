@@ -17,7 +17,6 @@
 #include "hp_common.h"
 #include "hprof.h"
 #include "kernels.h"
-#include "pool.h"
 
 namespace uvhp {
 
@@ -52,7 +51,6 @@ class Tracker {
   // TrackBase::set_num_features (TrackBase.h:152): after an initializer succeeds (VioManagerHelper.cpp:124)
   void set_num_features(int n);
   void set_host_prof(HostProf *p) { hp_ = p; }
-  void set_pool(WorkPool *p) { pool_ = p; }  // the engine's host workers (per-point host work of the feeds)
   int device_syncs = 0;     // host waits in the last feed
   double sync_wait = 0.0;   // seconds blocked in them
   // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand
@@ -107,7 +105,6 @@ class Tracker {
   std::unordered_map<int, std::vector<int>> subset_cache_;
   std::function<void()> in_flight_;
   hipEvent_t ev_match_ = nullptr;
-  WorkPool *pool_ = nullptr;
   HostProf own_hp_;                // used when the engine does not share its own
   HostProf *hp_ = &own_hp_;        // the engine's section timer (UVIO_HP_HOST_PROF)
   // host-to-device uploads on their own stream: the DMA transfer overlaps the kernels queued before it (the

@@ -463,3 +463,19 @@ def compress(A):
     R = np.zeros((nc, nc))
     N.check(lib.uvio_hp_compress(_dp(A), m, nc - 1, _dp(R)), what="uvio_hp_compress")
     return R
+
+
+def undistort(cam, uv, return_ambiguous=False):
+    """CamBase::undistort_f (CamBase.h:89) of n pixel points on the device (uvio_hp_undistort); cam is a
+    Camera of the options.  With return_ambiguous, also the per-point flags of the points the library
+    recomputed with the host's libm tan (equidistant points next to a float rounding boundary)."""
+    lib = N.load()
+    uv = np.ascontiguousarray(uv, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros_like(uv)
+    amb = np.zeros(uv.shape[0], dtype=np.uint8)
+    intr = np.array(cam.intrinsics[:], dtype=np.float64)
+    fp = C.POINTER(C.c_float)
+    rc = lib.uvio_hp_undistort(int(cam.model), _dp(intr), uv.shape[0], uv.ctypes.data_as(fp), out.ctypes.data_as(fp),
+                               amb.ctypes.data_as(C.POINTER(C.c_uint8)))
+    N.check(rc, what="uvio_hp_undistort")
+    return (out, amb) if return_ambiguous else out
