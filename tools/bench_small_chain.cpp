@@ -4,7 +4,7 @@
 // Prints the average µs per call over REPS back-to-back calls (HIP events, caches warm) and a checksum of the
 // outputs, so two library builds or an A/B switch (UVIO_HP_MS_SPLIT: M and S as two launches) can be compared
 // for speed and for bit-equality.  Results: profiles/r04t_small_chain.txt.
-// Usage: bench_small_chain [REPS [N LDP n r LDH]] (the k_ekf_MS / full-update shapes).
+// Usage: bench_small_chain [REPS [N LDP n r LDH [TALL]]] (the k_ekf_MS / full-update shapes).
 // Build: hipcc -O2 -std=c++17 -I uvio_amd/csrc -I include tools/bench_small_chain.cpp -L uvio_amd -l:libuvio_hp.so
 //        -Wl,-rpath,'$ORIGIN/../uvio_amd' -o build/bench_small_chain
 #include <hip/hip_runtime.h>
@@ -52,6 +52,7 @@ int main(int argc, char **argv) {
   const int uN = argc > 2 ? atoi(argv[2]) : 313, uldp = argc > 3 ? atoi(argv[3]) : uN;
   const int un = argc > 4 ? atoi(argv[4]) : 163, ur = argc > 5 ? atoi(argv[5]) : 100;
   const int uldh = argc > 6 ? atoi(argv[6]) : un;
+  const bool utall = argc > 7 ? atoi(argv[7]) != 0 : true;  // 0: no T from a chi2 gate (delayed initialization)
   std::mt19937_64 rng(11);
   std::uniform_real_distribution<double> U(-1.0, 1.0);
   hipStream_t s;
@@ -98,7 +99,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&sc.M, sizeof(double) * N * r));
     CK(hipMalloc(&sc.S, sizeof(double) * 4 * r * r));
     sc.neg = dneg;
-    sc.Tall = dT;
+    sc.Tall = utall ? dT : nullptr;
     sc.ldt = ldh;
     launch_ekf_phaseA(s, dP, ldp, N, dH, ldh, r, n, dI, 1e-4, sc);
     CK(hipStreamSynchronize(s));
@@ -135,7 +136,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&sc.dx, sizeof(double) * (N + 2)));
     CK(hipMalloc(&sc.Dinv, sizeof(double) * 256 * (r / 16 + 2)));
     sc.neg = dneg;
-    sc.Tall = dT;
+    sc.Tall = utall ? dT : nullptr;
     sc.ldt = ldh;
     const int reps2 = reps < 50 ? reps : 50;  // P shrinks with every update
     CK(hipEventRecord(e0, s));

@@ -73,6 +73,14 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
     // T = H P_II is already in HBM from the batch's chi2 gate (k_gemm_HPg, rejected features' rows zeroed
     // there with their H rows), so S_up[a][b] = H_a T_b^T directly: one upper tile pair (a <= b) per wave,
     // one chain of loads instead of forming T_b first (same products, same ascending k order).
+    // ldt < 0: Tall is this update's M = P[:, I] H^T (N x r, launched after the M blocks), whose rows hidx are
+    // T^T: T[b][k] = M[hidx[k]][b], the products and k order with which the column blocks below form T.
+    const bool gath = ldt < 0;
+    int *hs = (int *)sh;
+    if (gath) {
+      for (int k = threadIdx.x; k < n; k += blockDim.x) hs[k] = hidx[k];
+      __syncthreads();
+    }
     const int nt = (r + 15) / 16;
     int pair = (blockIdx.x - nbM) * (kMSThreads / 64) + wid, at = 0;
     if (pair >= nt * (nt + 1) / 2) return;
@@ -82,11 +90,13 @@ __global__ void __launch_bounds__(kMSThreads) k_ekf_MS(const double *__restrict_
     }
     const int bt = at + pair;
     const int ar = 16 * at + r16, br = 16 * bt + r16;
-    const double *Ha = H + (size_t)min(ar, r - 1) * ldh, *Tb = Tall + (size_t)min(br, r - 1) * ldt;
+    const double *Ha = H + (size_t)min(ar, r - 1) * ldh;
+    const double *Tb = gath ? Tall + min(br, r - 1) : Tall + (size_t)min(br, r - 1) * ldt;
     const bool av = ar < r, bv = br < r;
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
     acc = tile_chain<16>(
-        0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return bv ? Tb[k] : 0.0; }, acc);
+        0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; },
+        [&](int k) { return bv ? (gath ? Tb[(size_t)hs[k] * r] : Tb[k]) : 0.0; }, acc);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int row = 16 * at + kq + 4 * q, col = 16 * bt + r16;
@@ -403,6 +413,18 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
   const double *Tall = sc.Tall;
   const int nbS = Tall ? (nt * (nt + 1) / 2 + wpb - 1) / wpb : nt;  // tile pairs, a wave each / column blocks
   double *Sup = sc.S + 2 * (size_t)r * r;
+  // No T from a chi2 gate (the delayed initialization's update): S from this update's own M in a second
+  // launch (rows hidx of M are T^T) instead of each S column block forming T from P (r04v: 26 us per launch in
+  // the cfg3 frame).  UVIO_HP_MS_FROM_P=1: the one-launch form (A/B).
+  static const bool from_p = std::getenv("UVIO_HP_MS_FROM_P") != nullptr;
+  if (!Tall && !from_p) {
+    const int nbG = (nt * (nt + 1) / 2 + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+                       nbM, sc.neg, (const double *)nullptr, 0);
+    hipLaunchKernelGGL(k_ekf_MS, dim3(nbG), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
+                       0, (int *)nullptr, (const double *)sc.M, -1);
+    return;
+  }
   static const bool split = std::getenv("UVIO_HP_MS_SPLIT") != nullptr;  // diagnostic: M, then S, as two launches
   if (split) {
     hipLaunchKernelGGL(k_ekf_MS, dim3(nbM), dim3(kMSThreads), lds, s, P, ldp, N, H, ldh, r, n, hidx, sigma2, sc.M, Sup,
