@@ -93,6 +93,31 @@ def test_product_fails_loudly_without_gpu(euroc_yaml):
         U.ekf_update(P, [0], [[1.0]], [0.5], 1.0)
 
 
+def test_undistort_arguments_and_no_gpu(euroc_yaml):
+    """uvio_hp_undistort: argument errors before any device work, an empty batch is a no-op, and points on a
+    CPU-only box fail loudly (E_DEVICE; the host never undistorts a batch by itself)."""
+    import numpy as np
+    import torch
+    import uvio_amd as U
+    from uvio_amd import _native as N
+    lib = N.load()
+    cam = np.zeros(8)
+    fp = C.POINTER(C.c_float)
+    uv = np.zeros(2, np.float32)
+    out = np.zeros(2, np.float32)
+    args = (cam.ctypes.data_as(C.POINTER(C.c_double)), 1, uv.ctypes.data_as(fp), out.ctypes.data_as(fp), None)
+    assert lib.uvio_hp_undistort(2, *args) == N.E_ARG  # no such camera model
+    assert lib.uvio_hp_undistort(0, None, 1, args[2], args[3], None) == N.E_ARG
+    assert lib.uvio_hp_undistort(0, args[0], -1, args[2], args[3], None) == N.E_ARG
+    assert lib.uvio_hp_undistort(1, args[0], 1, None, args[3], None) == N.E_ARG
+    assert lib.uvio_hp_undistort(0, args[0], 0, None, None, None) == 0
+    o = U.load_options(euroc_yaml)
+    assert U.undistort(o.cams[0], np.zeros((0, 2), np.float32)).shape == (0, 2)
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="E_DEVICE"):
+            U.undistort(o.cams[0], np.ones((3, 2), np.float32))
+
+
 def _cfg(name):
     return os.path.join(ROOT, "configs", name, "estimator_config.yaml")
 
