@@ -29,7 +29,9 @@ extern "C" {
 
 #define UVIO_HP_OK 0
 #define UVIO_HP_E_ARG (-1)      /* bad argument / size */
-#define UVIO_HP_E_STATE (-2)    /* not initialized, or call not valid in this state */
+#define UVIO_HP_E_STATE (-2)    /* not initialized, or call not valid in this state; every state-changing call
+                                   after a fatal error (E_NUMERIC / E_DEVICE / E_INTERNAL, where the reference
+                                   std::exit's) returns it: the estimator is stopped, destroy the handle */
 #define UVIO_HP_E_DEVICE (-3)   /* HIP runtime error or no MI355X device */
 #define UVIO_HP_E_NUMERIC (-4)  /* negative covariance diagonal (ref: std::exit) */
 #define UVIO_HP_E_CONFIG (-5)   /* config file missing / unparsable */

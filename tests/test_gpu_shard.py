@@ -5,8 +5,9 @@
   EuRoC stream and at the BASELINE sizes it exists for (bench.py cfg4: 800 MSCKF features x 52 measurements,
   cfg5: 1500 features, IMU intrinsics, UWB), where the tiled T GEMM (m >= 4096), the MFMA Gram (m >= 8192),
   the chunked batch build (>= 256 features) and the n > 135 information-form factors run.
-* world 2 and 4 on one MI355X at cfg4 / cfg5 (one fresh process per rank, host all-reduce over gloo, since
-  RCCL needs one GPU per rank): EVERY rank runs its own oracle in lock-step at the strict bounds (its MSCKF
+* world 2 and 4 on one MI355X at cfg4 / cfg5, and world 8 at cfg5 (BASELINE.json's "8xMI355X sharded
+  compression" split, 8 ranks of the 1500-feature update) (one fresh process per rank, host all-reduce over
+  gloo, since RCCL needs one GPU per rank): EVERY rank runs its own oracle in lock-step at the strict bounds (its MSCKF
   per-feature results are its shard of the oracle's), the replicas' states and covariances are bit-identical
   after every frame, and the shards are disjoint and together make up the oracle's update.
 * world 2 on the EuRoC stream: the sharded run agrees with an unsharded run of the same stream.
@@ -196,7 +197,7 @@ def _rank_lockstep(rank, world, port, q, wl):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("wl,world", [("cfg4", 2), ("cfg4", 4), ("cfg5", 2), ("cfg5", 4)])
+@pytest.mark.parametrize("wl,world", [("cfg4", 2), ("cfg4", 4), ("cfg5", 2), ("cfg5", 4), ("cfg5", 8)])
 def test_sharded_gloo_lockstep_baseline_size(wl, world):
     from conftest import record_steer
     from test_gpu_parity import STEER_MARGIN

@@ -161,3 +161,97 @@ def test_lockstep_images(euroc_yaml):
     assert sum(a["timing"]["n_msckf"] for a, _ in steps) > 0
     assert sum(a["timing"]["n_slam_delayed"] for a, _ in steps) > 0
     P._check_lockstep(steps)
+
+
+def _predetect_pair(opts, s, r, n, subset_frame=None, subset=None):
+    """Two estimators on one stream, one with the next-frame detection run ahead on the worker thread and the
+    detection stream (the default), one with it off (UVIO_HP_NO_PREDETECT=1): after every frame the states,
+    covariances, track ids and points must be bit-identical.  Frame `subset_frame` feeds only the cameras
+    `subset` (a camera set different from the last feed's: the run-ahead result is discarded)."""
+    import uvio_amd as U
+    old = os.environ.pop("UVIO_HP_NO_PREDETECT", None)
+    try:
+        a = U.VioManager(opts)
+        os.environ["UVIO_HP_NO_PREDETECT"] = "1"
+        b = U.VioManager(opts)
+    finally:
+        os.environ.pop("UVIO_HP_NO_PREDETECT", None)
+        if old is not None:
+            os.environ["UVIO_HP_NO_PREDETECT"] = old
+    for m in (a, b):
+        m.initialize_with_gt(s.gt_state(s.t0))
+    nf = 0
+    n_msckf = 0
+    for kind, t, i in s.events():
+        if t < s.t0 - 0.4:
+            continue
+        if kind == "imu":
+            for m in (a, b):
+                m.feed_measurement_imu(t, s.wm[i], s.am[i])
+            continue
+        if kind != "cam" or t <= s.t0:
+            continue
+        nf += 1
+        cams = list(subset) if nf == subset_frame else list(range(s.K))
+        imgs = [r.render(k, *s.camera_pose(i, k), frame_seed=i).cpu().numpy() for k in cams]
+        for m in (a, b):
+            m.feed_measurement_camera(t, cams, imgs)
+        xa, xb = a.get_state_vector()[0], b.get_state_vector()[0]
+        assert np.array_equal(xa, xb), ("state", nf)
+        assert np.array_equal(a.get_cov(), b.get_cov()), ("covariance", nf)
+        for c in range(s.K):
+            ia, ua = a.get_tracks(c)
+            ib, ub = b.get_tracks(c)
+            assert np.array_equal(ia, ib) and np.array_equal(ua, ub), ("tracks", nf, c)
+        n_msckf += a.get_timing()["n_msckf"]
+        if nf >= n:
+            break
+    a.close()
+    b.close()
+    assert nf == n and n_msckf > 0
+
+
+def test_predetect_on_off_bit_identical_cfg1_mono(euroc_yaml):
+    """cfg1 (EuRoC mono, bench.py): the detection run ahead under the update chain changes nothing"""
+    import uvio_amd as U
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(euroc_yaml, num_cameras=1, use_stereo=0, init_max_features=200, max_msckf_in_update=100,
+                          max_slam_features=20, max_slam_in_update=10, dt_slam_delay=0.3)
+    n = 24
+    s = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=4)
+    _predetect_pair(opts, s, SceneRenderer(opts, device="cuda"), n)
+
+
+def test_predetect_on_off_bit_identical_four_cameras():
+    """the 4-camera rig (each camera tracked on its own, feed_multi), with one frame of 3 cameras"""
+    import uvio_amd as U
+    from uvio_amd.render import SceneRenderer
+    from uvio_amd.sim import SimStream
+    cfg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "rpng_sim_uwb",
+                       "estimator_config.yaml")
+    opts = U.load_options(cfg, init_max_features=800, max_msckf_in_update=200, max_slam_features=20,
+                          max_slam_in_update=10, dt_slam_delay=0.3)
+    n = 20
+    s = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=5, spawn=4)
+    _predetect_pair(opts, s, SceneRenderer(opts, device="cuda"), n, subset_frame=12, subset=[0, 2, 3])
+
+
+def test_second_device_image_frames(euroc_yaml):
+    """A manager created for GPU 1 (the N > 1 bench ranks' form) feeds image frames -- its tracker's run-ahead
+    detection binds that device on the worker thread -- and its estimate equals the GPU 0 manager's bit for bit.
+    Needs two GPUs (skipped on a one-GPU box)."""
+    import torch
+    import uvio_amd as U
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU")
+    opts, s, r = _setup(euroc_yaml, 16, init_max_features=200, max_msckf_in_update=100, max_slam_features=20,
+                        max_slam_in_update=10, dt_slam_delay=0.3)
+    out = []
+    for dev in (0, 1):
+        m = U.VioManager(opts, device=dev)
+        s.run(m, n_frames=14, renderer=r)
+        out.append((m.get_state_vector()[0], m.get_cov(), m.get_tracks(0)))
+        m.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2][0], out[1][2][0]) and np.array_equal(out[0][2][1], out[1][2][1])

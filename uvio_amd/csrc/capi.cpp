@@ -10,6 +10,10 @@ using namespace uvhp;
 struct uvio_hp {
   Engine *e = nullptr;
   std::string err;
+  // set by a fatal error of a state-changing call (the reference std::exit's on these: negative covariance
+  // diagonal, StateHelper.cpp:112,181; a device or internal error likewise leaves the frame half applied, e.g.
+  // measurements already trimmed from the feature database): every later state-changing call is refused
+  std::string fatal;
 };
 
 // an exception that is not an HpError is a host-side logic error (e.g. std::out_of_range from a map
@@ -22,6 +26,7 @@ static std::string internal_error(const uvio_hp *h, const std::exception &ex) {
 
 #define HP_GUARD(h, body)                                    \
   try {                                                      \
+    if ((h) && (h)->e) HP_HIP(hipSetDevice((h)->e->device())); \
     body                                                     \
   } catch (const HpError &ex) {                              \
     if (h) (h)->err = ex.what();                             \
@@ -29,6 +34,19 @@ static std::string internal_error(const uvio_hp *h, const std::exception &ex) {
   } catch (const std::exception &ex) {                       \
     if (h) (h)->err = internal_error(h, ex);                 \
     return UVIO_HP_E_INTERNAL;                               \
+  }
+
+// a state-changing entry: refused after a fatal error; a fatal result stops the estimator
+static bool is_fatal(int rc) { return rc == UVIO_HP_E_NUMERIC || rc == UVIO_HP_E_DEVICE || rc == UVIO_HP_E_INTERNAL; }
+#define HP_FEED(h, call)                                                                         \
+  if (!(h)->fatal.empty()) {                                                                     \
+    (h)->err = "estimator stopped by an earlier fatal error (" + (h)->fatal + ")";             \
+    return UVIO_HP_E_STATE;                                                                      \
+  }                                                                                              \
+  {                                                                                              \
+    const int rc_ = [&]() -> int { HP_GUARD(h, return (call);) }();                              \
+    if (is_fatal(rc_)) (h)->fatal = (h)->err;                                                    \
+    return rc_;                                                                                  \
   }
 
 extern "C" {
@@ -94,19 +112,19 @@ int uvio_hp_feed_imu_batch(uvio_hp_t *h, int n, const double *t, const double *w
 int uvio_hp_feed_simulation(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const int *counts, const uint64_t *ids,
                             const float *uv) {
   if (!h || ncam <= 0 || !cam_ids || !counts) return UVIO_HP_E_ARG;
-  HP_GUARD(h, return h->e->feed_simulation(t, ncam, cam_ids, counts, ids, uv);)
+  HP_FEED(h, h->e->feed_simulation(t, ncam, cam_ids, counts, ids, uv))
 }
 
 int uvio_hp_feed_camera(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
                         const int *strides, const uint8_t *const *masks) {
   if (!h || ncam <= 0 || !cam_ids || !imgs || !strides) return UVIO_HP_E_ARG;
-  HP_GUARD(h, return h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, false);)
+  HP_FEED(h, h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, false))
 }
 
 int uvio_hp_feed_camera_device(uvio_hp_t *h, double t, int ncam, const int *cam_ids, const uint8_t *const *imgs,
                                const int *strides, const uint8_t *const *masks) {
   if (!h || ncam <= 0 || !cam_ids || !imgs || !strides) return UVIO_HP_E_ARG;
-  HP_GUARD(h, return h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, true);)
+  HP_FEED(h, h->e->feed_camera(t, ncam, cam_ids, imgs, strides, masks, true))
 }
 
 int uvio_hp_get_tracks(uvio_hp_t *h, int cam, uint64_t *ids, float *uv, int cap, int *n) {
@@ -145,7 +163,7 @@ int uvio_hp_get_pyramid(uvio_hp_t *h, int cam, int level, int *w, int *hgt, uint
 
 int uvio_hp_feed_uwb(uvio_hp_t *h, double t, int n, const uint64_t *ids, const double *ranges) {
   if (!h || n < 0) return UVIO_HP_E_ARG;
-  HP_GUARD(h, return h->e->feed_uwb(t, n, ids, ranges);)
+  HP_FEED(h, h->e->feed_uwb(t, n, ids, ranges))
 }
 
 int uvio_hp_init_anchors(uvio_hp_t *h, int n, const uvio_hp_anchor_t *a) {
@@ -233,39 +251,39 @@ int uvio_hp_set_state(uvio_hp_t *h, const double *val, const double *fej, int le
 }
 int uvio_hp_propagate_and_clone(uvio_hp_t *h, double t) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_propagate_and_clone(t); })
+  HP_FEED(h, h->e->api_propagate_and_clone(t))
 }
 int uvio_hp_msckf_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
                          const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_update(Engine::API_MSCKF, nfeat, featids, meas_off, meas, out); })
+  HP_FEED(h, h->e->api_update(Engine::API_MSCKF, nfeat, featids, meas_off, meas, out))
 }
 int uvio_hp_slam_update(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
                         const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_update(Engine::API_SLAM, nfeat, featids, meas_off, meas, out); })
+  HP_FEED(h, h->e->api_update(Engine::API_SLAM, nfeat, featids, meas_off, meas, out))
 }
 int uvio_hp_slam_delayed_init(uvio_hp_t *h, int nfeat, const uint64_t *featids, const int *meas_off,
                               const uvio_hp_feat_meas_t *meas, uvio_hp_feat_result_t *out) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_update(Engine::API_DELAYED, nfeat, featids, meas_off, meas, out); })
+  HP_FEED(h, h->e->api_update(Engine::API_DELAYED, nfeat, featids, meas_off, meas, out))
 }
 int uvio_hp_slam_change_anchors(uvio_hp_t *h) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_change_anchors(); })
+  HP_FEED(h, h->e->api_change_anchors())
 }
 int uvio_hp_marginalize_slam(uvio_hp_t *h) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_marginalize_slam(); })
+  HP_FEED(h, h->e->api_marginalize_slam())
 }
 int uvio_hp_marginalize_old_clone(uvio_hp_t *h) {
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_marginalize_old_clone(); })
+  HP_FEED(h, h->e->api_marginalize_old_clone())
 }
 int uvio_hp_uwb_update_single(uvio_hp_t *h, double t, uint64_t anchor_id, double range, int *applied) {
   (void)t;  // the reference's Jacobian does not read the measurement time (UVioUpdaterHelper.cpp:147-241)
   if (!h) return UVIO_HP_E_ARG;
-  HP_GUARD(h, { return h->e->api_uwb_update_single(anchor_id, range, applied); })
+  HP_FEED(h, h->e->api_uwb_update_single(anchor_id, range, applied))
 }
 
 int uvio_hp_debug_last_msckf(uvio_hp_t *h, uint64_t *ids, double *pG, int *status, double *chi2, int cap, int *n) {

@@ -328,6 +328,9 @@ class Engine {
   int feed_uwb(double t, int n, const uint64_t *ids, const double *ranges);
   Tracker *tracker() { return tracker_.get(); }
   int init_anchors(int n, const uvio_hp_anchor_t *a);
+  // HIP's current device is per host thread: every C-ABI entry binds the engine's device first, so a handle
+  // created for GPU k may be driven from any thread
+  int device() const { return device_; }
 
   // getters
   bool initialized() const { return is_initialized_; }

@@ -460,10 +460,16 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
       {"pyramid", "k_hist_multi,k_pyr_pair", 0},
+      {"fast", "k_fast_score,k_fast_select", 0},
+      {"subpix", "k_subpix", 0},
   };
+  // the tracker's detection stream (predetect on the worker thread) keeps its own event pairs
+  const KProf *pre = nullptr;
   if (flush) {
     HP_HIP(hipStreamSynchronize(d_.stream));
     kprof_.harvest(true);
+    if (tracker_) pre = &tracker_->pre_prof();
+    // LK bytes are counted on the device by both streams' timed launches (LkSlots::bytes), never credited
     if (tracker_) kprof_.bytes[KC_LK] = (double)tracker_->lk_bytes();
   }
   *n = KC_COUNT;
@@ -473,10 +479,10 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
     std::snprintf(o.name, sizeof(o.name), "%s", info[k].name);
     std::snprintf(o.kernels, sizeof(o.kernels), "%s", info[k].kernels);
     o.bound = info[k].bound;
-    o.launches = kprof_.launches[k];
-    o.seconds = kprof_.secs[k];
-    o.flops = kprof_.flops[k];
-    o.bytes = kprof_.bytes[k];
+    o.launches = kprof_.launches[k] + (pre ? pre->launches[k] : 0);
+    o.seconds = kprof_.secs[k] + (pre ? pre->secs[k] : 0.0);
+    o.flops = kprof_.flops[k] + (pre ? pre->flops[k] : 0.0);
+    o.bytes = kprof_.bytes[k] + (pre ? pre->bytes[k] : 0.0);
   }
 }
 

@@ -505,7 +505,7 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     if (nc == cell0[r]) continue;
     req_cam[r] = nf;
     fj.img[nf] = q.p->img[0];
-    fj.score[nf] = cs_[q.cam].d_score;
+    fj.score[nf] = cs_.at(q.cam).d_score;  // at(): may run on the worker (predetect)
     fj.w[nf] = W;
     fj.sw[nf] = size_x;
     fj.sh[nf] = size_y;
@@ -515,7 +515,16 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
   if (nc == 0) return;
   fj.ncam = nf;
   upload(b.cells, b.hp(b.cells), 2 * nc * sizeof(int));
-  launch_fast_multi(cur_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
+  {
+    KScope ks(kcur(), KC_FAST);
+    launch_fast_multi(cur_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
+  }
+  // algorithmic bytes: each cell's pixels read by the score pass, its score map written and read by the selection
+  if (kcur()) {
+    double px = 0.0;
+    for (int k = 0; k < nf; k++) px += (double)fj.sw[k] * fj.sh[k] * (fj.cell_end[k] - (k ? fj.cell_end[k - 1] : 0));
+    kcur()->credit(KC_FAST, 0.0, 3.0 * px);
+  }
   HP_HIP(hipMemcpyAsync(b.hp(b.fastn), b.fastn, span(b.fastn, b.fast + (size_t)3 * nc * nfg), hipMemcpyDeviceToHost, cur_));
   sync();
   const int *h_fastn = b.hp(b.fastn);
@@ -557,7 +566,12 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     sj.ncam++;
   }
   upload(b.det, h_det, 2 * np * sizeof(float));
-  launch_subpix_multi(cur_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
+  {
+    KScope ks(kcur(), KC_SUBPIX);
+    launch_subpix_multi(cur_, sj, b.det, b.spmask, kSubpixWin, kSubpixIters, kSubpixEps * kSubpixEps);
+  }
+  // algorithmic bytes: per corner the (2 win + 3)^2 image patch its iterations sample, the point read and written
+  if (kcur()) kcur()->credit(KC_SUBPIX, 0.0, (double)np * ((2 * kSubpixWin + 3) * (2 * kSubpixWin + 3) + 16));
   const bool do_lk = lk_to && nr == 1;
   if (do_lk) {
     LkSlots lk{};
@@ -567,10 +581,10 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
     lk.p1[0] = b.det1;
     lk.st[0] = b.detst;
     lk.n[0] = np;
-    // the kernel-class timing brackets the library stream only: a predetect's LK is not timed (nor counted)
-    lk.bytes = (kp_ && kp_->on && !pre_mode_) ? d_lk_bytes_ : nullptr;
+    // timed on the stream it runs on (the library's, or the detection stream's pairs while predetecting)
+    lk.bytes = (kcur() && kcur()->on) ? d_lk_bytes_ : nullptr;
     {
-      KScope ks(pre_mode_ ? nullptr : kp_, KC_LK);
+      KScope ks(kcur(), KC_LK);
       launch_lk(cur_, lk, 1, win_, pyr_levels_, kLkIters, kLkEps, true);
     }
     HP_HIP(hipMemcpyAsync(h_det, b.det, span(b.det, b.detst + np), hipMemcpyDeviceToHost, cur_));
@@ -1183,6 +1197,9 @@ void Tracker::predetect() {
   }
   if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
   if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
+  kp_pre_.stream = sd_;
+  kp_pre_.on = kp_ && kp_->on;
+  kp_pre_.harvest(false);
   pre_.currid0 = currid;
   pre_.cams = last_cams_;
   pre_.pts.assign(n, {});
@@ -1234,6 +1251,8 @@ void Tracker::worker_loop() {
     w_busy_ = true;
     lk.unlock();
     try {
+      // HIP's current device is per thread: bind the engine's before any HIP call of this task
+      HP_HIP(hipSetDevice(dev_));
       predetect();
     } catch (...) {
       w_err_ = std::current_exception();
@@ -1246,12 +1265,22 @@ void Tracker::worker_loop() {
 
 void Tracker::predetect_async() {
   predetect_join();
+  HP_HIP(hipGetDevice(&dev_));  // the engine's device (bound by the calling C-ABI entry)
   if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });
   {
     std::lock_guard<std::mutex> lk(wm_);
     w_task_ = true;
   }
   wcv_.notify_all();
+}
+
+const KProf &Tracker::pre_prof() {
+  predetect_join();
+  if (sd_) {
+    HP_HIP(hipStreamSynchronize(sd_));
+    kp_pre_.harvest(true);
+  }
+  return kp_pre_;
 }
 
 void Tracker::predetect_join() {

@@ -18,6 +18,8 @@ enum KClass {
   KC_LDL,          // k_ekf_fact: LDL^T / Cholesky (+ inverse) of the innovation covariance (inside KC_EKF)
   KC_LK,           // k_lk: pyramidal LK
   KC_PYR,          // k_hist_multi + k_pyr_pair: equalizeHist + pyramid + Scharr
+  KC_FAST,         // k_fast_score + k_fast_select: grid FAST + NMS + per-cell top-k (Grider_GRID.h:108-151)
+  KC_SUBPIX,       // k_subpix: cornerSubPix of the new corners (Grider_GRID.h:174)
   KC_COUNT
 };
 

@@ -68,6 +68,9 @@ class Tracker {
   void predetect_join();
   int pre_syncs = 0;        // host waits / seconds of the last predetect (on its own thread: off the frame)
   double pre_wait = 0.0;
+  // the kernel-class timing of the detection stream (the predetect's FAST / sub-pixel / stereo LK launches on
+  // sd_, recorded from the worker thread): joins the predetect, waits for its stream, harvests every pair
+  const KProf &pre_prof();
 
  private:
   struct CamState {
@@ -94,6 +97,8 @@ class Tracker {
   const CamParams *cams_;
   hipStream_t s_;
   KProf *kp_ = nullptr;
+  KProf kp_pre_;  // the detection stream's event pairs (used by the worker thread while pre_mode_)
+  KProf *kcur() { return pre_mode_ ? &kp_pre_ : kp_; }
   unsigned long long *d_lk_bytes_ = nullptr;
   bool downsample_ = false;  // VioManager.cpp:270-278: the inputs are 2w x 2h and pyrDown'ed first
   int num_features_, threshold_, grid_x_, grid_y_, min_px_dist_, histogram_method_;
@@ -145,6 +150,7 @@ class Tracker {
   std::mutex wm_;
   std::condition_variable wcv_;
   bool w_task_ = false, w_busy_ = false, w_quit_ = false;
+  int dev_ = 0;  // the engine's HIP device, bound on the worker before each task
   std::exception_ptr w_err_;
   void worker_loop();
   void discard_predetect() {
