@@ -29,7 +29,9 @@ makes the sharded run the value instead.
 Other workloads (--workload, SURVEY.md §8 cfg 1-5; parity-test cases and stress lines):
   cfg1  EuRoC MH_01-shaped MONO 752x480 images (configs/euroc_mav, max_cameras 1), 11 clones, <= 100 MSCKF
   cfg2  EuRoC V1_02-shaped stereo 752x480 images (configs/euroc_mav), 11 clones, <= 200 MSCKF + 50 SLAM
-  cfg2l cfg2 with track loss (scene churn), 400 tracks
+  cfg2l cfg2 with track loss (scene churn: each texture panel redraws every 8 frames), 400 tracks
+  cfg3t cfg3's rig and window with a TrackSIM feed at BASELINE's MSCKF load: 400 features per update, each seen
+        in every clone by both cameras (the N = 1 line's "msckf_load" companion, --msckf-load-steps)
   cfg4 / cfg5  the backend stress at BASELINE's feature counts: TrackSIM feed with 800 / 1500 MSCKF features
         per update, each seen in every clone (26 clones x 2 cameras / 31 clones x 1 of 4 cameras, + 6 UWB
         anchors and IMU intrinsics + g-sensitivity at cfg5) -- the shapes BASELINE.json's cfg4 / cfg5 name
@@ -77,19 +79,29 @@ WORKLOADS = {
                   dt_slam_delay=1.0),
              dict(spawn=4),
              "cfg2 EuRoC V1_02-shaped stereo 752x480 images, 11 clones, <=200 MSCKF + 50 SLAM"),
-    # cfg2 with real track loss: 400 stereo tracks over a scene whose texture panels redraw every 4 frames
-    # (render.py churn), so each update holds 100+ lost / marginalized MSCKF features
+    # cfg2 with real track loss: 400 stereo tracks over a scene whose texture panels each redraw every 8 frames
+    # at their own phase (render.py churn), so a track lives a few frames and is lost with several observations
+    # (round 4's churn 3 lost most tracks after 2 observations: 1.3 rows per feature)
     "cfg2l": ("euroc_mav", "images",
               dict(init_max_features=800, max_msckf_in_update=200, max_slam_features=50, max_slam_in_update=25,
                    dt_slam_delay=1.0),
-              dict(spawn=4, churn=3),
-              "cfg2l EuRoC V1_02-shaped stereo 752x480 images with track loss (scene churn 1/3 per frame), 400 "
+              dict(spawn=4, churn=8),
+              "cfg2l EuRoC V1_02-shaped stereo 752x480 images with track loss (scene churn 1/8 per frame), 400 "
               "tracks, 11 clones, <=200 MSCKF + 50 SLAM"),
     "cfg3": ("tum_vi", "images",
              dict(max_clone_size=20, init_max_features=800, num_pts=400, max_msckf_in_update=400,
                   max_slam_features=50, max_slam_in_update=25, dt_slam_delay=1.0),
              dict(spawn=4),
              "cfg3 TUM-VI room1-shaped stereo fisheye 512x512 images, 20 clones, 400 tracks/cam, <=400 MSCKF + 50 SLAM"),
+    # cfg3 at BASELINE's MSCKF load (the N = 1 line's "msckf_load" companion): the TUM-VI stereo rig and window
+    # of cfg3 with a TrackSIM feed whose every update holds 400 MSCKF features seen in every clone by both
+    # cameras (up to 400 x 81 = 32,400 stacked rows), so the MFMA paths (tiled T GEMM,
+    # MFMA Gram, information-form factors) run every frame
+    "cfg3t": ("tum_vi", "tracks",
+              dict(max_clone_size=20, max_msckf_in_update=400, max_slam_features=50, max_slam_in_update=25,
+                   dt_slam_delay=1.0),
+              dict(spawn=400, frac_lost=0.0, frac_long=0.02),
+              "cfg3t TUM-VI room1-shaped stereo fisheye 512x512 tracks, 20 clones, 400 MSCKF feats x 42 meas + 50 SLAM"),
     # the backend stress at the BASELINE feature counts: every MSCKF update holds 800 / 1500 features seen in
     # every clone (TrackSIM feed); the feature-sharded multi-GPU lines run these
     "cfg4": ("uzhfpv_outdoor_45", "tracks",
@@ -120,7 +132,8 @@ WORKLOADS = {
 ALIASES = {"cfg4t": "cfg4", "cfg5t": "cfg5"}
 # oracle frames in the cpu_baseline sample (~10-30 s of CPU work per workload)
 CPU_CV_THREADS = 4  # num_opencv_threads of every reference config
-CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg2l": 60, "cfg3": 60, "cfg4i": 20, "cfg5i": 10, "cfg4": 3, "cfg5": 2}
+CPU_FRAMES = {"cfg1": 150, "cfg2": 120, "cfg2l": 60, "cfg3": 60, "cfg4i": 20, "cfg5i": 10, "cfg3t": 6, "cfg4": 3,
+              "cfg5": 2}
 # shader clock for cycle counts (MI355X peak engine clock, MI355X_MICROARCH.md) and the CU count
 SCLK_HZ = 2.4e9
 N_CU = 256
@@ -403,6 +416,8 @@ def main():
     ap.add_argument("--sharded-steps", type=int, default=100,
                     help="N > 1: timed frames of the feature-sharded companion run (0 = skip)")
     ap.add_argument("--shard-min", type=int, default=64, help="smallest MSCKF update that is sharded")
+    ap.add_argument("--msckf-load-steps", type=int, default=60,
+                    help="N = 1 cfg3 line: timed frames of the cfg3t companion at BASELINE's MSCKF load (0 = skip)")
     ap.add_argument("--ktime-period", type=int, default=None,
                     help="kernel-class event timing on every k-th frame of the timed region (0 = off; default: every "
                          "frame for --steps <= 50, else every 10th)")
@@ -534,6 +549,10 @@ def main():
     if frames is not None and world == 1 and not args.no_host_feed:
         mgr.close()
         host_feed = host_feed_pass(U, opts, sim, frames, warm, args.steps, barrier, x_ref=[r[2] for r in rec])
+    msckf_load = None
+    if world == 1 and wl == "cfg3" and not shard and args.msckf_load_steps > 0:
+        mgr.close()
+        msckf_load = msckf_load_companion(U, args, dev)
     sharded = None
     if world > 1 and not shard and args.sharded_steps > 0:
         mgr.close()
@@ -598,6 +617,7 @@ def main():
             "rooflines": rl,
             "host_feed": host_feed,
             "feature_sharded": sharded,
+            "msckf_load": msckf_load,
             "cpu_baseline": cpu,
         }
         result_out.write(json.dumps(out) + "\n")
@@ -605,6 +625,60 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def msckf_load_companion(U, args, dev):
+    """cfg3 at BASELINE's MSCKF load (workload cfg3t): the same rig, window and limits as the cfg3 line, fed
+    TrackSIM tracks so that every update holds 400 MSCKF features seen in all 21 clones by both cameras.  Its own
+    frame rate, per-class rooflines (live HIP-event timing) and dominant class, as the main line reports them."""
+    import torch
+    wl = "cfg3t"
+    opts = workload_options(U, wl)
+    warm = int(opts.max_clone_size) + 4
+    steps = args.msckf_load_steps
+    sim = make_stream(opts, warm + steps + 4, seed=5, workload=wl)
+    mgr = U.VioManager(opts, device=dev.index)
+    drv = Driver(sim, mgr, None)
+    for _ in range(warm):
+        drv.step()
+    mgr.set_kernel_timing(1 if steps <= 50 else 5)
+    ks0 = mgr.kernel_stats(flush=True)
+    torch.cuda.synchronize()
+    acc = {"n_msckf": 0, "rows": 0, "cols": 0}
+    stages = ("tracking", "propagation", "msckf_update", "slam_update", "slam_delayed", "marg", "chain_wait")
+    st = dict.fromkeys(stages, 0.0)
+    rec = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        drv.step()
+        rec.append(mgr.get_timing_raw())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ks1 = mgr.kernel_stats(flush=True)
+    mgr.close()
+    for r in rec:
+        tm = r.as_dict()
+        acc["n_msckf"] += tm["n_msckf"]
+        acc["rows"] += tm["msckf_rows"]
+        acc["cols"] = max(acc["cols"], tm["msckf_cols"])
+        for k in stages:
+            st[k] += tm[k]
+    rl = {}
+    for k, a in ks1.items():
+        b = ks0[k]
+        d = dict(a, launches=a["launches"] - b["launches"], seconds=a["seconds"] - b["seconds"],
+                 flops=a["flops"] - b["flops"], bytes=a["bytes"] - b["bytes"])
+        if d["launches"] > 0:
+            rl[k] = roofline_entry(k, d, wl)
+    cand = {k: v for k, v in rl.items() if k != "ekf_update"}
+    dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
+    return {"workload": WORKLOADS[wl][4], "steps": steps, "warmup": warm, "value": steps / el, "unit": "frames/s",
+            "ms_per_step": 1e3 * el / steps, "mean_msckf_feats": acc["n_msckf"] / steps,
+            "mean_msckf_rows": acc["rows"] / steps, "H_cols": acc["cols"],
+            "stage_ms": {k: round(1e3 * v / steps, 4) for k, v in st.items()},
+            "roofline": rl.get(dom), "rooflines": rl,
+            "note": "TrackSIM feed (VioManager::feed_measurement_simulation) of a cfg3-shaped stream: every MSCKF update "
+                    "at BASELINE's 400 features; the line's value is the image-fed cfg3 run"}
 
 
 def sharded_companion(U, args, world, rank, dev, barrier):

@@ -112,6 +112,22 @@ int main(int argc, char **argv) {
     sum += ms;
   }
   printf("k_lk %d points, %d levels: best %.1f us, mean %.1f us\n", npts, L, 1e3f * best, 1e3f * sum / reps);
+  {  // results digest (FNV-1a over the tracked points and statuses): equal digests = bit-identical results
+    std::vector<float> q(2 * npts);
+    std::vector<uint8_t> sv(npts);
+    CK(hipMemcpy(q.data(), dq, 8 * npts, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(sv.data(), st, npts, hipMemcpyDeviceToHost));
+    unsigned long long hsum = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+      for (size_t i = 0; i < n; i++) hsum = (hsum ^ ((const uint8_t *)p)[i]) * 1099511628211ull;
+    };
+    mix(q.data(), q.size() * 4);
+    mix(sv.data(), sv.size());
+    int ok = 0;
+    for (auto v : sv) ok += v;
+    printf("results digest %016llx  tracked %d of %d\n", hsum, ok, npts);
+  }
+#ifdef UVHP_LK_PROF
   std::vector<LkProf> pr(npts);
   CK(hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(g_lk_prof), npts * sizeof(LkProf)));
   std::vector<int> idx(npts);
@@ -129,5 +145,6 @@ int main(int argc, char **argv) {
     printf("  %5d  %8llu %6llu %6llu(%d) %7llu(%d) %d  per-iter %.0f\n", idx[k], q.total, q.setup, q.stage, q.n_stage,
            q.iter, q.n_iter, q.n_level, q.n_iter ? (double)q.iter / q.n_iter : 0.0);
   }
+#endif
   return 0;
 }
