@@ -431,35 +431,22 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-// OPT (ldl_wave_inv's option bits, 0 = the round-4 form): kOptRawRcp -- l = v * rcp(d) without the Newton step
-// (v_rcp_f64's own rounding; one dependent FMA less per column); kOptLdsBcast -- the pivot column's later entries
-// (w[K+3..15]) reach the lanes through an LDS broadcast (one store by the block rows, wave-ordered broadcast
-// reads) instead of two v_readlane each; the two entries the next step needs first (d, w[K+2]) stay readlanes.
-constexpr int kOptRawRcp = 1, kOptSpin = 2, kOptLdsBcast = 4;
-template <int SMAX, int K, int OPT = 0>
+template <int SMAX, int K>
 __device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n, int lane, double d,
-                                            const double (&w)[16], double *wb = nullptr) {
+                                            const double (&w)[16]) {
   if constexpr (K < 16) {
     if (oJ + K >= n) return;
-    constexpr bool newton = !(OPT & kOptRawRcp);
     const double x = __builtin_amdgcn_rcp(d);
-    const double e = newton ? fma(-d, x, 1.0) : 0.0;
+    const double e = fma(-d, x, 1.0);
     const double l0 = v[0][K] * x;
-    const double l = (lane > K) ? (newton ? fma(l0, e, l0) : l0) : 0.0;
+    const double l = (lane > K) ? fma(l0, e, l0) : 0.0;
     v[0][K] = (lane > K) ? l : v[0][K];
     double dn = 0.0, wn[16];
     if constexpr (K + 1 < 16) {
       v[0][K + 1] = fma(-l, w[K + 1], v[0][K + 1]);
       dn = readlane_f64(v[0][K + 1], K + 1);
-      if constexpr ((OPT & kOptLdsBcast) && K + 3 < 16) {
-        if (K + 2 < 16) wn[K + 2] = readlane_f64(v[0][K + 1], K + 2);
-        if (lane < 16) wb[lane] = v[0][K + 1];  // in-order LDS per wave: the reads below see it
 #pragma unroll
-        for (int p = K + 3; p < 16; p++) wn[p] = wb[p];
-      } else {
-#pragma unroll
-        for (int p = K + 2; p < 16; p++) wn[p] = readlane_f64(v[0][K + 1], p);
-      }
+      for (int p = K + 2; p < 16; p++) wn[p] = readlane_f64(v[0][K + 1], p);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -467,12 +454,12 @@ __device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n
 #pragma unroll
     for (int s = 1; s < SMAX; s++) {  // rows 64 s + lane: all below the panel's diagonal block
       const double ls0 = v[s][K] * x;
-      const double ls = newton ? fma(ls0, e, ls0) : ls0;
+      const double ls = fma(ls0, e, ls0);
       v[s][K] = ls;
 #pragma unroll
       for (int p = K + 1; p < 16; p++) v[s][p] = fma(-ls, w[p], v[s][p]);
     }
-    if constexpr (K + 1 < 16) panel_steps<SMAX, K + 1, OPT>(v, oJ, n, lane, dn, wn, wb);
+    if constexpr (K + 1 < 16) panel_steps<SMAX, K + 1>(v, oJ, n, lane, dn, wn);
   }
 }
 
@@ -504,7 +491,7 @@ __device__ __forceinline__ void quad_inv_steps(double (&x)[4], const double *A, 
 // own v_readlane) and 48 further rows in lanes 16 .. 63 (wave w: rows 16 + 48 w ..), so a panel of up to
 // 16 + 48 W rows costs one SMAX = 1 column step per column instead of an SMAX = ceil(rows / 64) step; waves
 // W .. are the helpers.  Every value is computed exactly as with W = 1.
-template <int SMAX, class LA, int W = 1, int OPT = 0>
+template <int SMAX, class LA, int W = 1>
 __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows, double *Dd, bool with_inv,
                                              double *Xd = nullptr, long long *prof = nullptr) {
   static_assert(W == 1 || SMAX == 1, "several panel waves hold one slot each");
@@ -516,7 +503,6 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
   if (!LA::square) with_inv = false;
   const int nslot = with_inv ? nb + 2 : (Xd ? nb + 1 : nb);
   __shared__ int colcnt;  // column-update tiles finished so far (helpers -> wave 0)
-  __shared__ double wbc[(OPT & kOptLdsBcast) ? 8 * 16 : 1];  // per panel wave: the pivot column broadcast
   if (threadIdx.x == 0) colcnt = 0;
   __syncthreads();
   int coltarget = 0;
@@ -529,7 +515,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         const int oJ = 16 * J;
         if (P >= 0) {
           while (__hip_atomic_load(&colcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < coltarget)
-            if constexpr (!(OPT & kOptSpin)) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(1);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         double v[SMAX][16];
@@ -542,8 +528,7 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         double w0[16];
 #pragma unroll
         for (int p = 1; p < 16; p++) w0[p] = readlane_f64(v[0][0], p);
-        panel_steps<SMAX, 0, OPT>(v, oJ, n, lane, readlane_f64(v[0][0], 0), w0,
-                                  (OPT & kOptLdsBcast) ? wbc + 16 * wid : nullptr);
+        panel_steps<SMAX, 0>(v, oJ, n, lane, readlane_f64(v[0][0], 0), w0);
         // the pivots: lane p < 16 still holds d_p on its diagonal (step p leaves its own row as it is)
 #pragma unroll
         for (int p = 0; p < 16; p++)

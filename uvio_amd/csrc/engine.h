@@ -304,6 +304,10 @@ struct DeviceBufs {
   int fout_cap = 0;            // per-feature result slots in fout / fout_host (one frame chain's batches)
   char *frame = nullptr;       // the frame chain's device state: clone / camera tables, pose values, mirror
   size_t frame_bytes = 0;
+  // the chained UWB ranges of one message (Engine::uwb_update_message): per range a region [accepted, negative
+  // diagonals, chi2, S | dx] of uwb_stride doubles (pinned mirror uwb_host) and its row h (16 doubles)
+  double *uwb_reg = nullptr, *uwb_host = nullptr, *uwb_h = nullptr;
+  size_t uwb_stride = 0;
 };
 
 // the per-feature measurement / variable tables of one feature in the reference iteration order (engine_update.cpp)
@@ -582,6 +586,9 @@ class Engine {
   int slam_delayed_init(std::vector<FeatP> &feats);
   int slam_change_anchors();
   int uwb_update_single(size_t anchor_id, double range);
+  // UpdaterUWB::update_single for every range of one UwbData message whose anchor is known, in the message's
+  // order, as one device chain with one readback; returns the number of applied updates
+  int uwb_update_message(const std::vector<std::pair<size_t, double>> &ranges);
   void marginalize_slam();
   void marginalize_old_clone();
   void db_update(size_t id, double t, size_t cam, float u, float v, float un, float vn);

@@ -32,11 +32,25 @@ Mx mul(const Mx &A, const Mx &B) {
   return C;
 }
 Mx mulT(const Mx &A, const Mx &B) {  // A * B^T
+  // B's nonzero columns per row, once: F and G of the IMU propagation are mostly zero (39 x 39 with the IMU
+  // intrinsics and g-sensitivity), and a zero term adds nothing to the ascending-k sum, so skipping it leaves
+  // every C(i, j) bit-identical (finite operands)
+  std::vector<int> nzk;
+  std::vector<int> nzo(B.r + 1, 0);
+  nzk.reserve((size_t)B.r * B.c);
+  for (int j = 0; j < B.r; j++) {
+    for (int k = 0; k < B.c; k++)
+      if (B(j, k) != 0.0) nzk.push_back(k);
+    nzo[j + 1] = (int)nzk.size();
+  }
   Mx C(A.r, B.r);
   for (int i = 0; i < A.r; i++)
     for (int j = 0; j < B.r; j++) {
       double s = 0;
-      for (int k = 0; k < A.c; k++) s += A(i, k) * B(j, k);
+      for (int e = nzo[j]; e < nzo[j + 1]; e++) {
+        const int k = nzk[e];
+        s += A(i, k) * B(j, k);
+      }
       C(i, j) = s;
     }
   return C;

@@ -226,7 +226,8 @@ Engine::~Engine() {
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,
-                  d_.ekf.Dinv, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame, d_.chi2S};
+                  d_.ekf.Dinv, d_.stg_d, d_.acc, d_.shard, d_.hidx_pre, d_.chain, d_.frame, d_.chi2S, d_.uwb_reg,
+                  d_.uwb_h};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (d_.pin) hipHostFree(d_.pin);
@@ -234,6 +235,7 @@ Engine::~Engine() {
   if (d_.stg_h) hipHostFree(d_.stg_h);
   if (d_.hidx_pre_h) hipHostFree(d_.hidx_pre_h);
   if (d_.chain_host) hipHostFree(d_.chain_host);
+  if (d_.uwb_host) hipHostFree(d_.uwb_host);
   for (auto &e : d_.ev_pre)
     if (e) hipEventDestroy(e);
   if (d_.ev_aux_in) hipEventDestroy(d_.ev_aux_in);
@@ -356,6 +358,10 @@ void Engine::alloc_device() {
   if (const char *e = std::getenv("UVIO_HP_NO_PREDETECT")) predetect_on_ = e[0] != '1';
   HP_HIP(hipHostMalloc(&d_.stg_h, d_.stg_cap, hipHostMallocDefault));
   HP_HIP(hipMalloc(&d_.stg_d, d_.stg_cap));
+  d_.uwb_stride = (size_t)d_.ldp + 4;
+  dalloc(&d_.uwb_reg, kUwbMaxRanges * d_.uwb_stride);
+  dalloc(&d_.uwb_h, kUwbMaxRanges * 16);
+  HP_HIP(hipHostMalloc((void **)&d_.uwb_host, sizeof(double) * kUwbMaxRanges * d_.uwb_stride, hipHostMallocDefault));
 }
 
 void Engine::upload_P_full(const std::vector<double> &Ph, int N) {

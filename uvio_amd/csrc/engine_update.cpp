@@ -386,15 +386,22 @@ int Engine::after_tracking(double t, const std::vector<int> &camids, clk::time_p
     }
   }
   if (!past_uwb_.empty()) {
+    HPROF("uwb");
     for (auto it = past_uwb_.begin(); it != past_uwb_.lower_bound(t); it++) {
       if (it->first < t && it->first > timestamp_) {
         bool valid = false;
         for (auto &r : it->second)
           if (anchors_.count(r.first)) valid = true;
         if (!valid) continue;
-        if (propagate_uwb(it->first) != 0) continue;
+        {
+          HPROF("uwb.prop");
+          if (propagate_uwb(it->first) != 0) continue;
+        }
+        HPROF("uwb.chain");
+        std::vector<std::pair<size_t, double>> rs;
         for (auto &r : it->second)
-          if (anchors_.count(r.first)) uwb_update_single(r.first, r.second);
+          if (anchors_.count(r.first)) rs.emplace_back(r.first, r.second);
+        uwb_update_message(rs);
       }
     }
     past_uwb_.erase(past_uwb_.begin(), past_uwb_.upper_bound(t));
@@ -1665,72 +1672,72 @@ int Engine::slam_change_anchors() {
 }
 
 // UpdaterUWB::update_single (UpdaterUWB.cpp:53-90) + UVioUpdaterHelper::get_uwb_jacobian_single
-// (UVioUpdaterHelper.cpp:147-241).  One row; chi2 gate on the device-computed innovation variance.
+// (UVioUpdaterHelper.cpp:147-241) for one range: a message of one range
 int Engine::uwb_update_single(size_t anchor_id, double range) {
+  if (anchors_.find(anchor_id) == anchors_.end()) return 0;
+  return uwb_update_message({{anchor_id, range}});
+}
+
+// The ranges of one message as ONE device chain (UVioManager.cpp:178-188 runs update_single per range, each
+// linearized at the state the previous one left): the linearization state (IMU pose, p_IinU, the message's
+// anchors) goes up once; per range k_uwb_row moves it by the previous range's dx when that was accepted (Var::update's
+// formulas) and forms the row, k_uwb_M forms M = P[:, I] h, k_uwb_update gates chi2 = res^2 / S on the device and
+// updates P and dx when accepted.  One readback returns every range's [accepted, negative diagonals, chi2, S | dx];
+// the host then applies the accepted dx's to its mean in order (the same values the device state moved by), so
+// each row is linearized exactly where the per-range path linearized it -- with two host waits per range (S for
+// the gate, then dx) instead of one per message.
+int Engine::uwb_update_message(const std::vector<std::pair<size_t, double>> &ranges) {
   stage_ = "UpdaterUWB::update_single";
-  auto it = anchors_.find(anchor_id);
-  if (it == anchors_.end()) return 0;
-  const VarP &an = it->second;
-  std::vector<int> hidx;
-  for (int k = 0; k < 6; k++) hidx.push_back(imu_->id + k);
-  int n = 6;
-  int c_cal = -1, c_anc = -1;
-  if (o_.do_calib_uwb_extrinsics) {
-    c_cal = n;
-    for (int k = 0; k < 3; k++) hidx.push_back(p_IinU_->id + k);
-    n += 3;
+  int applied = 0;
+  for (size_t c0 = 0; c0 < ranges.size(); c0 += kUwbMaxRanges) {
+    const int nr = (int)std::min(ranges.size() - c0, (size_t)kUwbMaxRanges);
+    DUwbState st{};
+    std::memcpy(st.q, imu_->val, sizeof(double) * 4);
+    std::memcpy(st.p, imu_->val + 4, sizeof(double) * 3);
+    std::memcpy(st.pU, p_IinU_->val, sizeof(double) * 3);
+    st.id_imu = imu_->id;
+    st.id_cal = o_.do_calib_uwb_extrinsics ? p_IinU_->id : -1;
+    st.nr = nr;
+    std::vector<int> hidx;
+    std::vector<int> off(nr), ncol(nr);
+    for (int j = 0; j < nr; j++) {
+      const VarP &an = anchors_.at(ranges[c0 + j].first);
+      std::memcpy(st.anc[j], an->val, sizeof(double) * 5);
+      st.range[j] = ranges[c0 + j].second;
+      st.id_anc[j] = an->fixed ? -1 : an->id;
+      off[j] = (int)hidx.size();
+      for (int k = 0; k < 6; k++) hidx.push_back(imu_->id + k);
+      if (o_.do_calib_uwb_extrinsics)
+        for (int k = 0; k < 3; k++) hidx.push_back(p_IinU_->id + k);
+      if (!an->fixed)
+        for (int k = 0; k < 5; k++) hidx.push_back(an->id + k);
+      ncol[j] = (int)hidx.size() - off[j];
+    }
+    DUwbState *dst = stage(&st, 1);
+    const int *dh = stage(hidx.data(), hidx.size());
+    stage_flush();
+    const double s2 = o_.uwb_sigma_range * o_.uwb_sigma_range;
+    const double thr = o_.uwb_chi2_multipler * chi2_table_[1];
+    for (int j = 0; j < nr; j++) {
+      double *reg = d_.uwb_reg + (size_t)j * d_.uwb_stride, *h = d_.uwb_h + 16 * j;
+      launch_uwb_row(d_.stream, dst, j, j ? reg - d_.uwb_stride : nullptr, h, reg);
+      launch_uwb_M(d_.stream, d_.P, d_.ldp, N_, h, dh + off[j], ncol[j], d_.ekf.M);
+      launch_uwb_update(d_.stream, d_.P, d_.ldp, N_, d_.ekf.M, h, dh + off[j], ncol[j], s2, thr, reg);
+    }
+    ++p_epoch_;
+    const size_t n = (size_t)(nr - 1) * d_.uwb_stride + 4 + N_;
+    HP_HIP(hipMemcpyAsync(d_.uwb_host, d_.uwb_reg, sizeof(double) * n, hipMemcpyDeviceToHost, d_.stream));
+    dev_sync();
+    for (int j = 0; j < nr; j++) {
+      const double *reg = d_.uwb_host + (size_t)j * d_.uwb_stride;
+      if (reg[0] == 0.0) continue;
+      if (*reinterpret_cast<const int *>(reg + 1) > 0)
+        throw HpError(UVIO_HP_E_NUMERIC, "UWB EKFUpdate: negative covariance diagonal");
+      apply_dx(reg + 4);
+      applied++;
+    }
   }
-  if (!an->fixed) {
-    c_anc = n;
-    for (int k = 0; k < 5; k++) hidx.push_back(an->id + k);
-    n += 5;
-  }
-  double R[9], mp[3], t[3], pU[3];
-  quat_2_Rot(imu_->val, R);
-  for (int k = 0; k < 3; k++) mp[k] = -p_IinU_->val[k];
-  m3t_vec(R, mp, t);
-  for (int k = 0; k < 3; k++) pU[k] = t[k] + imu_->val[4 + k];
-  double d[3] = {an->val[0] - pU[0], an->val[1] - pU[1], an->val[2] - pU[2]};
-  double dn = norm3(d);
-  double beta = an->val[4], gam = an->val[3];
-  double res = range - ((1 + beta) * dn + gam);
-  double Hn[3] = {d[0] / dn, d[1] / dn, d[2] / dn};
-  std::vector<double> H(n + 1, 0.0);
-  double S[9], RS[9];
-  skew(mp, S);
-  m3_mul_at(R, S, RS);  // R^T skew(-p_IinU)
-  for (int j = 0; j < 3; j++) {
-    H[j] = (1 + beta) * (Hn[0] * RS[j] + Hn[1] * RS[3 + j] + Hn[2] * RS[6 + j]);
-    H[3 + j] = (1 + beta) * (-Hn[j]);
-  }
-  double HnRT[3];
-  m3_vec(R, Hn, HnRT);  // (H_n R^T)_j = sum_k Hn_k R_jk ... row vector H_n * R^T
-  for (int j = 0; j < 3; j++) HnRT[j] = Hn[0] * R[3 * j] + Hn[1] * R[3 * j + 1] + Hn[2] * R[3 * j + 2];
-  if (c_cal >= 0)
-    for (int j = 0; j < 3; j++) H[c_cal + j] = (1 + beta) * HnRT[j];
-  if (c_anc >= 0) {
-    for (int j = 0; j < 3; j++) H[c_anc + j] = (1 + beta) * HnRT[j];  // reference quirk, kept
-    H[c_anc + 3] = 1;
-    H[c_anc + 4] = dn;
-  }
-  H[n] = res;
-  double s2 = o_.uwb_sigma_range * o_.uwb_sigma_range;
-  // upload row + index, phase A (M, S), read S, gate, phase B
-  const double *dH = stage(H.data(), (size_t)n + 1);
-  const int *dh = stage(hidx.data(), (size_t)n);
-  stage_flush();
-  d_.ekf.gate = nullptr;  // a single range: no accepted-count gate (the host gates on chi2 below)
-  launch_ekf_phaseA(d_.stream, d_.P, d_.ldp, N_, dH, n + 1, 1, n, dh, s2, d_.ekf);
-  double Sval;
-  HP_HIP(hipMemcpyAsync(&Sval, d_.ekf.S + 2, sizeof(double), hipMemcpyDeviceToHost, d_.stream));
-  dev_sync();
-  double chi2 = res * res / Sval;
-  if (chi2 > o_.uwb_chi2_multipler * chi2_table_[1]) return 0;
-  launch_ekf_phaseB(d_.stream, d_.P, d_.ldp, N_, 1, dH + n, 1, d_.ekf);
-  ++p_epoch_;
-  read_dx("UWB EKFUpdate");
-  apply_dx(d_.dx_host);
-  return 1;
+  return applied;
 }
 
 }  // namespace uvhp

@@ -228,6 +228,46 @@ HPD void cam_distort_jac(const CamParams &c, double x, double y, double *dzn, do
 // True when the float rounding of v is not decided by v's leading 40 bits: a result that differs from v by a
 // few ulps (the equidistant model's tan, whose last bit differs between libm and the device) could round to
 // the other float.  Away from such a boundary (all but <= 2^-15 of the float spacing) the float is the same.
+// UpdaterUWB::update_single's row (UVioUpdaterHelper::get_uwb_jacobian_single, UVioUpdaterHelper.cpp:147-241):
+// the range from the IMU pose (q_GtoI, p_IinG), p_IinU and the anchor [p_AinG, const_bias, dist_bias];
+// H[0..n-1] over the columns [IMU theta (3), IMU p (3), p_IinU (3) if cal, anchor (5) if anc], H[n] = residual.
+// Shared by the host and the device (the chained UWB update) so both form the row with the same operations.
+HPD int uwb_row(const double *q, const double *pI, const double *pIinU, const double *an, bool cal, bool anc, double range,
+                double *H) {
+  double R[9], mp[3], t[3], pU[3];
+  quat_2_Rot(q, R);
+  for (int k = 0; k < 3; k++) mp[k] = -pIinU[k];
+  m3t_vec(R, mp, t);
+  for (int k = 0; k < 3; k++) pU[k] = t[k] + pI[k];
+  const double d[3] = {an[0] - pU[0], an[1] - pU[1], an[2] - pU[2]};
+  const double dn = norm3(d);
+  const double beta = an[4], gam = an[3];
+  const double res = range - ((1 + beta) * dn + gam);
+  const double Hn[3] = {d[0] / dn, d[1] / dn, d[2] / dn};
+  double S[9], RS[9];
+  skew(mp, S);
+  m3_mul_at(R, S, RS);  // R^T skew(-p_IinU)
+  for (int j = 0; j < 3; j++) {
+    H[j] = (1 + beta) * (Hn[0] * RS[j] + Hn[1] * RS[3 + j] + Hn[2] * RS[6 + j]);
+    H[3 + j] = (1 + beta) * (-Hn[j]);
+  }
+  double HnRT[3];  // the row vector H_n R^T
+  for (int j = 0; j < 3; j++) HnRT[j] = Hn[0] * R[3 * j] + Hn[1] * R[3 * j + 1] + Hn[2] * R[3 * j + 2];
+  int n = 6;
+  if (cal) {
+    for (int j = 0; j < 3; j++) H[n + j] = (1 + beta) * HnRT[j];
+    n += 3;
+  }
+  if (anc) {
+    for (int j = 0; j < 3; j++) H[n + j] = (1 + beta) * HnRT[j];  // reference quirk (UVioUpdaterHelper.cpp:236), kept
+    H[n + 3] = 1;
+    H[n + 4] = dn;
+    n += 5;
+  }
+  H[n] = res;
+  return n;
+}
+
 HPD bool float_round_ambiguous(double v) {
   const double e = fabs(v) * 0x1p-40;
   return (float)(v - e) != (float)(v + e);

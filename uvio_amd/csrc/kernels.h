@@ -149,6 +149,29 @@ void launch_gram_reduce_chol(hipStream_t s, const double *partials, int nchunks,
 constexpr int kMaxEkfRows = 255;        // rows of one direct (uncompressed) EKF update (+ residual <= 256)
 constexpr int kMaxDynLds = 152 * 1024;  // dynamic LDS budget of the single-workgroup solvers
 // S holds 5 r^2 doubles for r rows
+// The ranges of one UwbData message as one device chain (Engine::uwb_update_message; UpdaterUWB::update_single,
+// UpdaterUWB.cpp:53-90, per range in the message's order): the linearization state of the message's rows, moved
+// by each accepted range's dx on the device with Var::update's formulas
+constexpr int kUwbMaxRanges = 16;
+struct DUwbState {
+  double q[4], p[3];               // IMU q_GtoI, p_IinG
+  double pU[3];                    // p_IinU
+  double anc[kUwbMaxRanges][5];    // range j's anchor [p_AinG, const_bias, dist_bias]
+  double range[kUwbMaxRanges];
+  int id_imu, id_cal;              // covariance ids (id_cal < 0: p_IinU not calibrated)
+  int id_anc[kUwbMaxRanges];       // < 0: fixed anchor (no columns)
+  int nr;
+};
+// range j: apply range j-1's dx to the state if it was accepted (prev: its region, null for j = 0), then form
+// the row h (n + 1 doubles, residual last) and zero the region's header
+void launch_uwb_row(hipStream_t s, DUwbState *st, int j, const double *prev, double *h, double *region);
+// M = P[:, hidx] h
+void launch_uwb_M(hipStream_t s, const double *P, int ldp, int N, const double *h, const int *hidx, int n, double *M);
+// S = h^T M[hidx] + s2, chi2 = res^2 / S against thr; accepted: P -= W W^T (W = M / sqrt S), dx = W res / sqrt S.
+// region: [accepted, negative diagonals (int), chi2, S | dx (N)]
+void launch_uwb_update(hipStream_t s, double *P, int ldp, int N, const double *M, const double *h, const int *hidx,
+                       int n, double s2, double thr, double *region);
+
 struct EkfScratch {
   double *M, *W, *S, *y, *dx;
   int *neg;

@@ -376,6 +376,90 @@ void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, co
                      calib_ext, calib_intr, xv, Nx, P, ldp, Ntot, slot, out);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Chained UWB ranges (kernels.h DUwbState)
+__global__ void k_uwb_row(DUwbState *st, int j, const double *__restrict__ prev, double *__restrict__ h,
+                          double *__restrict__ region) {
+  if (threadIdx.x != 0) return;
+  DUwbState &u = *st;
+  if (prev && prev[0] != 0.0) {
+    // Var::update of the previous range's dx (engine_state.cpp): IMU quaternion boxplus + position, p_IinU and
+    // the anchors additive
+    const double *dx = prev + 4;
+    quat_boxplus(u.q, dx + u.id_imu);
+    for (int k = 0; k < 3; k++) u.p[k] += dx[u.id_imu + 3 + k];
+    if (u.id_cal >= 0)
+      for (int k = 0; k < 3; k++) u.pU[k] += dx[u.id_cal + k];
+    for (int a = 0; a < u.nr; a++)
+      if (u.id_anc[a] >= 0)
+        for (int k = 0; k < 5; k++) u.anc[a][k] += dx[u.id_anc[a] + k];
+  }
+  uwb_row(u.q, u.p, u.pU, u.anc[j], u.id_cal >= 0, u.id_anc[j] >= 0, u.range[j], h);
+  region[0] = 0.0;
+  region[1] = 0.0;  // the negative-diagonal count (int bits)
+  region[2] = region[3] = 0.0;
+}
+
+void launch_uwb_row(hipStream_t s, DUwbState *st, int j, const double *prev, double *h, double *region) {
+  hipLaunchKernelGGL(k_uwb_row, dim3(1), dim3(64), 0, s, st, j, prev, h, region);
+}
+
+__global__ void __launch_bounds__(256) k_uwb_M(const double *__restrict__ P, int ldp, int N, const double *__restrict__ h,
+                                               const int *__restrict__ hidx, int n, double *__restrict__ M) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const double *Pr = P + (size_t)i * ldp;
+  double a = 0.0;
+  for (int k = 0; k < n; k++) a = fma(Pr[hidx[k]], h[k], a);
+  M[i] = a;
+}
+
+void launch_uwb_M(hipStream_t s, const double *P, int ldp, int N, const double *h, const int *hidx, int n, double *M) {
+  hipLaunchKernelGGL(k_uwb_M, dim3((N + 255) / 256), dim3(256), 0, s, P, ldp, N, h, hidx, n, M);
+}
+
+// tile pair (bi, bj), bi <= bj, of the 16 x 16 tiles of P, one element per thread
+__global__ void __launch_bounds__(256) k_uwb_update(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
+                                                    const double *__restrict__ h, const int *__restrict__ hidx, int n,
+                                                    double s2, double thr, double *__restrict__ region, int nb) {
+  // the innovation variance and the gate, the same arithmetic in every block
+  double S = 0.0;
+  for (int k = 0; k < n; k++) S = fma(h[k], M[hidx[k]], S);
+  S += s2;
+  const double res = h[n];
+  const double chi2 = res * res / S;
+  const bool acc = !(chi2 > thr);  // UpdaterUWB.cpp:73-79: rejected when chi2 > multiplier * chi2_0.95(1)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    region[0] = acc ? 1.0 : 0.0;
+    region[2] = chi2;
+    region[3] = S;
+  }
+  if (!acc) return;
+  int b = blockIdx.x, bi = 0;
+  while (b >= nb - bi) {
+    b -= nb - bi;
+    bi++;
+  }
+  const int bj = bi + b;
+  const int ei = threadIdx.x >> 4, ej = threadIdx.x & 15;
+  const int gi = 16 * bi + ei, gj = 16 * bj + ej;
+  const double rs = 1.0 / sqrt(S);
+  if (gi < N && gj < N && (bi < bj || ej >= ei)) {
+    const double v = P[(size_t)gi * ldp + gj] - (M[gi] * rs) * (M[gj] * rs);
+    P[(size_t)gi * ldp + gj] = v;
+    P[(size_t)gj * ldp + gi] = v;
+    if (gi == gj && v < 0.0) atomicAdd(reinterpret_cast<int *>(region + 1), 1);
+  }
+  if (bi == bj && ei == 0 && gj < N) region[4 + gj] = (M[gj] * rs) * (res * rs);
+}
+
+void launch_uwb_update(hipStream_t s, double *P, int ldp, int N, const double *M, const double *h, const int *hidx,
+                       int n, double s2, double thr, double *region) {
+  const int nb = (N + 15) / 16;
+  hipLaunchKernelGGL(k_uwb_update, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, P, ldp, N, M, h, hidx, n, s2, thr, region,
+                     nb);
+}
+
 static void ensure_ekf_lds_attrs() {
   static bool done = false;
   if (done) return;
