@@ -16,7 +16,7 @@ if [ "$PART" = "1" ]; then
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg3_bench_driver_form.json 2> $O/cfg3_driver.err
   export TMPDIR=/tmp
   for wl in cfg3 cfg2; do
-    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run -- python3 $R/bench.py --workload $wl --cpu-frames 0 --no-host-feed > $O/prof_$wl.log 2>&1)
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run -- python3 $R/bench.py --workload $wl --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/prof_$wl.log 2>&1)
     python tools/prof_summary.py $O/prof_$wl/run_kernel_trace.csv > $O/${TAG}_${wl}_per_frame.txt
     cp $O/prof_$wl/run_kernel_stats.csv $O/${TAG}_${wl}_kernel_stats.csv
     rm -f $O/prof_$wl/run_kernel_trace.csv

@@ -7,7 +7,7 @@ cd $R && mkdir -p $O
 export TMPDIR=/tmp
 for wl in "$@"; do
   steps=200; [ $wl != cfg2 ] && [ $wl != cfg3 ] && steps=60
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run -- python3 $R/bench.py --workload $wl --steps $steps --cpu-frames 0 --no-host-feed > $O/bench_$wl.json 2> $O/bench_$wl.err)
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$wl -o run -- python3 $R/bench.py --workload $wl --steps $steps --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/bench_$wl.json 2> $O/bench_$wl.err)
   python tools/prof_summary.py $O/prof_$wl/run_kernel_trace.csv > $O/per_frame_$wl.txt
   python tools/gap_summary.py $O/prof_$wl/run_kernel_trace.csv > $O/gaps_$wl.txt
   rm -f $O/prof_$wl/run_kernel_trace.csv
