@@ -578,7 +578,7 @@ void Engine::predict_and_compute(const ImuSample &dm, const ImuSample &dp, doubl
     Qc(6 + k, 6 + k) = o_.sigma_wb * o_.sigma_wb / dt;
     Qc(9 + k, 9 + k) = o_.sigma_ab * o_.sigma_ab / dt;
   }
-  Mx GQ = mul(G, Qc);
+  Mx GQ = mul(G, Qc);  // (zero G entries skipped: Qc is diagonal, so this is G(i, j) Qc(j, j))
   Mx Qd = mulT(GQ, G);
   for (int i = 0; i < n; i++)
     for (int j = 0; j < n; j++) Qdout[(size_t)i * n + j] = 0.5 * (Qd(i, j) + Qd(j, i));
@@ -590,25 +590,53 @@ void Engine::predict_and_compute(const ImuSample &dm, const ImuSample &dp, doubl
 }
 
 void Engine::accumulate_phi(const std::vector<ImuSample> &prop, std::vector<double> &Phi, std::vector<double> &Qd, int n) {
-  Mx P(n, n), Q(n, n);
-  for (int i = 0; i < n; i++) P(i, i) = 1.0;
-  std::vector<double> F((size_t)n * n), Qi((size_t)n * n);
+  // Propagator.cpp:87-130: Phi = F Phi, Qd = F Qd F^T + Qdi, symmetrized, per IMU interval.  F is mostly zero (39 x
+  // 39 with the IMU intrinsics and g-sensitivity), so the products run over its nonzeros (one compressed-row list
+  // per interval) in the order mul / mulT sum them (ascending k, zero terms skipped, which add nothing): the same
+  // bits, without the per-interval allocations of dense temporaries
+  const size_t nn = (size_t)n * n;
+  std::vector<double> P(nn, 0.0), Q(nn, 0.0), F(nn), Qi(nn), T(nn), T2(nn);
+  for (int i = 0; i < n; i++) P[(size_t)i * n + i] = 1.0;
+  std::vector<int> nzk(nn), nzo(n + 1);
+  std::vector<double> nzv(nn);
+  auto f_times = [&](const std::vector<double> &B, std::vector<double> &C) {  // C = F B
+    for (int i = 0; i < n; i++) {
+      double *c = C.data() + (size_t)i * n;
+      for (int j = 0; j < n; j++) c[j] = 0.0;
+      for (int e = nzo[i]; e < nzo[i + 1]; e++) {
+        const double a = nzv[e];
+        const double *b = B.data() + (size_t)nzk[e] * n;
+        for (int j = 0; j < n; j++) c[j] += a * b[j];
+      }
+    }
+  };
   if (prop.size() > 1) {
-    for (size_t i = 0; i + 1 < prop.size(); i++) {
-      predict_and_compute(prop[i], prop[i + 1], F.data(), Qi.data(), n);
-      Mx Fm(n, n);
-      Fm.d = F;
-      P = mul(Fm, P);
-      Mx FQ = mul(Fm, Q);
-      Mx FQF = mulT(FQ, Fm);
+    for (size_t s = 0; s + 1 < prop.size(); s++) {
+      predict_and_compute(prop[s], prop[s + 1], F.data(), Qi.data(), n);
+      int m = 0;
+      for (int i = 0; i < n; i++) {
+        nzo[i] = m;
+        for (int k = 0; k < n; k++) {
+          const double v = F[(size_t)i * n + k];
+          if (v != 0.0) nzk[m] = k, nzv[m++] = v;
+        }
+      }
+      nzo[n] = m;
+      f_times(P, T);
+      P.swap(T);
+      f_times(Q, T);  // F Q
       for (int a = 0; a < n; a++)
-        for (int b = 0; b < n; b++) FQF(a, b) += Qi[(size_t)a * n + b];
+        for (int b = 0; b < n; b++) {  // (F Q) F^T + Qdi
+          double sum = 0;
+          for (int e = nzo[b]; e < nzo[b + 1]; e++) sum += T[(size_t)a * n + nzk[e]] * nzv[e];
+          T2[(size_t)a * n + b] = sum + Qi[(size_t)a * n + b];
+        }
       for (int a = 0; a < n; a++)
-        for (int b = 0; b < n; b++) Q(a, b) = 0.5 * (FQF(a, b) + FQF(b, a));
+        for (int b = 0; b < n; b++) Q[(size_t)a * n + b] = 0.5 * (T2[(size_t)a * n + b] + T2[(size_t)b * n + a]);
     }
   }
-  Phi = P.d;
-  Qd = Q.d;
+  Phi.swap(P);
+  Qd.swap(Q);
 }
 
 void Engine::last_w(const std::vector<ImuSample> &prop, double *w) {
@@ -655,11 +683,18 @@ int Engine::propagate_and_clone(double timestamp) {
     have_last_prop_time_offset_ = true;
   }
   double t_off_new = calib_dt_->val[0];
-  std::vector<ImuSample> prop = select_imu_readings(timestamp_ + last_prop_time_offset_, timestamp + t_off_new);
+  std::vector<ImuSample> prop;
+  {
+    HPROF("prop.select");
+    prop = select_imu_readings(timestamp_ + last_prop_time_offset_, timestamp + t_off_new);
+  }
   int n;
   std::vector<int> ids = phi_order_ids(&n);
   std::vector<double> Phi, Qd;
-  accumulate_phi(prop, Phi, Qd, n);
+  {
+    HPROF("prop.phi");
+    accumulate_phi(prop, Phi, Qd, n);
+  }
   double lw[3];
   last_w(prop, lw);
   // the clone's time-offset column (augment_clone, StateHelper.cpp:579-616) goes up with Phi / Qd
