@@ -193,3 +193,37 @@ def test_uwb_update_single_matches_oracle(euroc_yaml):
             _same_state(g, o)
     assert applied >= 3 and gated >= 3
     g.close()
+
+
+def test_fatal_error_stops_the_handle(euroc_yaml):
+    """A negative covariance diagonal after an update is fatal in the reference (StateHelper.cpp:171-182,
+    std::exit): the call returns UVIO_HP_E_NUMERIC and every later state-changing call UVIO_HP_E_STATE naming it,
+    while the getters still read the state."""
+    import uvio_amd as U
+    from uvio_amd import _native as N
+    from uvio_amd.sim import SimStream
+    from test_gpu_parity import make_anchors
+    opts = U.load_options(euroc_yaml, max_msckf_in_update=60, max_slam_features=0, use_uwb=1,
+                          do_calib_uwb_extrinsics=1, min_dist_to_use_uwb=0.05)
+    anchors = make_anchors(N)
+    n = 8
+    sim = SimStream(opts, duration=(n + 2) / opts.track_frequency + 1.2, seed=4, spawn=40, anchors=anchors,
+                    uwb_rate=10.0, uwb_sigma=0.1)
+    g = U.VioManager(opts)
+    sim.run(g, n_frames=n, after_init=lambda m: m.try_to_initialize_uwb_anchors(anchors))
+    x, _ = g.get_state_vector()
+    P = g.get_cov()
+    P[-1, -1] = -1.0  # the last variable (outside the range's columns) gets a negative variance
+    g.set_state(x, g.get_fej_vector(), P)
+    t, _ = g.get_imu_state()
+    a = anchors[-1]
+    p_U = sim.traj.R_ItoG(t) @ (-np.array(opts.p_IinU[:])) + sim.traj.pos(t)
+    rng = (1 + a.dist_bias) * np.linalg.norm(np.array(a.p_AinG[:]) - p_U) + a.const_bias
+    with pytest.raises(RuntimeError, match="E_NUMERIC"):
+        g.uwb_update_single(t, a.id, rng)
+    with pytest.raises(RuntimeError, match="E_STATE.*stopped"):
+        g.uwb_update_single(t, a.id, rng)
+    with pytest.raises(RuntimeError, match="E_STATE"):
+        g.propagate_and_clone(t + 0.05)
+    assert g.get_cov().shape == P.shape and np.all(np.isfinite(g.get_state_vector()[0]))
+    g.close()
