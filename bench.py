@@ -621,6 +621,11 @@ def main():
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "strong" if shard else "weak",
+            "value_definition": ("feature-sharded: every rank runs the same stream, each MSCKF update split across the "
+                                 "ranks (one RCCL all-reduce); value = frames of that one stream / wall time") if shard
+                                else ("one independent estimator per GPU on its own stream (the N = 1 workload, seed 5 + "
+                                      "rank), value = all ranks' frames / the slowest rank's wall time; the north star's "
+                                      "feature-sharded update at N > 1 is the feature_sharded object"),
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic %s-shaped stream (uvio_amd/sim.py, seed %s) with ray-cast images "

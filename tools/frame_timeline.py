@@ -1,6 +1,8 @@
 """One frame's device timeline from a rocprofv3 kernel trace: every kernel / blit in launch order with its start
 relative to the frame's histogram launch, its duration and the idle gap before it.  Frames are cut at
-k_hist_multi.   usage: frame_timeline.py trace.csv [first_frame] [count]"""
+k_hist_multi (UVIO_TL_CUT=<kernel> cuts at another kernel, e.g. k_prop_clone for TrackSIM workloads).
+usage: frame_timeline.py trace.csv [first_frame] [count]"""
+import os
 import csv
 import sys
 
@@ -8,7 +10,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']) for r in rows)
 last_torch = max([i for i, e in enumerate(ev) if 'at::' in e[2]] + [-1])
 seg = ev[last_torch + 1:]
-starts = [i for i, e in enumerate(seg) if 'k_hist_multi' in e[2]]
+CUT = os.environ.get('UVIO_TL_CUT', 'k_hist_multi')
+starts = [i for i, e in enumerate(seg) if CUT in e[2]]
 f0 = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2
 cnt = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 

@@ -7,11 +7,11 @@ cd $R && mkdir -p $O
 for wl in "$@"; do
   for i in $(seq 1 $N); do
     if [ $((i % 2)) = 1 ]; then
-      timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
-      env $E timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
+      timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
+      env $E timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
     else
-      env $E timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
-      timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
+      env $E timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/${wl}_old_$i.json 2> $O/${wl}_old_$i.err
+      timeout -k 10 300 python -u bench.py --workload $wl --steps $S --cpu-frames 0 --no-host-feed --msckf-load-steps 0 > $O/${wl}_new_$i.json 2> $O/${wl}_new_$i.err
     fi
   done
 done
