@@ -628,104 +628,124 @@ __device__ __forceinline__ float px_clamped(const uint8_t *img, int w, int h, in
   return (float)img[(size_t)y * w + x];
 }
 
-// One 64-lane workgroup per point.  Lanes build the (win_w + 2)^2 bilinear patch and the 121 per-pixel
-// terms in LDS; lane 0 then accumulates them in the oracle's raster order (the double sums are
-// order-sensitive), so the result is bit-identical to the sequential cornerSubPix.
+// One 64-lane workgroup (one wave) per point.  Lanes build the (win_w + 2)^2 bilinear patch and the
+// per-pixel terms in LDS; lanes 0..4 then accumulate the five series, each in the oracle's raster order
+// (the double sums are order-sensitive), so the result is bit-identical to the sequential cornerSubPix.
+// The window is a template constant: the five raster sums unroll completely, so the LDS reads of each series
+// stream ahead of its dependent add chain instead of stalling on every group of eight.  The five sums reach
+// every lane by v_readlane and every lane runs the 2x2 solve on the same values: the position stays in
+// registers and the iteration needs two barriers, not four.
 constexpr int kSubpixMaxWin = 5, kSubpixMargin = 3;
+__device__ __forceinline__ double lane_f64(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int WIN>
 __global__ void __launch_bounds__(64) k_subpix(SubpixJob job, float *__restrict__ pts, const float *__restrict__ mask,
-                                               int win, int max_iters, double eps2) {
-  constexpr int kBw = 2 * kSubpixMaxWin + 3, kT = (2 * kSubpixMaxWin + 1) * (2 * kSubpixMaxWin + 1);
-  constexpr int kTile = kBw + 1 + 2 * kSubpixMargin;
-  __shared__ float tile[kTile * kTile];  // clamped image neighbourhood (u8 as float)
-  __shared__ float buf[kBw * kBw];
-  __shared__ double tg[5][kT];
-  __shared__ double sums[5];
-  __shared__ float cur[2];
-  __shared__ int done;
+                                               int max_iters, double eps2) {
+  constexpr int WW = 2 * WIN + 1, BW = WW + 2, NT = WW * WW, NTP = NT + (NT & 1);
+  constexpr int S = BW + 1 + 2 * kSubpixMargin, NL = (S * S + 63) / 64, NB = (BW * BW + 63) / 64, NK = (NT + 63) / 64;
+  __shared__ float tile[S * S];  // clamped image neighbourhood (u8 as float)
+  __shared__ float buf[BW * BW];
+  __shared__ double tg[5 * NTP];
   const int p = xcd_contiguous(blockIdx.x, gridDim.x), lane = threadIdx.x;  // neighbouring corners on one XCD
   int cam = 0;
   while (cam < job.ncam - 1 && p >= job.end[cam]) cam++;
   if (p >= job.end[cam]) return;
   const uint8_t *__restrict__ img = job.img[cam];
   const int w = job.w[cam], h = job.h[cam];
-  const int win_w = 2 * win + 1, bw = win_w + 2, nt = win_w * win_w, S = bw + 1 + 2 * kSubpixMargin;
   const float cTx = pts[2 * p], cTy = pts[2 * p + 1];
-  if (lane == 0) {
-    cur[0] = cTx;
-    cur[1] = cTy;
-    done = 0;
-  }
-  __syncthreads();
+  double mk[NK];  // this lane's mask weights, read once
+#pragma unroll
+  for (int r = 0; r < NK; r++) mk[r] = lane + 64 * r < NT ? (double)mask[lane + 64 * r] : 0.0;
+  float cIx = cTx, cIy = cTy;
   int ox = -(1 << 28), oy = -(1 << 28);
   for (int iter = 0; iter < max_iters; iter++) {
-    const float cIx = cur[0], cIy = cur[1];
-    const float cx = cIx - (bw - 1) * 0.5f, cy = cIy - (bw - 1) * 0.5f;
+    const float cx = cIx - (BW - 1) * 0.5f, cy = cIy - (BW - 1) * 0.5f;
     const int ix = (int)floorf(cx), iy = (int)floorf(cy);
     const float a = cx - ix, b = cy - iy;
     const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
     if (ix - ox < 0 || ix - ox > 2 * kSubpixMargin || iy - oy < 0 || iy - oy > 2 * kSubpixMargin) {
       ox = ix - kSubpixMargin;
       oy = iy - kSubpixMargin;
-      constexpr int NT = (kTile * kTile + 63) / 64;  // all of a lane's loads in flight before the LDS stores
-      float v[NT];
+      float v[NL];  // all of a lane's loads in flight before the LDS stores
 #pragma unroll
-      for (int k = 0; k < NT; k++) {
+      for (int k = 0; k < NL; k++) {
         const int e = min(lane + 64 * k, S * S - 1), ty = e / S;
         v[k] = px_clamped(img, w, h, ox + e - ty * S, oy + ty);
       }
 #pragma unroll
-      for (int k = 0; k < NT; k++)
+      for (int k = 0; k < NL; k++)
         if (lane + 64 * k < S * S) tile[lane + 64 * k] = v[k];
       __syncthreads();
     }
-    for (int e = lane; e < bw * bw; e += 64) {
-      const int i = e / bw, j = e - i * bw;
-      const float *t = tile + (iy - oy + i) * S + (ix - ox + j);
-      buf[e] = t[0] * a11 + t[1] * a12 + t[S] * a21 + t[S + 1] * a22;
-    }
-    __syncthreads();
-    for (int k = lane; k < nt; k += 64) {
-      const int i = k / win_w, j = k - i * win_w;
-      const float *sp = buf + (i + 1) * bw + 1;
-      const double m = mask[k];
-      const double tgx = sp[j + 1] - sp[j - 1];
-      const double tgy = sp[j + bw] - sp[j - bw];
-      const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
-      const double pxv = j - win, py = i - win;
-      tg[0][k] = gxx;
-      tg[1][k] = gxy;
-      tg[2][k] = gyy;
-      tg[3][k] = gxx * pxv + gxy * py;
-      tg[4][k] = gxy * pxv + gyy * py;
-    }
-    __syncthreads();
-    if (lane < 5) {  // one series per lane, each in raster order
-      double acc = 0;
-      for (int k = 0; k < nt; k++) acc += tg[lane][k];
-      sums[lane] = acc;
-    }
-    __syncthreads();
-    if (lane == 0) {
-      const double sa = sums[0], sb = sums[1], sc = sums[2], bb1 = sums[3], bb2 = sums[4];
-      const double det = sa * sc - sb * sb;
-      if (fabs(det) <= 4.930380657631324e-32) {  // DBL_EPSILON^2
-        done = 1;
-      } else {
-        const double scale = 1.0 / det;
-        const float nx = (float)(cIx + sc * scale * bb1 - sb * scale * bb2);
-        const float ny = (float)(cIy - sb * scale * bb1 + sa * scale * bb2);
-        const double err = (double)(nx - cIx) * (nx - cIx) + (double)(ny - cIy) * (ny - cIy);
-        cur[0] = nx;
-        cur[1] = ny;
-        if (nx < 0 || nx >= w || ny < 0 || ny >= h || !(err > eps2)) done = 1;
+#pragma unroll
+    for (int r = 0; r < NB; r++) {
+      const int e = lane + 64 * r;
+      if (e < BW * BW) {
+        const int i = e / BW, j = e - i * BW;
+        const float *t = tile + (iy - oy + i) * S + (ix - ox + j);
+        buf[e] = t[0] * a11 + t[1] * a12 + t[S] * a21 + t[S + 1] * a22;
       }
     }
     __syncthreads();
-    if (done) break;
+#pragma unroll
+    for (int r = 0; r < NK; r++) {
+      const int k = lane + 64 * r;
+      if (k < NT) {
+        const int i = k / WW, j = k - i * WW;
+        const float *sp = buf + (i + 1) * BW + 1;
+        const double m = mk[r];
+        const double tgx = sp[j + 1] - sp[j - 1];
+        const double tgy = sp[j + BW] - sp[j - BW];
+        const double gxx = tgx * tgx * m, gxy = tgx * tgy * m, gyy = tgy * tgy * m;
+        const double pxv = j - WIN, py = i - WIN;
+        tg[k] = gxx;
+        tg[NTP + k] = gxy;
+        tg[2 * NTP + k] = gyy;
+        tg[3 * NTP + k] = gxx * pxv + gxy * py;
+        tg[4 * NTP + k] = gxy * pxv + gyy * py;
+      }
+    }
+    __syncthreads();
+    double acc = 0;
+    if (lane < 5) {  // one series per lane, each in raster order
+      // double-buffered chunks of 12: the next chunk's LDS reads are in flight while this one is added (the
+      // scheduler would otherwise keep one read ahead of the dependent add chain)
+      constexpr int C = 12, NC = (NT + C - 1) / C;
+      const double *row = tg + lane * NTP;
+      double q[2][C];
+#pragma unroll
+      for (int i = 0; i < C; i++)
+        if (i < NT) q[0][i] = row[i];
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < C; i++)
+          if ((c + 1) * C + i < NT) q[(c + 1) & 1][i] = row[(c + 1) * C + i];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < C; i++)
+          if (c * C + i < NT) acc += q[c & 1][i];
+      }
+    }
+    const double sa = lane_f64(acc, 0), sb = lane_f64(acc, 1), sc = lane_f64(acc, 2), bb1 = lane_f64(acc, 3),
+                 bb2 = lane_f64(acc, 4);
+    const double det = sa * sc - sb * sb;
+    if (fabs(det) <= 4.930380657631324e-32) break;  // DBL_EPSILON^2
+    const double scale = 1.0 / det;
+    const float nx = (float)(cIx + sc * scale * bb1 - sb * scale * bb2);
+    const float ny = (float)(cIy - sb * scale * bb1 + sa * scale * bb2);
+    const double err = (double)(nx - cIx) * (nx - cIx) + (double)(ny - cIy) * (ny - cIy);
+    cIx = nx;
+    cIy = ny;
+    if (nx < 0 || nx >= w || ny < 0 || ny >= h || !(err > eps2)) break;
+    __syncthreads();  // tg and buf are rewritten by the next iteration
   }
   if (lane == 0) {
-    float cIx = cur[0], cIy = cur[1];
-    if (fabsf(cIx - cTx) > win || fabsf(cIy - cTy) > win) {
+    if (fabsf(cIx - cTx) > WIN || fabsf(cIy - cTy) > WIN) {
       cIx = cTx;
       cIy = cTy;
     }
@@ -1370,8 +1390,20 @@ void launch_subpix_multi(hipStream_t s, const SubpixJob &job, float *pts, const 
   if (job.ncam <= 0 || job.ncam > kMaxCams) return;
   const int n = job.end[job.ncam - 1];
   if (n <= 0) return;
-  if (win > kSubpixMaxWin) throw std::runtime_error("cornerSubPix window larger than the kernel's LDS patch");
-  hipLaunchKernelGGL(k_subpix, dim3(n), dim3(64), 0, s, job, pts, mask, win, max_iters, eps2);
+  switch (win) {
+#define UVHP_SUBPIX(W)                                                                            \
+  case W:                                                                                         \
+    hipLaunchKernelGGL(k_subpix<W>, dim3(n), dim3(64), 0, s, job, pts, mask, max_iters, eps2); \
+    break;
+    UVHP_SUBPIX(1)
+    UVHP_SUBPIX(2)
+    UVHP_SUBPIX(3)
+    UVHP_SUBPIX(4)
+    UVHP_SUBPIX(5)
+#undef UVHP_SUBPIX
+    default:
+      throw std::runtime_error("cornerSubPix window outside the kernel's 1..5 instantiations");
+  }
 }
 
 void launch_subpix(hipStream_t s, const uint8_t *img, int w, int h, float *pts, int n, const float *mask, int win,
