@@ -18,6 +18,8 @@ __device__ void slots_body(const double *Ain, int r, int inv, long long *prof, l
   extern __shared__ double lds[];
   const int ld = r | 1;
   double *A = lds, *D = lds + (size_t)(r + 1) * ld;
+  for (int e = threadIdx.x; e < (r + 1) * ld + r + 1; e += blockDim.x) lds[e] = 0.0;  // no stale LDS in the output
+  __syncthreads();
   for (int e = threadIdx.x; e < r * r + r; e += blockDim.x) {
     const int a = e / r, b = e - a * r;
     if (b <= a || a == r) A[(size_t)a * ld + b] = Ain[e];
@@ -93,6 +95,15 @@ int main() {
         for (int j = 0; j < 10 && p[32 + j]; j++) printf(" %lld", p[32 + j]);
         printf("\n");
       }
+    }
+    for (int v = 0; v < 3; v += 2) {  // to compare builds of dense_lds.h bit for bit
+      unsigned long long h = 1469598103934665603ull;
+      for (double d : out[v]) {
+        unsigned long long u;
+        std::memcpy(&u, &d, 8);
+        h = (h ^ u) * 1099511628211ull;
+      }
+      printf("r=%3d variant %d factor + inverse digest %016llx\n", r, v, h);
     }
     for (int v = 1; v < 3; v++) {
       size_t nd = 0;

@@ -431,24 +431,28 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane), hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
+// Software-pipelined: step K receives the pivot's reciprocal x = v_rcp_f64(d_K) and e = 1 - d_K x from step
+// K - 1, which issued the reciprocal as soon as d_K was read out (pinned there: the compiler would sink it
+// into step K), so its latency runs under the read-out instead of in front of step K; the bulk of the row
+// update is issued before the read-out and covers the next pivot column's FMA latency.  With one panel row per
+// lane (SMAX = 1) the 16 steps have no branch between them: the whole panel is one scheduling region, and a
+// last panel narrower than 16 columns runs its padding steps on zero columns whose results are never stored
+// (rcp(0) = inf makes them NaN there; the branch per step cost 20 % of the panel, tools/bench_wave_slots.hip,
+// profiles/r05_ldl_panel_pipeline.txt).  With SMAX > 1 the per-step branch stays (removing it measured 7-10 %
+// slower there).  Lanes <= K (rows of the diagonal block above the pivot) apply their multiplier to
+// upper-triangle entries that are never read out or stored; the pivot lane keeps d_K in its column K.  Every
+// stored value is the one the unpipelined step computes (bit-identical factors and inverses).
 template <int SMAX, int K>
-__device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n, int lane, double d,
+__device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n, int lane, double x, double e,
                                             const double (&w)[16]) {
   if constexpr (K < 16) {
-    if (oJ + K >= n) return;
-    const double x = __builtin_amdgcn_rcp(d);
-    const double e = fma(-d, x, 1.0);
+    if constexpr (SMAX > 1)
+      if (oJ + K >= n) return;
     const double l0 = v[0][K] * x;
-    const double l = (lane > K) ? fma(l0, e, l0) : 0.0;
+    const double l = fma(l0, e, l0);
     v[0][K] = (lane > K) ? l : v[0][K];
-    double dn = 0.0, wn[16];
-    if constexpr (K + 1 < 16) {
-      v[0][K + 1] = fma(-l, w[K + 1], v[0][K + 1]);
-      dn = readlane_f64(v[0][K + 1], K + 1);
-#pragma unroll
-      for (int p = K + 2; p < 16; p++) wn[p] = readlane_f64(v[0][K + 1], p);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    if constexpr (K + 1 < 16) v[0][K + 1] = fma(-l, w[K + 1], v[0][K + 1]);
+    // the bulk of the row update first: its issue covers the next pivot column's FMA latency
 #pragma unroll
     for (int p = K + 2; p < 16; p++) v[0][p] = fma(-l, w[p], v[0][p]);
 #pragma unroll
@@ -459,7 +463,16 @@ __device__ __forceinline__ void panel_steps(double (&v)[SMAX][16], int oJ, int n
 #pragma unroll
       for (int p = K + 1; p < 16; p++) v[s][p] = fma(-ls, w[p], v[s][p]);
     }
-    if constexpr (K + 1 < 16) panel_steps<SMAX, K + 1>(v, oJ, n, lane, dn, wn);
+    double xn = 0.0, en = 0.0, wn[16];
+    if constexpr (K + 1 < 16) {
+      const double dn = readlane_f64(v[0][K + 1], K + 1);
+      xn = __builtin_amdgcn_rcp(dn);
+      asm volatile("" : "+v"(xn));
+      en = fma(-dn, xn, 1.0);
+#pragma unroll
+      for (int p = K + 2; p < 16; p++) wn[p] = readlane_f64(v[0][K + 1], p);
+    }
+    if constexpr (K + 1 < 16) panel_steps<SMAX, K + 1>(v, oJ, n, lane, xn, en, wn);
   }
 }
 
@@ -528,7 +541,8 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
         double w0[16];
 #pragma unroll
         for (int p = 1; p < 16; p++) w0[p] = readlane_f64(v[0][0], p);
-        panel_steps<SMAX, 0>(v, oJ, n, lane, readlane_f64(v[0][0], 0), w0);
+        const double d0 = readlane_f64(v[0][0], 0), x0 = __builtin_amdgcn_rcp(d0);
+        panel_steps<SMAX, 0>(v, oJ, n, lane, x0, fma(-d0, x0, 1.0), w0);
         // the pivots: lane p < 16 still holds d_p on its diagonal (step p leaves its own row as it is)
 #pragma unroll
         for (int p = 0; p < 16; p++)
