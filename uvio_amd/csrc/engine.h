@@ -573,10 +573,18 @@ class Engine {
     hipEvent_t copied = nullptr;
     bool copy_pending = false, valid = false;
     double time = -1;
+    // the frame's job as taken at the reference's point (poses, landmarks, camera models, observations in
+    // frame_obs_), run by retri_flush at the next feed's tracking wait or on demand
+    bool pend = false, pend_undist = false;
+    double pend_t = -1;
+    RetriJob pend_job{};
+    std::vector<DRetriSlam> pend_sl;
+    CamParams pend_cams[UVIO_HP_MAX_CAMS];
   } rt_;
-  std::vector<DRetriObs> frame_obs_;  // the simulated feed's observations of the current frame
-  void retri_alloc(int nobs);
+  std::vector<DRetriObs> frame_obs_;  // this frame's observations (simulated feed, or the tracker's last tracks)
+  void retri_alloc(int nobs, int nslam);
   void retriangulate_active_tracks(double t, const std::vector<int> &camids);
+  void retri_flush();
 
  public:
   int get_active_tracks(double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid, int cap);

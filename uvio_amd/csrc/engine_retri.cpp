@@ -6,6 +6,11 @@
 // tracks' positions (active_tracks_posinG) and their depth in camera 0 (active_tracks_uvd), which stay in HBM
 // until a caller asks for them; the per-track running triangulation systems (active_feat_linsys_*) persist in
 // a featid-keyed hash table on the device (kernels_feat.hip, k_retri_*).
+// Since nothing reads those outputs before get_active_tracks, the frame only takes its inputs at the
+// reference's point (the clone and camera poses, the SLAM landmarks, the camera models, the observations) and
+// retri_flush runs the undistortion and the launches later: inside the next image feed's tracking wait (the
+// host is idle there while LK + RANSAC run), at the next simulated feed, or when get_active_tracks asks.  The
+// same inputs give the same results; the frame's critical path loses the undistortion and the launches.
 #include <algorithm>
 #include <cstring>
 
@@ -13,7 +18,7 @@
 
 namespace uvhp {
 
-void Engine::retri_alloc(int nobs) {
+void Engine::retri_alloc(int nobs, int nslam) {
   int need = 1024;
   while (need < 2 * std::max(nobs, 1)) need *= 2;
   if (nobs > rt_.obs_cap) {
@@ -64,7 +69,7 @@ void Engine::retri_alloc(int nobs) {
     }
     rt_.cap = need;
   }
-  const int ns = std::max((int)slam_.size(), 1);
+  const int ns = std::max(nslam, 1);
   if (ns > rt_.slam_cap) {
     if (rt_.d_slam) HP_HIP(hipFree(rt_.d_slam));
     HP_HIP(hipMalloc(&rt_.d_slam, sizeof(DRetriSlam) * 2 * ns));
@@ -79,6 +84,7 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
   if (camids.empty() || camids[0] != 0) return;
   auto cit = clones_.find(t);
   if (cit == clones_.end()) throw HpError(UVIO_HP_E_STATE, "retriangulate_active_tracks: no clone at the frame time");
+  retri_flush();  // not reached with a job pending: every feed flushes first (the simulated feed before refilling frame_obs_)
   // observations: the simulated feed keeps its own (frame_obs_); the KLT tracker's last tracks otherwise
   if (tracker_) {
     frame_obs_.clear();
@@ -96,41 +102,8 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
       }
     }
   }
-  const int nobs = (int)frame_obs_.size();
-  {
-    HPROF("retri.wait_copy");
-    if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // last frame's upload read h_obs
-    rt_.copy_pending = false;
-  }
-  retri_alloc(nobs);
-  // the observations go straight into the pinned upload buffer, on the pool: undistort_cv with the camera
-  // models as of now for the tracker's points, and for the simulated feed's when this frame's updates may have
-  // moved the intrinsics since the feed undistorted the same pixels (StateHelper.cpp:190-195)
-  {
-    HPROF("retri.undist");
-    DRetriObs *h = rt_.h_obs;
-    const bool undist = tracker_ || o_.do_calib_camera_intrinsics;
-    pool_.parallel_for(frame_obs_.size(), undist ? 512 : 8192, [&](size_t b, size_t e) {
-      if (!undist) {
-        std::memcpy(h + b, frame_obs_.data() + b, sizeof(DRetriObs) * (e - b));
-        return;
-      }
-      for (size_t k = b; k < e; k++) {
-        DRetriObs o = frame_obs_[k];
-        cam_undistort_f(cams_[o.cam], o.u, o.v, o.un, o.vn);
-        h[k] = o;
-      }
-    });
-  }
-  RetriJob job{};
-  job.nobs = nobs;
-  job.cap = rt_.cap;
-  job.obs = rt_.d_obs;
-  job.scratch = rt_.scratch;
-  job.keys_old = rt_.keys[rt_.cur];
-  job.ent_old = rt_.ent[rt_.cur];
-  job.keys_new = rt_.keys[1 - rt_.cur];
-  job.ent_new = rt_.ent[1 - rt_.cur];
+  RetriJob &job = rt_.pend_job;
+  job = RetriJob{};
   // current clone, per-camera poses (R_GtoCi = R_ItoC R_GtoI, p_CiinG = p_IinG - R_GtoCi^T p_IinC)
   const VarP &clone = cit->second;
   double R_GtoI[9];
@@ -151,7 +124,8 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
   job.min_dist = o_.fi_min_dist;
   job.max_dist = o_.fi_max_dist;
   // SLAM landmarks (the state estimate takes priority over the triangulation)
-  std::vector<DRetriSlam> sl;
+  std::vector<DRetriSlam> &sl = rt_.pend_sl;
+  sl.clear();
   for (auto &kv : slam_) {
     const VarP &lm = kv.second;
     DRetriSlam d{};
@@ -171,6 +145,55 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
     for (int k = 0; k < 3; k++) d.pos[k] = p[k];
     sl.push_back(d);
   }
+  // undistort_cv with the camera models as of now for the tracker's points, and for the simulated feed's when
+  // this frame's updates may have moved the intrinsics since the feed undistorted the same pixels
+  // (StateHelper.cpp:190-195)
+  rt_.pend_undist = tracker_ || o_.do_calib_camera_intrinsics;
+  if (rt_.pend_undist)
+    for (int c = 0; c < o_.num_cameras; c++) rt_.pend_cams[c] = cams_[c];
+  rt_.pend_t = t;
+  rt_.pend = true;
+}
+
+// the pending job: the undistortion (on the pool, straight into the pinned upload buffer), the uploads and the
+// launches (k_retri_*); the results replace the previous frame's
+void Engine::retri_flush() {
+  if (!rt_.pend) return;
+  rt_.pend = false;
+  const int nobs = (int)frame_obs_.size();
+  {
+    HPROF("retri.wait_copy");
+    if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // the previous upload read h_obs
+    rt_.copy_pending = false;
+  }
+  RetriJob &job = rt_.pend_job;
+  const std::vector<DRetriSlam> &sl = rt_.pend_sl;
+  retri_alloc(nobs, (int)sl.size());
+  {
+    HPROF("retri.undist");
+    DRetriObs *h = rt_.h_obs;
+    const bool undist = rt_.pend_undist;
+    const CamParams *cams = rt_.pend_cams;
+    pool_.parallel_for(frame_obs_.size(), undist ? 512 : 8192, [&](size_t b, size_t e) {
+      if (!undist) {
+        std::memcpy(h + b, frame_obs_.data() + b, sizeof(DRetriObs) * (e - b));
+        return;
+      }
+      for (size_t k = b; k < e; k++) {
+        DRetriObs o = frame_obs_[k];
+        cam_undistort_f(cams[o.cam], o.u, o.v, o.un, o.vn);
+        h[k] = o;
+      }
+    });
+  }
+  job.nobs = nobs;
+  job.cap = rt_.cap;
+  job.obs = rt_.d_obs;
+  job.scratch = rt_.scratch;
+  job.keys_old = rt_.keys[rt_.cur];
+  job.ent_old = rt_.ent[rt_.cur];
+  job.keys_new = rt_.keys[1 - rt_.cur];
+  job.ent_new = rt_.ent[1 - rt_.cur];
   job.nslam = (int)sl.size();
   job.slam = rt_.d_slam;
   if (nobs) {
@@ -186,12 +209,13 @@ void Engine::retriangulate_active_tracks(double t, const std::vector<int> &camid
   launch_retriangulate(d_.stream, job);
   rt_.cur = 1 - rt_.cur;
   rt_.nslam = job.nslam;
-  rt_.time = t;
+  rt_.time = rt_.pend_t;
   rt_.valid = true;
 }
 
 // VioManager::get_active_tracks (VioManager.h:114)
 int Engine::get_active_tracks(double *t, uint64_t *ids, double *posinG, double *uvd, int *uvd_valid, int cap) {
+  retri_flush();
   *t = rt_.valid ? rt_.time : -1;
   if (!rt_.valid) return 0;
   dev_sync();
