@@ -568,7 +568,7 @@ class Engine {
     unsigned long long *keys[2] = {nullptr, nullptr};
     DRetriEntry *ent[2] = {nullptr, nullptr};
     DRetriObs *d_obs = nullptr, *h_obs = nullptr;
-    DRetriSlam *d_slam = nullptr;
+    DRetriSlam *d_slam = nullptr, *h_slam = nullptr;
     double *scratch = nullptr;
     hipEvent_t copied = nullptr;
     bool copy_pending = false, valid = false;

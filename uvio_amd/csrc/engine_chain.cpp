@@ -510,6 +510,11 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       HPROF("chain.predetect");
       tracker_->predetect_async();
     }
+    // the previous frame's retriangulation (engine_retri.cpp; its own stream, so this wait does not cover it)
+    if (rt_.pend) {
+      HPROF("chain.retri");
+      retri_flush();
+    }
     if (chain_overlap_) {
       HPROF("chain.overlap");
       auto f = std::move(chain_overlap_);

@@ -8,9 +8,10 @@
 // a featid-keyed hash table on the device (kernels_feat.hip, k_retri_*).
 // Since nothing reads those outputs before get_active_tracks, the frame only takes its inputs at the
 // reference's point (the clone and camera poses, the SLAM landmarks, the camera models, the observations) and
-// retri_flush runs the undistortion and the launches later: inside the next image feed's tracking wait (the
-// host is idle there while LK + RANSAC run), at the next simulated feed, or when get_active_tracks asks.  The
-// same inputs give the same results; the frame's critical path loses the undistortion and the launches.
+// retri_flush runs the undistortion, the uploads and the launches later, on the auxiliary stream: while the
+// host waits for the next frame's update chain (engine_chain.cpp), at the next simulated feed (which refills
+// the observations), at the next retriangulation if no chain ran, or when get_active_tracks asks.  The same
+// inputs give the same results; the frame's critical path loses the undistortion and the launches.
 #include <algorithm>
 #include <cstring>
 
@@ -19,8 +20,11 @@
 namespace uvhp {
 
 void Engine::retri_alloc(int nobs, int nslam) {
+  const int ns = std::max(nslam, 1);
   int need = 1024;
   while (need < 2 * std::max(nobs, 1)) need *= 2;
+  // buffers the auxiliary stream may still read are replaced only after it has drained
+  if (nobs > rt_.obs_cap || need > rt_.cap || ns > rt_.slam_cap) HP_HIP(hipStreamSynchronize(d_.aux));
   if (nobs > rt_.obs_cap) {
     const int oc = std::max(nobs, 2 * rt_.obs_cap);
     if (rt_.d_obs) HP_HIP(hipFree(rt_.d_obs));
@@ -69,10 +73,11 @@ void Engine::retri_alloc(int nobs, int nslam) {
     }
     rt_.cap = need;
   }
-  const int ns = std::max(nslam, 1);
   if (ns > rt_.slam_cap) {
     if (rt_.d_slam) HP_HIP(hipFree(rt_.d_slam));
+    if (rt_.h_slam) HP_HIP(hipHostFree(rt_.h_slam));
     HP_HIP(hipMalloc(&rt_.d_slam, sizeof(DRetriSlam) * 2 * ns));
+    HP_HIP(hipHostMalloc(&rt_.h_slam, sizeof(DRetriSlam) * 2 * ns, hipHostMallocDefault));
     rt_.slam_cap = 2 * ns;
   }
 }
@@ -163,7 +168,7 @@ void Engine::retri_flush() {
   const int nobs = (int)frame_obs_.size();
   {
     HPROF("retri.wait_copy");
-    if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // the previous upload read h_obs
+    if (rt_.copy_pending) HP_HIP(hipEventSynchronize(rt_.copied));  // the previous uploads read h_obs / h_slam
     rt_.copy_pending = false;
   }
   RetriJob &job = rt_.pend_job;
@@ -196,17 +201,16 @@ void Engine::retri_flush() {
   job.ent_new = rt_.ent[1 - rt_.cur];
   job.nslam = (int)sl.size();
   job.slam = rt_.d_slam;
-  if (nobs) {
-    HP_HIP(hipMemcpyAsync(rt_.d_obs, rt_.h_obs, sizeof(DRetriObs) * nobs, hipMemcpyHostToDevice, d_.stream));
-    HP_HIP(hipEventRecord(rt_.copied, d_.stream));
+  // both uploads from pinned buffers that only this job writes (the last one's copies have run: copied)
+  if (!sl.empty()) std::memcpy(rt_.h_slam, sl.data(), sizeof(DRetriSlam) * sl.size());
+  if (nobs) HP_HIP(hipMemcpyAsync(rt_.d_obs, rt_.h_obs, sizeof(DRetriObs) * nobs, hipMemcpyHostToDevice, d_.aux));
+  if (!sl.empty())
+    HP_HIP(hipMemcpyAsync(rt_.d_slam, rt_.h_slam, sizeof(DRetriSlam) * sl.size(), hipMemcpyHostToDevice, d_.aux));
+  if (nobs || !sl.empty()) {
+    HP_HIP(hipEventRecord(rt_.copied, d_.aux));
     rt_.copy_pending = true;
   }
-  if (!sl.empty()) {
-    const DRetriSlam *st = stage(sl.data(), sl.size());
-    stage_flush();
-    HP_HIP(hipMemcpyAsync(rt_.d_slam, st, sizeof(DRetriSlam) * sl.size(), hipMemcpyDeviceToDevice, d_.stream));
-  }
-  launch_retriangulate(d_.stream, job);
+  launch_retriangulate(d_.aux, job);
   rt_.cur = 1 - rt_.cur;
   rt_.nslam = job.nslam;
   rt_.time = rt_.pend_t;
@@ -219,6 +223,7 @@ int Engine::get_active_tracks(double *t, uint64_t *ids, double *posinG, double *
   *t = rt_.valid ? rt_.time : -1;
   if (!rt_.valid) return 0;
   dev_sync();
+  HP_HIP(hipStreamSynchronize(d_.aux));
   std::vector<unsigned long long> keys(rt_.cap);
   std::vector<DRetriEntry> ent(rt_.cap);
   std::vector<DRetriSlam> sl(rt_.nslam);

@@ -223,6 +223,7 @@ Engine::~Engine() {
   for (void *p : rptrs)
     if (p) hipFree(p);
   if (rt_.h_obs) hipHostFree(rt_.h_obs);
+  if (rt_.h_slam) hipHostFree(rt_.h_slam);
   if (rt_.copied) hipEventDestroy(rt_.copied);
   void *ptrs[] = {d_.P, d_.P2, d_.T, d_.Phi, d_.Q, d_.dnc, d_.iold, d_.feats, d_.meas, d_.vars, d_.clones, d_.cams,
                   d_.chi2, d_.H, d_.Tall, d_.partials, d_.R, d_.hidx, d_.ekf.M, d_.ekf.W, d_.ekf.S, d_.ekf.y,

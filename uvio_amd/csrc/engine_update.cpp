@@ -298,16 +298,13 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
   // launches in the same stream order, the host's share hidden under the tracker's wait.
   // An exception of the early propagation is held until the tracker has finished its frame (results
   // consumed, buffers flipped) and rethrown then; its host time is booked as propagation, not tracking.
-  // The previous frame's retriangulation (engine_retri.cpp) runs there too, after the propagation, or right
-  // after the tracker when the frame has no matching step.
   bool early = false;
   int early_rc = 0;
   std::exception_ptr early_exc;
   std::function<void()> in_flight;
   early_prop_s_ = 0.0;
-  const bool early_prop = propagation_can_precede_tracking(t);
-  in_flight = [&, t, early_prop]() {
-    if (early_prop) {
+  if (propagation_can_precede_tracking(t))
+    in_flight = [&, t]() {
       HPROF("prop");
       early = true;
       auto p0 = clk::now();
@@ -317,9 +314,7 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
         early_exc = std::current_exception();
       }
       early_prop_s_ = secs(p0, clk::now());
-    }
-    if (!early_exc) retri_flush();
-  };
+    };
   {
     HPROF("track.feed");
     tracker_->feed(
@@ -330,7 +325,6 @@ int Engine::feed_camera(double t, int ncam, const int *cam_ids, const uint8_t *c
         std::move(in_flight));
   }
   if (early_exc) std::rethrow_exception(early_exc);
-  retri_flush();
   if (early && early_rc) return early_rc;
   struct FrameFlag {
     bool &f;
