@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 for wl in "$@"; do
   steps=100
   case $wl in cfg4|cfg5) steps=20 ;; cfg4i|cfg5i) steps=50 ;; esac
-  B="$R/bench.py --workload $wl --steps $steps --warmup 20 --cpu-frames 0"
+  B="$R/bench.py --workload $wl --steps $steps --warmup 20 --cpu-frames 0 --no-host-feed --msckf-load-steps 0"
   (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pf_$wl -o run -- python3 $B > $O/pf_$wl.log 2>&1)
   (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pw_$wl -o run -- python3 $B > $O/pw_$wl.log 2>&1)
   (cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $O/pm_$wl -o run -- python3 $B > $O/pm_$wl.log 2>&1)
