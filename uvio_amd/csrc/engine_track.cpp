@@ -373,7 +373,10 @@ const std::vector<int> &Tracker::subsets(int count) {
 void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
                    const uint8_t *const *masks, bool device_imgs, const DbSink &db,
                    std::function<void()> in_flight) {
-  predetect_join();
+  {
+    HostProfScope hs(*hp_, "trk.join");
+    predetect_join();
+  }
   in_flight_ = std::move(in_flight);
   device_syncs = 0;
   sync_wait = 0.0;
@@ -911,8 +914,14 @@ void Tracker::match_run(MatchJob *jobs, int nj) {
     ns++;
   }
   if (ns == 0) return;
-  upload(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters));
-  ensure_pyr();
+  {
+    HostProfScope hs(*hp_, "trk.upload");
+    upload(b.p0[lo], b.hp(b.p0[lo]), span(b.p0[lo], b.sub[hi] + 7 * kRansacIters));
+  }
+  {
+    HostProfScope hs(*hp_, "trk.pyr");
+    ensure_pyr();
+  }
   lk.undistort = 1;  // RANSAC's undistortion in the LK epilogue (one launch less on the frame's critical path)
   lk.bytes = (kp_ && kp_->on) ? d_lk_bytes_ : nullptr;
   {
@@ -1098,9 +1107,12 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
     detect_stereo(cl, cr, ll, lr, A.mask_last, B.mask_last, pl_old, pr_old, il_old, ir_old);
   }
   MatchJob jm[2];
-  ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two slots
-  match_prepare(0, ll, nl, cl, cl, pl_old, jm[0]);
-  match_prepare(1, lr, nr, cr, cr, pr_old, jm[1]);
+  {
+    HostProfScope hs(*hp_, "trk.prep");
+    ensure_cap((int)std::max(pl_old.size(), pr_old.size()));  // no reallocation between the two slots
+    match_prepare(0, ll, nl, cl, cl, pl_old, jm[0]);
+    match_prepare(1, lr, nr, cr, cr, pr_old, jm[1]);
+  }
   {
     HostProfScope hs(*hp_, "trk.match");
     match_run(jm, 2);

@@ -5,7 +5,8 @@
 //                            pyrDown 5x5 (sum + 128) >> 8 and Scharr dx/dy int16 (calcSharrDeriv), reflect-101,
 //                            two pyramid levels per launch
 //   k_fast_cells             FAST-9 + 3x3 NMS + top-k per grid cell (one workgroup per valid cell)
-//   k_subpix                 cornerSubPix, one thread per point (sequential sums = oracle order)
+//   k_subpix<WIN>            cornerSubPix, one wavefront per point (five raster-order sums, one lane each = oracle
+//                            order; window size a template constant)
 //   k_lk                     pyramidal LK, one wavefront per point, exact integer window sums
 //   k_undistort              cv::undistortPoints restatement (hp_math.h)
 //   k_ransac_hyp / _select   7-point RANSAC: all hypotheses in parallel, then the sequential
