@@ -651,7 +651,10 @@ def main():
             "ate_rmse_m": acc_ate["pos_m"],
             "ate": {"align": "posyaw (ov_eval AlignTrajectory.cpp:84-106)", "pos_rmse_m": acc_ate["pos_m"],
                     "ori_rmse_deg": acc_ate["ori_deg"], "unaligned_pos_rmse_m": raw["pos_m"],
-                    "frames": args.steps},
+                    "frames": args.steps,
+                    "note": (None if args.steps >= 100 else
+                             "fewer than 100 frames: the posyaw alignment absorbs the drift of so short a segment, "
+                             "the number says nothing about accuracy (the 300-frame default line is the accuracy check)")},
             "roofline": rl.get(dom),
             "roofline_selected_by": dom_by,
             "rooflines": rl,
