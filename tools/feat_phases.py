@@ -38,6 +38,11 @@ for mode in sorted(set(a[:, 0])):
         print("mode %d %s launches-feats %d  meas %.1f nf %.1f | " % (mode, "batch" if big else "single", len(sel),
               sel[:, 2].mean(), sel[:, 3].mean()) + "  ".join("%s %.0f" % (n, v) for n, v in zip(names, np.nanmean(d, axis=0))),
               " total %.0f cyc" % np.nanmean(ts[:, 7] - ts[:, 0]))
+        if mode == 3:  # nullspace sub-phases: reflectors formed (wave 0), barrier, applied
+            sub = sel[:, [7, 12, 13, 14, 8]].astype(float)
+            ds = np.diff(sub, axis=1)
+            print("      nullspace: reflectors %.0f  barrier %.0f  apply %.0f  barrier %.0f  cyc" % tuple(np.nanmean(ds, axis=0)))
+            continue
         c = sel[:, 12:16].astype(float)
         c = c[c[:, 3] > 0]
         if len(c):

@@ -469,10 +469,28 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       const DFeat &F = b.feats[j];
       const int Ni = N0 + 3 * j, nup = 2 * F.nmeas - 3;
       bp.tri_in = tri_out + j;
+      const char *tsdump = std::getenv("UVIO_HP_FEAT_TS");  // debug only: the candidate's phase cycle counts
+      if (tsdump) {
+        HP_HIP(hipMalloc(&bp.dbg_ts, sizeof(long long) * 16));
+        HP_HIP(hipMemsetAsync(bp.dbg_ts, 0, sizeof(long long) * 16, d_.stream));
+      }
       {
         KScope ks(&kprof_, KC_FEATURE);
         launch_feature_linearize(d_.stream, bp, cand->t_feats + j, cand->t_meas, cand->t_vars, fr_cl, fr_cam, d_.P,
                                  d_.chi2, d_.H, fo3 + j, F.nmeas, F.nf);
+      }
+      if (tsdump) {  // synchronous copy-back: debug runs only
+        long long h[16];
+        HP_HIP(hipStreamSynchronize(d_.stream));
+        HP_HIP(hipMemcpy(h, bp.dbg_ts, sizeof(h), hipMemcpyDeviceToHost));
+        HP_HIP(hipFree(bp.dbg_ts));
+        bp.dbg_ts = nullptr;
+        if (FILE *fp = std::fopen(tsdump, "ab")) {
+          long long rec[16] = {3, 1, F.nmeas, F.nf};
+          for (int k = 0; k < 12; k++) rec[4 + k] = h[k];
+          std::fwrite(rec, sizeof(long long), 16, fp);
+          std::fclose(fp);
+        }
       }
       EkfScratch sc = d_.ekf;
       sc.dx = region(new_region());

@@ -833,8 +833,10 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       g1 = wave_sum(g1);
       g2 = wave_sum(g2);
       if (lane == 0) red[0] = g0, red[1] = g1, red[2] = g2;
+      if (F.mode == 3) FEAT_TS(8)  // debug sub-phases of a single candidate (no chi2 stamps there)
     }
     __syncthreads();
+    if (F.mode == 3) FEAT_TS(9)
     const double b1 = sh.beta[0], b2 = sh.beta[1], b3 = sh.beta[2];
     const double g21 = red[0], g31 = red[1], g32 = red[2];
     if (ldl <= 64)
@@ -843,6 +845,7 @@ __global__ void __launch_bounds__(256) k_feature(DBatchParams bp, const DFeat *_
       ns_apply<2>(Hl, V, rows, ldl, tid, b1, b2, b3, g21, g31, g32);
     else
       ns_apply<1>(Hl, V, rows, ldl, tid, b1, b2, b3, g21, g31, g32);
+    if (F.mode == 3) FEAT_TS(10)
     __syncthreads();
     r0 = 3;
   }
