@@ -311,12 +311,7 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
   // LDL^T with the serial chain on one wave (dense_lds.h ldl_wave): the residual row leaves as
   // y = D^-1 L_u^-1 r, so chi2 = r^T S^-1 r = sum_k d_k y_k^2
   double *Dd = Lp;
-  // 65-112 rows: two panel waves of one panel row per lane (dense_lds.h "Panel waves") instead of one wave with
-  // two rows per lane; beyond, one wave (three panel waves measured no faster at 512 threads)
-  if (R + 1 > 64 && R + 1 <= 16 + 48 * 2)
-    ldl_wave_inv<1, SqLayout, 2>(S, SqLayout{ldS}, R, R + 1, Dd, false);
-  else
-    ldl_wave(S, SqLayout{ldS}, R, R + 1, Dd, false);
+  ldl_wave(S, SqLayout{ldS}, R, R + 1, Dd, false);
   CHI2_TS(2)
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {
