@@ -516,12 +516,15 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
   if (!LA::square) with_inv = false;
   const int nslot = with_inv ? nb + 2 : (Xd ? nb + 1 : nb);
   __shared__ int colcnt;  // column-update tiles finished so far (helpers -> wave 0)
-  if (threadIdx.x == 0) colcnt = 0;
+  __shared__ int pload;   // W > 1: panel waves that have read their panel so far (-> wave 0's store of the block rows)
+  if (threadIdx.x == 0) colcnt = 0, pload = 0;
   __syncthreads();
-  int coltarget = 0;
+  int coltarget = 0, ptarget = 0;
   for (int J = 0; J < nslot; J++) {
     const int P = J - 1;
     if (P >= 0 && J < nb) coltarget += nbr - J;
+    if (W > 1 && J < nb)
+      for (int w = 0; w < W; w++) ptarget += (w == 0 || 16 + 48 * w < nrows - 16 * J) ? 1 : 0;
     const long long tslot = prof ? (long long)clock64() : 0;
     if (wid < W) {
       if (J < nb && (wid == 0 || 16 + 48 * wid < nrows - 16 * J)) {
@@ -538,6 +541,10 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
 #pragma unroll
           for (int p = 0; p < 16; p++) v[s][p] = (i < nrows && oJ + p < n && p <= ro) ? A[la(i, oJ + p)] : 0.0;
         }
+        if (W > 1) {  // this wave's reads of the block rows are done (wave 0 overwrites them with the factor)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_fetch_add(&pload, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         double w0[16];
 #pragma unroll
         for (int p = 1; p < 16; p++) w0[p] = readlane_f64(v[0][0], p);
@@ -547,6 +554,14 @@ __device__ __forceinline__ void ldl_wave_inv(double *A, LA la, int n, int nrows,
 #pragma unroll
         for (int p = 0; p < 16; p++)
           if (wid == 0 && lane == p && oJ + p < n) Dd[oJ + p] = v[0][p];
+        // W > 1: every panel wave reads the block's own rows, wave 0 alone writes their factor back; it waits until
+        // all have read them (normally long done: the read is the first thing a panel wave does, the factor takes
+        // thousands of cycles, but a wave descheduled on a busy CU could otherwise read factored values)
+        if (W > 1 && wid == 0) {
+          while (__hip_atomic_load(&pload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ptarget)
+            __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
 #pragma unroll
         for (int s = 0; s < SMAX; s++) {
           const int ro = prow(s), i = oJ + ro;
