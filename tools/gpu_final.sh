@@ -4,7 +4,9 @@
 #           timelines) copied into profiles/ first (the bench picks its roofline class from the committed same-code
 #           summary), then GPU tests, smoke, the cfg3 (default) and cfg2 bench lines with CPU baselines, the driver form;
 #   part 2: the other workloads' bench lines (cfg3t, cfg2l, cfg4i, cfg5i, cfg4 over 300 frames, cfg5).
-# usage: bash tools/gpu_final.sh TAG [1|2]
+# Tags sort by name: bench.py reads the newest-named profiles/rNN*_<workload>_per_frame.txt, so a re-run takes a
+# later-sorting tag.  Part 3: the part-1 bench lines alone.
+# usage: bash tools/gpu_final.sh TAG [1|2|3]
 set -e
 TAG=${1:-rXX}; PART=${2:-1}
 R=$GRAFT_REPO_ROOT
@@ -25,6 +27,12 @@ if [ "$PART" = "1" ]; then
   done
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg3_bench.json 2> $O/cfg3.err
+  timeout -k 10 400 python -u bench.py --workload cfg2 > $O/${TAG}_cfg2_bench.json 2> $O/cfg2.err
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg3_bench_driver_form.json 2> $O/cfg3_driver.err
+  timeout -k 10 300 python -u bench.py --steps 300 --cpu-frames 0 --msckf-load-steps 0 > $O/${TAG}_cfg3_bench_300.json 2> $O/cfg3_300.err
+elif [ "$PART" = "3" ]; then
+  # the bench lines of part 1 alone (per-frame summaries already committed under this tag)
   timeout -k 10 400 python -u bench.py > $O/${TAG}_cfg3_bench.json 2> $O/cfg3.err
   timeout -k 10 400 python -u bench.py --workload cfg2 > $O/${TAG}_cfg2_bench.json 2> $O/cfg2.err
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/${TAG}_cfg3_bench_driver_form.json 2> $O/cfg3_driver.err
