@@ -371,6 +371,50 @@ def make_anchors(N):
     return out
 
 
+def test_lockstep_uwb_outliers_inside_messages(euroc_yaml):
+    """The ranges of one UwbData message run as one device chain (engine_update.cpp uwb_update_message): each
+    range's chi2 gate is decided on the device and a rejected range must leave the device-side state the next
+    range is linearized at untouched.  Every message carries a 20 m outlier in its third range: lock-step against
+    the oracle (UpdaterUWB.cpp:53-90 per range, UVioManager.cpp:178-188), and the device run must equal, bit for
+    bit, a device run of the same stream with the outliers removed from the messages (a gated range changes
+    nothing in the reference)."""
+    import uvio_amd as U
+    from uvio_amd import _native as N
+    from uvio_amd.sim import SimStream
+    opts = U.load_options(euroc_yaml, max_msckf_in_update=60, max_slam_features=0, use_uwb=1,
+                          do_calib_uwb_extrinsics=1, min_dist_to_use_uwb=0.05)
+    for k, v in enumerate([0.05, -0.02, 0.03]):
+        opts.p_IinU[k] = v
+    anchors = make_anchors(N)
+    n = 24
+
+    def stream(outliers):
+        sim = SimStream(opts, duration=n / opts.track_frequency + 1.2, seed=7, spawn=60, anchors=anchors,
+                        uwb_rate=10.0, uwb_sigma=0.1)
+        msgs = []
+        for t, ids, rs in sim.uwb:
+            ids, rs = list(ids), list(rs)
+            if outliers:
+                rs[2] += 20.0
+            else:
+                del ids[2], rs[2]
+            msgs.append((t, ids, rs))
+        sim.uwb = msgs
+        return sim
+
+    init = lambda m: m.try_to_initialize_uwb_anchors(anchors)
+    steps = run_lockstep(opts, stream(True), n, after_init=init)
+    _check_lockstep(steps)
+    runs = []
+    for outliers in (True, False):
+        g = U.VioManager(opts)
+        stream(outliers).run(g, n_frames=n, after_init=init)
+        runs.append((g.get_state_vector()[0], g.get_cov()))
+        g.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1]), \
+        (np.abs(runs[0][0] - runs[1][0]).max(), np.abs(runs[0][1] - runs[1][1]).max())
+
+
 def test_lockstep_uwb_parity(euroc_yaml):
     """UpdaterUWB::update_single (UpdaterUWB.cpp:53-90) + UVioPropagator + anchor init, lock-step."""
     import uvio_amd as U
