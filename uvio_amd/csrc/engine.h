@@ -409,6 +409,24 @@ class Engine {
     return db_.erase(it);
   }
   size_t currid_;
+  // default-constructed features made while the host waits for the device chain (refill_feature_stock), so
+  // that a feed's inserts -- sequential, in observation order -- do not allocate and clear each new object
+  std::vector<FeatP> feat_stock_;
+  size_t stock_target_ = 0;  // 1.5 x the last feed's new features
+  FeatP new_feature(size_t id) {
+    FeatP f;
+    if (!feat_stock_.empty()) {
+      f = std::move(feat_stock_.back());
+      feat_stock_.pop_back();
+    } else {
+      f = std::make_shared<Feature>();
+    }
+    f->featid = id;
+    return f;
+  }
+  void refill_feature_stock() {
+    while (feat_stock_.size() < stock_target_) feat_stock_.push_back(std::make_shared<Feature>());
+  }
   // ---- manager ----
   bool is_initialized_ = false;
   // VioManager::thread_init_success (VioManager.h:226): the initializer succeeded on an earlier frame; the

@@ -539,6 +539,10 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       chain_overlap_ = nullptr;
       f();
     }
+    {
+      HPROF("chain.stock");
+      refill_feature_stock();
+    }
     dev_sync();
   }
   auto tm3 = clk::now();

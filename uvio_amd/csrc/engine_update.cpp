@@ -124,8 +124,7 @@ void Engine::db_update(size_t id, double t, size_t cam, float u, float v, float 
   if (it != db_.end()) {
     f = it->second.get();
   } else {
-    FeatP nf = std::make_shared<Feature>();
-    nf->featid = id;
+    FeatP nf = new_feature(id);
     f = nf.get();
     db_insert(id, std::move(nf));
   }
@@ -182,96 +181,112 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
     camids.push_back(cid);
     cam_of.insert(cam_of.end(), counts[i], cid);
   }
-  // undistort every observation (independent, on the pool), then the database updates in order
-  std::vector<float> uvn(2 * cam_of.size());
-  {
-    HPROF("feed.undistort");
-    pool_.parallel_for(cam_of.size(), 2048, [&](size_t b, size_t e) {
-      for (size_t k = b; k < e; k++) cam_undistort_f(cams_[cam_of[k]], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
-    });
-  }
   // FeatureDatabase::update_feature for every observation, in order, in three passes with the same
-  // result: (a) look up the known features (read-only, on the pool), (b) insert the new ids into db_
-  // sequentially in observation order (db_'s iteration order depends on it), (c) append each
-  // observation to its feature; features are split across workers by pointer, and every worker walks
-  // the observations in order, so each feature's appends keep the sequential order.
+  // result: (a) undistort every observation, record it for the retriangulation and look up the known
+  // features (independent per observation, read-only on db_, one pool job), (b) insert the new ids into db_
+  // sequentially in observation order (db_'s iteration order depends on it), (c) append each observation
+  // to its feature; features are split across workers by pointer, and every worker walks the observations
+  // in order, so each feature's appends keep the sequential order.
   const size_t nobs = cam_of.size();
+  std::vector<float> uvn(2 * nobs);
   std::vector<Feature *> fp(nobs, nullptr);
+  frame_obs_.resize(nobs);
   {
-    HPROF("feed.lookup");
+    HPROF("feed.undistort_lookup");
     pool_.parallel_for(nobs, 2048, [&](size_t b, size_t e) {
       for (size_t k = b; k < e; k++) {
-        auto it = db_.find((size_t)ids[k] + currid_);
+        const size_t id = (size_t)ids[k] + currid_;
+        cam_undistort_f(cams_[cam_of[k]], uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1]);
+        DRetriObs &o = frame_obs_[k];
+        o.featid = (unsigned long long)id;
+        o.u = uv[2 * k];
+        o.v = uv[2 * k + 1];
+        o.un = uvn[2 * k];
+        o.vn = uvn[2 * k + 1];
+        o.cam = cam_of[k];
+        o.pad = 0;
+        auto it = db_.find(id);
         if (it != db_.end()) fp[k] = it->second.get();
       }
     });
   }
+  // (b) and (c) as one pool job: its first task inserts the new ids in observation order while the other
+  // tasks append the observations of the features db_ already held (they touch neither db_ nor a new
+  // feature); then the new features' observations are appended.  Every feature's observations are all in
+  // one of the two groups, so its appends keep the sequential order.
   {
-    HPROF("feed.insert");
-    for (size_t k = 0; k < nobs; k++) {
-      if (fp[k]) continue;
-      const size_t id = (size_t)ids[k] + currid_;
-      auto it = db_.find(id);  // a new id seen by an earlier camera of this frame
-      if (it == db_.end()) {
-        auto f = std::make_shared<Feature>();
-        f->featid = id;
-        it = db_insert(id, f);
-      }
-      fp[k] = it->second.get();
-    }
-  }
-  {
-    HPROF("feed.obs_append");
-    frame_obs_.resize(nobs);
-    for (size_t k = 0; k < nobs; k++) {
-      DRetriObs &o = frame_obs_[k];
-      o.featid = (unsigned long long)(ids[k] + currid_);
-      o.u = uv[2 * k];
-      o.v = uv[2 * k + 1];
-      o.un = uvn[2 * k];
-      o.vn = uvn[2 * k + 1];
-      o.cam = cam_of[k];
-      o.pad = 0;
-    }
-    // bucket the observations by owning worker once (a counting sort that keeps observation order inside a
-    // bucket), then each worker appends its bucket with the feature objects prefetched a few entries ahead
-    // -- the appends are cache-miss bound (feature, its track array, the measurement storage)
+    HPROF("feed.db");
     const uint32_t nw = (uint32_t)pool_.threads();
-    std::vector<uint32_t> start(nw + 1, 0), order(nobs);
-    std::vector<uint16_t> owner(nobs);
-    for (size_t k = 0; k < nobs; k++) {
-      const uint64_t h = (uint64_t)((uintptr_t)fp[k] >> 6) * 0x9E3779B97F4A7C15ull;
-      owner[k] = (uint16_t)(((h >> 32) * nw) >> 32);
-      start[owner[k] + 1]++;
-    }
-    for (uint32_t w = 0; w < nw; w++) start[w + 1] += start[w];
-    {
-      std::vector<uint32_t> pos(start.begin(), start.end() - 1);
-      for (size_t k = 0; k < nobs; k++) order[pos[owner[k]]++] = (uint32_t)k;
-    }
-    pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
+    std::vector<uint32_t> known, fresh;
+    known.reserve(nobs);
+    for (size_t k = 0; k < nobs; k++) (fp[k] ? known : fresh).push_back((uint32_t)k);
+    // bucket a list of observations by owning worker (a counting sort that keeps observation order inside a
+    // bucket); a worker appends its bucket with the feature objects prefetched a few entries ahead -- the
+    // appends are cache-miss bound (feature, its track array, the measurement storage)
+    struct Buckets {
+      std::vector<uint32_t> start, order;
+    };
+    auto bucket = [&](const std::vector<uint32_t> &obs, Buckets &bk) {
+      bk.start.assign(nw + 1, 0);
+      bk.order.resize(obs.size());
+      std::vector<uint16_t> owner(obs.size());
+      for (size_t i = 0; i < obs.size(); i++) {
+        const uint64_t h = (uint64_t)((uintptr_t)fp[obs[i]] >> 6) * 0x9E3779B97F4A7C15ull;
+        owner[i] = (uint16_t)(((h >> 32) * nw) >> 32);
+        bk.start[owner[i] + 1]++;
+      }
+      for (uint32_t w = 0; w < nw; w++) bk.start[w + 1] += bk.start[w];
+      std::vector<uint32_t> pos(bk.start.begin(), bk.start.end() - 1);
+      for (size_t i = 0; i < obs.size(); i++) bk.order[pos[owner[i]]++] = obs[i];
+    };
+    auto append = [&](const Buckets &bk, uint32_t w) {
+      const uint32_t i0 = bk.start[w], i1 = bk.start[w + 1];
+      for (uint32_t i = i0; i < i1; i++) {
+        // two-stage software prefetch: the feature object's first three lines (its tracks) 32 ahead, then
+        // the append slot of the observation's camera track 16 ahead
+        if (i + 32 < i1) {
+          const char *p = (const char *)fp[bk.order[i + 32]];
+          __builtin_prefetch(p, 1);
+          __builtin_prefetch(p + 64, 1);
+          __builtin_prefetch(p + 128, 1);
+        }
+        if (i + 16 < i1) {
+          const size_t k2 = bk.order[i + 16];
+          for (const CamTrack &c : fp[k2]->tracks)
+            if ((int)c.cam == cam_of[k2]) __builtin_prefetch(c.m.v.data() + c.m.v.size(), 1);
+        }
+        const size_t k = bk.order[i];
+        fp[k]->track((size_t)cam_of[k]).m.push_back(FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
+      }
+    };
+    Buckets bk_known, bk_fresh;
+    bucket(known, bk_known);
+    const size_t db0 = db_.size();
+    pool_.parallel_for((size_t)nw + 1, 1, [&](size_t b, size_t e) {
       for (size_t w = b; w < e; w++) {
-        const uint32_t i0 = start[w], i1 = start[w + 1];
-        for (uint32_t i = i0; i < i1; i++) {
-          // two-stage software prefetch: the feature object's first three lines (its tracks) 32 ahead, then
-          // the append slot of the observation's camera track 16 ahead
-          if (i + 32 < i1) {
-            const char *p = (const char *)fp[order[i + 32]];
-            __builtin_prefetch(p, 1);
-            __builtin_prefetch(p + 64, 1);
-            __builtin_prefetch(p + 128, 1);
-          }
-          if (i + 16 < i1) {
-            const size_t k2 = order[i + 16];
-            for (const CamTrack &c : fp[k2]->tracks)
-              if ((int)c.cam == cam_of[k2]) __builtin_prefetch(c.m.v.data() + c.m.v.size(), 1);
-          }
-          const size_t k = order[i];
-          fp[k]->track((size_t)cam_of[k]).m.push_back(
-              FeatMeas{uv[2 * k], uv[2 * k + 1], uvn[2 * k], uvn[2 * k + 1], t});
+        if (w > 0) {
+          append(bk_known, (uint32_t)w - 1);
+          continue;
+        }
+        HPROF("feed.insert");  // on whichever thread takes task 0; no other task touches the profile
+        for (uint32_t k : fresh) {
+          const size_t id = (size_t)ids[k] + currid_;
+          auto it = db_.find(id);  // a new id seen by an earlier camera of this frame
+          if (it == db_.end()) it = db_insert(id, new_feature(id));
+          fp[k] = it->second.get();
         }
       }
     });
+    stock_target_ = std::min<size_t>(3 * (db_.size() - db0) / 2 + 16, 16384);
+    hprof_.count("feed.new_features", (double)(db_.size() - db0));
+    hprof_.count("feed.obs", (double)nobs);
+    hprof_.count("feed.db_size", (double)db_.size());
+    if (!fresh.empty()) {
+      bucket(fresh, bk_fresh);
+      pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
+        for (size_t w = b; w < e; w++) append(bk_fresh, (uint32_t)w);
+      });
+    }
   }
   return after_tracking(t, camids, rT1);
 }
@@ -494,10 +509,14 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
         flag[i] = (uint8_t)((lost ? 1 : 0) | (has ? 2 : 0));
       }
     });
+    HPROF("select.lists");
     for (size_t i = 0; i < all.size(); i++) {
       if (flag[i] & 1) feats_lost.push_back(*all[i]);
       if (flag[i] & 2) feats_marg.push_back(*all[i]);
     }
+    hprof_.count("select.db_size", (double)all.size());
+    hprof_.count("select.lost", (double)feats_lost.size());
+    hprof_.count("select.marg", (double)feats_marg.size());
   }
   std::vector<FeatP> feats_maxtracks;
   {

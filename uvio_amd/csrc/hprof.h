@@ -12,12 +12,22 @@ namespace uvhp {
 
 struct HostProf {
   bool on = std::getenv("UVIO_HP_HOST_PROF") != nullptr;
-  std::map<std::string, std::pair<double, long>> acc;
+  std::map<std::string, std::pair<double, long>> acc, cnt;
+  // a per-frame quantity (sizes, counts) averaged over the calls
+  void count(const char *name, double v) {
+    if (!on) return;
+    auto &a = cnt[name];
+    a.first += v;
+    a.second++;
+  }
   ~HostProf() {
     if (!on) return;
     for (auto &kv : acc)
       std::fprintf(stderr, "hprof %-28s %10.3f ms  %8ld calls  %8.2f us/call\n", kv.first.c_str(),
                    1e3 * kv.second.first, kv.second.second, 1e6 * kv.second.first / std::max(1L, kv.second.second));
+    for (auto &kv : cnt)
+      std::fprintf(stderr, "hcount %-27s mean %12.1f over %8ld calls\n", kv.first.c_str(),
+                   kv.second.first / std::max(1L, kv.second.second), kv.second.second);
   }
 };
 

@@ -7,7 +7,7 @@
 // frames/s against 8 threads in the same-box A/B profiles/r04o_env_ab.txt).
 //
 // A frame issues a dozen parallel loops a few tens of microseconds apart, so a worker that finishes one
-// spins for a while (kSpinUs) on the job generation before it sleeps on the condition variable, and the
+// spins for a while (spin_us_) on the job generation before it sleeps on the condition variable, and the
 // caller never waits for a worker that has not joined the job: it closes the job when its own share of
 // chunks runs out and waits only for the workers that took part (a late sleeper wakes to a closed job).
 #pragma once
@@ -29,6 +29,7 @@ class WorkPool {
     int n = (int)std::thread::hardware_concurrency();
     n = n > 0 ? std::min(n, 16) : 1;
     if (const char *e = std::getenv("UVIO_HP_THREADS")) n = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("UVIO_HP_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
     for (int i = 1; i < n; i++) th_.emplace_back([this] { worker(); });
   }
   ~WorkPool() {
@@ -77,7 +78,7 @@ class WorkPool {
     std::mutex err_mu;
     std::exception_ptr err;
   };
-  static constexpr int kSpinUs = 200;
+  int spin_us_ = 200;  // kept spinning after a job (UVIO_HP_SPIN_US: A/B runs)
   static void relax() { __builtin_ia32_pause(); }
   static void run(Job &job) {
     for (;;) {
@@ -98,7 +99,7 @@ class WorkPool {
       const auto t0 = std::chrono::steady_clock::now();
       while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
         relax();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
       }
       Job *j = nullptr;
       {
