@@ -1,5 +1,5 @@
 // Host unit test of the feature database's per-camera measurement storage (uvio_amd/csrc/engine.h MeasList /
-// TrackSet) and of the host work pool (pool.h): random push / trim / erase sequences against a plain vector
+// TrackSet), of the host work pool (pool.h) and of the database's slab node allocator: random push / trim / erase sequences against a plain vector
 // model, checking every query and the cached first / last times; many back-to-back pool jobs.  Built and run by tests/test_host_structs.py (no GPU needed).
 #include <cstdio>
 #include <random>
@@ -108,6 +108,46 @@ int main() {
       sum += s;
     });
     CHECK(sum.load() == 100000L * 99999L / 2);
+  }
+  // the feature database's slab node allocator (engine.h NodeSlabs / SlabAlloc): a map on the slabs and a plain
+  // std::unordered_map under the same operation sequence (a sliding window of consecutive ids, as the
+  // simulated feeds insert and erase them, plus random keys) iterate in the same order with the same values
+  {
+    uvhp::NodeSlabs slabs;
+    using SMap = std::unordered_map<size_t, long, std::hash<size_t>, std::equal_to<size_t>,
+                                    uvhp::SlabAlloc<std::pair<const size_t, long>>>;
+    SMap a{uvhp::SlabAlloc<std::pair<const size_t, long>>(&slabs)};
+    std::unordered_map<size_t, long> b;
+    size_t next = 1000, oldest = 1000;
+    for (int frame = 0; frame < 300; frame++) {
+      const int nnew = 500 + (int)(rng() % 1500);
+      for (int i = 0; i < nnew; i++, next++) {
+        a.emplace(next, (long)next * 3);
+        b.emplace(next, (long)next * 3);
+      }
+      for (int i = 0; i < 50; i++) {  // random keys, some present
+        const size_t k = rng() % (next + 5000);
+        a.emplace(k, -(long)k);
+        b.emplace(k, -(long)k);
+      }
+      while (next - oldest > 40000) {  // the window's oldest features leave
+        a.erase(oldest);
+        b.erase(oldest);
+        oldest++;
+      }
+      for (int i = 0; i < 300; i++) {  // scattered erasures
+        const size_t k = oldest + rng() % (next - oldest);
+        a.erase(k);
+        b.erase(k);
+      }
+      CHECK(a.size() == b.size() && a.bucket_count() == b.bucket_count());
+      auto ia = a.begin();
+      auto ib = b.begin();
+      bool same = true;
+      for (; ia != a.end() && ib != b.end(); ++ia, ++ib) same = same && ia->first == ib->first && ia->second == ib->second;
+      CHECK(same && ia == a.end() && ib == b.end());
+    }
+    a.clear();
   }
   std::printf(fails ? "meas_list_test: %d failures\n" : "meas_list_test: ok\n", fails);
   return fails ? 1 : 0;

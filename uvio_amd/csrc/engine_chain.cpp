@@ -92,11 +92,12 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       }
     });
     std::vector<FeatP> keep;
+    keep.reserve(up.size());
     for (size_t i = 0; i < up.size(); i++) {
       if (few[i])
         up[i]->to_delete = true;
       else
-        keep.push_back(up[i]);
+        keep.push_back(std::move(up[i]));
     }
     up.swap(keep);
   }

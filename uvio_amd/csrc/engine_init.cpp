@@ -32,7 +32,7 @@ void Engine::db_cleanup_measurements(double t) {
 // FeatureHelper::compute_disparity (FeatureHelper.h:123-181) over the raw pixel coordinates of every
 // feature and camera: per track the first measurement newer than oldest_time and the last one older than
 // newest_time after it (-1 disables a bound).  Returns the number of disparities; the mean in *mean.
-static int compute_disparity(const std::unordered_map<size_t, FeatP> &db, double *mean, double newest_time,
+static int compute_disparity(const DbMap &db, double *mean, double newest_time,
                              double oldest_time) {
   std::vector<double> disp;
   for (const auto &kv : db) {

@@ -480,8 +480,13 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       }
     }
     HPROF("select.flags");
-    std::vector<uint8_t> flag(all.size(), 0);  // bit 0 lost, bit 1 marg
-    pool_.parallel_for(all.size(), 1024, [&](size_t b, size_t e) {
+    // each chunk's lost / marg lists built by the thread that flagged it (the reference-count increments
+    // then hit lines that thread has just read), joined in chunk order = db_ order
+    constexpr size_t kChunk = 1024;
+    const size_t nchunk = (all.size() + kChunk - 1) / kChunk;
+    std::vector<std::vector<FeatP>> lost_c(nchunk), marg_c(nchunk);
+    pool_.parallel_for(all.size(), kChunk, [&](size_t b, size_t e) {
+      std::vector<FeatP> &lo = lost_c[b / kChunk], &ma = marg_c[b / kChunk];
       for (size_t i = b; i < e; i++) {
         if (i + 8 < e) __builtin_prefetch(fs[i + 8]);
         const Feature &f = *fs[i];
@@ -506,13 +511,18 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
             }
           lost = found;
         }
-        flag[i] = (uint8_t)((lost ? 1 : 0) | (has ? 2 : 0));
+        if (lost) lo.push_back(*all[i]);
+        if (has) ma.push_back(*all[i]);
       }
     });
     HPROF("select.lists");
-    for (size_t i = 0; i < all.size(); i++) {
-      if (flag[i] & 1) feats_lost.push_back(*all[i]);
-      if (flag[i] & 2) feats_marg.push_back(*all[i]);
+    size_t nl = 0, nm = 0;
+    for (size_t c = 0; c < nchunk; c++) nl += lost_c[c].size(), nm += marg_c[c].size();
+    feats_lost.reserve(nl);
+    feats_marg.reserve(nm);
+    for (size_t c = 0; c < nchunk; c++) {
+      std::move(lost_c[c].begin(), lost_c[c].end(), std::back_inserter(feats_lost));
+      std::move(marg_c[c].begin(), marg_c[c].end(), std::back_inserter(feats_marg));
     }
     hprof_.count("select.db_size", (double)all.size());
     hprof_.count("select.lost", (double)feats_lost.size());
@@ -528,12 +538,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
           reached = true;
           break;
         }
-      if (reached)
-        feats_maxtracks.push_back(f);
-      else
-        keep.push_back(f);
+      (reached ? feats_maxtracks : keep).push_back(std::move(f));  // (moves: no reference-count traffic)
     }
-    feats_marg = keep;
+    feats_marg = std::move(keep);
   }
   int curr_aruco = 0;
   for (auto &l : slam_)
@@ -543,7 +550,8 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     int amount = (o_.max_slam_features + curr_aruco) - (int)slam_.size();
     int valid = std::min(amount, (int)feats_maxtracks.size());
     if (valid > 0) {
-      feats_slam.insert(feats_slam.end(), feats_maxtracks.end() - valid, feats_maxtracks.end());
+      feats_slam.insert(feats_slam.end(), std::make_move_iterator(feats_maxtracks.end() - valid),
+                        std::make_move_iterator(feats_maxtracks.end()));
       feats_maxtracks.erase(feats_maxtracks.end() - valid, feats_maxtracks.end());
     }
   }
@@ -563,9 +571,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     else
       slam_delayed.push_back(f);
   }
-  std::vector<FeatP> up = feats_lost;
-  up.insert(up.end(), feats_marg.begin(), feats_marg.end());
-  up.insert(up.end(), feats_maxtracks.begin(), feats_maxtracks.end());
+  std::vector<FeatP> up = std::move(feats_lost);
+  up.insert(up.end(), std::make_move_iterator(feats_marg.begin()), std::make_move_iterator(feats_marg.end()));
+  up.insert(up.end(), std::make_move_iterator(feats_maxtracks.begin()), std::make_move_iterator(feats_maxtracks.end()));
   // VioManager.cpp:518 std::sort by measurement count (compare_feat), on the counts computed once: std::sort's
   // permutation depends only on the comparison outcomes, which are the same
   {
