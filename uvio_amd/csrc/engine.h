@@ -157,8 +157,12 @@ struct TrackSet {
   CamTrack &front() { return t[0]; }
   CamTrack &insert_front(size_t cam) {
     if (n >= UVIO_HP_MAX_CAMS) throw std::runtime_error("feature observed by more than UVIO_HP_MAX_CAMS cameras");
+    // the first unused slot moves to the front: its storage may have been reserved ahead (Engine's feature stock)
+    CamTrack spare = std::move(t[n]);
     for (int i = n; i > 0; i--) t[i] = std::move(t[i - 1]);
-    t[0] = CamTrack{cam, {}};
+    t[0] = std::move(spare);
+    t[0].cam = cam;
+    t[0].m.clear();  // (keeps the capacity)
     n++;
     return t[0];
   }
@@ -495,8 +499,16 @@ class Engine {
     f->featid = id;
     return f;
   }
+  // each stocked feature also gets the storage of its first track reserved (every new feature has one; the
+  // feed's first append to it then does not allocate; reserving all cameras' tracks cost more than it saved
+  // at cfg5, where a feature is seen by ~2.6 of 4 cameras)
   void refill_feature_stock() {
-    while (feat_stock_.size() < stock_target_) feat_stock_.push_back(std::make_shared<Feature>());
+    const int r = g_track_reserve.load(std::memory_order_relaxed);
+    while (feat_stock_.size() < stock_target_) {
+      FeatP f = std::make_shared<Feature>();
+      if (r > 0) f->tracks.t[0].m.v.reserve((size_t)r);
+      feat_stock_.push_back(std::move(f));
+    }
   }
   // ---- manager ----
   bool is_initialized_ = false;

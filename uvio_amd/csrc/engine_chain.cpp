@@ -225,10 +225,17 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     auto it = std::make_unique<ChainItem>();
     it->kind = 0;
     it->fv = up;
-    build_clone_cam_tables(it->b, false);
-    add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
+    {
+      HPROF("chain.msckf.build.tables");
+      build_clone_cam_tables(it->b, false);
+    }
+    {
+      HPROF("chain.msckf.build.add");
+      add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
+    }
     msk = it.get();
     items.push_back(std::move(it));
+    HPROF("chain.msckf.build.stage");
     stage_group({msk});
   }
   char *const frame = d_.frame;

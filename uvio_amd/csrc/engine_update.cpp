@@ -216,7 +216,9 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
   // one of the two groups, so its appends keep the sequential order.
   {
     HPROF("feed.db");
-    const uint32_t nw = (uint32_t)pool_.threads();
+    // 4 buckets per thread: the known features' buckets share the threads with the insert task and are
+    // taken dynamically (one bucket per thread left one thread with two while the others waited)
+    const uint32_t nw = 4 * (uint32_t)pool_.threads();
     std::vector<uint32_t> known, fresh;
     known.reserve(nobs);
     for (size_t k = 0; k < nobs; k++) (fp[k] ? known : fresh).push_back((uint32_t)k);
@@ -260,8 +262,12 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
       }
     };
     Buckets bk_known, bk_fresh;
-    bucket(known, bk_known);
+    {
+      HPROF("feed.db.bucket");
+      bucket(known, bk_known);
+    }
     const size_t db0 = db_.size();
+    auto tj0 = clk::now();
     pool_.parallel_for((size_t)nw + 1, 1, [&](size_t b, size_t e) {
       for (size_t w = b; w < e; w++) {
         if (w > 0) {
@@ -277,11 +283,17 @@ int Engine::feed_simulation(double t, int ncam, const int *cam_ids, const int *c
         }
       }
     });
+    if (hprof_.on) {
+      auto &a = hprof_.acc["feed.db.job"];
+      a.first += secs(tj0, clk::now());
+      a.second++;
+    }
     stock_target_ = std::min<size_t>(3 * (db_.size() - db0) / 2 + 16, 16384);
     hprof_.count("feed.new_features", (double)(db_.size() - db0));
     hprof_.count("feed.obs", (double)nobs);
     hprof_.count("feed.db_size", (double)db_.size());
     if (!fresh.empty()) {
+      HPROF("feed.db.fresh");
       bucket(fresh, bk_fresh);
       pool_.parallel_for((size_t)nw, 1, [&](size_t b, size_t e) {
         for (size_t w = b; w < e; w++) append(bk_fresh, (uint32_t)w);
