@@ -273,6 +273,23 @@ struct SlabAlloc {
   template <class U>
   bool operator!=(const SlabAlloc<U> &o) const { return s != o.s; }
 };
+// clone time -> slot of a batch's clone table (built in time order): a sorted array searched by bisection
+// (add_feature looks up every measurement's clone twice; a std::map node chase per lookup was most of the
+// MSCKF batch build at cfg4 / cfg5)
+struct SlotTable {
+  std::vector<double> t;
+  void clear() { t.clear(); }
+  void push(double x) { t.push_back(x); }  // ascending
+  int find(double x) const {
+    auto it = std::lower_bound(t.begin(), t.end(), x);
+    return (it != t.end() && *it == x) ? (int)(it - t.begin()) : -1;
+  }
+  int at(double x) const {
+    const int s = find(x);
+    if (s < 0) throw std::out_of_range("measurement time is not a clone time");
+    return s;
+  }
+};
 using DbMap = std::unordered_map<size_t, FeatP, std::hash<size_t>, std::equal_to<size_t>,
                                  SlabAlloc<std::pair<const size_t, FeatP>>>;
 
@@ -387,7 +404,7 @@ struct DeviceBufs {
 // the per-feature measurement / variable tables of one feature in the reference iteration order (engine_update.cpp)
 class Engine;
 void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
-                 std::map<double, int> &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
+                 const SlotTable &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
                  std::vector<DMeas> &meas, std::vector<DVar> &vars, int &rows, const Var *landmark, int landmark_canon);
 // algorithmic FP64 FLOPs / bytes of one EKFUpdate (engine_state.cpp)
 double ekf_flops(double N, double n, double r);
@@ -730,7 +747,7 @@ class Engine {
     long long stg_epoch = -1;  // staging ring epoch of the meas / vars reservation
     size_t n_meas() const { return meas_dev ? n_meas_dev : meas.size(); }
     size_t n_vars() const { return vars_dev ? n_vars_dev : vars.size(); }
-    std::map<double, int> slot_of_time;
+    SlotTable slot_of_time;
     int fout_off = 0;  // its per-feature results in d_.fout / d_.fout_host start here
   };
   void build_clone_cam_tables(Batch &b, bool include_landmarks);

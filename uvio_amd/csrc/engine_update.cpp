@@ -780,7 +780,6 @@ void Engine::build_clone_cam_tables(Batch &b, bool include_landmarks) {
     }
     b.cams.push_back(dc);
   }
-  int slot = 0;
   for (auto &c : clones_) {
     DClone d{};
     quat_2_Rot(c.second->val, d.R);
@@ -790,7 +789,7 @@ void Engine::build_clone_cam_tables(Batch &b, bool include_landmarks) {
     d.canon = canon;
     for (int k = 0; k < 6; k++) b.hidx.push_back(c.second->id + k);
     canon += 6;
-    b.slot_of_time[c.first] = slot++;
+    b.slot_of_time.push(c.first);  // slot = index in time order
     b.clones.push_back(d);
   }
   (void)include_landmarks;
@@ -800,7 +799,7 @@ void Engine::build_clone_cam_tables(Batch &b, bool include_landmarks) {
 // Builds the per-feature measurement / variable tables in the reference iteration order
 // (get_feature_jacobian_full's x_order, UpdaterHelper.cpp:200-262) and appends them to the batch.
 void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_options_t &o, const std::vector<DCam> &cams,
-                        std::map<double, int> &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
+                        const SlotTable &slot_of_time, const std::vector<DClone> &clones, std::vector<DFeat> &feats,
                         std::vector<DMeas> &meas, std::vector<DVar> &vars, int &rows, const Var *landmark,
                         int landmark_canon) {
   DFeat F{};
@@ -828,10 +827,9 @@ void add_feature(Engine *, const FeatP &f, int mode, int rep, const uvio_hp_opti
   // a global landmark's anchor clone may have been marginalized (change_anchors only re-anchors relative
   // representations, UpdaterSLAM.cpp:481-500) and get_feature_jacobian_full never reads it for a global
   // representation (UpdaterHelper.cpp:226-262): slot 0 is a placeholder the kernel does not use
-  auto anc = slot_of_time.find(anchor_time);
-  if (anc == slot_of_time.end() && (rel || !landmark))
-    throw HpError(UVIO_HP_E_STATE, "feature anchor clone is not in the window");
-  F.anchor_slot = (anc == slot_of_time.end()) ? 0 : anc->second;
+  const int anc = slot_of_time.find(anchor_time);
+  if (anc < 0 && (rel || !landmark)) throw HpError(UVIO_HP_E_STATE, "feature anchor clone is not in the window");
+  F.anchor_slot = (anc < 0) ? 0 : anc;
   int loc = 0;
   std::vector<int> clone_loc(clones.size(), -1);  // slot -> local col
   int ext_loc[UVIO_HP_MAX_CAMS], intr_loc[UVIO_HP_MAX_CAMS];
