@@ -373,17 +373,22 @@ const std::vector<int> &Tracker::subsets(int count) {
 void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const *imgs, const int *strides,
                    const uint8_t *const *masks, bool device_imgs, const DbSink &db,
                    std::function<void()> in_flight) {
-  {
+  if (histogram_method_ == 2)
+    throw HpError(UVIO_HP_E_CONFIG, "histogram_method 2 (CLAHE) is not implemented by the KLT front-end");
+  if (ncam > kMaxCams) throw HpError(UVIO_HP_E_ARG, "too many cameras in one feed");
+  // The predetection (worker thread, detection stream) reads only the last frame's pyramids, points, ids and masks.
+  // When every camera of this feed already has its state (no insertion into cs_ while the worker reads it), this
+  // frame's pyramids -- the other slot -- are launched first and built while the host joins the worker.
+  bool early_pyr = true;
+  for (int k = 0; k < ncam; k++)
+    if (cs_.find(cam_ids[k]) == cs_.end()) early_pyr = false;
+  if (!early_pyr) {
     HostProfScope hs(*hp_, "trk.join");
     predetect_join();
   }
   in_flight_ = std::move(in_flight);
   device_syncs = 0;
   sync_wait = 0.0;
-  if (pre_.valid && pre_.cams != std::vector<int>(cam_ids, cam_ids + ncam)) discard_predetect();
-  if (histogram_method_ == 2)
-    throw HpError(UVIO_HP_E_CONFIG, "histogram_method 2 (CLAHE) is not implemented by the KLT front-end");
-  if (ncam > kMaxCams) throw HpError(UVIO_HP_E_ARG, "too many cameras in one feed");
   PyrJob job{};
   job.ncam = ncam;
   job.equalize = histogram_method_ == 1;
@@ -452,6 +457,12 @@ void Tracker::feed(double t, int ncam, const int *cam_ids, const uint8_t *const 
     HP_HIP(hipEventRecord(ev_pyr_, s_));
     if (kp_) kp_->credit(KC_PYR, 0.0, pyramid_bytes(job));
   };
+  if (early_pyr) {
+    ensure_pyr();
+    HostProfScope hs(*hp_, "trk.join");
+    predetect_join();
+  }
+  if (pre_.valid && pre_.cams != std::vector<int>(cam_ids, cam_ids + ncam)) discard_predetect();
   if (ncam == 2 && use_stereo_) {
     feed_stereo(t, cam_ids[0], cam_ids[1], db);
   } else if (ncam > 2 && use_stereo_) {
