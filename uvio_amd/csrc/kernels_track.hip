@@ -539,87 +539,114 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
     }
   }
   __syncthreads();
-  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order)
+  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order of Grider_GRID):
+  // every candidate whose response is above a threshold t, plus the lowest raster indices of those AT t -- t
+  // from a 256-bin response histogram, the raster cut from a bitmap of the tied candidates over the cell (in the
+  // score map's LDS, no longer needed) -- then the <= kmax selected keys sorted on one wavefront.  A handful of
+  // barriers instead of a bitonic sort of every candidate (log2(P) (log2(P) + 1) / 2 barrier passes).
   const int n = min(ncand, kFastMaxCand);
-  unsigned *ckey = (unsigned *)cand_s;
-  for (int a = threadIdx.x; a < n; a += blockDim.x) ckey[a] = ((unsigned)(255 - cand_s[a]) << 16) | (unsigned)cand_idx[a];
-  int P = 1;
-  while (P < n) P <<= 1;
-  if (n > 0 && P <= kFastMaxCand) {
-    // a bitonic sort of the keys padded to a power of two (the padding sorts last): log2(P) (log2(P) + 1) / 2
-    // barrier-separated compare-exchange passes instead of kmax sequential min rounds; the keys are unique,
-    // so the first kmax are the selection's exactly
-    for (int a = n + threadIdx.x; a < P; a += blockDim.x) ckey[a] = 0xFFFFFFFFu;
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = threadIdx.x; i < P; i += blockDim.x) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const unsigned a0 = ckey[i], b0 = ckey[ixj];
-            if ((a0 > b0) == ((i & k) == 0)) {
-              ckey[i] = b0;
-              ckey[ixj] = a0;
-            }
-          }
+  const int m = min(n, kmax);
+  __shared__ int hist[256];
+  __shared__ int s_t, s_above, s_cut, s_nsel;
+  __shared__ unsigned sel[kFastMaxK];
+  unsigned *bm = reinterpret_cast<unsigned *>(score);
+  const int nwords = (area + 31) >> 5;
+  for (int a = threadIdx.x; a < 256; a += blockDim.x) hist[a] = 0;
+  for (int a = threadIdx.x; a < nwords; a += blockDim.x) bm[a] = 0u;
+  if (threadIdx.x == 0) s_cut = -1, s_nsel = 0;
+  __syncthreads();
+  for (int a = threadIdx.x; a < n; a += blockDim.x) atomicAdd(&hist[cand_s[a]], 1);
+  __syncthreads();
+  const int wid = threadIdx.x >> 6;
+  if (wid == 0) {
+    // t = the largest response with count(response >= t) >= m; above = count(response > t).  Lane l holds
+    // bins 255 - 4l .. 252 - 4l; an inclusive prefix over lanes walks the responses downward.
+    int cnt4[4], tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      cnt4[q] = hist[255 - 4 * lane - q];
+      tot += cnt4[q];
+    }
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    int cum = incl - tot;
+    if (m > 0 && cum < m && incl >= m) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (cum + cnt4[q] >= m) {
+          s_t = 255 - 4 * lane - q;
+          s_above = cum;
+          break;
         }
-        __syncthreads();
+        cum += cnt4[q];
       }
-    for (int r = threadIdx.x; r < min(n, kmax); r += blockDim.x) {
-      const unsigned key = ckey[r];
+    }
+  }
+  __syncthreads();
+  const int t = m > 0 ? s_t : 256, need = m > 0 ? m - s_above : 0;  // tied candidates to take (>= 1 when m > 0)
+  for (int a = threadIdx.x; a < n; a += blockDim.x)
+    if (cand_s[a] == t) atomicOr(&bm[cand_idx[a] >> 5], 1u << (cand_idx[a] & 31));
+  __syncthreads();
+  if (wid == 0 && need > 0) {
+    // raster index of the need-th tied candidate: per-lane word ranges, popcount prefix over lanes
+    const int per = (nwords + 63) / 64, q0 = lane * per, q1 = min(nwords, q0 + per);
+    int cnt = 0;
+    for (int q = q0; q < q1; q++) cnt += __popc(bm[q]);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int excl = incl - cnt;
+    if (excl < need && incl >= need) {
+      int r = need - excl;
+      for (int q = q0; q < q1; q++) {
+        unsigned x = bm[q];
+        const int pc = __popc(x);
+        if (r <= pc) {
+          for (; r > 1; r--) x &= x - 1u;
+          s_cut = q * 32 + __ffs(x) - 1;
+          break;
+        }
+        r -= pc;
+      }
+    }
+  }
+  __syncthreads();
+  const int cut = s_cut;
+  for (int a = threadIdx.x; a < n; a += blockDim.x) {
+    const int sc = cand_s[a], ia = cand_idx[a];
+    if (sc > t || (sc == t && ia <= cut)) {
+      const int slot = atomicAdd(&s_nsel, 1);
+      if (slot < kFastMaxK) sel[slot] = ((unsigned)(255 - sc) << 16) | (unsigned)ia;
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    // bitonic sort of the <= 64 selected keys across the wavefront's lanes (padding sorts last)
+    unsigned key = lane < min(s_nsel, kFastMaxK) ? sel[lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const unsigned other = (unsigned)__shfl_xor((int)key, j, 64);
+        const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+        key = keep_min ? min(key, other) : max(key, other);
+      }
+    if (lane < m) {
       const int ia = (int)(key & 0xFFFFu);
-      float *o = out + ((size_t)c * kmax + r) * 3;
+      float *o = out + ((size_t)c * kmax + lane) * 3;
       o[0] = (float)(x0 + ia % sw);
       o[1] = (float)(y0 + ia / sw);
       o[2] = (float)(255 - (int)(key >> 16));
     }
-    if (threadIdx.x == 0) out_n[c] = min(n, kmax);
-    return;
+    if (lane == 0) out_n[c] = m;
   }
-  // (more candidates than the padded sort fits) kmax rounds of a wavefront min over each wave's strided
-  // share of the candidates, then the same over the waves' winners on wave 0
-  __shared__ unsigned wtop[(kFastThreads / 64) * kFastMaxK];
-  const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  __syncthreads();
-  for (int r = 0; r < kmax; r++) {
-    unsigned m = 0xFFFFFFFFu;
-    int at = -1;
-    for (int a = wid * 64 + lane; a < n; a += blockDim.x)
-      if (ckey[a] < m) {
-        m = ckey[a];
-        at = a;
-      }
-    unsigned wm = m;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wm = min(wm, (unsigned)__shfl_xor((int)wm, o, 64));
-    if (at >= 0 && m == wm) ckey[at] = 0xFFFFFFFFu;
-    if (lane == 0) wtop[wid * kmax + r] = wm;
-  }
-  __syncthreads();
-  if (wid == 0) {
-    const int nt = nw * kmax;
-    for (int r = 0; r < kmax; r++) {
-      unsigned m = 0xFFFFFFFFu;
-      int at = -1;
-      for (int a = lane; a < nt; a += 64)
-        if (wtop[a] < m) {
-          m = wtop[a];
-          at = a;
-        }
-      unsigned wm = m;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) wm = min(wm, (unsigned)__shfl_xor((int)wm, o, 64));
-      if (at >= 0 && m == wm) wtop[at] = 0xFFFFFFFFu;
-      if (lane == 0 && wm != 0xFFFFFFFFu) {
-        const int ia = (int)(wm & 0xFFFFu);
-        float *o = out + ((size_t)c * kmax + r) * 3;
-        o[0] = (float)(x0 + ia % sw);
-        o[1] = (float)(y0 + ia / sw);
-        o[2] = (float)(255 - (int)(wm >> 16));
-      }
-    }
-  }
-  if (threadIdx.x == 0) out_n[c] = min(n, kmax);
 }
 
 // ---------------------------------------------------------------- cornerSubPix
