@@ -374,6 +374,18 @@ int uvio_hp_compress(const double *A, int m, int n, double *R_out);
  * points whose float could depend on the last bit of tan are recomputed on the host (ambiguous[i] = 1,
  * may be null), so uvn equals the host libm result for every point. */
 int uvio_hp_undistort(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *ambiguous);
+/* Grider_GRID.h:128 (std::sort(pts_new, Grider_FAST::compare_response)) as the device's FAST cell selection
+ * runs it, on caller-given cells: cell c's responses resp[off[c] .. off[c+1]) in cv::FAST's raster order.
+ * arrangement (off[ncell] ints) receives each cell's raster indices as libstdc++'s introsort loop leaves them
+ * (std::sort's result is their stable order by response); for kmax in 1..64 top (ncell * kmax ints) receives the
+ * first min(n, kmax) raster indices of the sorted cell (unused slots untouched).  depth < 0: the reference's
+ * 2 lg n depth limit; 0 forces the heap-sort fallback (std::partial_sort(first, last, last)).  kmax 0: the whole
+ * cell is arranged. */
+int uvio_hp_debug_grid_order(const uint8_t *resp, const int *off, int ncell, int kmax, int depth, int *arrangement,
+                             int *top);
+/* the tracker's FAST cells since the handle was created and how many of them had more than 16 candidates
+ * (the cells where std::sort's introsort order, not a stable one, decides the selection) */
+int uvio_hp_debug_grid_stats(uvio_hp_t *h, uint64_t *cells, uint64_t *introsort_cells);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,7 @@ def load():
         lib.orc_scharr.argtypes = [u8, i32, i32, i16]
         lib.orc_pyramid_levels.argtypes = [i32, i32, i32, i32]
         lib.orc_fast.argtypes = [u8, i32, i32, i32, i32, i32, i32, i32, f32, i32, C.POINTER(C.c_int)]
+        lib.orc_grid_order.argtypes = [f32, i32, i32, C.POINTER(C.c_int)]
         lib.orc_corner_subpix.argtypes = [u8, i32, i32, f32, i32, i32, i32, C.c_double]
         lib.orc_lk.argtypes = [u8, u8, i32, i32, i32, i32, i32, C.c_float, f32, f32, u8, i32]
         lib.orc_ransac_mask.argtypes = [f32, f32, f32, f32, i32, C.c_double, C.c_double, i32, u8]
@@ -354,6 +355,17 @@ def fast(img, thr, roi=None):
     rc = load().orc_fast(_u8(img), w, h, x0, y0, rw, rh, thr, _f32(out), cap, C.byref(n))
     assert rc == 0
     return out[:n.value]
+
+
+def grid_order(resp, mode=0):
+    """Grider_GRID.h:128 on one cell's cv::FAST responses (raster order): the raster indices in the order
+    std::sort(compare_response) leaves them (mode 0), std::stable_sort (1) or std::partial_sort over the
+    whole range (2, introsort's heap-sort fallback)."""
+    r = np.ascontiguousarray(resp, dtype=np.float32).ravel()
+    out = np.zeros(r.size, dtype=np.int32)
+    rc = load().orc_grid_order(_f32(r), r.size, mode, out.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc == 0
+    return out
 
 
 def corner_subpix(img, pts, win=5, max_iters=20, eps=1e-3):

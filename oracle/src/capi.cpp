@@ -465,6 +465,24 @@ int orc_fast(const uint8_t *src, int w, int h, int x0, int y0, int rw, int rh, i
   }
   return (int)kp.size() <= cap ? 0 : UVIO_HP_E_CAPACITY;
 }
+// Grider_GRID.h:128 on one cell: n responses in cv::FAST's raster order -> order[i] = the raster index of the
+// i-th keypoint after std::sort(compare_response) (mode 0, the reference), std::stable_sort (mode 1, the tie
+// order rounds 1-5 used) or std::partial_sort(first, last, last) (mode 2, introsort's depth-limit heap path).
+int orc_grid_order(const float *resp, int n, int mode, int *order) {
+  std::vector<KeyPt> kp(n);
+  for (int i = 0; i < n; i++) kp[i] = KeyPt{(float)i, 0.f, resp[i]};
+  auto cmp = [](const KeyPt &a, const KeyPt &b) { return a.response > b.response; };
+  if (mode == 0)
+    grid_sort(kp);
+  else if (mode == 1)
+    std::stable_sort(kp.begin(), kp.end(), cmp);
+  else if (mode == 2)
+    std::partial_sort(kp.begin(), kp.end(), kp.end(), cmp);
+  else
+    return UVIO_HP_E_ARG;
+  for (int i = 0; i < n; i++) order[i] = (int)kp[i].x;
+  return 0;
+}
 // cornerSubPix in place on n points (x, y)
 int orc_corner_subpix(const uint8_t *src, int w, int h, float *pts, int n, int win, int max_iters, double eps) {
   std::vector<KeyPt> kp(n);

@@ -264,6 +264,13 @@ std::vector<KeyPt> fast_roi(const GrayImg &img, int x0, int y0, int w, int h, in
   return kp;
 }
 
+// ---- Grider_GRID.h:128: std::sort(pts_new, Grider_FAST::compare_response) ----
+// libstdc++'s own std::sort on the cv::FAST sequence (raster order): the permutation of equal responses is
+// the reference's (see tracker.h).
+void grid_sort(std::vector<KeyPt> &kp) {
+  std::sort(kp.begin(), kp.end(), [](const KeyPt &a, const KeyPt &b) { return a.response > b.response; });
+}
+
 // ---- cornerSubPix (cornersubpix.cpp) over getRectSubPix (u8 -> float, replicated border) ----
 static void rect_subpix(const GrayImg &img, int ww, int hh, float cx, float cy, float *dst) {
   cx -= (ww - 1) * 0.5f;

@@ -7,10 +7,19 @@
 //     equalizeHist, buildOpticalFlowPyramid (pyrDown + Scharr), FAST-9 (+NMS), cornerSubPix,
 //     calcOpticalFlowPyrLK, findFundamentalMat(FM_RANSAC) with cv::RNG((uint64)-1).
 // Parity of this front-end against OpenCV itself is unpinned (no OpenCV here); the product's GPU
-// kernels are checked against this restatement.  Where OpenCV's result depends on an
-// implementation detail that is not observable (std::sort tie order of equal FAST responses, the
-// float vs int accumulation of LK sums), this file fixes one deterministic choice and the device
-// follows the same choice: equal responses keep raster order; LK sums are exact integers.
+// kernels are checked against this restatement.
+//   * Equal FAST responses: Grider_GRID.h:128 sorts each cell's cv::FAST output (raster order, fast.cpp
+//     pushes row by row, x ascending) with std::sort and the response-only Grider_FAST::compare_response.
+//     std::sort is not stable, and its tie order IS observable (it decides which corners a cell keeps and
+//     so every ++currid of TrackKLT.cpp:483-520): grid_sort calls libstdc++'s std::sort itself on the same
+//     sequence (introsort, _S_threshold 16, median-of-three, unguarded partition, heap-sort fallback at
+//     depth 2 lg n; the same algorithm in the GCC 7-13 libstdc++ the reference's ROS distributions ship).
+//     Rounds 1-5 used the stable order here and on the device; that was not the reference's.
+//   * LK window sums: OpenCV's calcOpticalFlowPyrLK (lkpyramid.cpp) accumulates the iteration's b-vector
+//     (ib1, ib2) in float and the products come from CV_DESCALE'd integers.  This restatement takes the
+//     sums as exact integers; the two agree whenever every partial float sum is exactly representable
+//     (|sum| < 2^24), which a 15x15 window of 8-bit/Scharr products can exceed.  Not checkable here
+//     (OpenCV is absent): this choice is unpinned, and the device follows it.
 #pragma once
 #include <functional>
 #include <cstdint>
@@ -47,6 +56,8 @@ std::vector<int16_t> scharr_deriv(const GrayImg &s);
 Pyramid build_pyramid(const GrayImg &img, int win, int max_level);
 // cv::FAST(img(roi), thr, nonmax) — keypoints in ROI coordinates, raster order
 std::vector<KeyPt> fast_roi(const GrayImg &img, int x0, int y0, int w, int h, int thr);
+// std::sort(kp, Grider_FAST::compare_response) (Grider_GRID.h:128, Grider_FAST.h compare_response)
+void grid_sort(std::vector<KeyPt> &kp);
 // cv::cornerSubPix(win 5x5, zeroZone -1, 20 iterations, eps 1e-3)
 void corner_subpix(const GrayImg &img, std::vector<KeyPt> &pts, int win, int max_iters, double eps);
 // cv::calcOpticalFlowPyrLK(win, maxLevel, COUNT|EPS 30 / 0.01, OPTFLOW_USE_INITIAL_FLOW, minEig 1e-4)

@@ -46,7 +46,7 @@ void TrackKLT::perform_griding(const GrayImg &img, const GrayImg &mask, const st
     int x = g.first * size_x, y = g.second * size_y;
     if (x + size_x > img.w || y + size_y > img.h) continue;
     std::vector<KeyPt> kp = fast_roi(img, x, y, size_x, size_y, threshold);
-    std::stable_sort(kp.begin(), kp.end(), [](const KeyPt &a, const KeyPt &b) { return a.response > b.response; });
+    grid_sort(kp);
     for (size_t i = 0; i < (size_t)num_features_grid && i < kp.size(); i++) {
       KeyPt p = kp[i];
       p.x += (float)x;

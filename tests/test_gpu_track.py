@@ -86,6 +86,8 @@ def test_tracks_bit_exact(euroc_yaml, stereo):
         n, b = _compare_tracks(g, o, [0, 1])
         total += n
         bad += b
+    cells, intro = g.grid_stats()
+    print("FAST cells %d, on std::sort's introsort path (> 16 candidates) %d" % (cells, intro))
     assert total > 25 * 2 * 50  # the scene keeps the tracker busy
     assert bad == 0, (bad, total)
 
@@ -121,6 +123,8 @@ def test_tracks_bit_exact_four_cameras():
         bad += b
         for c in cams:
             per_cam[c] += len(o.get_tracks(c)[0])
+    cells, intro = g.grid_stats()
+    print("FAST cells %d, on std::sort's introsort path (> 16 candidates) %d" % (cells, intro))
     assert np.all(per_cam > n * 40), per_cam  # every camera keeps tracks
     assert bad == 0, (bad, total)
 

@@ -151,6 +151,8 @@ SIGNATURES = [
     ("shard_init_rccl", _I, [C.c_void_p, _I, _I, _P(C.c_uint8), _I]),
     ("shard_init_host", _I, [C.c_void_p, _I, _I, C.c_void_p, C.c_void_p, _I]),
     ("shard_partition", _I, [_P(_I), _I, _I, _P(_I)]),
+    ("debug_grid_order", _I, [_P(C.c_uint8), _P(_I), _I, _I, _I, _P(_I), _P(_I)]),
+    ("debug_grid_stats", _I, [C.c_void_p, _P(C.c_uint64), _P(C.c_uint64)]),
 ]
 
 # uvio_hp_allreduce_fn: int (*)(double *buf, size_t count, void *user)

@@ -388,4 +388,25 @@ int uvio_hp_undistort(int model, const double cam[8], int n, const float *uv, fl
   }
 }
 
+int uvio_hp_debug_grid_order(const uint8_t *resp, const int *off, int ncell, int kmax, int depth, int *arrangement,
+                             int *top) {
+  try {
+    return Engine::grid_order_standalone(resp, off, ncell, kmax, depth, arrangement, top);
+  } catch (const HpError &ex) {
+    return ex.code;
+  } catch (...) {
+    return UVIO_HP_E_DEVICE;
+  }
+}
+
+int uvio_hp_debug_grid_stats(uvio_hp_t *h, uint64_t *cells, uint64_t *introsort_cells) {
+  if (!h) return UVIO_HP_E_ARG;
+  unsigned long long c = 0;
+  unsigned long long i = 0;
+  HP_GUARD(h, if (h->e->tracker()) h->e->tracker()->grid_stats(&c, &i);)
+  if (cells) *cells = c;
+  if (introsort_cells) *introsort_cells = i;
+  return 0;
+}
+
 }  // extern "C"

@@ -454,6 +454,8 @@ class Engine {
                                    double sigma2, double *dx_out, bool compress = false);
   static int compress_standalone(const double *A, int m, int n, double *R_out);
   static int undistort_standalone(int model, const double cam[8], int n, const float *uv, float *uvn, uint8_t *amb);
+  static int grid_order_standalone(const uint8_t *resp, const int *off, int ncell, int kmax, int depth,
+                                   int *arrangement, int *top);
 
  private:
   uvio_hp_options_t o_;

@@ -943,4 +943,43 @@ int Engine::undistort_standalone(int model, const double cam[8], int n, const fl
   return 0;
 }
 
+int Engine::grid_order_standalone(const uint8_t *resp, const int *off, int ncell, int kmax, int depth,
+                                  int *arrangement, int *top) {
+  if (ncell < 0 || !off || kmax < 0 || kmax > 64 || (kmax > 0 && !top)) return UVIO_HP_E_ARG;
+  if (ncell == 0) return 0;
+  int nmax = 0;
+  for (int c = 0; c < ncell; c++) {
+    if (off[c + 1] < off[c]) return UVIO_HP_E_ARG;
+    nmax = std::max(nmax, off[c + 1] - off[c]);
+  }
+  const int total = off[ncell];
+  if (total > 0 && (!resp || !arrangement)) return UVIO_HP_E_ARG;
+  if (nmax > 16384) return UVIO_HP_E_CAPACITY;  // 8 bytes of LDS per candidate
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return UVIO_HP_E_DEVICE;
+  hipStream_t s;
+  HP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  uint8_t *d_resp = nullptr;
+  int *d_off = nullptr, *d_arr = nullptr, *d_top = nullptr;
+  const size_t ntop = (size_t)ncell * (size_t)std::max(kmax, 1);
+  HP_HIP(hipMalloc(&d_resp, std::max(total, 1)));
+  HP_HIP(hipMalloc(&d_off, sizeof(int) * (size_t)(ncell + 1)));
+  HP_HIP(hipMalloc(&d_arr, sizeof(int) * (size_t)std::max(total, 1)));
+  HP_HIP(hipMalloc(&d_top, sizeof(int) * ntop));
+  if (total > 0) HP_HIP(hipMemcpyAsync(d_resp, resp, (size_t)total, hipMemcpyHostToDevice, s));
+  HP_HIP(hipMemcpyAsync(d_off, off, sizeof(int) * (size_t)(ncell + 1), hipMemcpyHostToDevice, s));
+  if (kmax > 0) HP_HIP(hipMemcpyAsync(d_top, top, sizeof(int) * ntop, hipMemcpyHostToDevice, s));
+  launch_grid_order_probe(s, d_resp, d_off, ncell, nmax, kmax, depth, d_arr, d_top);
+  HP_HIP(hipGetLastError());
+  if (total > 0) HP_HIP(hipMemcpyAsync(arrangement, d_arr, sizeof(int) * (size_t)total, hipMemcpyDeviceToHost, s));
+  if (kmax > 0) HP_HIP(hipMemcpyAsync(top, d_top, sizeof(int) * ntop, hipMemcpyDeviceToHost, s));
+  HP_HIP(hipStreamSynchronize(s));
+  hipFree(d_resp);
+  hipFree(d_off);
+  hipFree(d_arr);
+  hipFree(d_top);
+  hipStreamDestroy(s);
+  return 0;
+}
+
 }  // namespace uvhp

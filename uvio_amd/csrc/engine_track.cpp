@@ -157,6 +157,8 @@ Tracker::Tracker(const uvio_hp_options_t &o, const CamParams *cams, hipStream_t 
   ensure_cap(std::max(1024, 8 * num_features_));
   HP_HIP(hipMalloc(&d_lk_bytes_, sizeof(unsigned long long)));
   HP_HIP(hipMemsetAsync(d_lk_bytes_, 0, sizeof(unsigned long long), s_));
+  HP_HIP(hipMalloc(&d_sort_stats_, sizeof(int)));
+  HP_HIP(hipMemsetAsync(d_sort_stats_, 0, sizeof(int), s_));
 }
 
 void Tracker::set_num_features(int n) {
@@ -187,6 +189,16 @@ unsigned long long Tracker::lk_bytes() {
   return v;
 }
 
+void Tracker::grid_stats(unsigned long long *cells, unsigned long long *introsort_cells) {
+  predetect_join();
+  if (sd_) HP_HIP(hipStreamSynchronize(sd_));
+  int v = 0;
+  HP_HIP(hipMemcpyAsync(&v, d_sort_stats_, sizeof(v), hipMemcpyDeviceToHost, s_));
+  HP_HIP(hipStreamSynchronize(s_));
+  if (cells) *cells = grid_cells_;
+  if (introsort_cells) *introsort_cells = (unsigned long long)v;
+}
+
 Tracker::~Tracker() {
   if (worker_.joinable()) {
     {
@@ -206,6 +218,7 @@ Tracker::~Tracker() {
     if (kv.second.d_score) (void)hipFree(kv.second.d_score);
   }
   if (d_lk_bytes_) (void)hipFree(d_lk_bytes_);
+  if (d_sort_stats_) (void)hipFree(d_sort_stats_);
   if (ev_match_) (void)hipEventDestroy(ev_match_);
   if (ev_up_) (void)hipEventDestroy(ev_up_);
   if (up_) (void)hipStreamDestroy(up_);
@@ -531,7 +544,8 @@ void Tracker::griding_multi(GridReq *reqs, int nr, const DPyr *lk_to, std::vecto
   upload(b.cells, b.hp(b.cells), 2 * nc * sizeof(int));
   {
     KScope ks(kcur(), KC_FAST);
-    launch_fast_multi(cur_, fj, b.cells, threshold_, nfg, b.fast, b.fastn);
+    launch_fast_multi(cur_, fj, b.cells, threshold_, nfg, b.fast, b.fastn, d_sort_stats_);
+    grid_cells_ += (unsigned long long)nc;
   }
   // algorithmic bytes: each cell's pixels read by the score pass, its score map written and read by the selection
   if (kcur()) {

@@ -336,7 +336,13 @@ struct FastJob {
   int w[kMaxCams], sw[kMaxCams], sh[kMaxCams], cell_end[kMaxCams];
   int ncam;
 };
-void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n);
+// sort_stats (optional, device): [0] += cells whose candidates took std::sort's introsort path (> 16 candidates)
+void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n,
+                       int *sort_stats = nullptr);
+// Test probe of the Grider_GRID.h:128 std::sort emulation: per cell (responses resp[off[c] .. off[c+1]) in raster
+// order) the arrangement after the introsort loop and, for kmax > 0, the top-min(n, kmax) raster indices in order
+void launch_grid_order_probe(hipStream_t s, const uint8_t *resp, const int *off, int ncell, int nmax, int kmax,
+                             int depth, int *arrangement, int *top);
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
                        int kmax, float *out, int *out_n, uint8_t *score_map);
 // cornerSubPix in place on the points (x, y) of up to kMaxCams images: points [end[k-1], end[k]) lie in img[k]

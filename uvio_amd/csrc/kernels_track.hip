@@ -4,7 +4,7 @@
 //   k_hist_multi + k_pyr_pair  equalizeHist (LDS histogram, LUT per workgroup from the global counts),
 //                            pyrDown 5x5 (sum + 128) >> 8 and Scharr dx/dy int16 (calcSharrDeriv), reflect-101,
 //                            two pyramid levels per launch
-//   k_fast_cells             FAST-9 + 3x3 NMS + top-k per grid cell (one workgroup per valid cell)
+//   k_fast_score/_select     FAST-9 + 3x3 NMS + top-k per grid cell in std::sort's tie order (one workgroup per cell)
 //   k_subpix<WIN>            cornerSubPix, one wavefront per point (five raster-order sums, one lane each = oracle
 //                            order; window size a template constant)
 //   k_lk                     pyramidal LK, one wavefront per point, exact integer window sums
@@ -471,17 +471,165 @@ __global__ void __launch_bounds__(256) k_fast_score(FastJob job, const int *__re
   }
 }
 
-// Phase 2: one workgroup per cell stages the cell's scores in LDS, keeps strict 3x3 maxima and
-// writes the top kmax by (response desc, raster asc) — the stable sort of Grider_GRID — as
-// (x, y, response) in image coordinates.  Strict NMS leaves no two adjacent survivors, so a cell
-// has at most ceil(sw/2) ceil(sh/2) candidates.
-constexpr int kFastThreads = 1024, kFastMaxK = 64;
+// ---- Grider_GRID.h:128 std::sort(pts_new, Grider_FAST::compare_response), emulated ----
+// A cell's cv::FAST keypoints come in raster order (fast.cpp pushes row by row, x ascending) and are sorted by
+// response only, with libstdc++'s introsort (stl_algo.h: __introsort_loop with _S_threshold 16,
+// __unguarded_partition_pivot's median of three moved to the front, recursion on the right part, heap sort
+// (__partial_sort) once 2 lg n levels are used up, then __final_insertion_sort).  std::sort is not stable: its
+// tie order is observable in which corners a cell keeps and in the order they get ids (TrackKLT.cpp:483-520).
+// The final insertion sort moves an element only past strictly smaller responses, so the sorted order is the
+// STABLE order of the arrangement the introsort loop leaves; the device reproduces that arrangement and then
+// selects by (response desc, arrangement position asc).  Candidates are packed as raster index | response << 16.
+__device__ __forceinline__ int cand_resp(int v) { return v >> 16; }
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// std::__adjust_heap + std::__push_heap (stl_heap.h) with comp(x, y) = resp(x) > resp(y); one lane.
+__device__ void heap_adjust(int *a, int hole, int len, int v) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (cand_resp(a[second]) > cand_resp(a[second - 1])) second--;
+    a[hole] = a[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    a[hole] = a[second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && cand_resp(a[parent]) > cand_resp(v)) {
+    a[hole] = a[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  a[hole] = v;
+}
+// std::__partial_sort(first, last, last) = __make_heap + __sort_heap: introsort's depth-limit fallback; one lane
+// (rare: it needs 2 lg n unbalanced partitions in a row).
+__device__ void heap_sort_seg(int *a, int len) {
+  if (len >= 2)
+    for (int parent = (len - 2) / 2;; parent--) {
+      heap_adjust(a, parent, len, a[parent]);
+      if (parent == 0) break;
+    }
+  for (int last = len; last > 1;) {
+    --last;
+    const int v = a[last];
+    a[last] = a[0];
+    heap_adjust(a, 0, last, v);
+  }
+}
+
+// __introsort_loop over arr[0, n) on ONE wavefront (every lane calls it; control is uniform).  One partition
+// step __unguarded_partition(first + 1, last, first) is computed in parallel: its left scan stops at the
+// positions L_1 < L_2 < ... holding response <= p, its right scan at R_1 > R_2 > ... holding response >= p
+// (p the pivot's response).  Before the scans cross they only pass unmodified positions, so the k-th swap
+// exchanges L_k and R_k for every k with L_k < R_k (a monotone condition), K swaps in all, and the cut is
+// min(L_{K+1}, R_K) (R_K holds L_K's element after the swap, where the left scan stops when no L lies
+// between).  The positions come from ballot prefix counts (pl ascending, pr ascending: R_k = pr[cr - k]).
+// Segments whose responses are all below t (the cell's k-th largest) are not refined: their order never
+// reaches the selection.  depth < 0: 2 lg n, the reference's limit.
+__device__ void grid_introsort(int *arr, int n, int t, int depth, unsigned short *pl, unsigned short *pr, int *stk,
+                               int lane) {
+  if (n <= 16) return;
+  if (depth < 0) depth = 2 * (31 - __clz(n));
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  if (lane == 0) stk[0] = 0, stk[1] = n, stk[2] = depth, stk[3] = 255;
+  int sp = 1;
+  wave_lds_sync();
+  while (sp > 0) {
+    sp--;
+    int f = uni(stk[4 * sp]), l = uni(stk[4 * sp + 1]), d = uni(stk[4 * sp + 2]);
+    const int ub = uni(stk[4 * sp + 3]);
+    wave_lds_sync();
+    while (l - f > 16 && ub >= t) {
+      if (d == 0) {
+        if (lane == 0) heap_sort_seg(arr + f, l - f);
+        wave_lds_sync();
+        break;
+      }
+      d--;
+      // __move_median_to_first(first, first + 1, mid, last - 1)
+      const int mid = f + (l - f) / 2;
+      const int ra = uni(cand_resp(arr[f + 1])), rb = uni(cand_resp(arr[mid])), rc = uni(cand_resp(arr[l - 1]));
+      int m;
+      if (ra > rb)
+        m = rb > rc ? mid : (ra > rc ? l - 1 : f + 1);
+      else if (ra > rc)
+        m = f + 1;
+      else if (rb > rc)
+        m = l - 1;
+      else
+        m = mid;
+      const int vf = uni(arr[f]), vm = uni(arr[m]);
+      const int p = cand_resp(vm);
+      wave_lds_sync();
+      if (lane == 0) arr[f] = vm, arr[m] = vf;
+      wave_lds_sync();
+      // scan stops of [f + 1, l)
+      int cl = 0, cr = 0;
+      for (int b = f + 1; b < l; b += 64) {
+        const int i = b + lane;
+        const int r = i < l ? cand_resp(arr[i]) : 0;
+        const bool isl = i < l && r <= p, isr = i < l && r >= p;
+        const unsigned long long bl = __ballot(isl), br = __ballot(isr);
+        if (isl) pl[cl + __popcll(bl & lt)] = (unsigned short)i;
+        if (isr) pr[cr + __popcll(br & lt)] = (unsigned short)i;
+        cl += __popcll(bl);
+        cr += __popcll(br);
+      }
+      wave_lds_sync();
+      const int mn = min(cl, cr);
+      int K = 0;
+      for (int k0 = 0; k0 < mn; k0 += 64) {
+        const int k = k0 + lane;
+        const unsigned long long b = __ballot(k < mn && pl[k] < pr[cr - 1 - k]);
+        K += __popcll(b);
+        if (b != ~0ull) break;
+      }
+      const int cut = min(K < cl ? uni(pl[K < cl ? K : 0]) : l, K > 0 ? uni(pr[K > 0 ? cr - K : 0]) : l);
+      for (int k0 = 0; k0 < K; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < K) {
+          const int a = pl[k], c = pr[cr - 1 - k];
+          const int va = arr[a], vc = arr[c];
+          arr[a] = vc;
+          arr[c] = va;
+        }
+      }
+      // the right part [cut, l) holds responses <= p; the left part [f, cut) continues here
+      if (l - cut > 16 && p >= t) {
+        if (lane == 0) stk[4 * sp] = cut, stk[4 * sp + 1] = l, stk[4 * sp + 2] = d, stk[4 * sp + 3] = p;
+        sp++;
+      }
+      wave_lds_sync();
+      l = cut;
+    }
+  }
+}
+
+// Phase 2: one workgroup per cell stages the cell's scores in LDS, keeps strict 3x3 maxima, arranges them in
+// raster order (cv::FAST's), runs the introsort emulation above and writes the top kmax by (response desc,
+// arrangement position asc) -- Grider_GRID.h:128's std::sort order -- as (x, y, response) in image coordinates.
+// Strict NMS leaves no two adjacent survivors, so a cell has at most ceil(sw/2) ceil(sh/2) candidates.
+constexpr int kFastThreads = 1024, kFastMaxK = 64, kSortStack = 64;
 __host__ __device__ inline int fast_max_cand(int sw, int sh) { return ((sw + 1) / 2) * ((sh + 1) / 2); }
 __host__ __device__ inline size_t fast_lds_bytes(int sw, int sh) {
   return (size_t)fast_max_cand(sw, sh) * 8 + (((size_t)sw * sh + 15) & ~(size_t)15);
 }
+__device__ __forceinline__ void fast_select_top(const int *arr, int n, int m, int t, int need, int lane, int wid,
+                                                unsigned *sel, int *s_cut, int *s_nsel);
+// (the selection tail shared with the probe kernel, below)
 __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const int *__restrict__ cells, int kmax,
-                                                              float *__restrict__ out, int *__restrict__ out_n) {
+                                                              float *__restrict__ out, int *__restrict__ out_n,
+                                                              int *__restrict__ sort_stats) {
   extern __shared__ int lds_fast[];
   const int c = blockIdx.x;
   const int cam = fast_cam(job, c);
@@ -489,9 +637,10 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
   const int w = job.w[cam], sw = job.sw[cam], sh = job.sh[cam];
   const int kFastMaxCand = fast_max_cand(sw, sh);
   const int area = sw * sh;
-  int *cand_idx = lds_fast, *cand_s = lds_fast + kFastMaxCand;
-  uint8_t *score = (uint8_t *)(cand_s + kFastMaxCand);
+  int *cand = lds_fast, *arr = lds_fast + kFastMaxCand;
+  uint8_t *score = (uint8_t *)(arr + kFastMaxCand);
   __shared__ int ncand;
+  __shared__ int stk[4 * kSortStack];
   const int x0 = cells[2 * c], y0 = cells[2 * c + 1];
   if (threadIdx.x == 0) ncand = 0;
   // eight loads in flight per thread before their LDS stores (a store right behind its load made one memory
@@ -532,33 +681,49 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
     base = __shfl(base, 0, 64);
     if (keep) {
       const int slot = base + __popcll(bal & ((1ull << lane) - 1ull));
-      if (slot < kFastMaxCand) {
-        cand_idx[slot] = e;
-        cand_s[slot] = sc;
-      }
+      if (slot < kFastMaxCand) cand[slot] = e | (sc << 16);
     }
   }
   __syncthreads();
-  // top kmax by key = (255 - response) << 16 | raster index (unique keys: the stable sort order of Grider_GRID):
-  // every candidate whose response is above a threshold t, plus the lowest raster indices of those AT t -- t
-  // from a 256-bin response histogram, the raster cut from a bitmap of the tied candidates over the cell (in the
-  // score map's LDS, no longer needed) -- then the <= kmax selected keys sorted on one wavefront.  A handful of
-  // barriers instead of a bitonic sort of every candidate (log2(P) (log2(P) + 1) / 2 barrier passes).
   const int n = min(ncand, kFastMaxCand);
   const int m = min(n, kmax);
+  // raster order: a bitmap of the candidates over the cell and its per-word prefix (in the score map's LDS, no
+  // longer needed) place candidate e at #{candidates before e}; the response histogram gives the threshold t
+  // (the m-th largest response) and above = #{response > t}
   __shared__ int hist[256];
   __shared__ int s_t, s_above, s_cut, s_nsel;
   __shared__ unsigned sel[kFastMaxK];
-  unsigned *bm = reinterpret_cast<unsigned *>(score);
   const int nwords = (area + 31) >> 5;
+  unsigned *bm = reinterpret_cast<unsigned *>(score);
+  int *wpre = reinterpret_cast<int *>(bm + nwords);
   for (int a = threadIdx.x; a < 256; a += blockDim.x) hist[a] = 0;
   for (int a = threadIdx.x; a < nwords; a += blockDim.x) bm[a] = 0u;
-  if (threadIdx.x == 0) s_cut = -1, s_nsel = 0;
+  if (threadIdx.x == 0) s_cut = -1, s_nsel = 0, s_t = 256, s_above = 0;
   __syncthreads();
-  for (int a = threadIdx.x; a < n; a += blockDim.x) atomicAdd(&hist[cand_s[a]], 1);
+  for (int a = threadIdx.x; a < n; a += blockDim.x) {
+    const int v = cand[a];
+    atomicOr(&bm[(v & 0xFFFF) >> 5], 1u << (v & 31));
+    atomicAdd(&hist[cand_resp(v)], 1);
+  }
   __syncthreads();
   const int wid = threadIdx.x >> 6;
   if (wid == 0) {
+    // exclusive popcount prefix over the bitmap's words: per-lane word ranges, prefix over lanes
+    const int per = (nwords + 63) / 64, q0 = lane * per, q1 = min(nwords, q0 + per);
+    int cnt = 0;
+    for (int q = q0; q < q1; q++) cnt += __popc(bm[q]);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    int run = incl - cnt;
+    for (int q = q0; q < q1; q++) {
+      wpre[q] = run;
+      run += __popc(bm[q]);
+    }
+  } else if (wid == 1) {
     // t = the largest response with count(response >= t) >= m; above = count(response > t).  Lane l holds
     // bins 255 - 4l .. 252 - 4l; an inclusive prefix over lanes walks the responses downward.
     int cnt4[4], tot = 0;
@@ -587,48 +752,21 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
     }
   }
   __syncthreads();
-  const int t = m > 0 ? s_t : 256, need = m > 0 ? m - s_above : 0;  // tied candidates to take (>= 1 when m > 0)
-  for (int a = threadIdx.x; a < n; a += blockDim.x)
-    if (cand_s[a] == t) atomicOr(&bm[cand_idx[a] >> 5], 1u << (cand_idx[a] & 31));
-  __syncthreads();
-  if (wid == 0 && need > 0) {
-    // raster index of the need-th tied candidate: per-lane word ranges, popcount prefix over lanes
-    const int per = (nwords + 63) / 64, q0 = lane * per, q1 = min(nwords, q0 + per);
-    int cnt = 0;
-    for (int q = q0; q < q1; q++) cnt += __popc(bm[q]);
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
-    }
-    const int excl = incl - cnt;
-    if (excl < need && incl >= need) {
-      int r = need - excl;
-      for (int q = q0; q < q1; q++) {
-        unsigned x = bm[q];
-        const int pc = __popc(x);
-        if (r <= pc) {
-          for (; r > 1; r--) x &= x - 1u;
-          s_cut = q * 32 + __ffs(x) - 1;
-          break;
-        }
-        r -= pc;
-      }
-    }
-  }
-  __syncthreads();
-  const int cut = s_cut;
   for (int a = threadIdx.x; a < n; a += blockDim.x) {
-    const int sc = cand_s[a], ia = cand_idx[a];
-    if (sc > t || (sc == t && ia <= cut)) {
-      const int slot = atomicAdd(&s_nsel, 1);
-      if (slot < kFastMaxK) sel[slot] = ((unsigned)(255 - sc) << 16) | (unsigned)ia;
-    }
+    const int v = cand[a], e = v & 0xFFFF;
+    arr[wpre[e >> 5] + __popc(bm[e >> 5] & ((1u << (e & 31)) - 1u))] = v;
   }
   __syncthreads();
+  const int t = s_t, need = m > 0 ? m - s_above : 0;  // tied candidates to take (>= 1 when m > 0)
+  if (wid == 0 && m > 0) {
+    unsigned short *pl = reinterpret_cast<unsigned short *>(cand), *pr = pl + kFastMaxCand;
+    grid_introsort(arr, n, t, -1, pl, pr, stk, lane);
+    if (sort_stats && lane == 0 && n > 16) atomicAdd(sort_stats, 1);
+  }
+  __syncthreads();
+  fast_select_top(arr, n, m, t, need, lane, wid, sel, &s_cut, &s_nsel);
   if (wid == 0) {
-    // bitonic sort of the <= 64 selected keys across the wavefront's lanes (padding sorts last)
+    // the <= 64 selected keys (255 - response) << 16 | position are sorted across the wavefront's lanes
     unsigned key = lane < min(s_nsel, kFastMaxK) ? sel[lane] : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 2; k <= 64; k <<= 1)
@@ -639,13 +777,102 @@ __global__ void __launch_bounds__(kFastThreads) k_fast_select(FastJob job, const
         key = keep_min ? min(key, other) : max(key, other);
       }
     if (lane < m) {
-      const int ia = (int)(key & 0xFFFFu);
+      const int ia = arr[key & 0xFFFFu] & 0xFFFF;
       float *o = out + ((size_t)c * kmax + lane) * 3;
       o[0] = (float)(x0 + ia % sw);
       o[1] = (float)(y0 + ia / sw);
       o[2] = (float)(255 - (int)(key >> 16));
     }
     if (lane == 0) out_n[c] = m;
+  }
+}
+
+// Every response above t, and the `need` tied ones at the lowest arrangement positions (found by wave 0 with a
+// ballot walk over the arrangement), become keys (255 - response) << 16 | position in sel.  Ends with a barrier.
+__device__ __forceinline__ void fast_select_top(const int *arr, int n, int m, int t, int need, int lane, int wid,
+                                                unsigned *sel, int *s_cut, int *s_nsel) {
+  if (wid == 0 && need > 0) {
+    int seen = 0;
+    for (int b = 0; b < n; b += 64) {
+      const int i = b + lane;
+      const unsigned long long bal = __ballot(i < n && cand_resp(arr[i]) == t);
+      const int pc = __popcll(bal);
+      if (seen + pc >= need) {
+        unsigned long long x = bal;
+        for (int r = need - seen; r > 1; r--) x &= x - 1ull;
+        if (lane == 0) *s_cut = b + __ffsll((long long)x) - 1;
+        break;
+      }
+      seen += pc;
+    }
+  }
+  __syncthreads();
+  const int cut = *s_cut;
+  for (int a = threadIdx.x; a < n; a += blockDim.x) {
+    const int sc = cand_resp(arr[a]);
+    if (sc > t || (sc == t && a <= cut)) {
+      const int slot = atomicAdd(s_nsel, 1);
+      if (slot < kFastMaxK) sel[slot] = ((unsigned)(255 - sc) << 16) | (unsigned)a;
+    }
+  }
+  (void)m;
+  __syncthreads();
+}
+
+// Test probe of the emulation (uvio_hp_debug_grid_order): one workgroup per cell, the cell's responses in raster
+// order; writes the arrangement's raster indices and, for kmax > 0, the cell's top-min(n, kmax) raster indices in
+// the selection's order.  depth < 0: the reference's 2 lg n; depth 0 forces the heap-sort fallback.
+__global__ void __launch_bounds__(kFastThreads) k_grid_order_probe(const uint8_t *__restrict__ resp,
+                                                                   const int *__restrict__ off, int kmax, int depth,
+                                                                   int *__restrict__ arrangement,
+                                                                   int *__restrict__ top) {
+  extern __shared__ int lds_probe[];
+  __shared__ int stk[4 * kSortStack];
+  __shared__ int hist[256];
+  __shared__ int s_t, s_above, s_cut, s_nsel;
+  __shared__ unsigned sel[kFastMaxK];
+  const int c = blockIdx.x, o0 = off[c], n = off[c + 1] - o0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int *arr = lds_probe;
+  unsigned short *pl = reinterpret_cast<unsigned short *>(arr + n), *pr = pl + n;
+  const int m = kmax > 0 ? min(n, kmax) : n;
+  for (int a = threadIdx.x; a < 256; a += blockDim.x) hist[a] = 0;
+  if (threadIdx.x == 0) s_cut = -1, s_nsel = 0, s_t = 256, s_above = 0;
+  __syncthreads();
+  for (int a = threadIdx.x; a < n; a += blockDim.x) {
+    arr[a] = a | ((int)resp[o0 + a] << 16);
+    atomicAdd(&hist[resp[o0 + a]], 1);
+  }
+  __syncthreads();
+  if (wid == 0 && m > 0) {
+    int cum = 0;
+    for (int r = 255; r >= 0; r--) {
+      if (cum + hist[r] >= m) {
+        s_t = r;
+        s_above = cum;
+        break;
+      }
+      cum += hist[r];
+    }
+  }
+  __syncthreads();
+  const int t = kmax > 0 ? s_t : -1, need = m > 0 ? m - s_above : 0;
+  if (wid == 0 && m > 0) grid_introsort(arr, n, t, depth, pl, pr, stk, lane);
+  __syncthreads();
+  for (int a = threadIdx.x; a < n; a += blockDim.x) arrangement[o0 + a] = arr[a] & 0xFFFF;
+  if (kmax <= 0) return;
+  fast_select_top(arr, n, m, s_t, need, lane, wid, sel, &s_cut, &s_nsel);
+  if (wid == 0) {
+    unsigned key = lane < min(s_nsel, kFastMaxK) ? sel[lane] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const unsigned other = (unsigned)__shfl_xor((int)key, j, 64);
+        const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+        key = keep_min ? min(key, other) : max(key, other);
+      }
+    if (lane < m) top[(size_t)c * kmax + lane] = arr[key & 0xFFFFu] & 0xFFFF;
   }
 }
 
@@ -1381,7 +1608,8 @@ __global__ void __launch_bounds__(256) k_ransac_select(RansacSlots job, int max_
 }
 
 // ---------------------------------------------------------------- launch wrappers
-void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n) {
+void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int thr, int kmax, float *out, int *out_n,
+                       int *sort_stats) {
   if (job.ncam <= 0 || job.ncam > kMaxCams) return;
   const int ncell = job.cell_end[job.ncam - 1];
   if (ncell <= 0) return;
@@ -1396,7 +1624,18 @@ void launch_fast_multi(hipStream_t s, const FastJob &job, const int *cells, int 
   if (lds > 64 * 1024 && set_dyn_lds((const void *)k_fast_select, (int)lds) < (int)lds)
     throw std::runtime_error("FAST cell too large for LDS");
   hipLaunchKernelGGL(k_fast_score, dim3(ncell, (shmax + kFastBand - 1) / kFastBand), dim3(256), 0, s, job, cells, thr);
-  hipLaunchKernelGGL(k_fast_select, dim3(ncell), dim3(kFastThreads), lds, s, job, cells, kmax, out, out_n);
+  hipLaunchKernelGGL(k_fast_select, dim3(ncell), dim3(kFastThreads), lds, s, job, cells, kmax, out, out_n, sort_stats);
+}
+
+void launch_grid_order_probe(hipStream_t s, const uint8_t *resp, const int *off, int ncell, int nmax, int kmax,
+                             int depth, int *arrangement, int *top) {
+  if (ncell <= 0) return;
+  if (kmax > kFastMaxK || nmax > 65536) throw std::runtime_error("grid order probe: cell beyond the kernel's limits");
+  const size_t lds = (size_t)nmax * 8;
+  if (lds > 64 * 1024 && set_dyn_lds((const void *)k_grid_order_probe, (int)lds) < (int)lds)
+    throw std::runtime_error("grid order probe: cell too large for LDS");
+  hipLaunchKernelGGL(k_grid_order_probe, dim3(ncell), dim3(kFastThreads), lds, s, resp, off, kmax, depth, arrangement,
+                     top);
 }
 
 void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const int *cells, int ncell, int sw, int sh, int thr,
@@ -1410,7 +1649,7 @@ void launch_fast_cells(hipStream_t s, const uint8_t *img, int w, int h, const in
   job.sh[0] = sh;
   job.cell_end[0] = ncell;
   job.ncam = 1;
-  launch_fast_multi(s, job, cells, thr, kmax, out, out_n);
+  launch_fast_multi(s, job, cells, thr, kmax, out, out_n, nullptr);
 }
 
 void launch_subpix_multi(hipStream_t s, const SubpixJob &job, float *pts, const float *mask, int win, int max_iters,

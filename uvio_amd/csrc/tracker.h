@@ -55,6 +55,9 @@ class Tracker {
   double sync_wait = 0.0;   // seconds blocked in them
   // LK algorithmic bytes accumulated on the device since creation (LkSlots::bytes), read on demand
   unsigned long long lk_bytes();
+  // Grider_GRID cells FAST'ed since creation and how many of them had more than 16 candidates (std::sort's
+  // introsort path, where its tie order differs from a stable one); joins the predetect, reads the device count
+  void grid_stats(unsigned long long *cells, unsigned long long *introsort_cells);
   // The next feed's detection, run ahead.  TrackKLT::perform_detection_{monocular,stereo} reads only the
   // previous frame's pyramid, points, ids and mask (TrackKLT.cpp:130, 249: img_pyramid_last, pts_last,
   // ids_last, img_mask_last), so it can run as soon as a feed has ended -- on its own stream, while the device
@@ -100,6 +103,8 @@ class Tracker {
   KProf kp_pre_;  // the detection stream's event pairs (used by the worker thread while pre_mode_)
   KProf *kcur() { return pre_mode_ ? &kp_pre_ : kp_; }
   unsigned long long *d_lk_bytes_ = nullptr;
+  int *d_sort_stats_ = nullptr;              // k_fast_select's count of introsort cells
+  unsigned long long grid_cells_ = 0;        // cells launched (host count, the feeding or the worker thread)
   bool downsample_ = false;  // VioManager.cpp:270-278: the inputs are 2w x 2h and pyrDown'ed first
   int num_features_, threshold_, grid_x_, grid_y_, min_px_dist_, histogram_method_;
   bool use_stereo_;

@@ -241,6 +241,13 @@ class VioManager:
                                uv.ctypes.data_as(C.POINTER(C.c_float)), cap, C.byref(n)), "get_tracks")
         return ids[:n.value].copy(), uv[:n.value].copy()
 
+    def grid_stats(self):
+        """(cells, introsort_cells): the tracker's FAST cells so far and how many had > 16 candidates (the
+        cells whose selection std::sort's introsort tie order decides, Grider_GRID.h:128)."""
+        c, i = C.c_uint64(), C.c_uint64()
+        self._check(self._call("debug_grid_stats", self._h, C.byref(c), C.byref(i)), "debug_grid_stats")
+        return int(c.value), int(i.value)
+
     def get_pyramid(self, cam, level):
         """(img u8 (h, w), der int16 (h, w, 2)) of the last pyramid level of camera `cam`."""
         w, h = C.c_int(), C.c_int()
@@ -463,6 +470,29 @@ def compress(A):
     R = np.zeros((nc, nc))
     N.check(lib.uvio_hp_compress(_dp(A), m, nc - 1, _dp(R)), what="uvio_hp_compress")
     return R
+
+
+def grid_order(cells, kmax=0, depth=-1):
+    """Grider_GRID.h:128's std::sort as the device's FAST selection runs it (uvio_hp_debug_grid_order).
+    cells: per cell the cv::FAST responses in raster order.  Returns (arrangements, tops): per cell the raster
+    indices as libstdc++'s introsort loop leaves them and, for kmax > 0, the first min(n, kmax) raster indices
+    of the sorted cell.  depth 0 forces the heap-sort fallback."""
+    lib = N.load()
+    off = np.zeros(len(cells) + 1, dtype=np.int32)
+    for i, c in enumerate(cells):
+        off[i + 1] = off[i] + len(c)
+    resp = np.zeros(max(int(off[-1]), 1), dtype=np.uint8)
+    for i, c in enumerate(cells):
+        resp[off[i]:off[i + 1]] = np.asarray(c, dtype=np.int64)
+    arr = np.zeros(max(int(off[-1]), 1), dtype=np.int32)
+    top = np.full(max(len(cells) * kmax, 1), -1, dtype=np.int32)
+    ip = C.POINTER(C.c_int)
+    rc = lib.uvio_hp_debug_grid_order(resp.ctypes.data_as(C.POINTER(C.c_uint8)), off.ctypes.data_as(ip), len(cells),
+                                      kmax, depth, arr.ctypes.data_as(ip), top.ctypes.data_as(ip))
+    N.check(rc, what="uvio_hp_debug_grid_order")
+    arrs = [arr[off[i]:off[i + 1]].copy() for i in range(len(cells))]
+    tops = [top[i * kmax:i * kmax + min(kmax, len(c))].copy() for i, c in enumerate(cells)] if kmax > 0 else None
+    return arrs, tops
 
 
 def undistort(cam, uv, return_ambiguous=False):
