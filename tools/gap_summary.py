@@ -6,11 +6,14 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 ev = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']) for r in rows)
+# the timed region starts after the last torch kernel (bench.py issues one right before it, so the warm-up of
+# TrackSIM workloads, which render nothing, stays out as well)
 last_torch = max([i for i, e in enumerate(ev) if 'at::' in e[2]] + [-1])
 seg = ev[last_torch + 1:]
 nframes = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-if nframes <= 0:
-    nframes = max(sum(1 for e in seg if 'k_hist_multi' in e[2]), sum(1 for e in seg if 'k_clone' in e[2]), 1)
+if nframes <= 0:  # image workloads: one equalizeHist launch per frame; TrackSIM workloads: one propagation per frame
+    nframes = max(sum(1 for e in seg if 'k_hist_multi' in e[2]),
+                  sum(1 for e in seg if 'k_clone' in e[2] or 'k_prop_clone' in e[2]), 1)
 
 
 def short(n):
