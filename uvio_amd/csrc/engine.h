@@ -604,6 +604,8 @@ class Engine {
   bool cov_propagate_clone(int s0, int p, const std::vector<int> &iold, const std::vector<double> &Phi,
                            const std::vector<double> &Q, bool do_dt, const double *ddnc);
   void marginalize(const VarP &v);
+  // a sequence of marginalize calls as one launch (the same covariance, k_marginalize_multi)
+  void marginalize_many(const std::vector<VarP> &ms);
   void check_neg_diag(const char *who);
   void info_prefactor(const std::vector<int> &hidx);
   // joins an information-form prefactor its update did not consume (an early return or an exception in

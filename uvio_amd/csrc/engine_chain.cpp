@@ -503,6 +503,18 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       EkfScratch sc = d_.ekf;
       sc.dx = region(new_region());
       double *Hrow = d_.H + (size_t)F.row_off * d_.ldh;
+      static const bool di_unfused = std::getenv("UVIO_HP_DI_UNFUSED") != nullptr;  // the eight-launch chain (A/B)
+      if (nup > 0 && !di_unfused) {
+        sc.chi2_gate = d_.acc;
+        sc.chi2_thr = o_.slam_chi2_multipler * chi2_table_[std::min(2 * F.nmeas, 999)];
+        sc.gate = nullptr;
+        KScope ks(&kprof_, KC_EKF);
+        launch_di_candidate(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, nup, n, cand->t_hidx, s2, sc, fo3 + j,
+                            sc.dx + Ni + 5, fr_cl, fr_cv, ncl, fr_cam, fr_camv, ncam, o_.do_calib_camera_pose,
+                            o_.do_calib_camera_intrinsics, sc.dx + Ni + 8);
+        kprof_.credit(KC_EKF, ekf_flops(Ni + 3, n, nup), ekf_bytes(Ni + 3, n, nup));
+        continue;
+      }
       launch_init_invertible(d_.stream, d_.P, d_.ldp, Ni, Hrow, d_.ldh, n, cand->t_hidx, nullptr, s2, sc, fo3 + j, d_.acc,
                              sc.dx + Ni + 5);
       if (nup > 0) {

@@ -318,6 +318,8 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.W, (size_t)cap * rmax);
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
+  dalloc(&d_.ekf.M3, (size_t)cap * 3);
+  dalloc(&d_.ekf.done, 16);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   d_.dx_bytes = sizeof(double) * (cap + 16);
   // one frame chain holds the MSCKF batch, the SLAM chunks and the delayed initialization's two passes
@@ -462,7 +464,7 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2_S,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
       {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm_mfma,k_info_cholZ,k_trinv16,"
-                     "k_trsm_lt,k_info_P",
+                     "k_trsm_lt,k_info_P,k_di_M,k_di_S,k_di_WP",
        1},
       {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
@@ -597,6 +599,39 @@ void Engine::marginalize(const VarP &m) {
   vars_ = keep;
   m->id = -1;
   N_ -= ms;
+}
+
+void Engine::marginalize_many(const std::vector<VarP> &ms) {
+  if (ms.empty()) return;
+  if (ms.size() == 1) {
+    marginalize(ms[0]);
+    return;
+  }
+  std::vector<uint8_t> gone((size_t)N_, 0);
+  for (const auto &m : ms)
+    for (int k = 0; k < m->size; k++) gone[(size_t)(m->id + k)] = 1;
+  std::vector<int> src, before((size_t)N_ + 1, 0);
+  src.reserve((size_t)N_);
+  for (int i = 0; i < N_; i++) {
+    before[(size_t)i + 1] = before[(size_t)i] + gone[(size_t)i];
+    if (!gone[(size_t)i]) src.push_back(i);
+  }
+  const int Nn = (int)src.size();
+  const int *dsrc = stage(src.data(), src.size());
+  stage_flush();
+  launch_marginalize_multi(d_.stream, d_.P, d_.P2, d_.ldp, Nn, dsrc);
+  std::swap(d_.P, d_.P2);
+  ++p_epoch_;
+  std::vector<VarP> keep;
+  keep.reserve(vars_.size());
+  for (auto &v : vars_)
+    if (!gone[(size_t)v->id]) {  // (variables are disjoint intervals: a removed start index is one of ms)
+      v->id -= before[(size_t)v->id];
+      keep.push_back(v);
+    }
+  vars_ = keep;
+  for (const auto &m : ms) m->id = -1;
+  N_ = Nn;
 }
 
 // algorithmic FP64 FLOPs of one EKFUpdate with r rows over n columns of an N-dim state (SURVEY.md §8(d)

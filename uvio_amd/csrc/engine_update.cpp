@@ -729,16 +729,19 @@ void Engine::cleanup_measurements(double t, bool skip_held) {
 }
 
 // StateHelper::marginalize_slam (StateHelper.cpp:631-645)
+// (the landmarks of one call leave the covariance in one launch, marginalize_many)
 void Engine::marginalize_slam() {
   stage_ = "marginalize_slam";
+  std::vector<VarP> ms;
   for (auto it = slam_.begin(); it != slam_.end();) {
     if (it->second->should_marg && (int)it->first > 4 * o_.max_aruco_features) {
-      marginalize(it->second);
+      ms.push_back(it->second);
       it = slam_.erase(it);
     } else {
       it++;
     }
   }
+  marginalize_many(ms);
 }
 
 // StateHelper::marginalize_old_clone (StateHelper.cpp:618-629)

@@ -114,6 +114,8 @@ bool launch_prop_clone(hipStream_t s, double *P, int ld, int N, int s0, int p, c
 void launch_marginalize(hipStream_t s, const double *P, double *Pout, int ld, int N, int m0, int ms);
 // Pout (Nn x Nn) <- P[src, src]: several variables marginalized at once (src: the kept indices, device)
 void launch_compact(hipStream_t s, const double *P, double *Pout, int ld, int Nn, const int *src);
+// several StateHelper::marginalize calls in one launch: kept indices src (ascending), Nn of them
+void launch_marginalize_multi(hipStream_t s, const double *P, double *Pout, int ld, int Nn, const int *src);
 // diagonal check: writes count of negative diagonal entries to *neg (device int)
 void launch_check_diag(hipStream_t s, const double *P, int ld, int N, int *neg);
 
@@ -187,6 +189,8 @@ struct EkfScratch {
   // rejected rows zeroed: k_ekf_MS then forms S_up = H T^T without recomputing T
   const double *Tall = nullptr;
   int ldt = 0;
+  double *M3 = nullptr;  // the delayed-init candidate's initialize_invertible M (N x 3)
+  int *done = nullptr;   // k_di_WP's completion counter
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.
@@ -234,6 +238,15 @@ struct DPoseVal {
 void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, const int *neg, const double *dx,
                         DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
                         int calib_intr, double *xv, int Nx, double *P, int ldp, int Ntot, int slot, double *out);
+// One delayed-initialization candidate (StateHelper::initialize): initialize_invertible of the landmark into the
+// slot Ni (H_Linv from fout->HfR, rows Hrow[0..2]), the chi2-gated EKF update of the other nup rows (Hrow + 3,
+// residual in column n; sc.chi2_gate: in = the linearization gate, out = accepted; sc.chi2_thr), and the chain
+// step of launch_chain_apply (tables moved by dx, or the slot cleared; [accepted, neg] into out), as four launches.
+// resout receives the residual column of the three initializing rows.
+void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double *Hrow, int ldh, int nup, int n,
+                         const int *hidx, double s2, EkfScratch &sc, const DFeatOut *fout, double *resout,
+                         DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
+                         int calib_intr, double *out);
 double chi2_quantile95(int dof);
 
 // ---- VioManager::retriangulate_active_tracks (VioManagerHelper.cpp:190-388) on the device ----

@@ -262,6 +262,24 @@ void launch_compact(hipStream_t s, const double *P, double *Pout, int ld, int Nn
   hipLaunchKernelGGL(k_compact, dim3((Nn + 127) / 128, Nn), dim3(128), 0, s, P, Pout, ld, Nn, src);
 }
 
+// StateHelper::marginalize (StateHelper.cpp:271-339) of several variables in one launch, with the result of the
+// sequence of single marginalizations: each one copies its lower-left block from the transposed upper-right
+// (Cov_new(x2,x1) = Cov_new(x1,x2)^T), so a lower element (i > j) of the final matrix comes from the upper
+// triangle exactly when some marginalized index lies between the kept pair, i.e. when more indices were removed
+// before src[i] than before src[j] (src[i] - i > src[j] - j); any order of the sequence gives the same matrix.
+__global__ void k_marginalize_multi(const double *__restrict__ P, double *__restrict__ Po, int ld, int Nn,
+                                    const int *__restrict__ src) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y;
+  if (j >= Nn || i >= Nn) return;
+  const int si = src[i], sj = src[j];
+  const bool flip = i > j && si - i > sj - j;
+  Po[(size_t)i * ld + j] = flip ? P[(size_t)sj * ld + si] : P[(size_t)si * ld + sj];
+}
+void launch_marginalize_multi(hipStream_t s, const double *P, double *Pout, int ld, int Nn, const int *src) {
+  if (Nn <= 0) return;
+  hipLaunchKernelGGL(k_marginalize_multi, dim3((Nn + 127) / 128, Nn), dim3(128), 0, s, P, Pout, ld, Nn, src);
+}
+
 __global__ void k_check_diag(const double *__restrict__ P, int ld, int N, int *neg) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < N && P[(size_t)i * ld + i] < 0.0) atomicAdd(neg, 1);

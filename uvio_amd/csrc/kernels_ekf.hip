@@ -317,6 +317,34 @@ __global__ void __launch_bounds__(256) k_ekf_WP(double *__restrict__ P, int ldp,
   }
 }
 
+// Thread t of one workgroup moves clone t (t < ncl) or camera t - ncl by dx: Var::update (PoseJPL: quat_boxplus,
+// p += dp; intrinsics +=) and the tables' rotation matrices (quat_2_Rot), the host's formulas
+__device__ void chain_tables_apply(int t, const double *__restrict__ dx, DClone *__restrict__ clones,
+                                   DPoseVal *__restrict__ cv, int ncl, DCam *__restrict__ cams,
+                                   DPoseVal *__restrict__ camv, int ncam, int calib_ext, int calib_intr) {
+  if (t < ncl) {  // PoseJPL::update of clone t, then the table's R_GtoI / p_IinG
+    DPoseVal &v = cv[t];
+    const double *d = dx + v.pid;
+    quat_boxplus(v.q, d);
+    for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
+    quat_2_Rot(v.q, clones[t].R);
+    for (int k = 0; k < 3; k++) clones[t].p[k] = v.p[k];
+  } else if (t < ncl + ncam) {
+    const int c = t - ncl;
+    DCam &dc = cams[c];
+    if (calib_ext && dc.pid_ext >= 0) {
+      DPoseVal &v = camv[c];
+      const double *d = dx + v.pid;
+      quat_boxplus(v.q, d);
+      for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
+      quat_2_Rot(v.q, dc.R_ItoC);
+      for (int k = 0; k < 3; k++) dc.p_IinC[k] = v.p[k];
+    }
+    if (calib_intr && dc.pid_intr >= 0)
+      for (int k = 0; k < 8; k++) dc.cam.v[k] += dx[dc.pid_intr + k];
+  }
+}
+
 // Delayed-initialization chain step (kernels.h launch_chain_apply).  Block 0 updates the tables (one thread
 // per clone / camera) when the candidate was accepted; every block clears a rejected candidate's slot.
 __global__ void __launch_bounds__(256) k_chain_apply(const DFeatOut *__restrict__ fout, const int *__restrict__ gate,
@@ -338,29 +366,7 @@ __global__ void __launch_bounds__(256) k_chain_apply(const DFeatOut *__restrict_
   } else if (dx && xv) {  // the additive mirror (landmarks): Var::update of a vector, val += dx
     for (int e = t; e < Nx; e += gridDim.x * blockDim.x) xv[e] += dx[e];
   }
-  if (acc && blockIdx.x == 0 && dx) {
-    if (t < ncl) {  // PoseJPL::update of clone t, then the table's R_GtoI / p_IinG
-      DPoseVal &v = cv[t];
-      const double *d = dx + v.pid;
-      quat_boxplus(v.q, d);
-      for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
-      quat_2_Rot(v.q, clones[t].R);
-      for (int k = 0; k < 3; k++) clones[t].p[k] = v.p[k];
-    } else if (t < ncl + ncam) {
-      const int c = t - ncl;
-      DCam &dc = cams[c];
-      if (calib_ext && dc.pid_ext >= 0) {
-        DPoseVal &v = camv[c];
-        const double *d = dx + v.pid;
-        quat_boxplus(v.q, d);
-        for (int k = 0; k < 3; k++) v.p[k] += d[3 + k];
-        quat_2_Rot(v.q, dc.R_ItoC);
-        for (int k = 0; k < 3; k++) dc.p_IinC[k] = v.p[k];
-      }
-      if (calib_intr && dc.pid_intr >= 0)
-        for (int k = 0; k < 8; k++) dc.cam.v[k] += dx[dc.pid_intr + k];
-    }
-  }
+  if (acc && blockIdx.x == 0 && dx) chain_tables_apply(t, dx, clones, cv, ncl, cams, camv, ncam, calib_ext, calib_intr);
   if (t == 0) {
     out[0] = acc ? 1.0 : 0.0;
     out[1] = neg ? (double)*neg : 0.0;
@@ -521,8 +527,7 @@ void launch_ekf_phaseA(hipStream_t s, const double *P, int ldp, int N, const dou
                      nbM, sc.neg, Tall, sc.ldt);
 }
 
-void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
-                       EkfScratch &sc) {
+static void launch_ekf_factor(hipStream_t s, int N, int r, const double *res, int res_stride, EkfScratch &sc) {
   ensure_ekf_lds_attrs();
   if (r + 1 > kWaveMaxRows) throw std::runtime_error("direct EKF update with more rows than the factorization panel");
   const size_t bytes = ekf_small_lds_bytes(r);
@@ -544,10 +549,341 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
   // lower triangle and the residual read, the factor written
   if (sc.kp) sc.kp->credit(KC_LDL, (double)r * r * r / 3.0 + (double)r * r, 8.0 * (1.5 * r * r + 2.0 * r));
   if (sc.chi2_gate) sc.gate = sc.chi2_gate;
+}
+
+void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const double *res, int res_stride,
+                       EkfScratch &sc) {
+  launch_ekf_factor(s, N, r, res, res_stride, sc);
   const int nb = (N + 15) / 16;
   const size_t lw = (size_t)(32 * (r | 1) + 1024) * sizeof(double);
-  hipLaunchKernelGGL(k_ekf_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, r, Linv, sc.y, sc.dx,
+  hipLaunchKernelGGL(k_ekf_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, r, sc.S, sc.y, sc.dx,
                      sc.neg, sc.gate, nb);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// One delayed-initialization candidate (StateHelper::initialize, StateHelper.cpp:393-577: initialize_invertible
+// of the landmark's 3 rows, then EKFUpdate of the other nup rows at the same factor that carries the chi2 test)
+// in four launches instead of eight (k_ekf_M_small, k_init_invertible, 2 x k_ekf_MS, k_ekf_fact, k_ekf_WP,
+// k_chain_apply):
+//   k_di_M    grid over the old state's 16-row blocks (rows < Ni): P[i, I] staged once; M_up = P[:, I] H_up^T on
+//             k_ekf_MS's tiles and M3 = P[:, I] H_init^T in k_ekf_M_small's GEMV order
+//   k_di_S    S_up from M_up's rows I (k_ekf_MS's gathered tile pairs); initialize_invertible (k_init_invertible's
+//             blocks: the landmark's cross-covariance columns and 3x3 block); the landmark's rows of M_up, from
+//             the same values k_init_invertible writes, on the tiles k_ekf_MS formed from P's new rows
+//   k_ekf_fact unchanged (the chi2 gate and the factor)
+//   k_di_WP   k_ekf_WP's tile pairs; the last workgroup to finish (agent-scope release / acquire around a
+//             counter) does k_chain_apply's work: the clone / camera tables moved by dx, or a rejected
+//             candidate's slot cleared, and [accepted, negative diagonals] into out
+// Every value is formed by the same expression, in the same order, as in the eight-launch chain (the old chain
+// stays behind UVIO_HP_DI_UNFUSED=1 for A/B runs).
+__global__ void __launch_bounds__(kMSThreads) k_di_M(const double *__restrict__ P, int ldp, int Ni,
+                                              const double *__restrict__ H, int ldh, int nup, int n,
+                                              const int *__restrict__ hidx, double *__restrict__ M,
+                                              double *__restrict__ M3, int *neg, int *done) {
+  extern __shared__ double sh[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *neg = 0;
+    *done = 0;
+  }
+  const int i0 = blockIdx.x * 16, lds = n | 1;
+  double *Ps = sh;
+  staged_copy(
+      16 * n,
+      [&](int e) {
+        const int i = e / n, k = e - i * n;
+        return (i0 + i < Ni) ? P[(size_t)(i0 + i) * ldp + hidx[k]] : 0.0;
+      },
+      [&](int e, double v) {
+        const int i = e / n, k = e - i * n;
+        Ps[i * lds + k] = v;
+      });
+  __syncthreads();
+  const double *Hup = H + 3 * (size_t)ldh;
+  const int nct = (nup + 15) / 16;
+  for (int t = wid; t < nct; t += kMSThreads / 64) {
+    const int j0 = 16 * t, jr = j0 + r16;
+    const double *Hr = Hup + (size_t)min(jr, nup - 1) * ldh;
+    const bool jv = jr < nup;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain<16>(
+        0, n, kq, [&](int k) { return Ps[r16 * lds + k]; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = i0 + kq + 4 * q, col = j0 + r16;
+      if (row < Ni && col < nup) M[(size_t)row * nup + col] = acc[q];
+    }
+  }
+  // M3: one wavefront per row, lanes over the columns, butterfly sum (k_ekf_M_small)
+  for (int i = wid; i < 16 && i0 + i < Ni; i += kMSThreads / 64) {
+    double acc[kSmallMRows] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = lane; k < n; k += 64) {
+      const double p = Ps[i * lds + k];
+#pragma unroll
+      for (int b = 0; b < 3; b++) acc[b] = fma(p, H[(size_t)b * ldh + k], acc[b]);
+    }
+#pragma unroll
+    for (int b = 0; b < kSmallMRows; b++)
+      for (int o = 32; o > 0; o >>= 1) acc[b] += __shfl_xor(acc[b], o, 64);
+    if (lane < 3) {
+      double v = acc[0];
+#pragma unroll
+      for (int b = 1; b < kSmallMRows; b++)
+        if (lane == b) v = acc[b];
+      M3[(size_t)(i0 + i) * 3 + lane] = v;
+    }
+  }
+}
+
+constexpr int kDiInitThreads = 512;  // k_di_S's initialize_invertible blocks: (3 Ni + 511) / 512 of them
+__global__ void __launch_bounds__(kMSThreads) k_di_S(double *__restrict__ P, int ldp, int Ni,
+                                              const double *__restrict__ H, int ldh, int nup, int n,
+                                              const int *__restrict__ hidx, double s2, double *__restrict__ M,
+                                              const double *__restrict__ M3, double *__restrict__ Sup,
+                                              const DFeatOut *__restrict__ fout, const int *__restrict__ gate,
+                                              double *__restrict__ resout, int nbG, int nbX) {
+  extern __shared__ double sh[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const double *Hup = H + 3 * (size_t)ldh;
+  const int b = blockIdx.x;
+  if (b < nbG) {
+    // S_up[a][b] = H_a T_b^T with T[b][k] = M[hidx[k]][b] (k_ekf_MS, ldt < 0)
+    int *hs = (int *)sh;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) hs[k] = hidx[k];
+    __syncthreads();
+    const int nt = (nup + 15) / 16;
+    int pair = b * (kMSThreads / 64) + wid, at = 0;
+    if (pair >= nt * (nt + 1) / 2) return;
+    while (pair >= nt - at) {
+      pair -= nt - at;
+      at++;
+    }
+    const int bt = at + pair;
+    const int ar = 16 * at + r16, br = 16 * bt + r16;
+    const double *Ha = Hup + (size_t)min(ar, nup - 1) * ldh;
+    const double *Tb = M + min(br, nup - 1);
+    const bool av = ar < nup, bv = br < nup;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain<16>(
+        0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return bv ? Tb[(size_t)hs[k] * nup] : 0.0; },
+        acc);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int row = 16 * at + kq + 4 * q, col = 16 * bt + r16;
+      if (row < nup && col < nup) Sup[(size_t)row * nup + col] = acc[q] + (row == col ? s2 : 0.0);
+    }
+    return;
+  }
+  __shared__ double Hinv[9], S3[9], PLL[9];
+  if (b < nbG + nbX) {
+    // initialize_invertible (k_init_invertible with N = Ni: block xb takes the cross-covariance elements
+    // xb * 512 ..; the first one also the 3x3 block)
+    const int xb = b - nbG, t = threadIdx.x + xb * kDiInitThreads;
+    if (resout && xb == 0 && threadIdx.x < 3) resout[threadIdx.x] = H[(size_t)threadIdx.x * ldh + n];
+    if (gate && *gate == 0) return;
+    if (threadIdx.x == 0) inv3_cofactor(fout->HfR, Hinv);
+    __syncthreads();
+    if (xb == 0) {
+      __shared__ double part[9][28];
+      const int e = threadIdx.x / 28, j = threadIdx.x % 28;
+      if (e < 9) {
+        const int a = e / 3, bb = e % 3;
+        double acc = 0.0;
+        for (int k = j; k < n; k += 28) acc += H[(size_t)a * ldh + k] * M3[(size_t)hidx[k] * 3 + bb];
+        part[e][j] = acc;
+      }
+      __syncthreads();
+      if (threadIdx.x < 9) {
+        const int a = threadIdx.x / 3, bb = threadIdx.x % 3;
+        double acc = 0.0;
+        for (int q = 0; q < 28; q++) acc += part[threadIdx.x][q];
+        S3[threadIdx.x] = acc + (a == bb ? s2 : 0.0);
+      }
+      __syncthreads();
+      if (threadIdx.x < 9) {
+        const int a = threadIdx.x / 3, bb = threadIdx.x % 3;
+        double acc = 0.0;
+        for (int c = 0; c < 3; c++)
+          for (int e2 = 0; e2 < 3; e2++) {
+            const double sce = (c <= e2) ? S3[c * 3 + e2] : S3[e2 * 3 + c];
+            acc += Hinv[a * 3 + c] * sce * Hinv[bb * 3 + e2];
+          }
+        PLL[threadIdx.x] = acc;
+      }
+    }
+    if (t < Ni * 3) {
+      const int i = t / 3, a = t % 3;
+      double acc = 0.0;
+      for (int bb = 0; bb < 3; bb++) acc += M3[(size_t)i * 3 + bb] * Hinv[a * 3 + bb];
+      P[(size_t)i * ldp + Ni + a] = -acc;
+      P[(size_t)(Ni + a) * ldp + i] = -acc;
+    }
+    if (xb == 0 && threadIdx.x < 9) {
+      const int a = threadIdx.x / 3, bb = threadIdx.x % 3;
+      P[(size_t)(Ni + a) * ldp + Ni + bb] = PLL[threadIdx.x];
+    }
+    return;
+  }
+  // the landmark's rows Ni .. Ni+2 of M_up: P[Ni + a][hidx[k]] as initialize_invertible writes it, then the
+  // 16-row tiles of k_ekf_MS (only these three rows of the tile are stored)
+  if (gate && *gate == 0) return;
+  double *Pl = sh;  // 3 x n
+  if (threadIdx.x == 0) inv3_cofactor(fout->HfR, Hinv);
+  __syncthreads();
+  for (int e = threadIdx.x; e < 3 * n; e += blockDim.x) {
+    const int a = e / n, k = e - a * n, i = hidx[k];
+    double acc = 0.0;
+    for (int bb = 0; bb < 3; bb++) acc += M3[(size_t)i * 3 + bb] * Hinv[a * 3 + bb];
+    Pl[e] = -acc;
+  }
+  __syncthreads();
+  const int nct = (nup + 15) / 16;
+  for (int t = wid; t < nct; t += kMSThreads / 64) {
+    const int j0 = 16 * t, jr = j0 + r16;
+    const double *Hr = Hup + (size_t)min(jr, nup - 1) * ldh;
+    const bool jv = jr < nup, rv = r16 < 3;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = tile_chain<16>(
+        0, n, kq, [&](int k) { return rv ? Pl[r16 * n + k] : 0.0; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
+    const int col = j0 + r16;
+    if (kq < 3 && col < nup) M[(size_t)(Ni + kq) * nup + col] = acc[0];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_di_WP(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
+                                               int r, const double *__restrict__ Linv, const double *__restrict__ y,
+                                               double *__restrict__ dx, int *neg, const int *gate, int nb, int *done,
+                                               int slot, const DFeatOut *__restrict__ fout, DClone *__restrict__ clones,
+                                               DPoseVal *__restrict__ cv, int ncl, DCam *__restrict__ cams,
+                                               DPoseVal *__restrict__ camv, int ncam, int calib_ext, int calib_intr,
+                                               double *__restrict__ out) {
+  extern __shared__ double sh[];
+  __shared__ int s_last;
+  const bool up = !gate || *gate != 0;
+  if (up) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    int b = blockIdx.x, bi = 0;
+    while (b >= nb - bi) {
+      b -= nb - bi;
+      bi++;
+    }
+    const int bj = bi + b;
+    const int ldw = r | 1;
+    double *Wi = sh, *Wj = sh + 16 * ldw, *red = sh + 32 * ldw;
+    const int ei = threadIdx.x >> 4, ej = threadIdx.x & 15;
+    const int gi = 16 * bi + ei, gj = 16 * bj + ej;
+    const bool pw = gi < N && gj < N && (bi < bj || ej >= ei);
+    const double pv = pw ? P[(size_t)gi * ldp + gj] : 0.0;
+    const int nct = (r + 15) / 16, ntask = (bi == bj ? 1 : 2) * nct;
+    for (int t = wid; t < ntask; t += 4) {
+      const int which = t / nct, ct = t - which * nct;
+      double *Wd = which ? Wj : Wi;
+      const int row = 16 * (which ? bj : bi) + r16, c = 16 * ct + r16;
+      const double *Mr = M + (size_t)min(row, N - 1) * r;
+      const double *Lr = Linv + (size_t)min(c, r - 1) * r;
+      const bool rv = row < N, cv2 = c < r;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = tile_chain(
+          0, min(16 * ct + 16, r), kq, [&](int k) { return rv ? Mr[k] : 0.0; },
+          [&](int k) { return cv2 ? Lr[k] : 0.0; }, acc);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (cv2) Wd[(kq + 4 * q) * ldw + c] = acc[q];
+    }
+    __syncthreads();
+    const double *Wb = (bi == bj) ? Wi : Wj;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 4 * wid; k0 < r; k0 += 16) {
+      const int k = k0 + kq;
+      const double a = (k < r) ? Wi[r16 * ldw + k] : 0.0;
+      const double bb = (k < r) ? Wb[r16 * ldw + k] : 0.0;
+      acc = mfma4(a, bb, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) red[wid * 256 + (kq + 4 * q) * 16 + r16] = acc[q];
+    __syncthreads();
+    if (pw) {
+      const int e = threadIdx.x;
+      const double s = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
+      const double v = pv - s;
+      P[(size_t)gi * ldp + gj] = v;
+      P[(size_t)gj * ldp + gi] = v;
+      if (gi == gj && v < 0.0) atomicAdd(neg, 1);
+    }
+    if (bi == bj && wid == 1) {
+      const int i = lane >> 2, part = lane & 3;
+      double a = 0.0;
+      for (int k = part; k < r; k += 4) a += Wi[i * ldw + k] * y[k];
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      if (part == 0 && 16 * bi + i < N) dx[16 * bi + i] = a;
+    }
+  }
+  // completion: every thread's stores released at agent scope before the block counts itself done
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // k_chain_apply (one workgroup): accepted -> the tables; rejected -> the slot's rows / columns over [0, N)
+  const bool acc = (!fout || fout->status == 0) && up;
+  const int t = threadIdx.x;
+  if (!acc) {
+    for (int e = t; e < 3 * N; e += blockDim.x) {
+      const int i = e / 3, a = e - 3 * i;
+      P[(size_t)(slot + a) * ldp + i] = 0.0;
+      P[(size_t)i * ldp + slot + a] = 0.0;
+    }
+  } else {
+    chain_tables_apply(t, dx, clones, cv, ncl, cams, camv, ncam, calib_ext, calib_intr);
+  }
+  if (t == 0) {
+    out[0] = acc ? 1.0 : 0.0;
+    out[1] = (double)__hip_atomic_load(neg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double *Hrow, int ldh, int nup, int n,
+                         const int *hidx, double s2, EkfScratch &sc, const DFeatOut *fout, double *resout,
+                         DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
+                         int calib_intr, double *out) {
+  if (nup <= 0 || nup + 1 > kWaveMaxRows) throw std::runtime_error("delayed-init candidate rows outside 1..255");
+  if (ncl + ncam > 256) throw std::runtime_error("update chain: more clones + cameras than one workgroup");
+  if (!sc.M3 || !sc.done || !sc.chi2_gate) throw std::runtime_error("delayed-init candidate: scratch not set up");
+  ensure_ekf_lds_attrs();
+  static bool attrs = false;
+  if (!attrs) {
+    if (set_dyn_lds((const void *)k_di_M, kMaxDynLds) < kMaxDynLds ||
+        set_dyn_lds((const void *)k_di_S, kMaxDynLds) < kMaxDynLds ||
+        set_dyn_lds((const void *)k_di_WP, kMaxDynLds) < kMaxDynLds)
+      throw std::runtime_error("dynamic LDS limit not granted for a delayed-init kernel");
+    attrs = true;
+  }
+  const size_t ldsM = (size_t)16 * (n | 1) * sizeof(double);
+  const size_t ldsS = std::max((size_t)n * sizeof(int), (size_t)3 * n * sizeof(double));
+  if (ldsM > (size_t)kMaxDynLds || ldsS > (size_t)kMaxDynLds)
+    throw std::runtime_error("delayed-init candidate with too many columns");
+  const int N = Ni + 3;
+  {
+    hipLaunchKernelGGL(k_di_M, dim3((Ni + 15) / 16), dim3(kMSThreads), ldsM, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
+                       sc.M, sc.M3, sc.neg, sc.done);
+    const int nt = (nup + 15) / 16, wpb = kMSThreads / 64;
+    const int nbG = (nt * (nt + 1) / 2 + wpb - 1) / wpb, nbX = (3 * Ni + kDiInitThreads - 1) / kDiInitThreads;
+    double *Sup = sc.S + 2 * (size_t)nup * nup;
+    hipLaunchKernelGGL(k_di_S, dim3(nbG + nbX + 1), dim3(kMSThreads), ldsS, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
+                       s2, sc.M, sc.M3, Sup, fout, sc.chi2_gate, resout, nbG, nbX);
+    launch_ekf_factor(s, N, nup, Hrow + 3 * (size_t)ldh + n, ldh, sc);
+    const int nb = (N + 15) / 16;
+    const size_t lw = (size_t)(32 * (nup | 1) + 1024) * sizeof(double);
+    hipLaunchKernelGGL(k_di_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, nup, sc.S, sc.y, sc.dx,
+                       sc.neg, sc.chi2_gate, nb, sc.done, Ni, fout, clones, cv, ncl, cams, camv, ncam, calib_ext,
+                       calib_intr, out);
+  }
 }
 
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,
