@@ -307,20 +307,37 @@ def pmc_class_traffic(workload, name, kernels):
     return None, None, None
 
 
+def library_sha16():
+    """sha256 (16 hex) of the product library this process loads (the build tools/prof_summary.py records)."""
+    import hashlib
+    from uvio_amd import _native as N
+    try:
+        return hashlib.sha256(open(N.LIB_PATH, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def committed_class_times(workload, classes):
     """Per-class device time per frame (us) from the newest committed rocprofv3 per-frame summary of this workload
-    (profiles/rNN*_<workload>_per_frame.txt, round 5 on: tools/prof_summary.py over a kernel trace of the same
-    bench command), summed over the class's kernels; ({class: us}, path) or ({}, None).  rocprof's device
-    timestamps rank the classes without the dispatch gap that the live HIP-event pairs include (the event before a
-    launch completes when the previous kernel does, so each timed launch also carries its ~5 us dispatch gap)."""
+    made with THIS library build (profiles/rNN*_<workload>_per_frame.txt, tools/prof_summary.py over a kernel trace
+    of the same bench command; its 'library sha256' line must equal the loaded library's), summed over the class's
+    kernels; ({class: us}, path, why) or ({}, None, why).  rocprof's device timestamps rank the classes without the
+    dispatch gap that the live HIP-event pairs include (the event before a launch completes when the previous kernel
+    does, so each timed launch also carries its ~5 us dispatch gap).  A summary of another build, or one whose
+    format does not parse, is skipped and `why` says so (the caller then ranks by the live timing)."""
     d = os.path.join(ROOT, "profiles")
     names = sorted((f for f in os.listdir(d) if f.endswith("_%s_per_frame.txt" % workload) and f >= "r05"),
                    reverse=True)
+    sha = library_sha16()
+    why = "no committed per-frame summary of %s" % workload
     for f in names:
-        per = {}
+        per, fsha = {}, None
         try:
             with open(os.path.join(d, f)) as fh:
                 for line in fh:
+                    if line.startswith("library sha256 "):
+                        fsha = line.split()[2]
+                        continue
                     if "n/frame" not in line or "per frame" not in line:
                         continue
                     head, rest = line.split("n/frame", 1)
@@ -328,10 +345,15 @@ def committed_class_times(workload, classes):
                     us = float(rest.split("per frame")[1].split("us")[0])
                     per[kname] = per.get(kname, 0.0) + us
         except (OSError, ValueError, IndexError):
+            why = "profiles/%s does not parse" % f
+            continue
+        if fsha is None or fsha != sha:
+            why = "newest summary profiles/%s is of another build (%s, loaded %s)" % (f, fsha, sha)
             continue
         if per:
-            return {c: sum(per.get(k, 0.0) for k in ks) for c, ks in classes.items()}, os.path.join("profiles", f)
-    return {}, None
+            return ({c: sum(per.get(k, 0.0) for k in ks) for c, ks in classes.items()}, os.path.join("profiles", f),
+                    "same build (library sha256 %s)" % sha)
+    return {}, None, why
 
 
 def max_over_ranks(x, device="cuda"):
@@ -604,13 +626,14 @@ def main():
         # several latency-bound kernels): by device time in the committed same-code rocprof summary of this
         # workload when there is one, else by this run's live HIP-event time
         cand = {k: v for k, v in rl.items() if k != "ekf_update"}
-        prof_t, prof_src = committed_class_times(wl, {k: v["kernels"] for k, v in cand.items()})
+        prof_t, prof_src, prof_why = committed_class_times(wl, {k: v["kernels"] for k, v in cand.items()})
         if prof_t:
             dom = max(cand, key=lambda k: prof_t.get(k, 0.0))
-            dom_by = {"source": prof_src, "device_us_per_frame": {k: round(v, 1) for k, v in prof_t.items()}}
+            dom_by = {"source": prof_src, "why": prof_why,
+                      "device_us_per_frame": {k: round(v, 1) for k, v in prof_t.items()}}
         else:
             dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
-            dom_by = {"source": "live HIP-event time of this run"}
+            dom_by = {"source": "live HIP-event time of this run", "why": prof_why}
         cpu = None
         if args.cpu_frames > 0:
             # the oracle needs only the clone window filled; fewer warm-up frames bound its run time
@@ -719,13 +742,13 @@ def msckf_load_companion(U, args, dev):
         if d["launches"] > 0:
             rl[k] = roofline_entry(k, d, wl)
     cand = {k: v for k, v in rl.items() if k != "ekf_update"}
-    prof_t, prof_src = committed_class_times(wl, {k: v["kernels"] for k, v in cand.items()})
+    prof_t, prof_src, prof_why = committed_class_times(wl, {k: v["kernels"] for k, v in cand.items()})
     if prof_t:
         dom = max(cand, key=lambda k: prof_t.get(k, 0.0))
-        dom_by = {"source": prof_src, "device_us_per_frame": {k: round(v, 1) for k, v in prof_t.items()}}
+        dom_by = {"source": prof_src, "why": prof_why, "device_us_per_frame": {k: round(v, 1) for k, v in prof_t.items()}}
     else:
         dom = max(cand, key=lambda k: cand[k]["device_s"]) if cand else None
-        dom_by = {"source": "live HIP-event time of this run"}
+        dom_by = {"source": "live HIP-event time of this run", "why": prof_why}
     return {"workload": WORKLOADS[wl][4], "steps": steps, "warmup": warm, "value": steps / el, "unit": "frames/s",
             "ms_per_step": 1e3 * el / steps, "mean_msckf_feats": acc["n_msckf"] / steps,
             "mean_msckf_rows": acc["rows"] / steps, "H_cols": acc["cols"],

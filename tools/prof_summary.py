@@ -1,6 +1,8 @@
 """Summarize a rocprofv3 kernel trace: per-kernel totals over the timed region (after the last torch kernel)."""
 import collections
 import csv
+import hashlib
+import os
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -29,3 +31,8 @@ for k in sorted(d, key=lambda k: -sum(d[k]))[:28]:
     v = d[k]
     print("%-34s n/frame %6.2f  avg %7.1f us  per frame %7.1f us  %5.1f%%" % (k[:34], len(v) / nframes, sum(v) / len(v),
                                                                         sum(v) / nframes, 100 * sum(v) / tot))
+# the library the trace ran (bench.py uses this summary only for the same build): sha256 of the .so, 16 hex
+lib = os.environ.get("UVIO_HP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "uvio_amd",
+                                                "libuvio_hp.so"))
+if os.path.exists(lib):
+    print("library sha256 %s" % hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16])

@@ -319,7 +319,6 @@ void Engine::alloc_device() {
   dalloc(&d_.ekf.S, (size_t)5 * rmax * rmax);
   dalloc(&d_.ekf.y, rmax);
   dalloc(&d_.ekf.M3, (size_t)cap * 3);
-  dalloc(&d_.ekf.done, 16);
   dalloc(&d_.ekf.Dinv, (size_t)(rmax / 16 + 1) * 256);
   d_.dx_bytes = sizeof(double) * (cap + 16);
   // one frame chain holds the MSCKF batch, the SLAM chunks and the delayed initialization's two passes
@@ -464,7 +463,7 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2_S,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
       {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm_mfma,k_info_cholZ,k_trinv16,"
-                     "k_trsm_lt,k_info_P,k_di_M,k_di_S,k_di_WP",
+                     "k_trsm_lt,k_info_P,k_di_M,k_di_S",
        1},
       {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},

@@ -1220,6 +1220,8 @@ void Tracker::feed_stereo(double t, int cl, int cr, const DbSink &db) {
 // stream.  Only when every camera of the last feed has tracks: a camera without tracks detects on the NEW
 // frame's pyramid (TrackKLT.cpp:104-110, 215-222), which does not exist yet.
 void Tracker::predetect() {
+  const bool pyr_waited = pre_pyr_waited_;
+  pre_pyr_waited_ = false;
   pre_syncs = 0;
   pre_wait = 0.0;
   if (pre_.valid || last_cams_.empty()) return;
@@ -1233,7 +1235,9 @@ void Tracker::predetect() {
       if (cs_.at(c).pts_last.empty()) return;
   }
   if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
-  if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
+  // the wait on the last pyramid launch: enqueued by predetect_async on the caller's thread (before the worker
+  // starts, so the next feed's re-record of ev_pyr_ cannot come first); here when called synchronously
+  if (!pyr_waited && ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
   kp_pre_.stream = sd_;
   kp_pre_.on = kp_ && kp_->on;
   kp_pre_.harvest(false);
@@ -1303,6 +1307,9 @@ void Tracker::worker_loop() {
 void Tracker::predetect_async() {
   predetect_join();
   HP_HIP(hipGetDevice(&dev_));  // the engine's device (bound by the calling C-ABI entry)
+  if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+  if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
+  pre_pyr_waited_ = true;
   if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });
   {
     std::lock_guard<std::mutex> lk(wm_);

@@ -225,9 +225,6 @@ HPD void cam_distort_jac(const CamParams &c, double x, double y, double *dzn, do
   }
 }
 
-// True when the float rounding of v is not decided by v's leading 40 bits: a result that differs from v by a
-// few ulps (the equidistant model's tan, whose last bit differs between libm and the device) could round to
-// the other float.  Away from such a boundary (all but <= 2^-15 of the float spacing) the float is the same.
 // UpdaterUWB::update_single's row (UVioUpdaterHelper::get_uwb_jacobian_single, UVioUpdaterHelper.cpp:147-241):
 // the range from the IMU pose (q_GtoI, p_IinG), p_IinU and the anchor [p_AinG, const_bias, dist_bias];
 // H[0..n-1] over the columns [IMU theta (3), IMU p (3), p_IinU (3) if cal, anchor (5) if anc], H[n] = residual.
@@ -268,6 +265,9 @@ HPD int uwb_row(const double *q, const double *pI, const double *pIinU, const do
   return n;
 }
 
+// True when the float rounding of v is not decided by v's leading 40 bits: a result that differs from v by a
+// few ulps (the equidistant model's tan, whose last bit differs between libm and the device) could round to
+// the other float.  Away from such a boundary (all but <= 2^-15 of the float spacing) the float is the same.
 HPD bool float_round_ambiguous(double v) {
   const double e = fabs(v) * 0x1p-40;
   return (float)(v - e) != (float)(v + e);

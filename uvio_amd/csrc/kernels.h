@@ -190,7 +190,6 @@ struct EkfScratch {
   const double *Tall = nullptr;
   int ldt = 0;
   double *M3 = nullptr;  // the delayed-init candidate's initialize_invertible M (N x 3)
-  int *done = nullptr;   // k_di_WP's completion counter
 };
 // W (N x r, ld r) = M L^-T for lower-triangular L (r x r, ld ldl); M row-major (ldm) or, with hidx, the
 // columns P[:, hidx] of P (ldm = ldp).  Dinv: scratch as in EkfScratch.
@@ -241,7 +240,7 @@ void launch_chain_apply(hipStream_t s, const DFeatOut *fout, const int *gate, co
 // One delayed-initialization candidate (StateHelper::initialize): initialize_invertible of the landmark into the
 // slot Ni (H_Linv from fout->HfR, rows Hrow[0..2]), the chi2-gated EKF update of the other nup rows (Hrow + 3,
 // residual in column n; sc.chi2_gate: in = the linearization gate, out = accepted; sc.chi2_thr), and the chain
-// step of launch_chain_apply (tables moved by dx, or the slot cleared; [accepted, neg] into out), as four launches.
+// step of launch_chain_apply (tables moved by dx, or the slot cleared; [accepted, neg] into out), as six launches.
 // resout receives the residual column of the three initializing rows.
 void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double *Hrow, int ldh, int nup, int n,
                          const int *hidx, double s2, EkfScratch &sc, const DFeatOut *fout, double *resout,

@@ -388,7 +388,11 @@ __global__ void k_uwb_row(DUwbState *st, int j, const double *__restrict__ prev,
                           double *__restrict__ region) {
   if (threadIdx.x != 0) return;
   DUwbState &u = *st;
-  if (prev && prev[0] != 0.0) {
+  // a negative covariance diagonal in an earlier range of the message halts the rest of it: the reference stops
+  // at that update (StateHelper.cpp:181, std::exit), so no later range may touch P (the host then reports E_NUMERIC)
+  const int *pi = reinterpret_cast<const int *>(prev + 1);
+  const bool halt = prev && (pi[0] > 0 || pi[1] != 0);
+  if (prev && prev[0] != 0.0 && !halt) {
     // Var::update of the previous range's dx (engine_state.cpp): IMU quaternion boxplus + position, p_IinU and
     // the anchors additive
     const double *dx = prev + 4;
@@ -402,7 +406,8 @@ __global__ void k_uwb_row(DUwbState *st, int j, const double *__restrict__ prev,
   }
   uwb_row(u.q, u.p, u.pU, u.anc[j], u.id_cal >= 0, u.id_anc[j] >= 0, u.range[j], h);
   region[0] = 0.0;
-  region[1] = 0.0;  // the negative-diagonal count (int bits)
+  region[1] = 0.0;  // the negative-diagonal count (int bits, low word) and the halt flag (high word)
+  if (halt) reinterpret_cast<int *>(region + 1)[1] = 1;
   region[2] = region[3] = 0.0;
 }
 
@@ -428,6 +433,7 @@ void launch_uwb_M(hipStream_t s, const double *P, int ldp, int N, const double *
 __global__ void __launch_bounds__(256) k_uwb_update(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
                                                     const double *__restrict__ h, const int *__restrict__ hidx, int n,
                                                     double s2, double thr, double *__restrict__ region, int nb) {
+  if (reinterpret_cast<const int *>(region + 1)[1] != 0) return;  // halted (k_uwb_row): not applied, region[0] = 0
   // the innovation variance and the gate, the same arithmetic in every block
   double S = 0.0;
   for (int k = 0; k < n; k++) S = fma(h[k], M[hidx[k]], S);
@@ -563,30 +569,26 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
 // ---------------------------------------------------------------------------------------------------
 // One delayed-initialization candidate (StateHelper::initialize, StateHelper.cpp:393-577: initialize_invertible
 // of the landmark's 3 rows, then EKFUpdate of the other nup rows at the same factor that carries the chi2 test)
-// in four launches instead of eight (k_ekf_M_small, k_init_invertible, 2 x k_ekf_MS, k_ekf_fact, k_ekf_WP,
+// in six launches instead of eight (k_ekf_M_small, k_init_invertible, 2 x k_ekf_MS, k_ekf_fact, k_ekf_WP,
 // k_chain_apply):
 //   k_di_M    grid over the old state's 16-row blocks (rows < Ni): P[i, I] staged once; M_up = P[:, I] H_up^T on
 //             k_ekf_MS's tiles and M3 = P[:, I] H_init^T in k_ekf_M_small's GEMV order
 //   k_di_S    S_up from M_up's rows I (k_ekf_MS's gathered tile pairs); initialize_invertible (k_init_invertible's
 //             blocks: the landmark's cross-covariance columns and 3x3 block); the landmark's rows of M_up, from
 //             the same values k_init_invertible writes, on the tiles k_ekf_MS formed from P's new rows
-//   k_ekf_fact unchanged (the chi2 gate and the factor)
-//   k_di_WP   k_ekf_WP's tile pairs; the last workgroup to finish (agent-scope release / acquire around a
-//             counter) does k_chain_apply's work: the clone / camera tables moved by dx, or a rejected
-//             candidate's slot cleared, and [accepted, negative diagonals] into out
+//   k_ekf_fact, k_ekf_WP, k_chain_apply unchanged
 // Every value is formed by the same expression, in the same order, as in the eight-launch chain (the old chain
-// stays behind UVIO_HP_DI_UNFUSED=1 for A/B runs).
+// stays behind UVIO_HP_DI_UNFUSED=1 for A/B runs; the 40-frame state digests of cfg3 and cfg3t are equal).
+// Measured and dropped: k_chain_apply folded into k_ekf_WP (the last workgroup to finish, after agent-scope
+// release / acquire fences around a completion counter, moving the tables): 22.8 us against 10.7 + 4.7 us.
 __global__ void __launch_bounds__(kMSThreads) k_di_M(const double *__restrict__ P, int ldp, int Ni,
                                               const double *__restrict__ H, int ldh, int nup, int n,
                                               const int *__restrict__ hidx, double *__restrict__ M,
-                                              double *__restrict__ M3, int *neg, int *done) {
+                                              double *__restrict__ M3, int *neg) {
   extern __shared__ double sh[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *neg = 0;
-    *done = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *neg = 0;  // the update's negative-diagonal count
   const int i0 = blockIdx.x * 16, lds = n | 1;
   double *Ps = sh;
   staged_copy(
@@ -752,115 +754,18 @@ __global__ void __launch_bounds__(kMSThreads) k_di_S(double *__restrict__ P, int
   }
 }
 
-__global__ void __launch_bounds__(256) k_di_WP(double *__restrict__ P, int ldp, int N, const double *__restrict__ M,
-                                               int r, const double *__restrict__ Linv, const double *__restrict__ y,
-                                               double *__restrict__ dx, int *neg, const int *gate, int nb, int *done,
-                                               int slot, const DFeatOut *__restrict__ fout, DClone *__restrict__ clones,
-                                               DPoseVal *__restrict__ cv, int ncl, DCam *__restrict__ cams,
-                                               DPoseVal *__restrict__ camv, int ncam, int calib_ext, int calib_intr,
-                                               double *__restrict__ out) {
-  extern __shared__ double sh[];
-  __shared__ int s_last;
-  const bool up = !gate || *gate != 0;
-  if (up) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int r16 = lane & 15, kq = lane >> 4;
-    int b = blockIdx.x, bi = 0;
-    while (b >= nb - bi) {
-      b -= nb - bi;
-      bi++;
-    }
-    const int bj = bi + b;
-    const int ldw = r | 1;
-    double *Wi = sh, *Wj = sh + 16 * ldw, *red = sh + 32 * ldw;
-    const int ei = threadIdx.x >> 4, ej = threadIdx.x & 15;
-    const int gi = 16 * bi + ei, gj = 16 * bj + ej;
-    const bool pw = gi < N && gj < N && (bi < bj || ej >= ei);
-    const double pv = pw ? P[(size_t)gi * ldp + gj] : 0.0;
-    const int nct = (r + 15) / 16, ntask = (bi == bj ? 1 : 2) * nct;
-    for (int t = wid; t < ntask; t += 4) {
-      const int which = t / nct, ct = t - which * nct;
-      double *Wd = which ? Wj : Wi;
-      const int row = 16 * (which ? bj : bi) + r16, c = 16 * ct + r16;
-      const double *Mr = M + (size_t)min(row, N - 1) * r;
-      const double *Lr = Linv + (size_t)min(c, r - 1) * r;
-      const bool rv = row < N, cv2 = c < r;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = tile_chain(
-          0, min(16 * ct + 16, r), kq, [&](int k) { return rv ? Mr[k] : 0.0; },
-          [&](int k) { return cv2 ? Lr[k] : 0.0; }, acc);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (cv2) Wd[(kq + 4 * q) * ldw + c] = acc[q];
-    }
-    __syncthreads();
-    const double *Wb = (bi == bj) ? Wi : Wj;
-    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 4 * wid; k0 < r; k0 += 16) {
-      const int k = k0 + kq;
-      const double a = (k < r) ? Wi[r16 * ldw + k] : 0.0;
-      const double bb = (k < r) ? Wb[r16 * ldw + k] : 0.0;
-      acc = mfma4(a, bb, acc);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) red[wid * 256 + (kq + 4 * q) * 16 + r16] = acc[q];
-    __syncthreads();
-    if (pw) {
-      const int e = threadIdx.x;
-      const double s = (red[e] + red[256 + e]) + (red[512 + e] + red[768 + e]);
-      const double v = pv - s;
-      P[(size_t)gi * ldp + gj] = v;
-      P[(size_t)gj * ldp + gi] = v;
-      if (gi == gj && v < 0.0) atomicAdd(neg, 1);
-    }
-    if (bi == bj && wid == 1) {
-      const int i = lane >> 2, part = lane & 3;
-      double a = 0.0;
-      for (int k = part; k < r; k += 4) a += Wi[i * ldw + k] * y[k];
-      a += __shfl_xor(a, 1, 64);
-      a += __shfl_xor(a, 2, 64);
-      if (part == 0 && 16 * bi + i < N) dx[16 * bi + i] = a;
-    }
-  }
-  // completion: every thread's stores released at agent scope before the block counts itself done
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // k_chain_apply (one workgroup): accepted -> the tables; rejected -> the slot's rows / columns over [0, N)
-  const bool acc = (!fout || fout->status == 0) && up;
-  const int t = threadIdx.x;
-  if (!acc) {
-    for (int e = t; e < 3 * N; e += blockDim.x) {
-      const int i = e / 3, a = e - 3 * i;
-      P[(size_t)(slot + a) * ldp + i] = 0.0;
-      P[(size_t)i * ldp + slot + a] = 0.0;
-    }
-  } else {
-    chain_tables_apply(t, dx, clones, cv, ncl, cams, camv, ncam, calib_ext, calib_intr);
-  }
-  if (t == 0) {
-    out[0] = acc ? 1.0 : 0.0;
-    out[1] = (double)__hip_atomic_load(neg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double *Hrow, int ldh, int nup, int n,
                          const int *hidx, double s2, EkfScratch &sc, const DFeatOut *fout, double *resout,
                          DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
                          int calib_intr, double *out) {
   if (nup <= 0 || nup + 1 > kWaveMaxRows) throw std::runtime_error("delayed-init candidate rows outside 1..255");
   if (ncl + ncam > 256) throw std::runtime_error("update chain: more clones + cameras than one workgroup");
-  if (!sc.M3 || !sc.done || !sc.chi2_gate) throw std::runtime_error("delayed-init candidate: scratch not set up");
+  if (!sc.M3 || !sc.chi2_gate) throw std::runtime_error("delayed-init candidate: scratch not set up");
   ensure_ekf_lds_attrs();
   static bool attrs = false;
   if (!attrs) {
     if (set_dyn_lds((const void *)k_di_M, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_S, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_WP, kMaxDynLds) < kMaxDynLds)
+        set_dyn_lds((const void *)k_di_S, kMaxDynLds) < kMaxDynLds)
       throw std::runtime_error("dynamic LDS limit not granted for a delayed-init kernel");
     attrs = true;
   }
@@ -871,7 +776,7 @@ void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double
   const int N = Ni + 3;
   {
     hipLaunchKernelGGL(k_di_M, dim3((Ni + 15) / 16), dim3(kMSThreads), ldsM, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
-                       sc.M, sc.M3, sc.neg, sc.done);
+                       sc.M, sc.M3, sc.neg);
     const int nt = (nup + 15) / 16, wpb = kMSThreads / 64;
     const int nbG = (nt * (nt + 1) / 2 + wpb - 1) / wpb, nbX = (3 * Ni + kDiInitThreads - 1) / kDiInitThreads;
     double *Sup = sc.S + 2 * (size_t)nup * nup;
@@ -880,10 +785,11 @@ void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double
     launch_ekf_factor(s, N, nup, Hrow + 3 * (size_t)ldh + n, ldh, sc);
     const int nb = (N + 15) / 16;
     const size_t lw = (size_t)(32 * (nup | 1) + 1024) * sizeof(double);
-    hipLaunchKernelGGL(k_di_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, nup, sc.S, sc.y, sc.dx,
-                       sc.neg, sc.chi2_gate, nb, sc.done, Ni, fout, clones, cv, ncl, cams, camv, ncam, calib_ext,
-                       calib_intr, out);
+    hipLaunchKernelGGL(k_ekf_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, nup, sc.S, sc.y, sc.dx,
+                       sc.neg, sc.chi2_gate, nb);
   }
+  launch_chain_apply(s, fout, sc.chi2_gate, sc.neg, sc.dx, clones, cv, ncl, cams, camv, ncam, calib_ext, calib_intr,
+                     nullptr, 0, P, ldp, N, Ni, out);
 }
 
 void launch_ekf_update(hipStream_t s, double *P, int ldp, int N, const double *H, int ldh, int r, int n,

@@ -139,6 +139,7 @@ class Tracker {
   void sync();
   // detection stream state: the detection functions launch on cur_ (s_, or sd_ while predetect runs)
   hipStream_t sd_ = nullptr, cur_ = nullptr;
+  bool pre_pyr_waited_ = false;  // predetect_async enqueued sd_'s wait on ev_pyr_ (the worker must not read it)
   hipEvent_t ev_pyr_ = nullptr;  // after the last pyramid launch on s_ (predetect reads that pyramid)
   bool pre_mode_ = false;
   struct PreDet {
