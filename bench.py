@@ -348,7 +348,8 @@ def committed_class_times(workload, classes):
             why = "profiles/%s does not parse" % f
             continue
         if fsha is None or fsha != sha:
-            why = "newest summary profiles/%s is of another build (%s, loaded %s)" % (f, fsha, sha)
+            if not why.startswith("newest"):
+                why = "newest summary profiles/%s is of another build (%s, loaded %s)" % (f, fsha, sha)
             continue
         if per:
             return ({c: sum(per.get(k, 0.0) for k in ks) for c, ks in classes.items()}, os.path.join("profiles", f),
