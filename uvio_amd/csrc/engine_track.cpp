@@ -1234,7 +1234,7 @@ void Tracker::predetect() {
     for (int c : last_cams_)
       if (cs_.at(c).pts_last.empty()) return;
   }
-  if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+  make_detect_stream();
   // the wait on the last pyramid launch: enqueued by predetect_async on the caller's thread (before the worker
   // starts, so the next feed's re-record of ev_pyr_ cannot come first); here when called synchronously
   if (!pyr_waited && ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
@@ -1304,10 +1304,29 @@ void Tracker::worker_loop() {
   }
 }
 
+// The detection stream.  UVIO_HP_PREDETECT_CU_MASK (experiments): hex CU-mask words, lowest CUs first ("ffffffff,0,..."),
+// restrict the run-ahead detection's kernels to those CUs (hipExtStreamCreateWithCUMask)
+void Tracker::make_detect_stream() {
+  if (sd_) return;
+  const char *m = std::getenv("UVIO_HP_PREDETECT_CU_MASK");
+  if (m && *m) {
+    std::vector<uint32_t> words;
+    for (const char *p = m; *p;) {
+      char *end = nullptr;
+      words.push_back((uint32_t)std::strtoul(p, &end, 16));
+      p = (*end == ',') ? end + 1 : end;
+      if (end == p && *p) break;
+    }
+    HP_HIP(hipExtStreamCreateWithCUMask(&sd_, (uint32_t)words.size(), words.data()));
+    return;
+  }
+  HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+}
+
 void Tracker::predetect_async() {
   predetect_join();
   HP_HIP(hipGetDevice(&dev_));  // the engine's device (bound by the calling C-ABI entry)
-  if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+  make_detect_stream();
   if (ev_pyr_) HP_HIP(hipStreamWaitEvent(sd_, ev_pyr_, 0));
   pre_pyr_waited_ = true;
   if (!worker_.joinable()) worker_ = std::thread([this] { worker_loop(); });

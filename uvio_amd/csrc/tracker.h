@@ -137,6 +137,7 @@ class Tracker {
   void alloc_pyr(CamState &c, int w, int h);
   void ensure_cap(int n);
   void sync();
+  void make_detect_stream();
   // detection stream state: the detection functions launch on cur_ (s_, or sd_ while predetect runs)
   hipStream_t sd_ = nullptr, cur_ = nullptr;
   bool pre_pyr_waited_ = false;  // predetect_async enqueued sd_'s wait on ev_pyr_ (the worker must not read it)
