@@ -1304,23 +1304,10 @@ void Tracker::worker_loop() {
   }
 }
 
-// The detection stream.  UVIO_HP_PREDETECT_CU_MASK (experiments): hex CU-mask words, lowest CUs first ("ffffffff,0,..."),
-// restrict the run-ahead detection's kernels to those CUs (hipExtStreamCreateWithCUMask)
+// The detection stream (created on first use).  Measured and dropped (gpurun_out/cum): restricting it to a CU subset
+// (hipExtStreamCreateWithCUMask, half / 7 of 8 / every other CU) left cfg3 within the run-to-run spread.
 void Tracker::make_detect_stream() {
-  if (sd_) return;
-  const char *m = std::getenv("UVIO_HP_PREDETECT_CU_MASK");
-  if (m && *m) {
-    std::vector<uint32_t> words;
-    for (const char *p = m; *p;) {
-      char *end = nullptr;
-      words.push_back((uint32_t)std::strtoul(p, &end, 16));
-      p = (*end == ',') ? end + 1 : end;
-      if (end == p && *p) break;
-    }
-    HP_HIP(hipExtStreamCreateWithCUMask(&sd_, (uint32_t)words.size(), words.data()));
-    return;
-  }
-  HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
+  if (!sd_) HP_HIP(hipStreamCreateWithFlags(&sd_, hipStreamNonBlocking));
 }
 
 void Tracker::predetect_async() {
