@@ -463,9 +463,9 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
       {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2_S,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
       {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm_mfma,k_info_cholZ,k_trinv16,"
-                     "k_trsm_lt,k_info_P,k_di_M,k_di_S,k_di_fact",
+                     "k_trsm_lt,k_info_P,k_di_M,k_di_S",
        1},
-      {"ldl", "k_ekf_fact,k_di_fact", 1},
+      {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
       {"pyramid", "k_hist_multi,k_pyr_pair", 0},
       {"fast", "k_fast_score,k_fast_select", 0},

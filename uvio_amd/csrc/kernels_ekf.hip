@@ -577,8 +577,6 @@ void launch_ekf_phaseB(hipStream_t s, double *P, int ldp, int N, int r, const do
 //             blocks: the landmark's cross-covariance columns and 3x3 block); the landmark's rows of M_up, from
 //             the same values k_init_invertible writes, on the tiles k_ekf_MS formed from P's new rows
 //   k_ekf_fact, k_ekf_WP, k_chain_apply unchanged
-// and, when the factor and the candidate's columns fit one workgroup's LDS (every BASELINE shape but cfg5's longest
-// tracks), k_di_S + k_ekf_fact as one launch (k_di_fact, below): five launches
 // Every value is formed by the same expression, in the same order, as in the eight-launch chain (the old chain
 // stays behind UVIO_HP_DI_UNFUSED=1 for A/B runs; the 40-frame state digests of cfg3 and cfg3t are equal).
 // Measured and dropped: k_chain_apply folded into k_ekf_WP (the last workgroup to finish, after agent-scope
@@ -640,7 +638,6 @@ __global__ void __launch_bounds__(kMSThreads) k_di_M(const double *__restrict__ 
   }
 }
 
-constexpr int kDiMaxCols = 512;      // k_di_fact's column map in LDS (the batch tables' canonical columns are < 512)
 constexpr int kDiInitThreads = 512;  // k_di_S's initialize_invertible blocks: (3 Ni + 511) / 512 of them
 __global__ void __launch_bounds__(kMSThreads) k_di_S(double *__restrict__ P, int ldp, int Ni,
                                               const double *__restrict__ H, int ldh, int nup, int n,
@@ -757,148 +754,6 @@ __global__ void __launch_bounds__(kMSThreads) k_di_S(double *__restrict__ P, int
   }
 }
 
-// k_di_S and k_ekf_fact in one workgroup: the S_up tile pairs (k_di_S's tiles, same operands and k order) go
-// straight into the factor's lower triangle in LDS; then k_ekf_fact's factor, y, chi2 gate and L^-1; then the
-// initialize_invertible work of k_di_S (the landmark's cross-covariance and 3x3 block, the landmark's rows of M_up)
-// on the same workgroup, gated like k_init_invertible by the linearization (the gate's value before the chi2 test).
-// Every value is formed by the same expression as in the two kernels it replaces.
-template <int W>
-__global__ void __launch_bounds__(kFactThreads) k_di_fact(double *__restrict__ P, int ldp, int Ni,
-                                                 const double *__restrict__ H, int ldh, int r, int n,
-                                                 const int *__restrict__ hidx, double s2, double *__restrict__ M,
-                                                 const double *__restrict__ M3, double *__restrict__ Linv_out,
-                                                 double *__restrict__ y_out, int *chi2_gate, double chi2_thr,
-                                                 double *__restrict__ gate_out, const DFeatOut *__restrict__ fout,
-                                                 double *__restrict__ resout) {
-  extern __shared__ double lds[];
-  __shared__ int hs[kDiMaxCols];
-  __shared__ double Hinv[9], S3[9], PLL[9], part[9][28];
-  __shared__ int s_gate_in;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  const int r16 = lane & 15, kq = lane >> 4;
-  const int ld = r | 1;
-  double *A = lds;
-  double *Dd = A + (size_t)(r + 1) * ld, *sd = Dd + r, *Pl = sd + r;
-  const double *Hup = H + 3 * (size_t)ldh;
-  if (threadIdx.x == 0) s_gate_in = *chi2_gate;  // the linearization's gate, before the chi2 test below
-  for (int k = threadIdx.x; k < n; k += blockDim.x) hs[k] = hidx[k];
-  for (int k = threadIdx.x; k < r; k += blockDim.x) A[(size_t)r * ld + k] = Hup[(size_t)k * ldh + n];
-  __syncthreads();
-  {
-    const int nt = (r + 15) / 16, npair = nt * (nt + 1) / 2;
-    for (int pair0 = wid; pair0 < npair; pair0 += nwv) {
-      int pair = pair0, at = 0;
-      while (pair >= nt - at) {
-        pair -= nt - at;
-        at++;
-      }
-      const int bt = at + pair;
-      const int ar = 16 * at + r16, br = 16 * bt + r16;
-      const double *Ha = Hup + (size_t)min(ar, r - 1) * ldh;
-      const double *Tb = M + min(br, r - 1);
-      const bool av = ar < r, bv = br < r;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = tile_chain<16>(
-          0, n, kq, [&](int k) { return av ? Ha[k] : 0.0; }, [&](int k) { return bv ? Tb[(size_t)hs[k] * r] : 0.0; },
-          acc);
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int row = 16 * at + kq + 4 * q, col = 16 * bt + r16;
-        if (row < r && col < r && row <= col) A[(size_t)col * ld + row] = acc[q] + (row == col ? s2 : 0.0);
-      }
-    }
-  }
-  __syncthreads();
-  ldl_wave_inv<1, SqLayout, W>(A, SqLayout{ld}, r, r + 1, Dd, true);
-  for (int k = threadIdx.x; k < r; k += blockDim.x) {
-    const double q = sqrt(Dd[k]);
-    sd[k] = q;
-    y_out[k] = A[(size_t)r * ld + k] * q;
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    double sacc = 0.0;
-    for (int k = threadIdx.x; k < r; k += 64) {
-      const double v = A[(size_t)r * ld + k] * sd[k];
-      sacc += v * v;
-    }
-    for (int o = 32; o > 0; o >>= 1) sacc += __shfl_down(sacc, o, 64);
-    if (threadIdx.x == 0) {
-      const int acc = (s_gate_in != 0) && !(sacc > chi2_thr);
-      *chi2_gate = acc;
-      gate_out[0] = sacc;
-      gate_out[1] = acc;
-    }
-  }
-  for (int e = threadIdx.x; e < r * r; e += blockDim.x) {
-    const int a = e / r, b = e - a * r;
-    double v = 0.0;
-    if (b < a)
-      v = A[(size_t)b * ld + a] / sd[a];
-    else if (b == a)
-      v = 1.0 / sd[a];
-    Linv_out[e] = v;
-  }
-  // initialize_invertible (k_init_invertible with N = Ni) and the landmark's rows Ni .. Ni+2 of M_up
-  if (resout && threadIdx.x < 3) resout[threadIdx.x] = H[(size_t)threadIdx.x * ldh + n];
-  if (s_gate_in == 0) return;
-  if (threadIdx.x == 0) inv3_cofactor(fout->HfR, Hinv);
-  {
-    const int e = threadIdx.x / 28, j = threadIdx.x % 28;
-    if (e < 9) {
-      const int a = e / 3, bb = e % 3;
-      double acc = 0.0;
-      for (int k = j; k < n; k += 28) acc += H[(size_t)a * ldh + k] * M3[(size_t)hs[k] * 3 + bb];
-      part[e][j] = acc;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 9) {
-    const int a = threadIdx.x / 3, bb = threadIdx.x % 3;
-    double acc = 0.0;
-    for (int q = 0; q < 28; q++) acc += part[threadIdx.x][q];
-    S3[threadIdx.x] = acc + (a == bb ? s2 : 0.0);
-  }
-  for (int e = threadIdx.x; e < 3 * n; e += blockDim.x) {
-    const int a = e / n, k = e - a * n, i = hs[k];
-    double acc = 0.0;
-    for (int bb = 0; bb < 3; bb++) acc += M3[(size_t)i * 3 + bb] * Hinv[a * 3 + bb];
-    Pl[e] = -acc;
-  }
-  __syncthreads();
-  if (threadIdx.x < 9) {
-    const int a = threadIdx.x / 3, bb = threadIdx.x % 3;
-    double acc = 0.0;
-    for (int c = 0; c < 3; c++)
-      for (int e2 = 0; e2 < 3; e2++) {
-        const double sce = (c <= e2) ? S3[c * 3 + e2] : S3[e2 * 3 + c];
-        acc += Hinv[a * 3 + c] * sce * Hinv[bb * 3 + e2];
-      }
-    P[(size_t)(Ni + a) * ldp + Ni + bb] = acc;
-  }
-  for (int t = threadIdx.x; t < Ni * 3; t += blockDim.x) {
-    const int i = t / 3, a = t % 3;
-    double acc = 0.0;
-    for (int bb = 0; bb < 3; bb++) acc += M3[(size_t)i * 3 + bb] * Hinv[a * 3 + bb];
-    P[(size_t)i * ldp + Ni + a] = -acc;
-    P[(size_t)(Ni + a) * ldp + i] = -acc;
-  }
-  const int nct = (r + 15) / 16;
-  for (int t = wid; t < nct; t += nwv) {
-    const int j0 = 16 * t, jr = j0 + r16;
-    const double *Hr = Hup + (size_t)min(jr, r - 1) * ldh;
-    const bool jv = jr < r, rv = r16 < 3;
-    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = tile_chain<16>(
-        0, n, kq, [&](int k) { return rv ? Pl[r16 * n + k] : 0.0; }, [&](int k) { return jv ? Hr[k] : 0.0; }, acc);
-    const int col = j0 + r16;
-    if (kq < 3 && col < r) M[(size_t)(Ni + kq) * r + col] = acc[0];
-  }
-}
-static size_t di_fact_lds_bytes(int r, int n) {
-  return ((size_t)(r + 1) * (r | 1) + 2 * (size_t)r + 3 * (size_t)n) * sizeof(double);
-}
-
 void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double *Hrow, int ldh, int nup, int n,
                          const int *hidx, double s2, EkfScratch &sc, const DFeatOut *fout, double *resout,
                          DClone *clones, DPoseVal *cv, int ncl, DCam *cams, DPoseVal *camv, int ncam, int calib_ext,
@@ -910,12 +765,7 @@ void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double
   static bool attrs = false;
   if (!attrs) {
     if (set_dyn_lds((const void *)k_di_M, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_S, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_fact<1>, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_fact<2>, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_fact<3>, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_fact<4>, kMaxDynLds) < kMaxDynLds ||
-        set_dyn_lds((const void *)k_di_fact<5>, kMaxDynLds) < kMaxDynLds)
+        set_dyn_lds((const void *)k_di_S, kMaxDynLds) < kMaxDynLds)
       throw std::runtime_error("dynamic LDS limit not granted for a delayed-init kernel");
     attrs = true;
   }
@@ -927,24 +777,12 @@ void launch_di_candidate(hipStream_t s, double *P, int ldp, int Ni, const double
   {
     hipLaunchKernelGGL(k_di_M, dim3((Ni + 15) / 16), dim3(kMSThreads), ldsM, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
                        sc.M, sc.M3, sc.neg);
-    const size_t ldsF = di_fact_lds_bytes(nup, n);
-    static const bool split = std::getenv("UVIO_HP_DI_SPLIT") != nullptr;  // k_di_S + k_ekf_fact (A/B)
-    if (!split && ldsF <= (size_t)kMaxDynLds && n <= kDiMaxCols) {
-      KScope ks(sc.kp, KC_LDL);
-      const int w = panel_waves(nup + 1);
-      auto *kf = w == 1 ? k_di_fact<1> : w == 2 ? k_di_fact<2> : w == 3 ? k_di_fact<3> : w == 4 ? k_di_fact<4>
-                                                                                             : k_di_fact<5>;
-      hipLaunchKernelGGL(kf, dim3(1), dim3(kFactThreads), ldsF, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx, s2, sc.M,
-                         sc.M3, sc.S, sc.y, sc.chi2_gate, sc.chi2_thr, sc.dx + N, fout, resout);
-      if (sc.kp) sc.kp->credit(KC_LDL, (double)nup * nup * nup / 3.0 + (double)nup * nup, 8.0 * (1.5 * nup * nup + 2.0 * nup));
-    } else {
-      const int nt = (nup + 15) / 16, wpb = kMSThreads / 64;
-      const int nbG = (nt * (nt + 1) / 2 + wpb - 1) / wpb, nbX = (3 * Ni + kDiInitThreads - 1) / kDiInitThreads;
-      double *Sup = sc.S + 2 * (size_t)nup * nup;
-      hipLaunchKernelGGL(k_di_S, dim3(nbG + nbX + 1), dim3(kMSThreads), ldsS, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
-                         s2, sc.M, sc.M3, Sup, fout, sc.chi2_gate, resout, nbG, nbX);
-      launch_ekf_factor(s, N, nup, Hrow + 3 * (size_t)ldh + n, ldh, sc);
-    }
+    const int nt = (nup + 15) / 16, wpb = kMSThreads / 64;
+    const int nbG = (nt * (nt + 1) / 2 + wpb - 1) / wpb, nbX = (3 * Ni + kDiInitThreads - 1) / kDiInitThreads;
+    double *Sup = sc.S + 2 * (size_t)nup * nup;
+    hipLaunchKernelGGL(k_di_S, dim3(nbG + nbX + 1), dim3(kMSThreads), ldsS, s, P, ldp, Ni, Hrow, ldh, nup, n, hidx,
+                       s2, sc.M, sc.M3, Sup, fout, sc.chi2_gate, resout, nbG, nbX);
+    launch_ekf_factor(s, N, nup, Hrow + 3 * (size_t)ldh + n, ldh, sc);
     const int nb = (N + 15) / 16;
     const size_t lw = (size_t)(32 * (nup | 1) + 1024) * sizeof(double);
     hipLaunchKernelGGL(k_ekf_WP, dim3(nb * (nb + 1) / 2), dim3(256), lw, s, P, ldp, N, sc.M, nup, sc.S, sc.y, sc.dx,
