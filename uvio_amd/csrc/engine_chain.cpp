@@ -62,6 +62,9 @@ struct Engine::ChainItem {
   int kind = 0;  // 0 MSCKF, 1 SLAM chunk, 2 delayed-init triangulation, 3 delayed-init candidates
   Engine::Batch b;
   std::vector<FeatP> fv;
+  // feature-sharded MSCKF batch (RCCL): fv is this rank's chunk of fv_all, the Gram is all-reduced in the chain
+  bool sharded = false;
+  std::vector<FeatP> fv_all;
   int region = -1;  // d_.chain region of its update (-1: none enqueued)
   int m = 0;        // stacked rows
   // the batch's staged tables (device addresses after the flush)
@@ -224,14 +227,28 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     HPROF("chain.msckf.build");
     auto it = std::make_unique<ChainItem>();
     it->kind = 0;
-    it->fv = up;
+    size_t lo = 0, hi = up.size();
+    if (shard_.enabled && shard_.nccl && (int)up.size() >= shard_.min_features) {
+      // UpdaterMSCKF::update split across the ranks inside the chain (shard.cpp: the same partition, pack and
+      // all-reduce as msckf_update_sharded; the all-reduce is enqueued on the chain's stream by RCCL)
+      std::vector<int> rows(up.size()), bounds(shard_.world + 1);
+      for (size_t i = 0; i < up.size(); i++) rows[i] = 2 * up[i]->count() - 3;
+      shard_partition(rows.data(), (int)up.size(), shard_.world, bounds.data());
+      lo = (size_t)bounds[shard_.rank];
+      hi = (size_t)bounds[shard_.rank + 1];
+      it->sharded = true;
+      it->fv_all = up;
+      it->fv.assign(up.begin() + lo, up.begin() + hi);
+    } else {
+      it->fv = up;
+    }
     {
       HPROF("chain.msckf.build.tables");
       build_clone_cam_tables(it->b, false);
     }
     {
       HPROF("chain.msckf.build.add");
-      add_features_to_batch(it->b, up, 0, up.size(), 0, o_.feat_rep_msckf);
+      add_features_to_batch(it->b, up, lo, hi, 0, o_.feat_rep_msckf);
     }
     msk = it.get();
     items.push_back(std::move(it));
@@ -365,15 +382,56 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
                        sc.dx + N_ + 8);
   };
 
+  // the sharded MSCKF update: this rank's Gram packed with its accepted count and rows, all-reduced over the ranks
+  // (every rank enqueues it, rows or not: it is a collective), then the information-form update of the summed
+  // Gram on every rank; the totals [accepted, rows] go to the region (N + 10, N + 11) for the replay
+  auto enqueue_sharded_update = [&](ChainItem &it, double s2) {
+    Batch &b = it.b;
+    const int m = b.rows, n = b.n_canon, ncol = n + 1;
+    it.region = new_region();
+    EkfScratch sc = d_.ekf;
+    sc.dx = region(it.region);
+    sc.gate = d_.acc;
+    int nch = 0;
+    if (m > 0) gram(m, ncol, &nch);
+    launch_shard_pack(d_.stream, d_.partials, nch, ncol, d_.fout + b.fout_off, (int)b.feats.size(), d_.acc, d_.shard);
+    shard_allreduce(d_.shard, (size_t)ncol * ncol + 2);
+    launch_shard_unpack(d_.stream, d_.shard, ncol, d_.acc);
+    HP_HIP(hipMemcpyAsync(sc.dx + N_ + 10, d_.shard + (size_t)ncol * ncol, 2 * sizeof(double), hipMemcpyDeviceToDevice,
+                          d_.stream));
+    const bool inflight = d_.pre_N >= 0;
+    const bool pre = inflight && d_.pre_N == N_ && d_.pre_hidx == b.hidx && d_.pre_epoch == p_epoch_;
+    d_.pre_hidx.clear();
+    d_.pre_N = -1;
+    if (pre) {
+      HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
+      KScope ks(&kprof_, KC_EKF);
+      launch_ekf_info_post(d_.stream, d_.P, d_.ldp, N_, d_.shard, 1, n, s2, d_.R, sc);
+    } else {
+      if (inflight) HP_HIP(hipStreamWaitEvent(d_.stream, d_.ev_aux_out, 0));
+      KScope ks(&kprof_, KC_EKF);
+      launch_ekf_info(d_.stream, d_.P, d_.ldp, N_, d_.shard, 1, n, b.hidx_dev, s2, d_.R, sc);
+    }
+    kprof_.credit(KC_EKF, ekf_flops(N_, n, n) - (pre ? (double)n * n * n / 3.0 + (double)N_ * n * n : 0.0),
+                  ekf_bytes(N_, n, n));
+    ++p_epoch_;
+    launch_chain_apply(d_.stream, nullptr, d_.acc, sc.neg, sc.dx, fr_cl, fr_cv, ncl, fr_cam, fr_camv, ncam,
+                       o_.do_calib_camera_pose, o_.do_calib_camera_intrinsics, fr_xv, N_, d_.P, d_.ldp, N_, -1,
+                       sc.dx + N_ + 8);
+  };
+
   // ---- 3) UpdaterMSCKF::update
   auto tl0 = clk::now();
   if (msk) {
     HPROF("chain.msckf");
     PrefactorJoin pj(this);
-    if (msk->b.rows > msk->b.n_canon || msk->b.rows > kMaxEkfRows) info_prefactor(msk->b.hidx);
+    if (msk->sharded || msk->b.rows > msk->b.n_canon || msk->b.rows > kMaxEkfRows) info_prefactor(msk->b.hidx);
     const double s2 = o_.msckf_sigma_pix * o_.msckf_sigma_pix;
     enqueue_batch(*msk, 0, s2, o_.msckf_chi2_multipler, true, nullptr);
-    if (msk->m >= 1) enqueue_update(*msk, s2);
+    if (msk->sharded)
+      enqueue_sharded_update(*msk, s2);
+    else if (msk->m >= 1)
+      enqueue_update(*msk, s2);
   }
   // ---- 1b) the SLAM chunks' and the delayed initialization's batches (host, while the MSCKF update runs)
   auto tb1 = clk::now();
@@ -576,6 +634,7 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     ChainItem &it = *itp;
     if (it.kind == 0) {
       finish_batch(it.b, 0, outs);
+      for (auto &f : it.fv_all) f->to_delete = true;  // sharded: every rank's features leave the database
       int acc = 0, acc_rows = 0;
       for (size_t i = 0; i < outs.size(); i++) {
         last_msckf_.push_back(FeatDebug{it.fv[i]->featid, {outs[i].p_FinG[0], outs[i].p_FinG[1], outs[i].p_FinG[2]},
@@ -590,6 +649,10 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
       if (it.region >= 0) {
         const double *base = d_.region_host(it.region);
         neg_check(base, N_);
+        if (it.sharded) {  // the update's acceptance and rows are every rank's (the all-reduced totals)
+          acc = base[N_ + 8] > 0.5 ? 1 : 0;
+          timing_.msckf_rows = (int)(base[N_ + 11] + 0.5);
+        }
         if (acc > 0) apply_dx(base);
       }
     } else if (it.kind == 1) {

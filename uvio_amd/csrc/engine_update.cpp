@@ -627,7 +627,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       for (auto &f : h) f->held = false;
     }
   } held_guard{*this, held};
-  if (!shard_.enabled && !no_chain_) {
+  // the chain also carries the RCCL-sharded MSCKF update (its all-reduce is enqueued); the host all-reduce (a
+  // callback mid-update) keeps the per-updater path
+  if ((!shard_.enabled || shard_.nccl) && !no_chain_) {
     if (do_clean) {
       held = pending_delete_;
       for (auto &f : held) f->held = true;
