@@ -1050,7 +1050,9 @@ __device__ __forceinline__ void wave_sum_rows_i32(const int (&v)[N], long long (
 }
 constexpr int kLkMargin = 4, kLkMaxWin = 16, kLkMaxTile = kLkMaxWin + 1 + 2 * kLkMargin;
 static_assert(kLkMaxWin * kLkMaxWin <= 4 * 64, "wave_sum_rows_i32 bound: at most 4 window pixels per lane");
-// one 64-lane workgroup per point; lanes own window pixels lane, lane+64, ... (225 for win 15).
+// one 64-lane workgroup per point; lanes own window pixels lane, lane+64, ... (225 for win 15).  (Round 6, measured
+// and dropped: the point on four wavefronts, one window pixel per thread and the wave partials summed through LDS
+// behind one barrier per sum -- bit-identical, 76.4 against 68 us per launch at cfg3, gpurun_out/r06h.)
 // (qx, qy) is nextPts[ptidx] of LKTrackerInvoker: it carries the result between levels, and an
 // early exit leaves it at its last written value, exactly as the oracle's p1[pi].
 #ifdef UVHP_LK_PROF
@@ -1314,233 +1316,6 @@ __device__ __forceinline__ float2 lk_point(const DPyr &prev, const DPyr &next, c
 #endif
   }
   return make_float2(qx, qy);  // the result every lane holds (wave-uniform)
-}
-
-// The same point on FOUR wavefronts (256 threads, one window pixel per thread for win <= 16): per iteration a
-// thread gathers 4 taps instead of 16, and the window sums add each wave's DPP row sums (exact int64, so the
-// order of the partials does not matter) through LDS with one barrier -- the same integers, hence the same
-// float results, as lk_point.  The iteration is a chain of dependent steps, so the shorter per-thread work
-// shortens the launch, whose length is its slowest point's (<= 30 iterations on each of 6 levels).
-constexpr int kLkWaves = 4, kLkThreads = 64 * kLkWaves;
-static_assert(kLkMaxWin * kLkMaxWin <= kLkThreads, "one window pixel per thread");
-template <int N>
-__device__ __forceinline__ void block_sum_i32(const int (&v)[N], long long (&out)[N], long long (*red)[kLkWaves][4]) {
-  long long w[N];
-  wave_sum_rows_i32<N>(v, w);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < N; k++) red[0][wave][k] = w[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < N; k++) out[k] = (red[0][0][k] + red[0][1][k]) + (red[0][2][k] + red[0][3][k]);
-}
-__device__ __forceinline__ float2 lk_point4(const DPyr &prev, const DPyr &next, const float *__restrict__ p0,
-                                          float *__restrict__ p1, uint8_t *__restrict__ status, int pi, int win,
-                                          int max_level, int max_iters, float crit_eps, int init_from_p0,
-                                          unsigned long long *bytes) {
-  const int tid = threadIdx.x;
-  const int maxL = min(max_level, min(prev.levels, next.levels) - 1);
-  const float halfw = (win - 1) * 0.5f;
-  const float FLT_SCALE = 1.f / (1 << 20);
-  const float WSCALE = (float)(1 << 14);
-  const int area = win * win;
-  const bool own = tid < area;
-  int Iw = 0, dIx = 0, dIy = 0;
-  __shared__ uint8_t Jt[kLkMaxTile * kLkMaxTile];
-  // the window sums' per-wave partials, double-buffered by use so one barrier per sum suffices
-  __shared__ long long red[2][kLkWaves][4];
-  int rb = 0;
-  const int S = win + 1 + 2 * kLkMargin;
-  const int e0 = min(tid, area - 1), wy = e0 / win, wx = e0 - wy * win, jo = wy * S + wx;
-  constexpr int kStageN = (kLkMaxTile * kLkMaxTile + kLkThreads - 1) / kLkThreads;
-  int sx[kStageN], sy[kStageN];
-#pragma unroll
-  for (int k = 0; k < kStageN; k++) {
-    const int e = min(tid + kLkThreads * k, S * S - 1);
-    sy[k] = e / S;
-    sx[k] = e - sy[k] * S;
-  }
-  float qx = init_from_p0 ? p0[2 * pi] : p1[2 * pi], qy = init_from_p0 ? p0[2 * pi + 1] : p1[2 * pi + 1];
-  uint8_t st = 1;
-  int nlev = 0, nit = 0;
-  const float p0x = p0[2 * pi], p0y = p0[2 * pi + 1];
-  int gi[4], gd[4], gm;  // this thread's pixel: the template's four taps, derivative taps, inside-level mask
-  auto gather = [&](int l) {
-    const uint8_t *I = prev.img[l];
-    const int *d32 = reinterpret_cast<const int *>(prev.der[l]);
-    const int Iw_ = prev.w[l], Ih_ = prev.h[l];
-    const float sc = (float)(1. / (1 << l));
-    float prx = p0x * sc, pry = p0y * sc;
-    prx -= halfw;
-    pry -= halfw;
-    const int ipx = min(max((int)floorf(prx), -win), Iw_ - 1), ipy = min(max((int)floorf(pry), -win), Ih_ - 1);
-    if (ipx >= 0 && ipx + win < Iw_ && ipy >= 0 && ipy + win < Ih_) {
-      const size_t o = (size_t)(ipy + wy) * Iw_ + ipx + wx;
-      gi[0] = I[o];
-      gi[1] = I[o + 1];
-      gi[2] = I[o + Iw_];
-      gi[3] = I[o + Iw_ + 1];
-      gd[0] = d32[o];
-      gd[1] = d32[o + 1];
-      gd[2] = d32[o + Iw_];
-      gd[3] = d32[o + Iw_ + 1];
-      gm = 0xf;
-      return;
-    }
-    const int X = ipx + wx, Y = ipy + wy;
-    const int rx0 = reflect101(X, Iw_), rx1 = reflect101(X + 1, Iw_);
-    const size_t ry0 = (size_t)reflect101(Y, Ih_) * Iw_, ry1 = (size_t)reflect101(Y + 1, Ih_) * Iw_;
-    gi[0] = I[ry0 + rx0];
-    gi[1] = I[ry0 + rx1];
-    gi[2] = I[ry1 + rx0];
-    gi[3] = I[ry1 + rx1];
-    const int cx0 = min(max(X, 0), Iw_ - 1), cx1 = min(max(X + 1, 0), Iw_ - 1);
-    const size_t cy0 = (size_t)min(max(Y, 0), Ih_ - 1) * Iw_, cy1 = (size_t)min(max(Y + 1, 0), Ih_ - 1) * Iw_;
-    gd[0] = d32[cy0 + cx0];
-    gd[1] = d32[cy0 + cx1];
-    gd[2] = d32[cy1 + cx0];
-    gd[3] = d32[cy1 + cx1];
-    const bool vx0 = X >= 0 && X < Iw_, vx1 = X + 1 >= 0 && X + 1 < Iw_;
-    const bool vy0 = Y >= 0 && Y < Ih_, vy1 = Y + 1 >= 0 && Y + 1 < Ih_;
-    gm = (vx0 && vy0) | (vx1 && vy0) << 1 | (vx0 && vy1) << 2 | (vx1 && vy1) << 3;
-  };
-  if (maxL >= 0) gather(maxL);
-  for (int level = maxL; level >= 0; level--) {
-    const uint8_t *J = next.img[level];
-    const int Iw_ = prev.w[level], Ih_ = prev.h[level], Jw_ = next.w[level], Jh_ = next.h[level];
-    const float sc = (float)(1. / (1 << level));
-    float prx = p0x * sc, pry = p0y * sc;
-    if (level == maxL) {
-      qx = qx * sc;
-      qy = qy * sc;
-    } else {
-      qx = qx * 2.f;
-      qy = qy * 2.f;
-    }
-    prx -= halfw;
-    pry -= halfw;
-    const int ipx = (int)floorf(prx), ipy = (int)floorf(pry);
-    if (ipx < -win || ipx >= Iw_ || ipy < -win || ipy >= Ih_) {
-      if (level == 0) st = 0;
-      if (level > 0) gather(level - 1);
-      continue;
-    }
-    float a = prx - ipx, b = pry - ipy;
-    int iw00 = (int)rintf((1.f - a) * (1.f - b) * WSCALE);
-    int iw01 = (int)rintf(a * (1.f - b) * WSCALE);
-    int iw10 = (int)rintf((1.f - a) * b * WSCALE);
-    int iw11 = (1 << 14) - iw00 - iw01 - iw10;
-    {
-      const int ival = descale(dot4_i24(gi[0], gi[1], gi[2], gi[3], iw00, iw01, iw10, iw11), 14 - 5);
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (!(gm >> k & 1)) gd[k] = 0;
-      auto lo = [](int v) { return (int)(int16_t)(v & 0xffff); };
-      auto hi = [](int v) { return v >> 16; };
-      const int ixv = descale(dot4_i24(lo(gd[0]), lo(gd[1]), lo(gd[2]), lo(gd[3]), iw00, iw01, iw10, iw11), 14);
-      const int iyv = descale(dot4_i24(hi(gd[0]), hi(gd[1]), hi(gd[2]), hi(gd[3]), iw00, iw01, iw10, iw11), 14);
-      Iw = own ? (int16_t)ival : 0;
-      dIx = own ? (int16_t)ixv : 0;
-      dIy = own ? (int16_t)iyv : 0;
-    }
-    if (level > 0) gather(level - 1);
-    long long s3[3];
-    block_sum_i32<3>({dIx * dIx, dIx * dIy, dIy * dIy}, s3, red + rb);
-    rb ^= 1;
-    const float A11 = (float)s3[0] * FLT_SCALE, A12 = (float)s3[1] * FLT_SCALE, A22 = (float)s3[2] * FLT_SCALE;
-    float D = A11 * A22 - A12 * A12;
-    const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
-    if (minEig < 1e-4f || D < 1.19209290e-07f) {
-      if (level == 0) st = 0;
-      continue;
-    }
-    D = 1.f / D;
-    nlev++;
-    float nx = qx - halfw, ny = qy - halfw;
-    float pdx = 0.f, pdy = 0.f;
-    int ox = -(1 << 28), oy = -(1 << 28);
-    for (int j = 0; j < max_iters; j++) {
-      const int inx = (int)floorf(nx), iny = (int)floorf(ny);
-      if (inx < -win || inx >= Jw_ || iny < -win || iny >= Jh_) {
-        if (level == 0) st = 0;
-        break;
-      }
-      if (inx - ox < 0 || inx - ox > 2 * kLkMargin || iny - oy < 0 || iny - oy > 2 * kLkMargin) {
-        __syncthreads();
-        ox = inx - kLkMargin;
-        oy = iny - kLkMargin;
-        uint8_t v[kStageN];
-        if (ox >= 0 && ox + S <= Jw_ && oy >= 0 && oy + S <= Jh_) {
-#pragma unroll
-          for (int k = 0; k < kStageN; k++) v[k] = J[(size_t)(oy + sy[k]) * Jw_ + ox + sx[k]];
-        } else {
-#pragma unroll
-          for (int k = 0; k < kStageN; k++) v[k] = J[(size_t)reflect101(oy + sy[k], Jh_) * Jw_ + reflect101(ox + sx[k], Jw_)];
-        }
-#pragma unroll
-        for (int k = 0; k < kStageN; k++)
-          if (tid + kLkThreads * k < S * S) Jt[tid + kLkThreads * k] = v[k];
-        __syncthreads();
-      }
-      a = nx - inx;
-      b = ny - iny;
-      iw00 = (int)rintf((1.f - a) * (1.f - b) * WSCALE);
-      iw01 = (int)rintf(a * (1.f - b) * WSCALE);
-      iw10 = (int)rintf((1.f - a) * b * WSCALE);
-      iw11 = (1 << 14) - iw00 - iw01 - iw10;
-      nit++;
-      const uint8_t *t = Jt + (iny - oy) * S + (inx - ox) + jo;
-      const int diff = descale(dot4_i24(t[0], t[1], t[S], t[S + 1], iw00, iw01, iw10, iw11), 14 - 5) - Iw;
-      long long s2[2];
-      block_sum_i32<2>({diff * dIx, diff * dIy}, s2, red + rb);
-      rb ^= 1;
-      const float b1 = (float)s2[0] * FLT_SCALE, b2 = (float)s2[1] * FLT_SCALE;
-      const float dx = (A12 * b2 - A22 * b1) * D;
-      const float dy = (A12 * b1 - A11 * b2) * D;
-      nx += dx;
-      ny += dy;
-      qx = nx + halfw;
-      qy = ny + halfw;
-      const float e2 = dx * dx + dy * dy;
-      bool conv = e2 < crit_eps * 0.9999f;
-      if (!conv && !(e2 > crit_eps * 1.0001f)) conv = (double)dx * dx + (double)dy * dy <= (double)crit_eps;
-      if (conv) break;
-      if (j > 0 && fabsf(dx + pdx) < 0.01f && fabsf(dy + pdy) < 0.01f) {
-        qx -= dx * 0.5f;
-        qy -= dy * 0.5f;
-        break;
-      }
-      pdx = dx;
-      pdy = dy;
-    }
-  }
-  if (tid == 0) {
-    p1[2 * pi] = qx;
-    p1[2 * pi + 1] = qy;
-    status[pi] = st;
-    if (bytes) atomicAdd(bytes, (unsigned long long)(256 * (5 * nlev + nit)));
-  }
-  return make_float2(qx, qy);
-}
-
-__global__ void __launch_bounds__(kLkThreads) k_lk4(LkSlots job, int win, int max_level, int max_iters,
-                                                    float crit_eps, int init_from_p0) {
-  const int idx = xcd_contiguous(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-  const int slot = idx / gridDim.x, p = idx - slot * gridDim.x;
-  if (p >= job.n[slot]) return;
-  const float2 q = lk_point4(job.prev[slot], job.next[slot], job.p0[slot], job.p1[slot], job.st[slot], p, win,
-                             max_level, max_iters, crit_eps, init_from_p0, job.bytes);
-  if (job.undistort && threadIdx.x < 2) {  // RANSAC's undistortion of this point, the k_undistort formula
-    const int w = threadIdx.x;
-    const float px = w ? q.x : job.p0[slot][2 * p], py = w ? q.y : job.p0[slot][2 * p + 1];
-    float x, y;
-    const bool amb = cam_undistort_f(w ? job.c1[slot] : job.c0[slot], px, py, x, y);
-    float *out = w ? job.p1n[slot] : job.p0n[slot];
-    out[2 * p] = x;
-    out[2 * p + 1] = y;
-    if (w && job.p1amb[slot]) job.p1amb[slot][p] = amb ? 1 : 0;
-  }
 }
 
 // one point of one slot per workgroup (both cameras' temporal tracks in one launch).  Consecutive points (the
@@ -1918,13 +1693,8 @@ void launch_lk(hipStream_t s, const LkSlots &job, int nslot, int win, int max_le
   for (int k = 0; k < nslot; k++) nmax = max(nmax, job.n[k]);
   if (nmax <= 0) return;
   if (win > kLkMaxWin) throw std::runtime_error("LK window larger than the kernel supports");
-  static const bool one_wave = std::getenv("UVIO_HP_LK_1WAVE") != nullptr;  // the one-wavefront kernel (A/B)
-  if (one_wave)
-    hipLaunchKernelGGL(k_lk, dim3(nmax, nslot), dim3(64), 0, s, job, win, max_level, max_iters, eps * eps,
-                       init_from_p0 ? 1 : 0);
-  else
-    hipLaunchKernelGGL(k_lk4, dim3(nmax, nslot), dim3(kLkThreads), 0, s, job, win, max_level, max_iters, eps * eps,
-                       init_from_p0 ? 1 : 0);
+  hipLaunchKernelGGL(k_lk, dim3(nmax, nslot), dim3(64), 0, s, job, win, max_level, max_iters, eps * eps,
+                     init_from_p0 ? 1 : 0);
 }
 
 void launch_ransac(hipStream_t s, const RansacSlots &job, int nslot, int max_iters, double conf, bool undistorted) {
