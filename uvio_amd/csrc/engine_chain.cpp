@@ -228,9 +228,9 @@ int Engine::update_frame(std::vector<FeatP> &up, std::vector<FeatP> &slam_upd, s
     auto it = std::make_unique<ChainItem>();
     it->kind = 0;
     size_t lo = 0, hi = up.size();
-    if (shard_.enabled && shard_.nccl && (int)up.size() >= shard_.min_features) {
+    if (shard_.enabled && (int)up.size() >= shard_.min_features) {
       // UpdaterMSCKF::update split across the ranks inside the chain (shard.cpp: the same partition, pack and
-      // all-reduce as msckf_update_sharded; the all-reduce is enqueued on the chain's stream by RCCL)
+      // all-reduce as msckf_update_sharded; over RCCL the all-reduce is enqueued on the chain's stream)
       std::vector<int> rows(up.size()), bounds(shard_.world + 1);
       for (size_t i = 0; i < up.size(); i++) rows[i] = 2 * up[i]->count() - 3;
       shard_partition(rows.data(), (int)up.size(), shard_.world, bounds.data());

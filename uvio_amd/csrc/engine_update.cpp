@@ -627,9 +627,9 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
       for (auto &f : h) f->held = false;
     }
   } held_guard{*this, held};
-  // the chain also carries the RCCL-sharded MSCKF update (its all-reduce is enqueued); the host all-reduce (a
-  // callback mid-update) keeps the per-updater path
-  if ((!shard_.enabled || shard_.nccl) && !no_chain_) {
+  // the chain also carries the feature-sharded MSCKF update: over RCCL its all-reduce is enqueued; the host
+  // all-reduce (a callback, for ranks that share a GPU) waits for this rank's Gram in the middle of the enqueueing
+  if (!no_chain_) {
     if (do_clean) {
       held = pending_delete_;
       for (auto &f : held) f->held = true;
