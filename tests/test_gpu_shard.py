@@ -11,6 +11,9 @@
   per-feature results are its shard of the oracle's), the replicas' states and covariances are bit-identical
   after every frame, and the shards are disjoint and together make up the oracle's update.
 * world 2 on the EuRoC stream: the sharded run agrees with an unsharded run of the same stream.
+* world 4 with at most 2 MSCKF features per update: every update leaves ranks with an empty chunk (no feature
+  kernel, no rows, a zero Gram and a zero accepted count in the all-reduce); the replicas stay bit-identical and
+  agree with an unsharded run.
 """
 import hashlib
 import os
@@ -29,8 +32,8 @@ EUROC = os.path.join(ROOT, "configs", "euroc_mav", "estimator_config.yaml")
 N_FRAMES = 30
 
 
-def _opts(U):
-    return U.load_options(EUROC, max_msckf_in_update=200, max_slam_features=20, max_slam_in_update=10,
+def _opts(U, max_msckf=200):
+    return U.load_options(EUROC, max_msckf_in_update=max_msckf, max_slam_features=20, max_slam_in_update=10,
                           dt_slam_delay=0.3)
 
 
@@ -61,7 +64,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, max_msckf=200):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -70,7 +73,7 @@ def _rank(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import uvio_amd as U
-    opts = _opts(U)
+    opts = _opts(U, max_msckf)
     s = _stream(opts)
     g = U.VioManager(opts, device=0)
     g.enable_feature_sharding(rank, world, backend="host", min_features=1)
@@ -120,6 +123,43 @@ def test_sharded_world2_gloo_one_gpu():
     for (x, _, nm, rows, _), (xr, tr) in zip(f0, ref):
         assert nm == tr["n_msckf"]
     assert _rel(f0[-1][0], ref[-1][0]) < 1e-6
+
+
+def test_sharded_more_ranks_than_features():
+    import uvio_amd as U
+    world, cap = 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, cap)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    frames = [o[1] for o in out]
+    assert all(len(f) == N_FRAMES for f in frames)
+    empty = updates = 0
+    for k in range(N_FRAMES):
+        frs = [f[k] for f in frames]
+        assert all(np.array_equal(frs[0][0], fr[0]) and np.array_equal(frs[0][1], fr[1]) for fr in frs), ("replicas diverged", k)
+        assert len({(fr[2], fr[3]) for fr in frs}) == 1
+        assert frs[0][2] <= cap
+        if frs[0][2] > 0:
+            assert sum(fr[4] for fr in frs) <= frs[0][2]  # each rank linearized only its chunk
+            updates += 1
+            empty += sum(1 for fr in frs if fr[4] == 0)
+    assert updates > 10 and empty >= 2 * updates  # >= 2 of the 4 ranks without a feature in every update
+    opts = _opts(U, cap)
+    s = _stream(opts)
+    g = U.VioManager(opts)
+    ref = []
+    s.run(g, n_frames=N_FRAMES, on_frame=lambda nf, t: ref.append((g.get_state_vector()[0], g.get_timing())))
+    g.close()
+    for fr, (xr, tr) in zip(frames[0], ref):
+        assert fr[2] == tr["n_msckf"]
+    assert _rel(frames[0][-1][0], ref[-1][0]) < 1e-6
 
 
 # ---- BASELINE sizes (bench.py cfg4 / cfg5 TrackSIM streams) ----
