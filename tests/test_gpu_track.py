@@ -129,6 +129,32 @@ def test_tracks_bit_exact_four_cameras():
     assert bad == 0, (bad, total)
 
 
+@pytest.mark.parametrize("stereo", [True, False])
+def test_tracks_blank_frames(euroc_yaml, stereo):
+    """Empty inputs to the front-end: uniform frames (no FAST corner, every LK window below the eigenvalue
+    threshold) between textured ones, and one camera blank while the other is not.  Detection finds no corner on
+    a blank frame, and LK into one keeps only what the previous image's gradients and RANSAC let through; the
+    ids and uv equal the oracle's after every frame."""
+    import uvio_amd as U
+    from oracle import oracle as O
+    over = {} if stereo else {"use_stereo": 0}
+    opts, s, r = _setup(euroc_yaml, 12, init_max_features=200, **over)
+    g, o = U.VioManager(opts), O.OracleManager(opts)
+    blank = np.full((opts.cams[0].height, opts.cams[0].width), 128, dtype=np.uint8)
+    plan = ["tt", "tt", "tt", "bb", "bb", "tt", "tt", "bt", "tb", "tt", "tt"]
+    total, counts = 0, []
+    for (i, t, imgs), p in zip(_frames(s, r, [0, 1], len(plan)), plan):
+        imgs = [blank if p[k] == "b" else imgs[k] for k in range(2)]
+        g.feed_measurement_camera(t, [0, 1], imgs, allow_uninit=True)
+        o.feed_measurement_camera(t, [0, 1], imgs, allow_uninit=True)
+        n, b = _compare_tracks(g, o, [0, 1])
+        assert b == 0, (i, p, b, n)
+        total += n
+        counts.append((p, n))
+    print("tracks per frame", counts)
+    assert total > 0
+
+
 def test_tracks_mono_masked(euroc_yaml):
     """Monocular feed with a user mask (TrackKLT mask path: kept points, grid cells, griding)."""
     import uvio_amd as U
