@@ -85,16 +85,21 @@ __global__ void __launch_bounds__(64) k_gemm_HPg(const double *__restrict__ H, i
 
 // The same product for large batches (configs 4-5: m ~ 80k stacked rows, n = 172-242): 256-thread
 // workgroups own a 64 x 64 tile of T, K runs in slabs of 16 staged in LDS (the H slab as rows, the
-// gathered P_can slab as a 16 x 64 block), each wave computes a 32 x 32 quarter with four MFMA tiles;
-// the next slab's global loads are issued before the current slab's MFMAs (register double buffer).
-// Operand reuse: every staged element feeds 4 MFMAs instead of 1 (k_gemm_HPg reloads per tile).
+// P_can slab as a 16 x 64 block), each wave computes a 32 x 32 quarter with four MFMA tiles.  Two LDS stages:
+// slab s + 1 is loaded (global -> registers) before slab s's MFMAs and written to the other stage after them,
+// one barrier per slab.  Operand reuse: every staged element feeds 4 MFMAs instead of 1 (k_gemm_HPg reloads per
+// tile).  HIDX: P_can gathered from P through hidx in the loads; without it P is P_can itself (dense n x n,
+// gathered once by k_gather_pcan), which is how the engine runs it.  A compile-time choice: the runtime branch
+// on hidx cost the pcan path half again its time (cfg5: 350 against 224 us per launch, tools/bench_hpg.hip).
+// The accumulation over k is the same ascending 4-wide MFMA chain per element in every variant (bit-identical).
 constexpr int HPB = 64, HPK = 16;
+template <bool HIDX>
 __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict__ H, int m, int n, int ldh,
                                                         const double *__restrict__ P, int ldp,
                                                         const int *__restrict__ hidx, double *__restrict__ T, int ldt,
                                                         int *zero) {
-  __shared__ double As[HPB][HPK + 1];
-  __shared__ double Bs[HPK][HPB + 1];
+  __shared__ double As[2][HPB][HPK + 1];
+  __shared__ double Bs[2][HPK][HPB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
@@ -105,13 +110,11 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
   const int wid = xcd_swizzle(blockIdx.x, gridDim.x), ti = wid / tc;
   const int i0 = ti * HPB, j0 = (wid - ti * tc) * HPB;
   // staging map: A slab element e = tid + 256 u (u < 4): row e / 16, k e % 16; B slab: k e / 64, col e % 64
-  // P_can operand: with hidx the gather P[hidx[k], hidx[c]]; without it P is P_can itself (dense n x n,
-  // gathered once by k_gather_pcan), so the B loads are plain coalesced rows with no dependent index load
   int pcol[4];
 #pragma unroll
   for (int u = 0; u < 4; u++) {
     const int c = j0 + ((tid + 256 * u) & 63);
-    pcol[u] = (c < n) ? (hidx ? hidx[c] : c) : 0;
+    pcol[u] = (c < n) ? (HIDX ? hidx[c] : c) : 0;
   }
   double ra[4], rb[4];
   auto load = [&](int k0) {
@@ -121,7 +124,15 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
       const int ar = i0 + (e >> 4), ak = k0 + (e & 15);
       ra[u] = (ar < m && ak < n) ? H[(size_t)ar * ldh + ak] : 0.0;
       const int bk = k0 + (e >> 6), bc = j0 + (e & 63);
-      rb[u] = (bk < n && bc < n) ? P[(size_t)(hidx ? hidx[bk] : bk) * ldp + pcol[u]] : 0.0;
+      rb[u] = (bk < n && bc < n) ? P[(size_t)(HIDX ? hidx[bk] : bk) * ldp + pcol[u]] : 0.0;
+    }
+  };
+  auto store = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = tid + 256 * u;
+      As[st][e >> 4][e & 15] = ra[u];
+      Bs[st][e >> 6][e & 63] = rb[u];
     }
   };
   dbl4 acc[2][2];
@@ -130,29 +141,28 @@ __global__ void __launch_bounds__(256) k_gemm_HPg_tiled(const double *__restrict
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
   load(0);
+  store(0);
+  __syncthreads();
+  int st = 0;
   for (int k0 = 0; k0 < n; k0 += HPK) {
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int e = tid + 256 * u;
-      As[e >> 4][e & 15] = ra[u];
-      Bs[e >> 6][e & 63] = rb[u];
-    }
-    __syncthreads();
-    if (k0 + HPK < n) load(k0 + HPK);
+    const bool more = k0 + HPK < n;
+    if (more) load(k0 + HPK);
 #pragma unroll
     for (int kk = 0; kk < HPK; kk += 4) {
       double a[2], b[2];
 #pragma unroll
       for (int t = 0; t < 2; t++) {
-        a[t] = As[32 * wr + 16 * t + r16][kk + kq];
-        b[t] = Bs[kk + kq][32 * wc + 16 * t + r16];
+        a[t] = As[st][32 * wr + 16 * t + r16][kk + kq];
+        b[t] = Bs[st][kk + kq][32 * wc + 16 * t + r16];
       }
 #pragma unroll
       for (int ta = 0; ta < 2; ta++)
 #pragma unroll
         for (int tb = 0; tb < 2; tb++) acc[ta][tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ta], b[tb], acc[ta][tb], 0, 0, 0);
     }
+    if (more) store(st ^ 1);  // the other stage: its last readers finished before the previous barrier
+    __syncthreads();
+    st ^= 1;
   }
 #pragma unroll
   for (int ta = 0; ta < 2; ta++)
@@ -360,9 +370,13 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   if (m >= 4096) {  // enough 64 x 64 tiles to fill the 256 CUs
     if (pcan)
       hipLaunchKernelGGL(k_gather_pcan, dim3((n * n + 255) / 256), dim3(256), 0, s, P, bp.ldp, hidx, n, pcan);
-    hipLaunchKernelGGL(k_gemm_HPg_tiled, dim3(((n + HPB - 1) / HPB) * ((m + HPB - 1) / HPB)), dim3(256), 0, s, H_all,
-                       m, n, bp.ldh, pcan ? pcan : P, pcan ? n : bp.ldp, pcan ? nullptr : hidx, T_all, bp.ldh,
-                       acc_count);
+    const dim3 grid(((n + HPB - 1) / HPB) * ((m + HPB - 1) / HPB));
+    if (pcan)
+      hipLaunchKernelGGL(k_gemm_HPg_tiled<false>, grid, dim3(256), 0, s, H_all, m, n, bp.ldh, pcan, n, nullptr, T_all,
+                         bp.ldh, acc_count);
+    else
+      hipLaunchKernelGGL(k_gemm_HPg_tiled<true>, grid, dim3(256), 0, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx, T_all,
+                         bp.ldh, acc_count);
   } else
     hipLaunchKernelGGL(k_gemm_HPg, dim3(8 * ((((n + 15) / 16) * ((m + 15) / 16) + 1) / 2)), dim3(64),
                        sizeof(int) * (size_t)n, s, H_all, m, n, bp.ldh, P, bp.ldp, hidx, T_all, bp.ldh, acc_count);
