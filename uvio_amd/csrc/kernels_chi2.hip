@@ -234,6 +234,92 @@ __global__ void __launch_bounds__(64 * kChiSWaves) k_chi2_S(DBatchParams bp, con
     if (i < R && j <= i) S[(size_t)i * ldS + j] = acc[q] + (i == j ? bp.sigma_pix_sq : 0.0);
   }
 }
+// The same S with one workgroup per feature: the feature's T and H rows are staged in LDS once per 32-column chunk
+// and shared by all its tiles (k_chi2_S reads them again for every tile, from L2 or HBM: about three times the bytes
+// at cfg4 / cfg5).  Wave w keeps the accumulators of tiles w, w + 4, ... across the chunks; every tile is the same
+// ascending chain of 4-wide MFMA steps over k as k_chi2_S's tile_chain (a step exists iff its first k is < n, zero
+// operands past n and past the feature's rows), so S is bit-identical.  Workgroup f serves feature f, on the XCD
+// that k_chi2's workgroup f reads S from.  (256 threads with 9 tiles per wave: 308 VGPRs, one wave per SIMD,
+// 191 / 147 us per launch at cfg5 / cfg4 against k_chi2_S's 209 / 206.)
+constexpr int kS2Threads = 512, kS2Waves = kS2Threads / 64, kS2KC = 32, kS2Tiles = 5;  // up to 40 >= 36 tiles, R <= 128
+__global__ void __launch_bounds__(kS2Threads) k_chi2_S2(DBatchParams bp, const DFeat *__restrict__ feats,
+                                                       const double *__restrict__ H_all, const double *__restrict__ T_all,
+                                                       const DFeatOut *__restrict__ out, double *__restrict__ Sbuf,
+                                                       size_t stride) {
+  extern __shared__ double lds[];
+  const int f = blockIdx.x;
+  if (f >= bp.nfeat) return;
+  const DFeatOut o = out[f];
+  if (o.status != 0 || o.rows <= 0) return;
+  const DFeat F = feats[f];
+  const int n = bp.n_canon, ldh = bp.ldh, c0 = (F.mode >= 2) ? 3 : 0, R = o.rows - c0;
+  if (R <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r16 = lane & 15, kq = lane >> 4;
+  const int nt = (R + 15) / 16, ntiles = nt * (nt + 1) / 2, Rp = 16 * nt;
+  constexpr int LDK = kS2KC + 1;  // odd row stride: the operand reads of a tile hit distinct banks
+  double *Ts = lds, *Hs = lds + (size_t)Rp * LDK;
+  const double *tg = T_all + (size_t)(F.row_off + c0) * ldh, *hg = H_all + (size_t)(F.row_off + c0) * ldh;
+  int ti[kS2Tiles], tj[kS2Tiles];
+#pragma unroll
+  for (int q = 0; q < kS2Tiles; q++) {
+    const int t = wid + kS2Waves * q;
+    int a = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+    while (a * (a + 1) / 2 > t) a--;
+    while ((a + 1) * (a + 2) / 2 <= t) a++;
+    ti[q] = a;
+    tj[q] = t - a * (a + 1) / 2;
+  }
+  dbl4 acc[kS2Tiles];
+#pragma unroll
+  for (int q = 0; q < kS2Tiles; q++) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+  // a chunk's loads all issued before its LDS stores (one memory round trip per chunk), the next chunk's issued
+  // before this chunk's MFMAs
+  constexpr int NU = 128 * kS2KC / kS2Threads;
+  double rt[NU], rh[NU];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int e = tid + kS2Threads * u, r = e / kS2KC, k = k0 + (e % kS2KC);
+      const bool in = r < R && k < n;
+      rt[u] = in ? tg[(size_t)r * ldh + k] : 0.0;
+      rh[u] = in ? hg[(size_t)r * ldh + k] : 0.0;
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < n; k0 += kS2KC) {
+    __syncthreads();  // the previous chunk's operand reads are done
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int e = tid + kS2Threads * u, r = e / kS2KC, c = e % kS2KC;
+      if (r < Rp) {
+        Ts[r * LDK + c] = rt[u];
+        Hs[r * LDK + c] = rh[u];
+      }
+    }
+    __syncthreads();
+    if (k0 + kS2KC < n) load(k0 + kS2KC);
+    for (int s = 0; s < kS2KC && k0 + s < n; s += 4) {
+#pragma unroll
+      for (int q = 0; q < kS2Tiles; q++)
+        if (wid + kS2Waves * q < ntiles) {
+          const double a = Ts[(16 * ti[q] + r16) * LDK + s + kq];
+          const double b = Hs[(16 * tj[q] + r16) * LDK + s + kq];
+          acc[q] = mfma4(a, b, acc[q]);
+        }
+    }
+  }
+  double *S = Sbuf + (size_t)f * stride;
+  const int ldS = R | 1;
+#pragma unroll
+  for (int q = 0; q < kS2Tiles; q++)
+    if (wid + kS2Waves * q < ntiles)
+#pragma unroll
+      for (int qq = 0; qq < 4; qq++) {
+        const int i = 16 * ti[q] + kq + 4 * qq, j = 16 * tj[q] + r16;
+        if (i < R && j <= i) S[(size_t)i * ldS + j] = acc[q][qq] + (i == j ? bp.sigma_pix_sq : 0.0);
+      }
+}
+
 __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
                                               double *__restrict__ T_all, const double *__restrict__ chi2_table,
                                               DFeatOut *__restrict__ out, int use_lds, int *acc_count,
@@ -411,8 +497,19 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
     }
     Sg = *sbuf;
     const int nt = (max_rows_f + 15) / 16, groups = (nt * (nt + 1) / 2 + kChiSWaves - 1) / kChiSWaves;
-    hipLaunchKernelGGL(k_chi2_S, dim3(8 * ((bp.nfeat + 7) / 8) * groups), dim3(64 * kChiSWaves), 0, s, bp, feats, H_all,
-                       T_all, out, Sg, stride, groups);
+    static const bool per_tile = std::getenv("UVIO_HP_CHI2_S_TILES") != nullptr;  // A/B switch: k_chi2_S
+    const size_t s2_bytes = (size_t)2 * 16 * nt * (kS2KC + 1) * sizeof(double);
+    if (!per_tile && nt * (nt + 1) / 2 <= kS2Waves * kS2Tiles) {
+      static int granted2 = -1;
+      if (granted2 < 0) granted2 = set_dyn_lds((const void *)k_chi2_S2, kMaxDynLds);
+      if (s2_bytes > 64 * 1024 && (int)s2_bytes > granted2)
+        throw std::runtime_error("k_chi2_S2 needs " + std::to_string(s2_bytes) + " B of LDS, granted " + std::to_string(granted2));
+      hipLaunchKernelGGL(k_chi2_S2, dim3(bp.nfeat), dim3(kS2Threads), s2_bytes, s, bp, feats, H_all, T_all, out, Sg,
+                         stride);
+    } else {
+      hipLaunchKernelGGL(k_chi2_S, dim3(8 * ((bp.nfeat + 7) / 8) * groups), dim3(64 * kChiSWaves), 0, s, bp, feats,
+                         H_all, T_all, out, Sg, stride, groups);
+    }
   }
   hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(kChi2Threads), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
                      acc_count, Sg, stride);
