@@ -320,6 +320,10 @@ __global__ void __launch_bounds__(kS2Threads) k_chi2_S2(DBatchParams bp, const D
       }
 }
 
+// SMAX: the factorization's panel rows per lane (dense_lds.h ldl_wave_inv), from the batch's largest feature: a
+// compile-time choice, so a batch of small features does not carry the register footprint of the largest instance
+// (one instance for all sizes took 214 VGPRs and one 512-thread workgroup per CU)
+template <int SMAX>
 __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DFeat *__restrict__ feats, double *__restrict__ H_all,
                                               double *__restrict__ T_all, const double *__restrict__ chi2_table,
                                               DFeatOut *__restrict__ out, int use_lds, int *acc_count,
@@ -407,7 +411,7 @@ __global__ void __launch_bounds__(kChi2Threads) k_chi2(DBatchParams bp, const DF
   // LDL^T with the serial chain on one wave (dense_lds.h ldl_wave): the residual row leaves as
   // y = D^-1 L_u^-1 r, so chi2 = r^T S^-1 r = sum_k d_k y_k^2
   double *Dd = Lp;
-  ldl_wave(S, SqLayout{ldS}, R, R + 1, Dd, false);
+  ldl_wave_inv<SMAX>(S, SqLayout{ldS}, R, R + 1, Dd, false);
   CHI2_TS(2)
   double c2 = 0.0;
   for (int k = tid; k < R; k += blockDim.x) {
@@ -471,8 +475,15 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
   size_t bytes = chi2_lds_bytes(max_rows_f, n);
   int use_lds = bytes <= kMaxDynLds;
   if (!use_lds) bytes = ((size_t)(max_rows_f + 1) * (max_rows_f | 1) + 4 * (size_t)(max_rows_f + 1)) * sizeof(double);
-  static int granted = -1;
-  if (granted < 0) granted = set_dyn_lds((const void *)k_chi2, kMaxDynLds);
+  // the instance for the batch's largest feature (R + 1 rows with the residual row)
+  const int smax = (max_rows_f + 1 + 63) / 64;
+  typedef void (*Chi2Fn)(DBatchParams, const DFeat *, double *, double *, const double *, DFeatOut *, int, int *,
+                         const double *, size_t);
+  static const Chi2Fn kChi2Fn[4] = {k_chi2<1>, k_chi2<2>, k_chi2<3>, k_chi2<4>};
+  const Chi2Fn chi2_fn = kChi2Fn[std::min(std::max(smax, 1), 4) - 1];
+  static int granted_inst[4] = {-1, -1, -1, -1};
+  int &granted = granted_inst[std::min(std::max(smax, 1), 4) - 1];
+  if (granted < 0) granted = set_dyn_lds((const void *)chi2_fn, kMaxDynLds);
   if (bytes > 64 * 1024 && (int)bytes > granted)
     throw std::runtime_error("k_chi2 needs " + std::to_string(bytes) + " B of LDS, granted " + std::to_string(granted));
   // features too large for the LDS staging: S over many CUs first (k_chi2_S), k_chi2 reads it
@@ -511,7 +522,7 @@ void launch_chi2_batch(hipStream_t s, const DBatchParams &bp, const DFeat *feats
                          H_all, T_all, out, Sg, stride, groups);
     }
   }
-  hipLaunchKernelGGL(k_chi2, dim3(bp.nfeat), dim3(kChi2Threads), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
+  hipLaunchKernelGGL(chi2_fn, dim3(bp.nfeat), dim3(kChi2Threads), bytes, s, bp, feats, H_all, T_all, chi2_table, out, use_lds,
                      acc_count, Sg, stride);
 }
 
