@@ -877,6 +877,201 @@ static int info_chol_mode(int nrows, int n, size_t *bytes) {
 }
 
 
+// ---- the information-form factors too large for LDS (n + 1 rows beyond the packed triangle, cfg5: 243): split ----
+// Mode 2 ran the one-workgroup factor out of global memory (cfg5: P_II 350 us, Z 290 us per launch).  The split runs
+// the same right-looking LDL^T in four launches, every stored value the one the one-workgroup factor computes:
+//   1  the first n1 columns (a multiple of 16) over ALL rows in LDS, the rows below n1 held in a trapezoid layout
+//      (ldl_wave_inv treats them as right-hand-side rows: the same panel steps and rank-16 tiles as in the full
+//      factor); L_u of those columns and their raw pivots to global memory (G, Dg), their diagonal-block inverses;
+//   2  the trailing block's Schur complement A22 - L21 D1 L21^T, tile by tile: the source value, then the rank-16
+//      updates by blocks 0 .. n1/16 - 1 in order, four MFMAs each with tile_rank16's operands (-L d, L) -- the chain
+//      the one-workgroup factor applies to those tiles, with the same intermediate values;
+//   3  the trailing block (n - n1 columns, N - n1 rows) factored in LDS, packed, its pivots and block inverses;
+//   4  info_chol_body's epilogue (sqrt of the pivots, the scaled block inverses) and the kernel's outputs.
+// SRC 0: P[hidx, hidx] (k_info_cholP), 1: E + s2 I with the augmented row (k_info_cholZ).
+struct TrapLayout {  // rows < n1: packed lower triangle; rows >= n1: n1 columns at an odd stride
+  static constexpr bool square = false;
+  int n1, ld;
+  size_t base;
+  __device__ __forceinline__ size_t operator()(int i, int j) const {
+    return i < n1 ? (size_t)i * (i + 1) / 2 + j : base + (size_t)(i - n1) * ld + j;
+  }
+};
+__host__ __device__ inline size_t trap_lds_doubles(int N, int n1) {
+  return (size_t)n1 * (n1 + 1) / 2 + (size_t)(N - n1) * (n1 | 1) + n1;  // + the pivots
+}
+template <int SRC>
+__device__ __forceinline__ double info_src(const double *src, int lds_, const int *hidx, double s2, int a, int b) {
+  if (SRC == 0) return src[(size_t)hidx[a] * lds_ + hidx[b]];
+  return src[(size_t)a * lds_ + b] + ((a == b) ? s2 : 0.0);
+}
+template <int W, int SRC>
+__global__ void __launch_bounds__(kFactThreads) k_info_split1(const double *__restrict__ src, int lds_,
+                                                              const int *__restrict__ hidx, double s2, int N, int n1,
+                                                              double *__restrict__ G, int ldg, double *__restrict__ Dg,
+                                                              double *__restrict__ Dinv) {
+  extern __shared__ double lds[];
+  const TrapLayout la{n1, n1 | 1, (size_t)n1 * (n1 + 1) / 2};
+  double *A = lds, *Dd = lds + la.base + (size_t)(N - n1) * la.ld;
+  staged_copy(
+      N * n1,
+      [&](int e) {
+        const int a = e / n1, b = e - a * n1;
+        return (b <= a) ? info_src<SRC>(src, lds_, hidx, s2, a, b) : 0.0;
+      },
+      [&](int e, double v) {
+        const int a = e / n1, b = e - a * n1;
+        if (b <= a) A[la(a, b)] = v;
+      });
+  __syncthreads();
+  ldl_wave_inv<1, TrapLayout, W>(A, la, n1, N, Dd, false, Dinv);
+  for (int e = threadIdx.x; e < N * n1; e += blockDim.x) {
+    const int a = e / n1, b = e - a * n1;
+    if (b < a) G[(size_t)a * ldg + b] = A[la(a, b)];
+  }
+  for (int k = threadIdx.x; k < n1; k += blockDim.x) Dg[k] = Dd[k];
+}
+// one wave per 16 x 16 lower tile (I, C) of the trailing block (rows n1 .. N - 1, columns n1 .. n - 1)
+template <int SRC>
+__global__ void __launch_bounds__(256) k_info_split_schur(const double *__restrict__ src, int lds_,
+                                                         const int *__restrict__ hidx, double s2, int N, int n, int n1,
+                                                         double *__restrict__ G, int ldg, const double *__restrict__ Dg) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kq = lane >> 4;
+  const int nbr = (N - n1 + 15) / 16, nbc = (n - n1 + 15) / 16;
+  int t = blockIdx.x * 4 + (threadIdx.x >> 6), I = 0;
+  // lower tiles (I, C), C <= min(I, nbc - 1), row-major
+  while (I < nbr && t >= min(I, nbc - 1) + 1) {
+    t -= min(I, nbc - 1) + 1;
+    I++;
+  }
+  if (I >= nbr) return;
+  const int C = t, i0 = n1 + 16 * I, j0 = n1 + 16 * C;
+  dbl4 acc;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    acc[q] = (row < N && col < n && col <= row) ? info_src<SRC>(src, lds_, hidx, s2, row, col) : 0.0;
+  }
+  const int arow = min(i0 + r16, N - 1), bcol = min(j0 + r16, n - 1);
+  const bool av = i0 + r16 < N, bv = j0 + r16 < n;
+  for (int oP = 0; oP < n1; oP += 16) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int kk = oP + 4 * u + kq;
+      a[u] = av ? -G[(size_t)arow * ldg + kk] * Dg[kk] : 0.0;
+      b[u] = bv ? G[(size_t)bcol * ldg + kk] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int row = i0 + kq + 4 * q, col = j0 + r16;
+    if (row < N && col < n && col <= row) G[(size_t)row * ldg + col] = acc[q];
+  }
+}
+template <int W>
+__global__ void __launch_bounds__(kFactThreads) k_info_split3(double *__restrict__ G, int ldg, int N, int n, int n1,
+                                                              double *__restrict__ Dg, double *__restrict__ Dinv) {
+  extern __shared__ double lds[];
+  const int m = n - n1, R = N - n1;
+  double *A = lds, *Dd = lds + packed_lds_doubles(R);
+  const PkLayout la{};
+  staged_copy(
+      R * m,
+      [&](int e) {
+        const int a = e / m, b = e - a * m;
+        return (b <= a) ? G[(size_t)(n1 + a) * ldg + n1 + b] : 0.0;
+      },
+      [&](int e, double v) {
+        const int a = e / m, b = e - a * m;
+        if (b <= a) A[la(a, b)] = v;
+      });
+  __syncthreads();
+  ldl_wave_inv<1, PkLayout, W>(A, la, m, R, Dd, false, Dinv + (size_t)256 * (n1 / 16));
+  for (int e = threadIdx.x; e < R * m; e += blockDim.x) {
+    const int a = e / m, b = e - a * m;
+    if (b < a) G[(size_t)(n1 + a) * ldg + n1 + b] = A[la(a, b)];
+  }
+  for (int k = threadIdx.x; k < m; k += blockDim.x) Dg[n1 + k] = Dd[k];
+}
+// info_chol_body's epilogue and the factor kernel's outputs.  OUT 0 (k_info_cholP): Laug, Lout; 1 (k_info_cholZ):
+// U (out0), w (out1, the augmented row).  Dg: the raw pivots, replaced by their square roots.
+template <int OUT>
+__global__ void __launch_bounds__(256) k_info_split_out(const double *__restrict__ G, int ldg, int n,
+                                                       double *__restrict__ Dg, double *__restrict__ Dinv,
+                                                       double *__restrict__ out0, double *__restrict__ out1) {
+  __shared__ double Ds[kWaveMaxRows];
+  for (int k = threadIdx.x; k < n; k += blockDim.x) Ds[k] = sqrt(Dg[k]);
+  __syncthreads();
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  const int nb = (n + 15) / 16;
+  for (int e = tid; e < 256 * nb; e += nth) {
+    const int row = 16 * (e >> 8) + ((e >> 4) & 15);
+    if (row < n) Dinv[e] = Dinv[e] / Ds[row];
+  }
+  if (OUT == 0) {
+    const int na = n + 1;
+    for (int e = tid; e < na * na; e += nth) {
+      const int a = e / na, b = e - a * na;
+      double v = 0.0;
+      if (a < n && b < n) v = (b < a) ? G[(size_t)a * ldg + b] * Ds[b] : (b == a ? Ds[a] : 0.0);
+      else if (a == n && b == n) v = 1.0;
+      out0[e] = v;
+      if (a < n && b < n) out1[(size_t)a * n + b] = v;
+    }
+  } else {
+    for (int j = tid; j < n; j += nth) out1[j] = G[(size_t)n * ldg + j] * Ds[j];
+    for (int e = tid; e < n * n; e += nth) {
+      const int a = e / n, b = e - a * n;
+      out0[e] = (b < a) ? G[(size_t)a * ldg + b] * Ds[b] : (b == a ? Ds[a] : 0.0);
+    }
+  }
+  // the pivots' square roots are written back only after every block has read the raw ones: not needed, Dg is
+  // scratch (each block forms its own Ds)
+}
+typedef void (*Split1Fn)(const double *, int, const int *, double, int, int, double *, int, double *, double *);
+typedef void (*Split3Fn)(double *, int, int, int, int, double *, double *);
+static const Split1Fn kSplit1[2][5] = {
+    {k_info_split1<1, 0>, k_info_split1<2, 0>, k_info_split1<3, 0>, k_info_split1<4, 0>, k_info_split1<5, 0>},
+    {k_info_split1<1, 1>, k_info_split1<2, 1>, k_info_split1<3, 1>, k_info_split1<4, 1>, k_info_split1<5, 1>}};
+static const Split3Fn kSplit3[5] = {k_info_split3<1>, k_info_split3<2>, k_info_split3<3>, k_info_split3<4>,
+                                    k_info_split3<5>};
+// the split's first block: the widest multiple of 16 whose trapezoid fits in LDS and leaves a trailing block that
+// fits packed; 0 when there is none
+static int info_split_n1(int N, int n) {
+  for (int n1 = (n - 1) / 16 * 16; n1 >= 16; n1 -= 16) {
+    const size_t t1 = trap_lds_doubles(N, n1) * sizeof(double);
+    const size_t t3 = (packed_lds_doubles(N - n1) + (n - n1)) * sizeof(double);
+    if (t1 <= (size_t)kMaxDynLds && t3 <= (size_t)kMaxDynLds) return n1;
+  }
+  return 0;
+}
+// the factor of an N x n matrix (N = n or n + 1) from SRC through the split; G (ld ldg) and Dg scratch
+template <int SRC, int OUT>
+static void launch_info_split(hipStream_t s, int n1, const double *src, int lds_, const int *hidx, double s2, int N,
+                              int n, double *G, int ldg, double *Dg, double *Dinv, double *out0, double *out1) {
+  static bool attrs = false;
+  if (!attrs) {
+    for (int w = 0; w < 5; w++)
+      if (set_dyn_lds((const void *)kSplit1[SRC][w], kMaxDynLds) < kMaxDynLds ||
+          set_dyn_lds((const void *)kSplit3[w], kMaxDynLds) < kMaxDynLds)
+        throw std::runtime_error("dynamic LDS limit not granted for the split information-form factor");
+    attrs = true;
+  }
+  hipLaunchKernelGGL(kSplit1[SRC][panel_waves(N) - 1], dim3(1), dim3(kFactThreads), trap_lds_doubles(N, n1) * sizeof(double),
+                     s, src, lds_, hidx, s2, N, n1, G, ldg, Dg, Dinv);
+  const int nbr = (N - n1 + 15) / 16, nbc = (n - n1 + 15) / 16;
+  int tiles = 0;
+  for (int I = 0; I < nbr; I++) tiles += std::min(I, nbc - 1) + 1;
+  hipLaunchKernelGGL(k_info_split_schur<SRC>, dim3((tiles + 3) / 4), dim3(256), 0, s, src, lds_, hidx, s2, N, n, n1, G,
+                     ldg, Dg);
+  hipLaunchKernelGGL(kSplit3[panel_waves(N - n1) - 1], dim3(1), dim3(kFactThreads),
+                     (packed_lds_doubles(N - n1) + (n - n1)) * sizeof(double), s, G, ldg, N, n, n1, Dg, Dinv);
+  hipLaunchKernelGGL(k_info_split_out<OUT>, dim3(32), dim3(256), 0, s, G, ldg, n, Dg, Dinv, out0, out1);
+}
+
 // P[i][j] -= sum_k V[i][k] V[j][k] - s2 sum_k X[i][k] X[j][k]  for j >= i, mirrored;  dx = X w;
 // negative-diagonal count.   (P+ = P - V (I - s2 Z^-1) V^T, see launch_ekf_info)
 // Grid over the upper 16 x 16 tile pairs (bi <= bj) of P, 4 waves: wave w accumulates both products over the
@@ -977,8 +1172,13 @@ void launch_ekf_info_pre(hipStream_t s, const double *P, int ldp, int N, int n, 
   if (n + 1 > kWaveMaxRows) throw std::runtime_error("information-form update wider than the factorization panel");
   size_t b1 = 0;
   const int m1 = info_chol_mode(n, n, &b1);
-  hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(kFactThreads), b1, s, P, ldp, hidx, n, Laug, Lf, sc.M,
-                     m1, sc.Dinv);
+  static const bool no_split = std::getenv("UVIO_HP_NO_INFO_SPLIT") != nullptr;  // A/B: the global-memory factor
+  const int s1 = (m1 == 2 && !no_split) ? info_split_n1(n, n) : 0;
+  if (s1 > 0)  // the raw pivots in T1 (free until the post half)
+    launch_info_split<0, 0>(s, s1, P, ldp, hidx, 0.0, n, n, sc.M, n | 1, Lf + (size_t)n * n, sc.Dinv, Laug, Lf);
+  else
+    hipLaunchKernelGGL(pick_info_kernel(kCholP, n, m1), dim3(1), dim3(kFactThreads), b1, s, P, ldp, hidx, n, Laug, Lf,
+                       sc.M, m1, sc.Dinv);
   launch_trsm_lt(s, P, ldp, hidx, N, n, Lf, n, sc.Dinv, sc.M, false);  // V = P[:,I] L^-T
 }
 
@@ -996,8 +1196,13 @@ void launch_ekf_info_post(hipStream_t s, double *P, int ldp, int N, const double
   launch_gemm_mfma(s, 1, 0, 2, 0, na, na, na, Laug, na, T1, na, E, na);     // Laug^T (G Laug)
   size_t b2 = 0;
   const int m2 = info_chol_mode(n + 1, n, &b2);
-  hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(kFactThreads), b2, s, E, n, sigma2, Uf, w, sc.W, m2,
-                     sc.Dinv);
+  static const bool no_split = std::getenv("UVIO_HP_NO_INFO_SPLIT") != nullptr;
+  const int s2 = (m2 == 2 && !no_split) ? info_split_n1(n + 1, n) : 0;
+  if (s2 > 0)  // the raw pivots in T1 (consumed by the second product above)
+    launch_info_split<1, 1>(s, s2, E, na, nullptr, sigma2, n + 1, n, sc.W, n | 1, T1, sc.Dinv, Uf, w);
+  else
+    hipLaunchKernelGGL(pick_info_kernel(kCholZ, n + 1, m2), dim3(1), dim3(kFactThreads), b2, s, E, n, sigma2, Uf, w, sc.W,
+                       m2, sc.Dinv);
   launch_trsm_lt(s, sc.M, n, nullptr, N, n, Uf, n, sc.Dinv, sc.W, false);  // X = V U^-T
   const int nb = (N + 15) / 16;
   const int per = (nb * (nb + 1) / 2 + kInfoPXcds - 1) / kInfoPXcds;
