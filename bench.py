@@ -281,7 +281,7 @@ def pmc_files(workload):
 # the kernels one timed "launch" of a class (one HIP-event pair around a launch chain, kprof.h) contains exactly
 # once: their PMC launch count is the class's group count
 CLASS_GROUP_KERNELS = {"feature": ["k_feature"], "chi2": ["k_chi2"], "gram": ["k_gram", "k_gram_mfma"],
-                       "ekf_update": ["k_ekf_fact", "k_info_cholZ"], "ldl": ["k_ekf_fact"], "lk": ["k_lk"],
+                       "ekf_update": ["k_ekf_fact", "k_info_P"], "ldl": ["k_ekf_fact"], "lk": ["k_lk"],
                        "pyramid": ["k_hist_multi"], "fast": ["k_fast_score"], "subpix": ["k_subpix"]}
 
 

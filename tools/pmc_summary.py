@@ -42,7 +42,7 @@ if len(sys.argv) > 4:
             out["kernels"][k]["mfma_f64_flops"] = 512.0 * sum(v) / len(v)
             b = B.get(k, [0.0])
             out["kernels"][k]["mfma_busy_cycles"] = sum(b) / len(b)
-grp = ["k_feature", "k_gemm_HPg", "k_gemm_HPg_tiled", "k_chi2_S", "k_chi2"]
+grp = ["k_feature", "k_gemm_HPg", "k_gemm_HPg_tiled", "k_chi2_S", "k_chi2_S2", "k_chi2"]
 # per launch group (one k_feature each; the T GEMM is one of the two variants; the delayed-init groups run
 # no chi2 kernel): the group kernels' total bytes over the number of groups
 ngroups = out["kernels"]["k_feature"]["launches"]

@@ -460,10 +460,10 @@ void Engine::kernel_stats(bool flush, uvio_hp_kstat_t *out, int cap, int *n) {
     int bound;
   } info[KC_COUNT] = {
       {"feature", "k_feature", 1},
-      {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2_S,k_chi2", 1},
+      {"chi2", "k_gather_pcan,k_gemm_HPg,k_gemm_HPg_tiled,k_chi2_S,k_chi2_S2,k_chi2", 1},
       {"gram", "k_gram,k_gram_mfma", 1},
       {"ekf_update", "k_ekf_MS,k_ekf_fact,k_ekf_WP,k_gram_reduce,k_info_cholP,k_gemm_mfma,k_info_cholZ,k_trinv16,"
-                     "k_trsm_lt,k_info_P,k_di_M,k_di_S",
+                     "k_trsm_lt,k_info_P,k_di_M,k_di_S,k_info_split1,k_info_split_schur,k_info_split3,k_info_split_out",
        1},
       {"ldl", "k_ekf_fact", 1},
       {"lk", "k_lk", 0},
