@@ -542,6 +542,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   }
   std::vector<FeatP> feats_maxtracks;
   {
+    HPROF("select.maxtracks");
     std::vector<FeatP> keep;
     for (auto &f : feats_marg) {
       bool reached = false;
@@ -575,7 +576,10 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
     if (!f2 && cur) lm.second->should_marg = true;
     if (lm.second->fail_count > 1) lm.second->should_marg = true;
   }
-  marginalize_slam();
+  {
+    HPROF("select.marg_slam");
+    marginalize_slam();
+  }
   std::vector<FeatP> slam_delayed, slam_upd;
   for (auto &f : feats_slam) {
     if (slam_.find(f->featid) != slam_.end())
@@ -589,6 +593,7 @@ int Engine::do_feature_propagate_update(double t, const std::vector<int> &camids
   // VioManager.cpp:518 std::sort by measurement count (compare_feat), on the counts computed once: std::sort's
   // permutation depends only on the comparison outcomes, which are the same
   {
+    HPROF("select.sort");
     std::vector<std::pair<int, FeatP>> keyed(up.size());
     for (size_t i = 0; i < up.size(); i++) keyed[i] = {up[i]->count(), std::move(up[i])};
     std::sort(keyed.begin(), keyed.end(),

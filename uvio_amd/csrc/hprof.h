@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <string>
 
 namespace uvhp {
@@ -13,9 +14,11 @@ namespace uvhp {
 struct HostProf {
   bool on = std::getenv("UVIO_HP_HOST_PROF") != nullptr;
   std::map<std::string, std::pair<double, long>> acc, cnt;
+  std::mutex mu;  // sections may close on a worker thread (the TrackSIM feed's propagation task)
   // a per-frame quantity (sizes, counts) averaged over the calls
   void count(const char *name, double v) {
     if (!on) return;
+    std::lock_guard<std::mutex> lk(mu);
     auto &a = cnt[name];
     a.first += v;
     a.second++;
@@ -40,6 +43,7 @@ struct HostProfScope {
   }
   ~HostProfScope() {
     if (!p.on) return;
+    std::lock_guard<std::mutex> lk(p.mu);
     auto &a = p.acc[name];
     a.first += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     a.second++;
